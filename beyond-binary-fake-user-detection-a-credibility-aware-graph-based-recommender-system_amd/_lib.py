@@ -1,0 +1,196 @@
+"""ctypes binding of libbbgr.so (the C ABI declared in include/bbgr.h).
+
+The shared library is the product: every device computation of this package
+goes through it. There is no CPU fallback — if the library is missing, or
+no GPU is visible when a kernel is called, this module raises.
+
+torch is imported first so that libbbgr.so binds to the HIP runtime torch
+already loaded (both carry SONAME libamdhip64.so.7): one runtime, one device
+context, torch's caching allocator owns every buffer we touch, and every call
+is ordered on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+import torch  # noqa: F401  (must load torch's HIP runtime before libbbgr.so)
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "lib" / "libbbgr.so"
+HEADER_PATH = PKG_DIR.parent / "include" / "bbgr.h"
+
+BBGR_OK = 0
+STATUS = {0: "BBGR_OK", -1: "BBGR_ERR_INVALID", -2: "BBGR_ERR_UNSUPPORTED",
+          -3: "BBGR_ERR_HIP", -4: "BBGR_ERR_WORKSPACE"}
+
+OP_GS, OP_METHOD_A, OP_J, OP_SYM = 0, 1, 2, 3
+NEG_CAP = 65536
+
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_float = ctypes.c_float
+c_double = ctypes.c_double
+c_void_p = ctypes.c_void_p
+c_size_t = ctypes.c_size_t
+c_uint64 = ctypes.c_uint64
+
+
+class BbgrError(RuntimeError):
+    """A libbbgr entry point returned a negative bbgr_status."""
+
+    def __init__(self, fn: str, rc: int, msg: str):
+        super().__init__(f"{fn} failed: {STATUS.get(rc, rc)}: {msg}")
+        self.rc = rc
+
+
+class CsrStruct(ctypes.Structure):
+    _fields_ = [
+        ("n_rows", c_int32), ("n_cols", c_int32), ("nnz", c_int64),
+        ("indptr", c_void_p), ("indices", c_void_p),
+        ("long_threshold", c_int32), ("chunk_edges", c_int32),
+        ("n_chunks", c_int32), ("n_split", c_int32),
+        ("chunks", c_void_p), ("split", c_void_p),
+    ]
+
+
+class SpmmArgs(ctypes.Structure):
+    _fields_ = [
+        ("d", c_int32),
+        ("x", c_void_p), ("ldx", c_int64),
+        ("weight_mode", c_int32),
+        ("edge_val", c_void_p), ("col_scale", c_void_p), ("col_scale_s", c_float),
+        ("y", c_void_p), ("ldy", c_int64),
+        ("y_scale", c_void_p), ("y_scale_s", c_float),
+        ("add", c_void_p), ("ldadd", c_int64),
+        ("add_scale", c_void_p), ("add_scale_s", c_float),
+        ("acc_in", c_void_p), ("ldacc_in", c_int64),
+        ("acc_out", c_void_p), ("ldacc_out", c_int64),
+        ("acc_scale", c_void_p), ("acc_scale_s", c_float),
+        ("gamma", c_float),
+        ("partial", c_void_p),
+    ]
+
+
+class BprArgs(ctypes.Structure):
+    _fields_ = [
+        ("batch", c_int64), ("d", c_int32),
+        ("n_users", c_int64), ("n_items", c_int64),
+        ("users", c_void_p), ("pos", c_void_p), ("neg", c_void_p),
+        ("uf", c_void_p), ("lduf", c_int64),
+        ("itf", c_void_p), ("ldif", c_int64),
+        ("ue", c_void_p), ("ldue", c_int64),
+        ("ie", c_void_p), ("ldie", c_int64),
+        ("pop", c_void_p),
+        ("reg", c_float), ("lambda_fair", c_float),
+        ("parts", c_void_p), ("dloss", c_void_p),
+        ("g_uf", c_void_p), ("ldguf", c_int64),
+        ("g_if", c_void_p), ("ldgif", c_int64),
+        ("g_ue", c_void_p), ("ldgue", c_int64),
+        ("g_ie", c_void_p), ("ldgie", c_int64),
+    ]
+
+
+_P = c_void_p
+_SIGNATURES = {
+    "bbgr_abi_version": ([], c_int32),
+    "bbgr_last_error": ([], ctypes.c_char_p),
+    "bbgr_device_info": ([ctypes.c_int, _P, ctypes.c_char_p, ctypes.c_int], c_int32),
+    "bbgr_sync": ([_P], c_int32),
+    "bbgr_csr_build": ([c_int64, _P, _P, c_int32, c_int32, _P, _P, _P, _P,
+                        ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_csr_plan_count": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(c_int32),
+                             ctypes.POINTER(c_int32), _P, ctypes.POINTER(c_size_t), _P],
+                            c_int32),
+    "bbgr_csr_plan_build": ([ctypes.POINTER(CsrStruct), _P, _P, _P,
+                             ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_operator_scales": ([c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P,
+                              _P, _P, _P, _P, _P], c_int32),
+    "bbgr_spmm": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(SpmmArgs), _P], c_int32),
+    "bbgr_bpr": ([ctypes.POINTER(BprArgs), _P], c_int32),
+    "bbgr_bpr_reduce": ([c_int64, _P, c_float, c_float, _P, _P], c_int32),
+    "bbgr_adam": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
+                   c_float, c_float, c_float, _P], c_int32),
+    "bbgr_rows_zero": ([c_int64, _P, _P, c_int64, c_int32, _P], c_int32),
+    "bbgr_rows_axpy": ([c_int64, _P, c_float, _P, c_int64, _P, c_int64, c_int32, _P],
+                       c_int32),
+    "bbgr_pop_cdf": ([c_int32, _P, c_double, _P, _P, ctypes.POINTER(c_size_t), _P],
+                     c_int32),
+    "bbgr_sample": ([c_int64, _P, _P, _P, c_int32, _P, c_float, c_int32, c_uint64,
+                     c_uint64, _P, _P, _P, _P], c_int32),
+    "bbgr_shuffle": ([c_int64, _P, _P, c_uint64, c_uint64, _P,
+                      ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_nonempty_rows": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P],
+                           c_int32),
+}
+
+_lib = None
+
+
+def header_symbols(header: Path = HEADER_PATH) -> list[str]:
+    """Every `bbgr_*(` function declared in include/bbgr.h."""
+    text = header.read_text()
+    return sorted(set(re.findall(r"\b(bbgr_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libbbgr.so (once). Raises loudly if it was not built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(
+                f"libbbgr.so not found at {LIB_PATH}; build it with "
+                f"`python -c 'import __graft_entry__ as g; g.build()'` or "
+                f"`make -C {PKG_DIR / 'csrc'}`")
+        handle = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+        for name, (argtypes, restype) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        if handle.bbgr_abi_version() != 1:
+            raise ImportError("libbbgr.so ABI version mismatch")
+        _lib = handle
+    return _lib
+
+
+def check(fn_name: str, rc: int) -> None:
+    if rc != BBGR_OK:
+        msg = lib().bbgr_last_error()
+        raise BbgrError(fn_name, rc, msg.decode() if msg else "")
+
+
+def call(fn_name: str, *args) -> None:
+    check(fn_name, getattr(lib(), fn_name)(*args))
+
+
+def require_gpu(t: torch.Tensor | None = None) -> None:
+    if not torch.cuda.is_available():
+        raise RuntimeError("bbgr kernels need a ROCm GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback")
+    if t is not None and not t.is_cuda:
+        raise ValueError("bbgr kernels take device tensors; got a CPU tensor")
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+def ld(t: torch.Tensor | None) -> int:
+    if t is None:
+        return 0
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("tables must be 2-D with unit column stride")
+    return t.stride(0)
+
+
+def workspace_query(fn_name: str, *args_before_ws, args_after=()) -> int:
+    """Run an entry point in size-query mode (workspace=NULL)."""
+    n = c_size_t(0)
+    call(fn_name, *args_before_ws, None, ctypes.byref(n), *args_after)
+    return n.value

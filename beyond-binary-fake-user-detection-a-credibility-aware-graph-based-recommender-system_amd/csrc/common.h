@@ -1,0 +1,80 @@
+// Shared helpers for the bbgr HIP sources: error state, launch checks,
+// Philox4x32-10 counter-based RNG. gfx950 (CDNA4, wave64) only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "bbgr.h"
+
+namespace bbgr {
+
+void set_error(const char *fmt, ...);
+
+inline int hip_fail(hipError_t e, const char *what) {
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return BBGR_ERR_HIP;
+}
+
+#define BBGR_HIP(call)                                                        \
+  do {                                                                        \
+    hipError_t e_ = (call);                                                   \
+    if (e_ != hipSuccess) return ::bbgr::hip_fail(e_, #call);                 \
+  } while (0)
+
+#define BBGR_LAUNCHED(name)                                                   \
+  do {                                                                        \
+    hipError_t e_ = hipGetLastError();                                        \
+    if (e_ != hipSuccess) return ::bbgr::hip_fail(e_, "launch " name);       \
+  } while (0)
+
+#define BBGR_REQUIRE(cond, msg)                                               \
+  do {                                                                        \
+    if (!(cond)) {                                                            \
+      ::bbgr::set_error("%s", msg);                                           \
+      return BBGR_ERR_INVALID;                                                \
+    }                                                                         \
+  } while (0)
+
+inline hipStream_t as_stream(bbgr_stream_t s) {
+  return reinterpret_cast<hipStream_t>(s);
+}
+
+inline bool aligned16(const void *p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+// Round a workspace carve offset up to 256 bytes.
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11). Counter (c0..c3), key (k0,k1).
+// ---------------------------------------------------------------------------
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0,
+                                               uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// 53-bit uniform double in [0,1) from two 32-bit words.
+__device__ __forceinline__ double u01_53(uint32_t a, uint32_t b) {
+  const uint64_t v = ((uint64_t)a << 32 | b) >> 11;
+  return (double)v * (1.0 / 9007199254740992.0);
+}
+
+}  // namespace bbgr

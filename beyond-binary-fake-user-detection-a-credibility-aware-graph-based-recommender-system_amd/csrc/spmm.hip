@@ -1,0 +1,336 @@
+// Fused CSR-SpMM for the LightGCN propagation (gfx950).
+//
+// Replaces torch.sparse.mm(M, X) at Version-2/lighgcn_cu_pop.py:483-484,
+// lightgcn_cu.py:431,434, lightgcn.py:323 (and the autograd backward of each,
+// which is the same product on the transposed CSR), fused with the layer-mean
+// accumulation of Version-2/lighgcn_cu_pop.py:488-489.
+//
+// Work decomposition (HBM/gather-bound, no MFMA):
+//   * one 16-lane group owns one output row; each lane holds D/64 float4 of the
+//     row, so a group reads a whole source row (D*4 bytes) with one coalesced
+//     16-B-per-lane load per float4 column block; a wave gathers 4 rows per
+//     load instruction and keeps 16/V rows in flight per group.
+//   * rows with deg > long_threshold are cut into chunks of <= chunk_edges
+//     edges; each chunk is one 256-thread workgroup (16 groups on contiguous
+//     edge sub-ranges, fixed-order LDS reduction). Chunk blocks come first in
+//     the grid so the heavy (power-law) rows start early.
+//   * rows cut into >1 chunk write per-chunk partials; a fix-up launch sums
+//     them in chunk order. Every reduction order is fixed: the result is
+//     bitwise deterministic (no atomics).
+#include <stdarg.h>
+
+#include "common.h"
+
+namespace bbgr {
+
+struct SpmmParams {
+  int n_rows;
+  int long_threshold;
+  int n_chunks;
+  const int *indptr;
+  const int *indices;
+  const int4 *chunks;
+  const int4 *split;
+  const float *x;
+  long ldx;
+  const float *edge_val;
+  const float *col_scale;
+  float col_scale_s;
+  float *y;
+  long ldy;
+  const float *y_scale;
+  float y_scale_s;
+  const float *add;
+  long ldadd;
+  const float *add_scale;
+  float add_scale_s;
+  const float *acc_in;
+  long ldacc_in;
+  float *acc_out;
+  long ldacc_out;
+  const float *acc_scale;
+  float acc_scale_s;
+  float gamma;
+  float *partial;
+};
+
+__device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
+  return make_float4(fmaf(a, x.x, y.x), fmaf(a, x.y, y.y), fmaf(a, x.z, y.z),
+                     fmaf(a, x.w, y.w));
+}
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4_mul(float a, float4 x) {
+  return make_float4(a * x.x, a * x.y, a * x.z, a * x.w);
+}
+
+// Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
+template <int D, int WMODE>
+__device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
+                                             int lane, float4 (&acc)[D / 64]) {
+  constexpr int V = D / 64;
+  constexpr int U = 16 / V;  // source rows in flight per group per batch
+  for (int e0 = eb; e0 < ee; e0 += 16) {
+    const int n = min(16, ee - e0);
+    int my = 0;
+    float mw = 0.f;
+    if (lane < n) {
+      my = P.indices[e0 + lane];
+      if (WMODE == 1) mw = P.edge_val[e0 + lane];
+      if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
+    }
+    for (int j0 = 0; j0 < n; j0 += U) {
+      float4 v[U][V];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int c = __shfl(my, j0 + j, 16);
+        if (j0 + j < n) {
+          const float4 *src =
+              reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + lane;
+#pragma unroll
+          for (int k = 0; k < V; ++k) v[j][k] = src[16 * k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < V; ++k) v[j][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (WMODE == 0) {
+#pragma unroll
+          for (int k = 0; k < V; ++k) acc[k] = f4_add(acc[k], v[j][k]);
+        } else {
+          const float w = __shfl(mw, j0 + j, 16);
+#pragma unroll
+          for (int k = 0; k < V; ++k) acc[k] = f4_fma(w, v[j][k], acc[k]);
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
+                                         const float4 (&T)[D / 64]) {
+  constexpr int V = D / 64;
+  if (P.y) {
+    const float ys = (P.y_scale ? P.y_scale[row] : 1.f) * P.y_scale_s;
+    float4 *dst = reinterpret_cast<float4 *>(P.y + (long)row * P.ldy) + lane;
+    if (P.add) {
+      const float as = (P.add_scale ? P.add_scale[row] : 1.f) * P.add_scale_s;
+      const float4 *ad =
+          reinterpret_cast<const float4 *>(P.add + (long)row * P.ldadd) + lane;
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+        dst[16 * k] = f4_fma(as, ad[16 * k], f4_mul(ys, T[k]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) dst[16 * k] = f4_mul(ys, T[k]);
+    }
+  }
+  if (P.acc_out) {
+    const float cs = (P.acc_scale ? P.acc_scale[row] : 1.f) * P.acc_scale_s;
+    float4 *dst =
+        reinterpret_cast<float4 *>(P.acc_out + (long)row * P.ldacc_out) + lane;
+    if (P.acc_in) {
+      const float4 *ai =
+          reinterpret_cast<const float4 *>(P.acc_in + (long)row * P.ldacc_in) +
+          lane;
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+        dst[16 * k] = f4_mul(P.gamma, f4_fma(cs, T[k], ai[16 * k]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) dst[16 * k] = f4_mul(P.gamma, f4_mul(cs, T[k]));
+    }
+  }
+}
+
+// Fixed-order reduction of the 16 group partials held in LDS; result lands in
+// red[0][*]. Called by all 256 threads.
+template <int D>
+__device__ __forceinline__ void block_reduce16(float4 *red, int g, int lane,
+                                               const float4 (&acc)[D / 64]) {
+  constexpr int V = D / 64;
+  constexpr int W = D / 4;  // float4 per row
+#pragma unroll
+  for (int k = 0; k < V; ++k) red[g * W + lane + 16 * k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < W) {
+    float4 s = red[threadIdx.x];
+#pragma unroll
+    for (int gg = 1; gg < 16; ++gg) s = f4_add(s, red[gg * W + threadIdx.x]);
+    red[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
+  constexpr int V = D / 64;
+  __shared__ float4 red[16 * (D / 4)];
+  const int g = threadIdx.x >> 4;
+  const int lane = threadIdx.x & 15;
+  float4 acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  if ((int)blockIdx.x < P.n_chunks) {
+    // ---- one chunk of a long row: whole workgroup --------------------------
+    const int4 ch = P.chunks[blockIdx.x];  // row, e_begin, e_end, slot
+    const int len = ch.z - ch.y;
+    const int per = (((len + 15) >> 4) + 15) & ~15;  // multiple of 16
+    const int gb = ch.y + g * per;
+    const int ge = min(ch.z, gb + per);
+    if (gb < ge) gather_range<D, WMODE>(P, gb, ge, lane, acc);
+    block_reduce16<D>(red, g, lane, acc);
+    if (g == 0) {
+      float4 T[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
+      if (ch.w < 0) {
+        epilogue<D>(P, ch.x, lane, T);
+      } else {
+        float4 *dst = reinterpret_cast<float4 *>(P.partial) + (long)ch.w * (D / 4) + lane;
+#pragma unroll
+        for (int k = 0; k < V; ++k) dst[16 * k] = T[k];
+      }
+    }
+    return;
+  }
+
+  // ---- short rows: one 16-lane group per row ------------------------------
+  const long row = (long)(blockIdx.x - P.n_chunks) * 16 + g;
+  if (row >= P.n_rows) return;
+  const int eb = P.indptr[row];
+  const int ee = P.indptr[row + 1];
+  if (ee - eb > P.long_threshold) return;  // owned by chunk blocks
+  gather_range<D, WMODE>(P, eb, ee, lane, acc);
+  epilogue<D>(P, (int)row, lane, acc);
+}
+
+// Rows split into >1 chunk: sum chunk partials in chunk order, then epilogue.
+template <int D>
+__global__ __launch_bounds__(256) void spmm_fixup_kernel(SpmmParams P) {
+  constexpr int V = D / 64;
+  __shared__ float4 red[16 * (D / 4)];
+  const int g = threadIdx.x >> 4;
+  const int lane = threadIdx.x & 15;
+  const int4 sp = P.split[blockIdx.x];  // row, slot_begin, n_slots
+  float4 acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sl = g; sl < sp.z; sl += 16) {
+    const float4 *src =
+        reinterpret_cast<const float4 *>(P.partial) + (long)(sp.y + sl) * (D / 4) + lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = f4_add(acc[k], src[16 * k]);
+  }
+  block_reduce16<D>(red, g, lane, acc);
+  if (g == 0) {
+    float4 T[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
+    epilogue<D>(P, sp.x, lane, T);
+  }
+}
+
+template <int D, int WMODE>
+static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
+  const long short_blocks = ((long)P.n_rows + 15) / 16;
+  const long grid = (long)P.n_chunks + short_blocks;
+  if (grid > 0) {
+    hipLaunchKernelGGL((spmm_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
+                       0, st, P);
+    BBGR_LAUNCHED("spmm_kernel");
+  }
+  if (n_split > 0) {
+    hipLaunchKernelGGL((spmm_fixup_kernel<D>), dim3((unsigned)n_split),
+                       dim3(256), 0, st, P);
+    BBGR_LAUNCHED("spmm_fixup_kernel");
+  }
+  return BBGR_OK;
+}
+
+template <int D>
+static int dispatch_wmode(const SpmmParams &P, int wmode, int n_split,
+                          hipStream_t st) {
+  switch (wmode) {
+    case 0: return launch_spmm<D, 0>(P, n_split, st);
+    case 1: return launch_spmm<D, 1>(P, n_split, st);
+    case 2: return launch_spmm<D, 2>(P, n_split, st);
+  }
+  set_error("bbgr_spmm: weight_mode %d not in {0,1,2}", wmode);
+  return BBGR_ERR_INVALID;
+}
+
+static bool ld_ok(const float *p, long ld, int d) {
+  return p == nullptr || (aligned16(p) && ld >= d && (ld & 3) == 0);
+}
+
+}  // namespace bbgr
+
+using namespace bbgr;
+
+extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
+                         bbgr_stream_t stream) {
+  BBGR_REQUIRE(csr && a, "bbgr_spmm: null csr/args");
+  BBGR_REQUIRE(csr->n_rows >= 0 && csr->n_cols >= 0 && csr->nnz >= 0,
+               "bbgr_spmm: negative csr size");
+  BBGR_REQUIRE(csr->indptr && (csr->nnz == 0 || csr->indices),
+               "bbgr_spmm: null csr arrays");
+  const int d = a->d;
+  if (d != 64 && d != 128 && d != 256) {
+    set_error("bbgr_spmm: embedding dim %d unsupported (64, 128, 256)", d);
+    return BBGR_ERR_UNSUPPORTED;
+  }
+  BBGR_REQUIRE(a->x || csr->nnz == 0, "bbgr_spmm: null x");
+  BBGR_REQUIRE(ld_ok(a->x, a->ldx, d) && ld_ok(a->y, a->ldy, d) &&
+                   ld_ok(a->add, a->ldadd, d) && ld_ok(a->acc_in, a->ldacc_in, d) &&
+                   ld_ok(a->acc_out, a->ldacc_out, d),
+               "bbgr_spmm: tables must be 16-byte aligned with ld >= d, ld % 4 == 0");
+  BBGR_REQUIRE(a->weight_mode != 1 || a->edge_val, "bbgr_spmm: weight_mode 1 needs edge_val");
+  BBGR_REQUIRE(a->weight_mode != 2 || a->col_scale, "bbgr_spmm: weight_mode 2 needs col_scale");
+  BBGR_REQUIRE(csr->n_chunks == 0 || csr->chunks, "bbgr_spmm: plan chunks missing");
+  BBGR_REQUIRE(csr->n_split == 0 || (csr->split && a->partial),
+               "bbgr_spmm: split rows need plan + partial workspace");
+  BBGR_REQUIRE(csr->n_chunks == 0 || csr->long_threshold > 0,
+               "bbgr_spmm: plan without long_threshold");
+
+  SpmmParams P;
+  P.n_rows = csr->n_rows;
+  P.long_threshold = csr->n_chunks ? csr->long_threshold : 0x7fffffff;
+  P.n_chunks = csr->n_chunks;
+  P.indptr = csr->indptr;
+  P.indices = csr->indices;
+  P.chunks = reinterpret_cast<const int4 *>(csr->chunks);
+  P.split = reinterpret_cast<const int4 *>(csr->split);
+  P.x = a->x;
+  P.ldx = a->ldx;
+  P.edge_val = a->edge_val;
+  P.col_scale = a->col_scale;
+  P.col_scale_s = a->col_scale_s;
+  P.y = a->y;
+  P.ldy = a->ldy;
+  P.y_scale = a->y_scale;
+  P.y_scale_s = a->y_scale_s;
+  P.add = a->add;
+  P.ldadd = a->ldadd;
+  P.add_scale = a->add_scale;
+  P.add_scale_s = a->add_scale_s;
+  P.acc_in = a->acc_in;
+  P.ldacc_in = a->ldacc_in;
+  P.acc_out = a->acc_out;
+  P.ldacc_out = a->ldacc_out;
+  P.acc_scale = a->acc_scale;
+  P.acc_scale_s = a->acc_scale_s;
+  P.gamma = a->gamma;
+  P.partial = a->partial;
+  hipStream_t st = as_stream(stream);
+  switch (d) {
+    case 64: return dispatch_wmode<64>(P, a->weight_mode, csr->n_split, st);
+    case 128: return dispatch_wmode<128>(P, a->weight_mode, csr->n_split, st);
+    default: return dispatch_wmode<256>(P, a->weight_mode, csr->n_split, st);
+  }
+}

@@ -1,0 +1,359 @@
+// Training-step kernels: fused BPR forward/backward, deterministic loss
+// reduction, Adam (torch.optim.Adam semantics), row zero / row axpy.
+//
+// Reference: LightGCN.bpr_loss  Version-2/lighgcn_cu_pop.py:495-508
+//            (lightgcn.py:333-349; lightgcn_cu.py:632-648 adds L_fair)
+//            opt.step()          Version-2/lighgcn_cu_pop.py:863 (Adam, :793)
+#include "common.h"
+
+namespace bbgr {
+
+struct BprParams {
+  long batch, n_users, n_items;
+  const long *users, *pos, *neg;
+  const float *uf, *itf, *ue, *ie;
+  long lduf, ldif, ldue, ldie;
+  const float *pop;
+  float reg, lambda_fair, inv_b;
+  float *parts;
+  const float *dloss;
+  float *g_uf, *g_if, *g_ue, *g_ie;
+  long ldguf, ldgif, ldgue, ldgie;
+};
+
+__device__ __forceinline__ float group16_sum(float v) {
+  v += __shfl_xor(v, 1, 16);
+  v += __shfl_xor(v, 2, 16);
+  v += __shfl_xor(v, 4, 16);
+  v += __shfl_xor(v, 8, 16);
+  return v;
+}
+
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+
+__device__ __forceinline__ void atomic_axpy4(float *dst, float a, float4 x) {
+  atomicAdd(dst + 0, a * x.x);
+  atomicAdd(dst + 1, a * x.y);
+  atomicAdd(dst + 2, a * x.z);
+  atomicAdd(dst + 3, a * x.w);
+}
+
+__device__ __forceinline__ void atomic_axpby4(float *dst, float a, float4 x,
+                                              float b, float4 y) {
+  atomicAdd(dst + 0, a * x.x + b * y.x);
+  atomicAdd(dst + 1, a * x.y + b * y.y);
+  atomicAdd(dst + 2, a * x.z + b * y.z);
+  atomicAdd(dst + 3, a * x.w + b * y.w);
+}
+
+// One 16-lane group per (user, pos, neg) triple.
+template <int D>
+__global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
+  constexpr int V = D / 64;
+  const long b = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  if (b >= P.batch) return;
+  const long u = P.users[b], ip = P.pos[b], in = P.neg[b];
+  if (u < 0 || u >= P.n_users || ip < 0 || ip >= P.n_items || in < 0 || in >= P.n_items) {
+    if (P.parts && lane == 0) {
+      P.parts[3 * b + 0] = 0.f;
+      P.parts[3 * b + 1] = 0.f;
+      P.parts[3 * b + 2] = 0.f;
+    }
+    return;  // whole group leaves together
+  }
+  float4 fu[V], fp[V], fn[V];
+  const float4 *pu = reinterpret_cast<const float4 *>(P.uf + u * P.lduf) + lane;
+  const float4 *pp = reinterpret_cast<const float4 *>(P.itf + ip * P.ldif) + lane;
+  const float4 *pn = reinterpret_cast<const float4 *>(P.itf + in * P.ldif) + lane;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    fu[k] = pu[16 * k];
+    fp[k] = pp[16 * k];
+    fn[k] = pn[16 * k];
+  }
+  float sp = 0.f, sn = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    sp += dot4(fu[k], fp[k]);
+    sn += dot4(fu[k], fn[k]);
+  }
+  sp = group16_sum(sp);
+  sn = group16_sum(sn);
+  const float x = sp - sn;
+  const float sig = 1.0f / (1.0f + expf(-x));
+  const bool need_reg = P.parts || P.g_ue || P.g_ie;
+  float4 eu[V], ep[V], en[V];
+  if (need_reg) {
+    const float4 *qu = reinterpret_cast<const float4 *>(P.ue + u * P.ldue) + lane;
+    const float4 *qp = reinterpret_cast<const float4 *>(P.ie + ip * P.ldie) + lane;
+    const float4 *qn = reinterpret_cast<const float4 *>(P.ie + in * P.ldie) + lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      eu[k] = qu[16 * k];
+      ep[k] = qp[16 * k];
+      en[k] = qn[16 * k];
+    }
+  }
+  if (P.parts) {
+    float r = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) r += dot4(eu[k], eu[k]) + dot4(ep[k], ep[k]) + dot4(en[k], en[k]);
+    r = group16_sum(r);
+    if (lane == 0) {
+      P.parts[3 * b + 0] = -logf(sig + 1e-12f);
+      P.parts[3 * b + 1] = r;
+      P.parts[3 * b + 2] = P.pop ? P.pop[ip] * sp : 0.f;
+    }
+  }
+  if (!(P.g_uf || P.g_if || P.g_ue || P.g_ie)) return;
+  const float G = (P.dloss ? *P.dloss : 1.0f) * P.inv_b;
+  // d/dx [-log(sigmoid(x) + 1e-12)] = -sigmoid'(x) / (sigmoid(x) + 1e-12)
+  const float gx = -(sig * (1.0f - sig)) / (sig + 1e-12f) * G;
+  const float gpos = gx + (P.pop ? P.lambda_fair * P.pop[ip] * G : 0.f);
+  const float gneg = -gx;
+  if (P.g_uf) {
+    float *d = P.g_uf + u * P.ldguf + 4 * lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) atomic_axpby4(d + 64 * k, gpos, fp[k], gneg, fn[k]);
+  }
+  if (P.g_if) {
+    float *dp = P.g_if + ip * P.ldgif + 4 * lane;
+    float *dn = P.g_if + in * P.ldgif + 4 * lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      atomic_axpy4(dp + 64 * k, gpos, fu[k]);
+      atomic_axpy4(dn + 64 * k, gneg, fu[k]);
+    }
+  }
+  const float gr = 2.0f * P.reg * G;
+  if (P.g_ue) {
+    float *d = P.g_ue + u * P.ldgue + 4 * lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) atomic_axpy4(d + 64 * k, gr, eu[k]);
+  }
+  if (P.g_ie) {
+    float *dp = P.g_ie + ip * P.ldgie + 4 * lane;
+    float *dn = P.g_ie + in * P.ldgie + 4 * lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      atomic_axpy4(dp + 64 * k, gr, ep[k]);
+      atomic_axpy4(dn + 64 * k, gr, en[k]);
+    }
+  }
+}
+
+// One workgroup, fixed summation order -> deterministic loss.
+__global__ __launch_bounds__(256) void bpr_reduce_kernel(long batch,
+                                                         const float *parts,
+                                                         float reg, float lam,
+                                                         float *loss) {
+  __shared__ float s0[256], s1[256], s2[256];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (long b = threadIdx.x; b < batch; b += 256) {
+    a0 += parts[3 * b + 0];
+    a1 += parts[3 * b + 1];
+    a2 += parts[3 * b + 2];
+  }
+  s0[threadIdx.x] = a0;
+  s1[threadIdx.x] = a1;
+  s2[threadIdx.x] = a2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      s0[threadIdx.x] += s0[threadIdx.x + w];
+      s1[threadIdx.x] += s1[threadIdx.x + w];
+      s2[threadIdx.x] += s2[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float inv = 1.0f / (float)batch;
+    loss[0] = s0[0] * inv + reg * (s1[0] * inv) + lam * (s2[0] * inv);
+  }
+}
+
+// torch.optim.Adam (single-tensor/foreach math), float4 vectorised.
+__global__ __launch_bounds__(256) void adam_kernel(long n4, float4 *p,
+                                                   const float4 *g, float4 *m,
+                                                   float4 *v, float lr, float b1,
+                                                   float b2, float eps, float wd,
+                                                   float bc1, float bc2s) {
+  const float step = lr / bc1;
+  const float w1 = 1.0f - b1;
+  const float w2 = 1.0f - b2;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    float *pf = &pp.x, *gf = &gg.x, *mf = &mm.x, *vf = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = gf[k];
+      if (wd != 0.f) gk = gk + wd * pf[k];
+      mf[k] = mf[k] + w1 * (gk - mf[k]);  // lerp(m, g, 1-beta1), weight < 0.5
+      vf[k] = vf[k] * b2 + w2 * gk * gk;
+      const float denom = sqrtf(vf[k]) / bc2s + eps;
+      pf[k] = pf[k] - step * (mf[k] / denom);
+    }
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
+__global__ void adam_tail_kernel(long n, long start, float *p, const float *g,
+                                 float *m, float *v, float lr, float b1, float b2,
+                                 float eps, float wd, float bc1, float bc2s) {
+  const long i = start + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float gk = g[i];
+  if (wd != 0.f) gk = gk + wd * p[i];
+  const float mk = m[i] + (1.0f - b1) * (gk - m[i]);
+  const float vk = v[i] * b2 + (1.0f - b2) * gk * gk;
+  m[i] = mk;
+  v[i] = vk;
+  p[i] = p[i] - (lr / bc1) * (mk / (sqrtf(vk) / bc2s + eps));
+}
+
+__global__ void rows_zero_kernel(long n, const long *idx, float *t, long ld,
+                                 int d) {
+  const long k = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (k >= n) return;
+  float *row = t + idx[k] * ld;
+  for (int c = threadIdx.x & 15; c < d; c += 16) row[c] = 0.f;
+}
+
+__global__ void rows_axpy_kernel(long n, const long *idx, float alpha,
+                                 const float *src, long lds, float *dst, long ldd,
+                                 int d) {
+  const long k = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (k >= n) return;
+  const long r = idx[k];
+  for (int c = threadIdx.x & 15; c < d; c += 16)
+    atomicAdd(dst + r * ldd + c, alpha * src[r * lds + c]);
+}
+
+}  // namespace bbgr
+
+using namespace bbgr;
+
+extern "C" int bbgr_bpr(const bbgr_bpr_args *a, bbgr_stream_t stream) {
+  BBGR_REQUIRE(a, "bbgr_bpr: null args");
+  BBGR_REQUIRE(a->batch >= 0, "bbgr_bpr: negative batch");
+  if (a->batch == 0) return BBGR_OK;
+  const int d = a->d;
+  if (d != 64 && d != 128 && d != 256) {
+    set_error("bbgr_bpr: embedding dim %d unsupported (64, 128, 256)", d);
+    return BBGR_ERR_UNSUPPORTED;
+  }
+  BBGR_REQUIRE(a->users && a->pos && a->neg && a->uf && a->itf,
+               "bbgr_bpr: null index/table");
+  BBGR_REQUIRE(a->n_users > 0 && a->n_items > 0, "bbgr_bpr: n_users/n_items must be set");
+  const bool need_reg = a->parts || a->g_ue || a->g_ie;
+  BBGR_REQUIRE(!need_reg || (a->ue && a->ie), "bbgr_bpr: ego tables required");
+  BprParams P;
+  P.batch = a->batch;
+  P.n_users = a->n_users;
+  P.n_items = a->n_items;
+  P.users = (const long *)a->users;
+  P.pos = (const long *)a->pos;
+  P.neg = (const long *)a->neg;
+  P.uf = a->uf; P.lduf = a->lduf;
+  P.itf = a->itf; P.ldif = a->ldif;
+  P.ue = a->ue; P.ldue = a->ldue;
+  P.ie = a->ie; P.ldie = a->ldie;
+  P.pop = a->pop;
+  P.reg = a->reg;
+  P.lambda_fair = a->lambda_fair;
+  P.inv_b = 1.0f / (float)a->batch;
+  P.parts = a->parts;
+  P.dloss = a->dloss;
+  P.g_uf = a->g_uf; P.ldguf = a->ldguf;
+  P.g_if = a->g_if; P.ldgif = a->ldgif;
+  P.g_ue = a->g_ue; P.ldgue = a->ldgue;
+  P.g_ie = a->g_ie; P.ldgie = a->ldgie;
+  const long lds[] = {P.lduf, P.ldif, P.ldue, P.ldie, P.ldguf, P.ldgif, P.ldgue, P.ldgie};
+  const void *ptrs[] = {P.uf, P.itf, P.ue, P.ie, P.g_uf, P.g_if, P.g_ue, P.g_ie};
+  for (int k = 0; k < 8; ++k) {
+    if (!ptrs[k]) continue;
+    BBGR_REQUIRE(aligned16(ptrs[k]) && lds[k] >= d && (lds[k] & 3) == 0,
+                 "bbgr_bpr: tables must be 16-byte aligned with ld >= d, ld % 4 == 0");
+  }
+  const unsigned grid = (unsigned)((a->batch + 15) / 16);
+  hipStream_t st = as_stream(stream);
+  switch (d) {
+    case 64: hipLaunchKernelGGL(bpr_kernel<64>, dim3(grid), dim3(256), 0, st, P); break;
+    case 128: hipLaunchKernelGGL(bpr_kernel<128>, dim3(grid), dim3(256), 0, st, P); break;
+    default: hipLaunchKernelGGL(bpr_kernel<256>, dim3(grid), dim3(256), 0, st, P); break;
+  }
+  BBGR_LAUNCHED("bpr_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_bpr_reduce(int64_t batch, const float *parts, float reg,
+                               float lambda_fair, float *loss,
+                               bbgr_stream_t stream) {
+  BBGR_REQUIRE(batch > 0 && parts && loss, "bbgr_bpr_reduce: bad args");
+  hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(256), 0, as_stream(stream),
+                     (long)batch, parts, reg, lambda_fair, loss);
+  BBGR_LAUNCHED("bpr_reduce_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_adam(int64_t n, float *param, const float *grad,
+                         float *exp_avg, float *exp_avg_sq, float lr, float beta1,
+                         float beta2, float eps, float weight_decay,
+                         float bias_correction1, float bias_correction2_sqrt,
+                         bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_adam: negative n");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(param && grad && exp_avg && exp_avg_sq, "bbgr_adam: null tensor");
+  hipStream_t st = as_stream(stream);
+  const bool vec = aligned16(param) && aligned16(grad) && aligned16(exp_avg) &&
+                   aligned16(exp_avg_sq);
+  const long n4 = vec ? n / 4 : 0;
+  if (n4 > 0) {
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n4,
+                       (float4 *)param, (const float4 *)grad, (float4 *)exp_avg,
+                       (float4 *)exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                       bias_correction1, bias_correction2_sqrt);
+    BBGR_LAUNCHED("adam_kernel");
+  }
+  const long start = n4 * 4;
+  if (start < n) {
+    hipLaunchKernelGGL(adam_tail_kernel, dim3((unsigned)((n - start + 255) / 256)),
+                       dim3(256), 0, st, (long)n, start, param, grad, exp_avg,
+                       exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                       bias_correction1, bias_correction2_sqrt);
+    BBGR_LAUNCHED("adam_tail_kernel");
+  }
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_rows_zero(int64_t n, const int64_t *idx, float *table,
+                              int64_t ld, int32_t d, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && d > 0 && ld >= d, "bbgr_rows_zero: bad sizes");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx && table, "bbgr_rows_zero: null arrays");
+  hipLaunchKernelGGL(rows_zero_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)idx, table, (long)ld, d);
+  BBGR_LAUNCHED("rows_zero_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha,
+                              const float *src, int64_t ldsrc, float *dst,
+                              int64_t lddst, int32_t d, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && d > 0 && ldsrc >= d && lddst >= d, "bbgr_rows_axpy: bad sizes");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx && src && dst, "bbgr_rows_axpy: null arrays");
+  hipLaunchKernelGGL(rows_axpy_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)idx, alpha, src,
+                     (long)ldsrc, dst, (long)lddst, d);
+  BBGR_LAUNCHED("rows_axpy_kernel");
+  return BBGR_OK;
+}

@@ -1,0 +1,192 @@
+"""Device CSR structures and the factored bipartite operators.
+
+Every propagation operator of the reference factors over ONE bipartite
+adjacency A (user-row CSR ``A_ui`` and its transpose, the item-row CSR
+``A_iu``) and four diagonal scale vectors:
+
+    item <- user:  M = diag(p) A_iu diag(q)     user <- item:  M = diag(s) A_ui diag(t)
+
+  * GS  (Version-2/lighgcn_cu_pop.py:429-452):  p = t = b, q = c*a, s = a
+  * Method A (version_1/lightgcn_cu_pop_long_tail_exposure.py:362-396):
+                                                p = t = b*alpha, q = c*a, s = a
+  * J   (lightgcn_cu.py:368-399; same weights, Jacobi layer order)
+  * SYM (lightgcn.py:352-372): the N x N symmetric D^-1/2 A D^-1/2 restricted
+        to its two off-diagonal blocks: p = t = deg_i^-1/2, q = s = deg_u^-1/2
+
+with a = 1/sqrt(max(deg_u,1)), b = 1/sqrt(max(deg_i,1)), c = credibility.
+The backward operators are the transposes, i.e. the same two CSRs with the
+roles of the scale vectors swapped — nothing else is stored.
+
+Duplicate (u, i) train pairs stay as repeated CSR entries: the SpMM sums them,
+which is what ``sparse_coo_tensor(...).coalesce()`` does with their values
+(Version-2/lighgcn_cu_pop.py:443,450; lightgcn_cu.py:393,397; lightgcn.py:363).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_handle
+
+DEFAULT_LONG_THRESHOLD = 256
+DEFAULT_CHUNK_EDGES = 2048
+
+
+def _as_device_i32(x, device) -> torch.Tensor:
+    if isinstance(x, np.ndarray):
+        t = torch.from_numpy(np.ascontiguousarray(x.astype(np.int32, copy=False)))
+    else:
+        t = torch.as_tensor(x)
+    return t.to(device=device, dtype=torch.int32).contiguous()
+
+
+class Csr:
+    """Row-sorted CSR on the device (int32 indptr/indices, columns sorted in
+    each row, duplicates kept) plus the SpMM load-balance plan."""
+
+    def __init__(self, rows, cols, n_rows: int, n_cols: int, device,
+                 edge_values: torch.Tensor | None = None,
+                 long_threshold: int = DEFAULT_LONG_THRESHOLD,
+                 chunk_edges: int = DEFAULT_CHUNK_EDGES):
+        _lib.require_gpu()
+        device = torch.device(device)
+        rows = _as_device_i32(rows, device)
+        cols = _as_device_i32(cols, device)
+        if rows.numel() != cols.numel():
+            raise ValueError("rows and cols must have the same length")
+        nnz = rows.numel()
+        if nnz >= 2**31 - 1:
+            raise ValueError("nnz must be < 2^31 for the int32 CSR")
+        if nnz and (int(rows.min()) < 0 or int(rows.max()) >= n_rows
+                    or int(cols.min()) < 0 or int(cols.max()) >= n_cols):
+            raise ValueError("edge index out of range")
+        self.n_rows, self.n_cols, self.nnz = int(n_rows), int(n_cols), int(nnz)
+        self.device = device
+        self.indptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=device)
+        self.indices = torch.empty(max(nnz, 1), dtype=torch.int32, device=device)
+        perm = (torch.empty(max(nnz, 1), dtype=torch.int32, device=device)
+                if edge_values is not None else None)
+        st = stream_handle()
+        ws_bytes = _lib.workspace_query(
+            "bbgr_csr_build", nnz, ptr(rows), ptr(cols), self.n_rows, self.n_cols,
+            ptr(self.indptr), ptr(self.indices), ptr(perm), args_after=(st,))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=device)
+        n = ctypes.c_size_t(ws_bytes)
+        call("bbgr_csr_build", nnz, ptr(rows), ptr(cols), self.n_rows, self.n_cols,
+             ptr(self.indptr), ptr(self.indices), ptr(perm), ptr(ws), ctypes.byref(n), st)
+        del ws
+        self.values = None
+        if edge_values is not None:
+            ev = torch.as_tensor(edge_values).to(device=device, dtype=torch.float32)
+            self.values = ev[perm[:nnz].long()].contiguous() if nnz else ev.new_zeros(1)
+        self._plan(long_threshold, chunk_edges)
+
+    def _plan(self, long_threshold: int, chunk_edges: int) -> None:
+        s = self.struct(with_plan=False)
+        s.long_threshold = long_threshold
+        s.chunk_edges = chunk_edges
+        st = stream_handle()
+        ws_bytes = _lib.workspace_query("bbgr_csr_plan_count", ctypes.byref(s), None,
+                                        None, args_after=(st,))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=self.device)
+        nb = ctypes.c_size_t(ws_bytes)
+        nc, ns = ctypes.c_int32(0), ctypes.c_int32(0)
+        call("bbgr_csr_plan_count", ctypes.byref(s), ctypes.byref(nc), ctypes.byref(ns),
+             ptr(ws), ctypes.byref(nb), st)
+        self.long_threshold, self.chunk_edges = long_threshold, chunk_edges
+        self.n_chunks, self.n_split = nc.value, ns.value
+        self.chunks = torch.empty(max(4 * self.n_chunks, 4), dtype=torch.int32,
+                                  device=self.device)
+        self.split = torch.empty(max(4 * self.n_split, 4), dtype=torch.int32,
+                                 device=self.device)
+        s.n_chunks, s.n_split = self.n_chunks, self.n_split
+        call("bbgr_csr_plan_build", ctypes.byref(s), ptr(self.chunks), ptr(self.split),
+             ptr(ws), ctypes.byref(nb), st)
+        self._struct = self.struct(with_plan=True)
+
+    def struct(self, with_plan: bool = True) -> _lib.CsrStruct:
+        s = _lib.CsrStruct()
+        s.n_rows, s.n_cols, s.nnz = self.n_rows, self.n_cols, self.nnz
+        s.indptr, s.indices = ptr(self.indptr), ptr(self.indices)
+        if with_plan:
+            s.long_threshold, s.chunk_edges = self.long_threshold, self.chunk_edges
+            s.n_chunks, s.n_split = self.n_chunks, self.n_split
+            s.chunks, s.split = ptr(self.chunks), ptr(self.split)
+        return s
+
+    def partial_workspace(self, d: int) -> torch.Tensor | None:
+        if self.n_split == 0:
+            return None
+        return torch.empty(self.n_chunks * d, dtype=torch.float32, device=self.device)
+
+    def degrees(self) -> torch.Tensor:
+        return (self.indptr[1:] - self.indptr[:-1])
+
+    def nbytes(self) -> int:
+        return 4 * (self.indptr.numel() + self.indices.numel())
+
+
+@dataclass
+class Scales:
+    """Per-row scale vectors of one operator pair (see module docstring)."""
+    kind: int
+    p: torch.Tensor   # [I] item rows of item<-user
+    q: torch.Tensor   # [U] user cols of item<-user
+    s: torch.Tensor   # [U] user rows of user<-item
+    t: torch.Tensor   # [I] item cols of user<-item
+    pt: torch.Tensor  # [I] p*t
+    qs: torch.Tensor  # [U] q*s
+    deg_u: torch.Tensor
+    deg_i: torch.Tensor
+
+
+class BipartiteGraph:
+    """The train edges of one split as two device CSRs (user rows, item rows)."""
+
+    def __init__(self, train_edges_2xE, num_users: int, num_items: int, device,
+                 long_threshold: int = DEFAULT_LONG_THRESHOLD,
+                 chunk_edges: int = DEFAULT_CHUNK_EDGES):
+        device = torch.device(device)
+        if isinstance(train_edges_2xE, torch.Tensor):
+            e = train_edges_2xE
+        else:
+            e = np.asarray(train_edges_2xE)
+        if e.shape[0] != 2:
+            raise ValueError("train_edges must have shape [2, E]")
+        u = _as_device_i32(e[0], device)
+        i = _as_device_i32(e[1], device)
+        self.num_users, self.num_items = int(num_users), int(num_items)
+        self.nnz = int(u.numel())
+        self.device = device
+        self.user_csr = Csr(u, i, num_users, num_items, device,
+                            long_threshold=long_threshold, chunk_edges=chunk_edges)
+        self.item_csr = Csr(i, u, num_items, num_users, device,
+                            long_threshold=long_threshold, chunk_edges=chunk_edges)
+        self._scales: dict = {}
+
+    def scales(self, kind: int, cred: torch.Tensor | None = None) -> Scales:
+        key = (kind, None if cred is None else cred.data_ptr())
+        if key in self._scales:
+            return self._scales[key]
+        U, I, dev = self.num_users, self.num_items, self.device
+        f = lambda n: torch.empty(max(n, 1), dtype=torch.float32, device=dev)  # noqa: E731
+        deg_u, deg_i = f(U), f(I)
+        p, q, s, t, pt, qs = f(I), f(U), f(U), f(I), f(I), f(U)
+        if cred is not None:
+            cred = cred.to(device=dev, dtype=torch.float32).contiguous().view(-1)
+            if cred.numel() != U:
+                raise ValueError(f"credibility vector has {cred.numel()} entries, expected {U}")
+        call("bbgr_operator_scales", kind, U, I, ptr(self.user_csr.indptr),
+             ptr(self.item_csr.indptr), ptr(cred), ptr(deg_u), ptr(deg_i), ptr(p),
+             ptr(q), ptr(s), ptr(t), ptr(pt), ptr(qs), stream_handle())
+        sc = Scales(kind, p[:I], q[:U], s[:U], t[:I], pt[:I], qs[:U], deg_u[:U], deg_i[:I])
+        sc._cred = cred  # keep alive
+        self._scales[key] = sc
+        return sc
+
+    def nbytes(self) -> int:
+        return self.user_csr.nbytes() + self.item_csr.nbytes()

@@ -1,0 +1,78 @@
+"""Drop-in for the model layer of Version-2/lighgcn_cu_pop.py.
+
+Same names, signatures, attributes and state_dict keys as the reference:
+
+  build_message_passing_mats(train_edges_2xE, num_users, num_items, cred_u, device)
+      -> (M_ui [U x I], M_iu [I x U])          Version-2/lighgcn_cu_pop.py:429-452
+  LightGCN(num_users, num_items, emb_dim, num_layers, M_ui, M_iu)   :458-508
+      .user_emb / .item_emb (nn.Embedding, xavier_uniform_), .M_ui, .M_iu,
+      .propagate() -> (u_final, i_final)   Gauss-Seidel order (:472-490)
+      .get_user_item_emb()
+      .bpr_loss(users, pos_items, neg_items, user_emb, item_emb, reg_weight)
+  state_dict keys: user_emb.weight, item_emb.weight (the operators are plain
+  attributes, not buffers, as in the reference).
+
+The operators are built ON the device from the int32 [2, E] edge array; no
+numpy weight math, no COO coalesce. Torch sparse COO operators are also
+accepted by LightGCN (converted once to explicit-value CSRs).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import bpr as _bpr
+from ._lib import OP_GS
+from .graph import BipartiteGraph
+from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator,
+                        resolve_pair, to_device_cred)
+from .propagate import ORDER_GS, OperatorPair, propagate as _propagate
+
+
+def _build(train_edges_2xE, num_users, num_items, cred_u, device, kind):
+    graph = BipartiteGraph(train_edges_2xE, num_users, num_items, device)
+    cred = to_device_cred(cred_u, num_users, graph.device)
+    sc = graph.scales(kind, cred)
+    pair = OperatorPair.factored(graph, sc)
+    M_ui = BipartiteOperator(pair, USER_FROM_ITEM, graph, kind)
+    M_iu = BipartiteOperator(pair, ITEM_FROM_USER, graph, kind)
+    return M_ui, M_iu
+
+
+def build_message_passing_mats(train_edges_2xE, num_users: int, num_items: int,
+                               cred_u: torch.Tensor, device: str):
+    """M_ui[u,i] = w_ui, M_iu[i,u] = c_u * w_ui,
+    w_ui = (1/sqrt(max(deg_u,1))) * (1/sqrt(max(deg_i,1)))  (Version-2:429-452)."""
+    return _build(train_edges_2xE, num_users, num_items, cred_u, device, OP_GS)
+
+
+class LightGCN(torch.nn.Module):
+    def __init__(self, num_users, num_items, emb_dim, num_layers, M_ui, M_iu):
+        super().__init__()
+        self.num_users = num_users
+        self.num_items = num_items
+        self.num_layers = num_layers
+        self.M_ui = M_ui
+        self.M_iu = M_iu
+        self._pair: OperatorPair | None = None
+
+        self.user_emb = torch.nn.Embedding(num_users, emb_dim)
+        self.item_emb = torch.nn.Embedding(num_items, emb_dim)
+        torch.nn.init.xavier_uniform_(self.user_emb.weight)
+        torch.nn.init.xavier_uniform_(self.item_emb.weight)
+
+    def _operator_pair(self) -> OperatorPair:
+        if self._pair is None:
+            self._pair = resolve_pair(self.M_iu, self.M_ui, self.num_users, self.num_items,
+                                      self.user_emb.weight.device)
+        return self._pair
+
+    def propagate(self):
+        return _propagate(self._operator_pair(), self.user_emb.weight, self.item_emb.weight,
+                          self.num_layers, ORDER_GS)
+
+    def get_user_item_emb(self):
+        return self.propagate()
+
+    def bpr_loss(self, users, pos_items, neg_items, user_emb, item_emb, reg_weight: float):
+        return _bpr.bpr_loss(users, pos_items, neg_items, user_emb, item_emb,
+                             self.user_emb.weight, self.item_emb.weight, reg_weight)

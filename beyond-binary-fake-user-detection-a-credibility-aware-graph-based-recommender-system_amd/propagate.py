@@ -1,0 +1,383 @@
+"""K-layer LightGCN propagation on the fused HIP SpMM, forward and backward.
+
+Three layer orders exist in the reference:
+
+  GS  (Gauss-Seidel; Version-2/lighgcn_cu_pop.py:472-490, version_1/*):
+        i_k = M_iu u_{k-1};  u_k = M_ui i_k          (uses the NEW item table)
+  J   (Jacobi; lightgcn_cu.py:420-448):
+        i_k = M_iu u_{k-1};  u_k = M_ui i_{k-1}      (uses the OLD item table)
+  SYM (lightgcn.py:318-325): x_k = A_hat x_{k-1} on the N x N symmetric
+        operator == J on its two off-diagonal blocks.
+
+Final tables are the layer means (Version-2:488-489), fused into the SpMM
+epilogue (acc_out = (acc_in + out_scale*T) * gamma, gamma = 1/(K+1) on the
+last layer).
+
+Factored operators (graph.Scales) are applied as diag(out) A diag(in): the
+producing SpMM writes its output already multiplied by the NEXT product's
+input scale (``feed`` vectors pt / qs), so later SpMMs read plain rows and
+stream no per-edge weights. The first product of a chain reads the raw
+weight table and applies the input scale per gathered row (weight_mode 2).
+
+Backward (autograd of the reference's torch.sparse.mm chain):
+with g = dL/d(final) and g' = g/(K+1),
+  GS: Gi_k = gI' + M_ui^T Gu_k ; Gu_{k-1} = gU' + M_iu^T Gi_k ; Gu_K = gU'
+      grad_u0 = Gu_0, grad_i0 = gI'
+  J : Gu_{k-1} = gU' + M_iu^T Gi_k ; Gi_{k-1} = gI' + M_ui^T Gu_k
+      (Gu_K = gU', Gi_K = gI'); grad_u0 = Gu_0, grad_i0 = Gi_0
+The transposes are the other CSR with the scale roles swapped.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import call, ld, ptr, stream_handle
+from .graph import BipartiteGraph, Csr, Scales
+
+ORDER_GS = "gs"
+ORDER_J = "jacobi"
+
+
+@dataclass
+class Product:
+    """One sparse product y = diag(out_scale) A diag(in_scale) x (factored) or
+    y = M x with explicit per-edge values (generic)."""
+    csr: Csr
+    vals: torch.Tensor | None
+    in_scale: torch.Tensor | None
+    out_scale: torch.Tensor | None
+    partial: dict
+
+    def workspace(self, d: int):
+        if self.csr.n_split == 0:
+            return None
+        w = self.partial.get(d)
+        if w is None:
+            w = self.csr.partial_workspace(d)
+            self.partial[d] = w
+        return w
+
+
+class OperatorPair:
+    """The four products of one bipartite operator pair (fwd item<-user,
+    fwd user<-item, and their transposes for the backward)."""
+
+    def __init__(self, fwd_item: Product, fwd_user: Product, bwd_item: Product,
+                 bwd_user: Product, num_users: int, num_items: int,
+                 feed_fwd_iu=None, feed_fwd_ui=None, feed_bwd_iu=None,
+                 feed_bwd_ui=None):
+        self.fwd_item, self.fwd_user = fwd_item, fwd_user
+        self.bwd_item, self.bwd_user = bwd_item, bwd_user
+        self.num_users, self.num_items = num_users, num_items
+        # feed vectors: output scale of a product x input scale of the next one
+        self.feed_fwd_iu, self.feed_fwd_ui = feed_fwd_iu, feed_fwd_ui
+        self.feed_bwd_iu, self.feed_bwd_ui = feed_bwd_iu, feed_bwd_ui
+
+    @classmethod
+    def factored(cls, graph: BipartiteGraph, sc: Scales) -> "OperatorPair":
+        Ai, Au = graph.item_csr, graph.user_csr
+        wi, wu = {}, {}
+        return cls(
+            fwd_item=Product(Ai, None, sc.q, sc.p, wi),
+            fwd_user=Product(Au, None, sc.t, sc.s, wu),
+            bwd_item=Product(Ai, None, sc.s, sc.t, wi),
+            bwd_user=Product(Au, None, sc.p, sc.q, wu),
+            num_users=graph.num_users, num_items=graph.num_items,
+            feed_fwd_iu=sc.pt, feed_fwd_ui=sc.qs, feed_bwd_iu=sc.pt, feed_bwd_ui=sc.qs)
+
+    @classmethod
+    def generic(cls, M_iu_csr: Csr, M_ui_csr: Csr, M_ui_T_csr: Csr, M_iu_T_csr: Csr,
+                num_users: int, num_items: int) -> "OperatorPair":
+        """Arbitrary per-edge values (e.g. a torch sparse COO handed in)."""
+        return cls(
+            fwd_item=Product(M_iu_csr, M_iu_csr.values, None, None, {}),
+            fwd_user=Product(M_ui_csr, M_ui_csr.values, None, None, {}),
+            bwd_item=Product(M_ui_T_csr, M_ui_T_csr.values, None, None, {}),
+            bwd_user=Product(M_iu_T_csr, M_iu_T_csr.values, None, None, {}),
+            num_users=num_users, num_items=num_items)
+
+
+class SpmmTimer:
+    """Brackets every bbgr_spmm launch (incl. its fix-up) with events on the
+    launching stream; used by bench.py inside the timed region."""
+
+    def __init__(self):
+        self.records = []   # (n_rows, nnz, d, start_event, end_event)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for rows, nnz, d, a, b in self.records:
+            k = (rows, nnz, d)
+            n, ms = out.get(k, (0, 0.0))
+            out[k] = (n + 1, ms + a.elapsed_time(b))
+        return out
+
+
+_timer: SpmmTimer | None = None
+
+
+def set_spmm_timer(t: SpmmTimer | None) -> None:
+    global _timer
+    _timer = t
+
+
+def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
+         y_scale_s: float = 1.0, add=None, add_scale=None, add_scale_s: float = 1.0,
+         acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
+         gamma: float = 1.0) -> None:
+    """One fused SpMM launch (bbgr_spmm) on the current stream."""
+    d = x.shape[1]
+    a = _lib.SpmmArgs()
+    a.d = d
+    a.x, a.ldx = ptr(x), ld(x)
+    if prod.vals is not None:
+        a.weight_mode, a.edge_val = 1, ptr(prod.vals)
+    elif first and prod.in_scale is not None:
+        a.weight_mode, a.col_scale, a.col_scale_s = 2, ptr(prod.in_scale), 1.0
+    else:
+        a.weight_mode = 0
+    a.y, a.ldy = ptr(y), ld(y)
+    a.y_scale, a.y_scale_s = ptr(y_scale), y_scale_s
+    a.add, a.ldadd = ptr(add), ld(add)
+    a.add_scale, a.add_scale_s = ptr(add_scale), add_scale_s
+    a.acc_in, a.ldacc_in = ptr(acc_in), ld(acc_in)
+    a.acc_out, a.ldacc_out = ptr(acc_out), ld(acc_out)
+    a.acc_scale, a.acc_scale_s = ptr(acc_scale), acc_scale_s
+    a.gamma = gamma
+    a.partial = ptr(prod.workspace(d))
+    if _timer is None:
+        call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
+        return
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
+    ev1.record()
+    _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d, ev0, ev1))
+
+
+def _check_table(name, t, rows, d=None):
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dim() != 2 or t.shape[0] != rows or (d is not None and t.shape[1] != d):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected [{rows}, {d}]")
+    if t.stride(1) != 1:
+        raise ValueError(f"{name} must have unit column stride")
+
+
+def _buffers(ws: dict | None, device, d: int):
+    """Allocator for the chain's intermediate tables; reuses ws[(tag, rows, d)]."""
+    def new(tag: str, n: int) -> torch.Tensor:
+        if ws is None:
+            return torch.empty(n, d, dtype=torch.float32, device=device)
+        key = (tag, n, d)
+        t = ws.get(key)
+        if t is None:
+            t = ws[key] = torch.empty(n, d, dtype=torch.float32, device=device)
+        return t
+    return new
+
+
+def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
+            order: str = ORDER_GS, out_u: torch.Tensor | None = None,
+            out_i: torch.Tensor | None = None, ws: dict | None = None):
+    """Final (layer-mean) user and item tables. u0 [U,d], i0 [I,d] fp32."""
+    U, I = pair.num_users, pair.num_items
+    d = u0.shape[1]
+    _check_table("user table", u0, U, d)
+    _check_table("item table", i0, I, d)
+    acc_u = torch.empty_like(u0, memory_format=torch.contiguous_format) if out_u is None else out_u
+    acc_i = torch.empty_like(i0, memory_format=torch.contiguous_format) if out_i is None else out_i
+    K = int(num_layers)
+    if K == 0:
+        acc_u.copy_(u0)
+        acc_i.copy_(i0)
+        return acc_u, acc_i
+    gl = 1.0 / (K + 1)
+    FI, FU = pair.fwd_item, pair.fwd_user
+    new = _buffers(ws, u0.device, d)
+    if order == ORDER_GS:
+        bufU, bufI = new("u0", U), new("i0", I)
+        for k in range(1, K + 1):
+            g = gl if k == K else 1.0
+            spmm(FI, u0 if k == 1 else bufU, k == 1, y=bufI, y_scale=pair.feed_fwd_iu,
+                 acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
+                 acc_scale=FI.out_scale, gamma=g)
+            spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
+                 acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
+                 acc_scale=FU.out_scale, gamma=g)
+    elif order == ORDER_J:
+        bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
+        cur = 0
+        for k in range(1, K + 1):
+            g = gl if k == K else 1.0
+            nxt = 1 - cur
+            spmm(FI, u0 if k == 1 else bufU[cur], k == 1,
+                 y=bufI[nxt] if k < K else None, y_scale=pair.feed_fwd_iu,
+                 acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
+                 acc_scale=FI.out_scale, gamma=g)
+            spmm(FU, i0 if k == 1 else bufI[cur], k == 1,
+                 y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,
+                 acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
+                 acc_scale=FU.out_scale, gamma=g)
+            cur = nxt
+    else:
+        raise ValueError(f"unknown propagation order {order!r}")
+    return acc_u, acc_i
+
+
+def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
+             order: str = ORDER_GS, out_u: torch.Tensor | None = None,
+             out_i: torch.Tensor | None = None, ws: dict | None = None,
+             grad_i0_dense: bool = True):
+    """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final)."""
+    U, I = pair.num_users, pair.num_items
+    d = gU.shape[1]
+    _check_table("user grad", gU, U, d)
+    _check_table("item grad", gI, I, d)
+    K = int(num_layers)
+    gu0 = torch.empty_like(gU, memory_format=torch.contiguous_format) if out_u is None else out_u
+    gi0 = torch.empty_like(gI, memory_format=torch.contiguous_format) if out_i is None else out_i
+    if K == 0:
+        gu0.copy_(gU)
+        gi0.copy_(gI)
+        return gu0, gi0
+    gl = 1.0 / (K + 1)
+    BI, BU = pair.bwd_item, pair.bwd_user
+    new = _buffers(ws, gU.device, d)
+    if order == ORDER_GS:
+        bufU, bufI = new("u0", U), new("i0", I)
+        for k in range(K, 0, -1):
+            first = k == K
+            spmm(BI, gU if first else bufU, first, y=bufI, y_scale=pair.feed_bwd_iu,
+                 y_scale_s=gl if first else 1.0,
+                 add=gI, add_scale=BU.in_scale, add_scale_s=gl)
+            if k > 1:
+                spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
+                     add=gU, add_scale=BI.in_scale, add_scale_s=gl)
+            else:
+                spmm(BU, bufI, False, y=gu0, y_scale=BU.out_scale,
+                     add=gU, add_scale=None, add_scale_s=gl)
+        if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
+            torch.mul(gI, gl, out=gi0)
+    elif order == ORDER_J:
+        bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
+        cur = 0
+        for k in range(K, 0, -1):
+            first = k == K
+            nxt = 1 - cur
+            ys = gl if first else 1.0
+            xu = gI if first else bufI[cur]   # input of BU (item table)
+            xi = gU if first else bufU[cur]   # input of BI (user table)
+            if k > 1:
+                spmm(BU, xu, first, y=bufU[nxt], y_scale=pair.feed_bwd_ui, y_scale_s=ys,
+                     add=gU, add_scale=BI.in_scale, add_scale_s=gl)
+                spmm(BI, xi, first, y=bufI[nxt], y_scale=pair.feed_bwd_iu, y_scale_s=ys,
+                     add=gI, add_scale=BU.in_scale, add_scale_s=gl)
+            else:
+                spmm(BU, xu, first, y=gu0, y_scale=BU.out_scale, y_scale_s=ys,
+                     add=gU, add_scale=None, add_scale_s=gl)
+                spmm(BI, xi, first, y=gi0, y_scale=BI.out_scale, y_scale_s=ys,
+                     add=gI, add_scale=None, add_scale_s=gl)
+            cur = nxt
+    else:
+        raise ValueError(f"unknown propagation order {order!r}")
+    return gu0, gi0
+
+
+class _PropagateFn(torch.autograd.Function):
+    """Differentiable (u0, i0) -> (u_final, i_final); replaces the autograd of
+    the reference's K x torch.sparse.mm + stack().mean() chain."""
+
+    @staticmethod
+    def forward(ctx, u0, i0, pair, num_layers, order):
+        _lib.require_gpu(u0)
+        u0c, i0c = u0.contiguous(), i0.contiguous()
+        uf, itf = forward(pair, u0c, i0c, num_layers, order)
+        ctx.pair, ctx.K, ctx.order = pair, num_layers, order
+        return uf, itf
+
+    @staticmethod
+    def backward(ctx, gU, gI):
+        pair = ctx.pair
+        if gU is None and gI is None:
+            return None, None, None, None, None
+        ref = gU if gU is not None else gI
+        d = ref.shape[1]
+        if gU is None:
+            gU = torch.zeros(pair.num_users, d, device=ref.device, dtype=torch.float32)
+        if gI is None:
+            gI = torch.zeros(pair.num_items, d, device=ref.device, dtype=torch.float32)
+        gu0, gi0 = backward(pair, gU.contiguous(), gI.contiguous(), ctx.K, ctx.order)
+        return gu0, gi0, None, None, None
+
+
+def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
+              order: str = ORDER_GS):
+    return _PropagateFn.apply(u0, i0, pair, num_layers, order)
+
+
+# ---------------------------------------------------------------------------
+# Square generic operator (lightgcn.py fed an arbitrary N x N sparse tensor)
+# ---------------------------------------------------------------------------
+class SquareOperator:
+    """x_{k+1} = A x_k with explicit values (A and A^T CSRs)."""
+
+    def __init__(self, A: Csr, At: Csr):
+        self.A, self.At = A, At
+        self.fwd = Product(A, A.values, None, None, {})
+        self.bwd = Product(At, At.values, None, None, {})
+        self.n = A.n_rows
+
+
+def square_forward(op: SquareOperator, x0: torch.Tensor, K: int):
+    d = x0.shape[1]
+    _check_table("node table", x0, op.n, d)
+    out = torch.empty_like(x0, memory_format=torch.contiguous_format)
+    if K == 0:
+        out.copy_(x0)
+        return out
+    gl = 1.0 / (K + 1)
+    bufs = [torch.empty_like(out), torch.empty_like(out)]
+    cur = 0
+    for k in range(1, K + 1):
+        spmm(op.fwd, x0 if k == 1 else bufs[cur], k == 1, y=bufs[1 - cur] if k < K else None,
+             acc_in=x0 if k == 1 else out, acc_out=out, gamma=gl if k == K else 1.0)
+        cur = 1 - cur
+    return out
+
+
+def square_backward(op: SquareOperator, g: torch.Tensor, K: int):
+    out = torch.empty_like(g, memory_format=torch.contiguous_format)
+    if K == 0:
+        out.copy_(g)
+        return out
+    gl = 1.0 / (K + 1)
+    # G_k = g' + A^T G_{k+1}, G_K = g'; grad_x0 = G_0
+    bufs = [torch.empty_like(out), torch.empty_like(out)]
+    cur = 0
+    for k in range(K, 0, -1):
+        first = k == K
+        spmm(op.bwd, g if first else bufs[cur], first,
+             y=out if k == 1 else bufs[1 - cur], y_scale_s=gl if first else 1.0,
+             add=g, add_scale_s=gl)
+        cur = 1 - cur
+    return out
+
+
+class _SquareFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x0, op, K):
+        _lib.require_gpu(x0)
+        ctx.op, ctx.K = op, K
+        return square_forward(op, x0.contiguous(), K)
+
+    @staticmethod
+    def backward(ctx, g):
+        return square_backward(ctx.op, g.contiguous(), ctx.K), None, None

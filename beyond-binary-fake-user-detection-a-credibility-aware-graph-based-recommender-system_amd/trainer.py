@@ -1,0 +1,144 @@
+"""Fused native training step of the reference's training loop.
+
+One step == Version-2/lighgcn_cu_pop.py:826-866 for one batch of users:
+  batch users (epoch permutation, :821-827) -> positive + pop-mix negative
+  sampling (:835-849) -> propagate() (:858, 2K SpMMs) -> bpr_loss (:859)
+  -> backward (:862, 2K transposed SpMMs) -> Adam (:863).
+Everything runs on the device on ONE stream with no host synchronisation;
+`loss` stays a device scalar until the caller reads it (the reference reads
+it every step with float(loss.item()), :865).
+
+Gradient tables that are sparse by construction (dL/d u_final, dL/d i_final:
+only batch rows) are kept all-zero between steps: the BPR kernel scatter-adds
+into them and the step re-zeroes exactly the touched rows afterwards.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import OP_GS, OP_J, OP_METHOD_A, OP_SYM, call, ld, ptr, stream_handle
+from .bpr import bpr_args
+from .graph import BipartiteGraph
+from .optim import adam_step
+from .propagate import ORDER_GS, ORDER_J, OperatorPair, backward, forward
+from .sampler import PopMixSampler, nonempty_rows, shuffle
+
+VARIANTS = {
+    # name: (operator kind, layer order, default negative sampler mix)
+    "v2_pop": (OP_GS, ORDER_GS, 0.7),        # Version-2/lighgcn_cu_pop.py
+    "cu_message": (OP_GS, ORDER_GS, 0.0),    # version_1/lightgcn_cu_message.py
+    "method_a": (OP_METHOD_A, ORDER_GS, 0.0),  # version_1/..._long_tail_exposure.py
+    "cu_fair": (OP_J, ORDER_J, 0.0),         # lightgcn_cu.py
+    "plain": (OP_SYM, ORDER_J, 0.0),         # lightgcn.py
+}
+
+
+class FusedTrainer:
+    def __init__(self, graph: BipartiteGraph, variant: str = "v2_pop", cred=None,
+                 emb_dim: int = 64, num_layers: int = 3, lr: float = 1e-3,
+                 reg: float = 1e-4, batch_size: int = 4096, neg_mix_pop: float | None = None,
+                 neg_pop_gamma: float = 0.75, neg_max_tries: int = 50,
+                 lambda_fair: float = 0.0, seed: int = 42, u0=None, i0=None):
+        _lib.require_gpu()
+        if variant not in VARIANTS:
+            raise ValueError(f"unknown variant {variant!r}; one of {sorted(VARIANTS)}")
+        kind, order, mix_default = VARIANTS[variant]
+        self.graph, self.variant, self.order = graph, variant, order
+        self.U, self.I, self.d, self.K = graph.num_users, graph.num_items, emb_dim, num_layers
+        self.lr, self.reg, self.B = lr, reg, batch_size
+        self.lambda_fair, self.seed = lambda_fair, seed
+        dev = graph.device
+        self.device = dev
+        cred_t = None
+        if cred is not None and kind != OP_SYM:
+            cred_t = torch.as_tensor(np.asarray(cred, np.float32)).to(dev).contiguous()
+        self.scales = graph.scales(kind, cred_t)
+        self.pair = OperatorPair.factored(graph, self.scales)
+
+        f32 = dict(dtype=torch.float32, device=dev)
+        if u0 is None:
+            g = torch.Generator(device="cpu").manual_seed(seed)
+            au = (6.0 / (self.U + emb_dim)) ** 0.5
+            ai = (6.0 / (self.I + emb_dim)) ** 0.5
+            u0 = (torch.rand(self.U, emb_dim, generator=g) * 2 - 1) * au
+            i0 = (torch.rand(self.I, emb_dim, generator=g) * 2 - 1) * ai
+        self.user_w = torch.as_tensor(u0, dtype=torch.float32).to(dev).contiguous()
+        self.item_w = torch.as_tensor(i0, dtype=torch.float32).to(dev).contiguous()
+        if self.user_w.shape != (self.U, emb_dim) or self.item_w.shape != (self.I, emb_dim):
+            raise ValueError("initial tables have the wrong shape")
+        z = lambda n: torch.zeros(n, emb_dim, **f32)  # noqa: E731
+        self.m_u, self.v_u, self.m_i, self.v_i = z(self.U), z(self.U), z(self.I), z(self.I)
+        self.uf = torch.empty(self.U, emb_dim, **f32)
+        self.itf = torch.empty(self.I, emb_dim, **f32)
+        self.g_uf, self.g_if = z(self.U), z(self.I)         # all-zero between steps
+        self.g_u0 = torch.empty(self.U, emb_dim, **f32)
+        self.g_i0 = torch.empty(self.I, emb_dim, **f32)
+        self.parts = torch.empty(3 * batch_size, **f32)
+        self.loss = torch.zeros((), **f32)
+        self.ws: dict = {}
+        self.pop = None
+        if lambda_fair != 0.0:   # lightgcn_cu.py:583-584: pop = deg_i / max(deg_i)
+            di = self.scales.deg_i
+            self.pop = (di / di.max().clamp(min=1.0)).contiguous()
+        mix = mix_default if neg_mix_pop is None else neg_mix_pop
+        self.sampler = PopMixSampler(graph.user_csr, graph.item_csr, self.I, mix_pop=mix,
+                                     gamma=neg_pop_gamma if mix > 0 else None,
+                                     max_tries=neg_max_tries, seed=seed)
+        self.train_users = nonempty_rows(graph.user_csr)
+        if self.train_users.numel() == 0:
+            raise RuntimeError("No train users with interactions. Check your threshold/split.")
+        self.epoch, self.cursor, self.step_count = 0, 0, 0
+        self.perm = None
+        self.pos = torch.empty(batch_size, dtype=torch.int64, device=dev)
+        self.neg = torch.empty(batch_size, dtype=torch.int64, device=dev)
+
+    # -- batching ---------------------------------------------------------------
+    def next_users(self) -> torch.Tensor:
+        n = self.train_users.numel()
+        if self.perm is None or self.cursor >= n:
+            self.epoch += 1
+            self.perm = shuffle(self.train_users, self.seed, self.epoch)
+            self.cursor = 0
+        users = self.perm[self.cursor: self.cursor + self.B]
+        self.cursor += self.B
+        return users
+
+    # -- one step ----------------------------------------------------------------
+    def step(self, users: torch.Tensor | None = None) -> torch.Tensor:
+        users = self.next_users() if users is None else users.to(torch.int64).contiguous()
+        B = users.numel()
+        pos, neg = self.sampler.sample(users, self.pos[:B], self.neg[:B])
+        self.forward()
+        st = stream_handle()
+        a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
+                     self.pop, self.lambda_fair, parts=self.parts[: 3 * B],
+                     g_uf=self.g_uf, g_if=self.g_if)
+        call("bbgr_bpr", ctypes.byref(a), st)
+        call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
+             ptr(self.loss), st)
+        backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
+                 out_i=self.g_i0, ws=self.ws)
+        # ego L2 term goes straight to the weight grads (Version-2:503-507)
+        a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
+                     g_ue=self.g_u0, g_ie=self.g_i0)
+        call("bbgr_bpr", ctypes.byref(a), st)
+        self.step_count += 1
+        adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
+        adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)
+        # restore the all-zero invariant of the sparse gradient tables
+        call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
+        call("bbgr_rows_zero", B, ptr(pos), ptr(self.g_if), ld(self.g_if), self.d, st)
+        call("bbgr_rows_zero", B, ptr(neg), ptr(self.g_if), ld(self.g_if), self.d, st)
+        return self.loss
+
+    def forward(self):
+        return forward(self.pair, self.user_w, self.item_w, self.K, self.order,
+                       out_u=self.uf, out_i=self.itf, ws=self.ws)
+
+    def state_dict(self) -> dict:
+        """Reference keys (Version-2:903): user_emb.weight / item_emb.weight."""
+        return {"user_emb.weight": self.user_w, "item_emb.weight": self.item_w}

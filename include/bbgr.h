@@ -1,0 +1,302 @@
+/*
+ * bbgr.h — C ABI of the MI355X-native LightGCN propagation + BPR training path.
+ *
+ * One shared library (libbbgr.so, hipcc --offload-arch=gfx950) exports every entry
+ * point below. Plain pointers and sizes only: no torch types cross this boundary.
+ *
+ * Conventions (every entry point):
+ *   - Caller-owned DEVICE buffers; no allocation inside hot calls. Entry points that
+ *     need scratch take (workspace, workspace_bytes); call them once with
+ *     workspace == NULL to query the size.
+ *   - Stream-ordered on the hipStream_t passed as `stream` (NULL = default stream).
+ *     No host synchronisation except in the entry points documented as "syncs"
+ *     (one-time operator planning only).
+ *   - Return BBGR_OK (0) or a negative bbgr_status; bbgr_last_error() gives text.
+ *   - Re-entrant across distinct streams.
+ *   - Index arrays are int32 for CSR structure (nnz < 2^31), int64 for batch
+ *     index vectors (they are torch.long in the reference).
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * reference repo root) is cited on its declaration.
+ */
+#ifndef BBGR_H
+#define BBGR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BBGR_ABI_VERSION 1
+
+typedef enum {
+  BBGR_OK = 0,
+  BBGR_ERR_INVALID = -1,     /* bad argument (null pointer, size, alignment) */
+  BBGR_ERR_UNSUPPORTED = -2, /* valid but not implemented (e.g. emb dim) */
+  BBGR_ERR_HIP = -3,         /* a HIP runtime call failed; see bbgr_last_error() */
+  BBGR_ERR_WORKSPACE = -4    /* workspace missing or too small */
+} bbgr_status;
+
+typedef void *bbgr_stream_t; /* a hipStream_t */
+
+/* ------------------------------------------------------------------------- */
+/* Library                                                                    */
+/* ------------------------------------------------------------------------- */
+int bbgr_abi_version(void);
+/* Text for the most recent failure on the calling host thread. */
+const char *bbgr_last_error(void);
+/* Device properties the planner uses (CU count, arch name). */
+int bbgr_device_info(int device, int *cu_count, char *arch_name, int arch_name_len);
+/* Blocks until `stream` has drained (the one explicit sync). */
+int bbgr_sync(bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* CSR structure                                                              */
+/*   Replaces: sparse_coo_tensor(...).coalesce() in                           */
+/*     Version-2/lighgcn_cu_pop.py:443,450; lightgcn_cu.py:393,397;          */
+/*     lightgcn.py:363,372 — and edges_to_user_csr, Version-2:309-327.        */
+/*   Duplicate (row,col) pairs are KEPT as repeated entries; summing repeated */
+/*   entries in the SpMM is what coalesce()'s value-sum does.                 */
+/* ------------------------------------------------------------------------- */
+
+/* Build a row-sorted CSR with columns sorted inside each row (stable:
+ * duplicates keep their input order). `perm_out` (nullable) receives, for every
+ * CSR slot, the input edge id it came from — used to permute per-edge values.
+ * Device arrays: rows[nnz], cols[nnz] -> indptr[n_rows+1], indices[nnz]. */
+int bbgr_csr_build(int64_t nnz, const int32_t *rows, const int32_t *cols,
+                   int32_t n_rows, int32_t n_cols, int32_t *indptr,
+                   int32_t *indices, int32_t *perm_out, void *workspace,
+                   size_t *workspace_bytes, bbgr_stream_t stream);
+
+/* Load-balance plan for the SpMM. Rows with degree > long_threshold are cut
+ * into chunks of at most chunk_edges edges; each chunk is one 256-thread
+ * workgroup. Rows cut into >1 chunk ("split rows") are finished by a fix-up
+ * pass. chunks[n_chunks][4] = {row, e_begin, e_end, slot (-1: sole chunk)};
+ * split[n_split][4] = {row, slot_begin, n_slots, 0}.                         */
+typedef struct {
+  int32_t n_rows;
+  int32_t n_cols;
+  int64_t nnz;
+  const int32_t *indptr;  /* [n_rows+1] device */
+  const int32_t *indices; /* [nnz] device */
+  int32_t long_threshold; /* 0 => default (256) */
+  int32_t chunk_edges;    /* 0 => default (2048) */
+  int32_t n_chunks;
+  int32_t n_split;
+  const int32_t *chunks; /* [n_chunks*4] device */
+  const int32_t *split;  /* [n_split*4] device */
+} bbgr_csr;
+
+/* Counts chunks and split rows for csr->long_threshold / chunk_edges (fills
+ * csr-side values into *n_chunks / *n_split). SYNCS `stream` (one-time). */
+int bbgr_csr_plan_count(const bbgr_csr *csr, int32_t *n_chunks, int32_t *n_split,
+                        void *workspace, size_t *workspace_bytes,
+                        bbgr_stream_t stream);
+/* Fills chunks[n_chunks*4] and split[n_split*4] (sizes from plan_count). */
+int bbgr_csr_plan_build(const bbgr_csr *csr, int32_t *chunks, int32_t *split,
+                        void *workspace, size_t *workspace_bytes,
+                        bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Operator scale vectors                                                     */
+/*   Replaces the numpy weight math of build_message_passing_mats             */
+/*   (Version-2/lighgcn_cu_pop.py:429-452), its Method-A variant              */
+/*   (version_1/lightgcn_cu_pop_long_tail_exposure.py:362-396),               */
+/*   build_cred_weighted_mats (lightgcn_cu.py:368-399) and build_norm_adj     */
+/*   (lightgcn.py:352-372).                                                   */
+/*                                                                            */
+/* Every operator of the reference factors as diag(row) * A * diag(col) over  */
+/* the 0/1(+multiplicity) adjacency A:                                        */
+/*   item<-user  M = diag(p) A_iu diag(q)      user<-item  M = diag(s) A_ui diag(t)
+ *   GS / J : p = t = b, q = c*a, s = a    (a = 1/sqrt(max(deg_u,1)),         */
+/*                                          b = 1/sqrt(max(deg_i,1)))         */
+/*   Method A: p = t = b*alpha, alpha = 1/log1p(max(deg_i,1))                 */
+/*   S (symmetric N x N): p = t = deg_i^-1/2, q = s = deg_u^-1/2 (inf -> 0)   */
+/* Outputs (device, fp32): deg_u[U], deg_i[I], p[I], q[U], s[U], t[I],        */
+/* pt[I] = p*t, qs[U] = q*s. cred (nullable => all ones) is clipped to [0,1]  */
+/* by the caller as the reference loader does.                                */
+/* ------------------------------------------------------------------------- */
+typedef enum {
+  BBGR_OP_GS = 0,       /* Version-2/lighgcn_cu_pop.py (credibility inside messages) */
+  BBGR_OP_METHOD_A = 1, /* version_1/lightgcn_cu_pop_long_tail_exposure.py     */
+  BBGR_OP_J = 2,        /* lightgcn_cu.py (same weights as GS, Jacobi order)  */
+  BBGR_OP_SYM = 3       /* lightgcn.py symmetric normalised adjacency         */
+} bbgr_op_kind;
+
+int bbgr_operator_scales(int32_t kind, int32_t n_users, int32_t n_items,
+                         const int32_t *indptr_u, const int32_t *indptr_i,
+                         const float *cred, float *deg_u, float *deg_i,
+                         float *p, float *q, float *s, float *t, float *pt,
+                         float *qs, bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Fused CSR-SpMM (the hot kernel)                                            */
+/*   Replaces torch.sparse.mm at Version-2/lighgcn_cu_pop.py:483-484,         */
+/*   lightgcn_cu.py:431,434, lightgcn.py:323 and the autograd backward of     */
+/*   each (transposed operator), plus the stack(...).mean(0) layer mean       */
+/*   (Version-2:488-489) as a fused accumulate epilogue.                      */
+/*                                                                            */
+/* For every row r of A:                                                      */
+/*   T_r = sum_{e in row r} w_e * x[col_e, :]                                  */
+/*        w_e = 1                     (weight_mode 0)                          */
+/*        w_e = edge_val[e]           (weight_mode 1, CSR slot order)          */
+/*        w_e = col_scale[col_e]*col_scale_s   (weight_mode 2)                 */
+/*   y[r]       = ys_r * T_r + as_r * add[r]            (if y   != NULL)      */
+/*                ys_r = (y_scale ? y_scale[r] : 1) * y_scale_s               */
+/*                as_r = (add_scale ? add_scale[r] : 1) * add_scale_s         */
+/*   acc_out[r] = (acc_in[r] + cs_r * T_r) * gamma       (if acc_out != NULL) */
+/*                cs_r = (acc_scale ? acc_scale[r] : 1) * acc_scale_s;        */
+/*                acc_in NULL => 0                                            */
+/* Tables are fp32 row-major with leading dimension ld* (floats, multiple of  */
+/* 4, 16-byte aligned base). d in {64, 128, 256}.                             */
+/* partial: workspace of (csr->n_chunks * d) floats when csr->n_split > 0.    */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t d;
+  const float *x;
+  int64_t ldx;
+  int32_t weight_mode;
+  const float *edge_val;
+  const float *col_scale;
+  float col_scale_s;
+  float *y;
+  int64_t ldy;
+  const float *y_scale;
+  float y_scale_s;
+  const float *add;
+  int64_t ldadd;
+  const float *add_scale;
+  float add_scale_s;
+  const float *acc_in;
+  int64_t ldacc_in;
+  float *acc_out;
+  int64_t ldacc_out;
+  const float *acc_scale;
+  float acc_scale_s;
+  float gamma;
+  float *partial;
+} bbgr_spmm_args;
+
+int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
+              bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Fused BPR loss: gather -> dot -> log-sigmoid -> (+reg, +fair) -> grads     */
+/*   Replaces LightGCN.bpr_loss, Version-2/lighgcn_cu_pop.py:495-508          */
+/*   (== lightgcn.py:333-349 with ego offset; lightgcn_cu.py:635-648 adds     */
+/*   lambda_fair * mean(pop[pos] * pos_score)) and its autograd backward.     */
+/*                                                                            */
+/* Per triple b (u, p, n):                                                    */
+/*   s+ = <uf[u], if[p]>, s- = <uf[u], if[n]>                                 */
+/*   parts[3b+0] = -log(sigmoid(s+ - s-) + 1e-12)                             */
+/*   parts[3b+1] = |ue[u]|^2 + |ie[p]|^2 + |ie[n]|^2   (ego tables)           */
+/*   parts[3b+2] = pop ? pop[p] * s+ : 0                                      */
+/* loss = mean(parts0) + reg * mean(parts1) + lambda_fair * mean(parts2).     */
+/* If grads requested, with G = dloss ? *dloss : 1 (device scalar):           */
+/*   g_uf[u] += .., g_if[p] += .., g_if[n] += ..   (dense tables, atomics)    */
+/*   g_ue[u] += 2 reg G/B ue[u], g_ie[p|n] += 2 reg G/B ie[p|n]               */
+/* Any grad pointer may be NULL to skip it. Index vectors are int64.          */
+/* A triple with an index outside [0,n_users) / [0,n_items) (e.g. the        */
+/* sampler's -1 for a user without positives) contributes zero everywhere.   */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int64_t batch;
+  int32_t d;
+  int64_t n_users;                 /* rows of uf / ue (bounds check) */
+  int64_t n_items;                 /* rows of itf / ie (bounds check) */
+  const int64_t *users;
+  const int64_t *pos;
+  const int64_t *neg;
+  const float *uf; int64_t lduf;   /* final user table */
+  const float *itf; int64_t ldif;  /* final item table */
+  const float *ue; int64_t ldue;   /* ego user table */
+  const float *ie; int64_t ldie;   /* ego item table */
+  const float *pop;                /* nullable, [I] */
+  float reg;
+  float lambda_fair;
+  float *parts;                    /* nullable, [3*batch] */
+  const float *dloss;              /* nullable device scalar */
+  float *g_uf; int64_t ldguf;
+  float *g_if; int64_t ldgif;
+  float *g_ue; int64_t ldgue;
+  float *g_ie; int64_t ldgie;
+} bbgr_bpr_args;
+
+int bbgr_bpr(const bbgr_bpr_args *args, bbgr_stream_t stream);
+
+/* loss[0] = sum(parts0)/B + reg*sum(parts1)/B + lambda_fair*sum(parts2)/B,
+ * fixed-order (deterministic) reduction in one workgroup. */
+int bbgr_bpr_reduce(int64_t batch, const float *parts, float reg,
+                    float lambda_fair, float *loss, bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Adam (torch.optim.Adam defaults: amsgrad=False, maximize=False)            */
+/*   Replaces opt.step() at Version-2/lighgcn_cu_pop.py:863 (Adam lr=1e-3,    */
+/*   :793). Host computes bias_correction1 = 1-beta1^t and                    */
+/*   bias_correction2_sqrt = sqrt(1-beta2^t) in double, as torch does.        */
+/*   m = lerp(m, g, 1-beta1); v = beta2 v + (1-beta2) g^2;                    */
+/*   p -= (lr/bc1) * m / (sqrt(v)/bc2_sqrt + eps)   (+ weight_decay*p in g)   */
+/* ------------------------------------------------------------------------- */
+int bbgr_adam(int64_t n, float *param, const float *grad, float *exp_avg,
+              float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
+              float weight_decay, float bias_correction1,
+              float bias_correction2_sqrt, bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Row utilities for the fused training step                                  */
+/* ------------------------------------------------------------------------- */
+/* table[idx[k], :d] = 0 for k < n (restores all-zero gradient tables). */
+int bbgr_rows_zero(int64_t n, const int64_t *idx, float *table, int64_t ld,
+                   int32_t d, bbgr_stream_t stream);
+/* dst[idx[k], :] += alpha * src[idx[k], :] (atomic; duplicates sum). */
+int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha, const float *src,
+                   int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
+                   bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Negative / positive sampling                                               */
+/*   Replaces the per-user host loop of Version-2/lighgcn_cu_pop.py:835-849:  */
+/*   sample_pos_item (:339-343), sample_neg_item_popmix (:349-376),           */
+/*   user_has_item (:330-336), uniform sample_neg_item (lightgcn.py:296-300), */
+/*   and pop_prob = (deg_i+1)^gamma / (sum + 1e-12)  (:805-810).              */
+/* RNG: Philox4x32-10, key = seed, counter = (counter, slot, draw).           */
+/* ------------------------------------------------------------------------- */
+/* cdf[i] = normalised inclusive prefix sum of (deg_i + 1)^gamma (fp64), the
+ * table numpy's Generator.choice(p=pop_prob) searches. */
+int bbgr_pop_cdf(int32_t n_items, const int32_t *indptr_i, double gamma,
+                 double *cdf, void *workspace, size_t *workspace_bytes,
+                 bbgr_stream_t stream);
+
+/* For each b < batch, user u = users[b]:
+ *   pos[b] = indices[indptr[u] + floor(U01 * deg_u)]   (-1 if deg_u == 0)
+ *   neg[b] = first of <= max_tries candidates not in row u, each drawn from
+ *            the pop CDF with probability mix_pop (cdf != NULL) else uniform;
+ *            then uniform draws until one is not in row u (capped at
+ *            BBGR_NEG_CAP draws; -1 and *fail_count += 1 if none found).
+ * indices must be sorted within each row (bbgr_csr_build guarantees it). */
+#define BBGR_NEG_CAP 65536
+int bbgr_sample(int64_t batch, const int64_t *users, const int32_t *indptr,
+                const int32_t *indices, int32_t n_items, const double *cdf,
+                float mix_pop, int32_t max_tries, uint64_t seed,
+                uint64_t counter, int64_t *pos, int64_t *neg,
+                int32_t *fail_count, bbgr_stream_t stream);
+
+/* out = a random permutation of in[0..n) (Philox keys + radix sort), the
+ * device form of rng.shuffle(train_users) (Version-2:821). */
+int bbgr_shuffle(int64_t n, const int64_t *in, int64_t *out, uint64_t seed,
+                 uint64_t counter, void *workspace, size_t *workspace_bytes,
+                 bbgr_stream_t stream);
+
+/* Users with at least one edge: out[0..*count) ascending (Version-2:797-798).
+ * *count is a DEVICE int64. */
+int bbgr_nonempty_rows(int32_t n_rows, const int32_t *indptr, int64_t *out,
+                       int64_t *count, void *workspace, size_t *workspace_bytes,
+                       bbgr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BBGR_H */

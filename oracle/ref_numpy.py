@@ -1,0 +1,292 @@
+"""ORACLE (test infrastructure only): float64 numpy/scipy restatement of the
+reference hot path. Each function cites the reference lines it follows
+(paths relative to the reference repository root).
+
+Operator VALUES are computed in float32 exactly as the reference's numpy code
+does (they are fp32 in the reference); propagation, loss and gradients are
+then evaluated in float64 — the "float64 truth" of the parity criterion.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+
+# ---------------------------------------------------------------------------
+# CSR helpers and samplers (Version-2/lighgcn_cu_pop.py:309-376)
+# ---------------------------------------------------------------------------
+def edges_to_user_csr(edges_2xE: np.ndarray, num_users: int):
+    """Version-2/lighgcn_cu_pop.py:309-327 (vectorised: stable sort by
+    (user, item) == mergesort by user then per-row np.sort)."""
+    u = edges_2xE[0].astype(np.int64)
+    it = edges_2xE[1].astype(np.int64)
+    order = np.lexsort((it, u))
+    counts = np.bincount(u, minlength=num_users)
+    indptr = np.zeros(num_users + 1, dtype=np.int64)
+    indptr[1:] = np.cumsum(counts)
+    return indptr, it[order].copy()
+
+
+def user_has_item(indptr, indices, user: int, item: int) -> bool:
+    """Version-2/lighgcn_cu_pop.py:330-336."""
+    start, end = indptr[user], indptr[user + 1]
+    if start == end:
+        return False
+    arr = indices[start:end]
+    j = np.searchsorted(arr, item)
+    return bool(j < (end - start) and arr[j] == item)
+
+
+def sample_pos_item(indptr, indices, user: int, rng: np.random.Generator):
+    """Version-2/lighgcn_cu_pop.py:339-343."""
+    start, end = indptr[user], indptr[user + 1]
+    if start == end:
+        return None
+    return int(indices[rng.integers(start, end)])
+
+
+def sample_neg_item(indptr, indices, user: int, num_items: int, rng: np.random.Generator):
+    """lightgcn.py:296-300 (uniform)."""
+    while True:
+        j = int(rng.integers(0, num_items))
+        if not user_has_item(indptr, indices, user, j):
+            return j
+
+
+def sample_neg_item_popmix(indptr, indices, user: int, num_items: int,
+                           rng: np.random.Generator, pop_prob: np.ndarray,
+                           mix_pop: float, max_tries: int):
+    """Version-2/lighgcn_cu_pop.py:349-376."""
+    for _ in range(max_tries):
+        if rng.random() < mix_pop:
+            j = int(rng.choice(num_items, p=pop_prob))
+        else:
+            j = int(rng.integers(0, num_items))
+        if not user_has_item(indptr, indices, user, j):
+            return j
+    while True:
+        j = int(rng.integers(0, num_items))
+        if not user_has_item(indptr, indices, user, j):
+            return j
+
+
+def pop_prob(train_edges_2xE: np.ndarray, num_items: int, gamma: float = 0.75):
+    """Version-2/lighgcn_cu_pop.py:805-810."""
+    item_deg = np.bincount(train_edges_2xE[1].astype(np.int64),
+                           minlength=num_items).astype(np.float64)
+    pop = np.power(item_deg + 1.0, gamma)
+    return (pop / (pop.sum() + 1e-12)).astype(np.float64)
+
+
+def sample_batch_reference_style(indptr, indices, users, num_items, rng, pop_prob_,
+                                 mix_pop=0.7, max_tries=50):
+    """The per-user host loop of Version-2/lighgcn_cu_pop.py:835-849."""
+    used, pos, neg = [], [], []
+    for u in users:
+        p = sample_pos_item(indptr, indices, int(u), rng)
+        if p is None:
+            continue
+        n = sample_neg_item_popmix(indptr, indices, int(u), num_items, rng,
+                                   pop_prob=pop_prob_, mix_pop=mix_pop, max_tries=max_tries)
+        used.append(int(u))
+        pos.append(p)
+        neg.append(n)
+    return np.array(used), np.array(pos), np.array(neg)
+
+
+# ---------------------------------------------------------------------------
+# Operator values (fp32, as the reference computes them)
+# ---------------------------------------------------------------------------
+def gs_values(edges_2xE, num_users, num_items, cred_u=None, method_a=False):
+    """Version-2/lighgcn_cu_pop.py:430-450 (method_a: version_1/
+    lightgcn_cu_pop_long_tail_exposure.py:379-392).
+    Returns (u, i, w_ui, w_iu): M_ui[u,i] += w_ui, M_iu[i,u] += w_iu."""
+    u = edges_2xE[0].astype(np.int64)
+    i = edges_2xE[1].astype(np.int64)
+    deg_u = np.bincount(u, minlength=num_users).astype(np.float32)
+    deg_i = np.bincount(i, minlength=num_items).astype(np.float32)
+    inv_sqrt_u = 1.0 / np.sqrt(np.maximum(deg_u, 1.0))
+    inv_sqrt_i = 1.0 / np.sqrt(np.maximum(deg_i, 1.0))
+    w_base = inv_sqrt_u[u] * inv_sqrt_i[i]
+    if method_a:
+        alpha_i = (1.0 / np.log1p(np.maximum(deg_i, 1.0))).astype(np.float32)
+        w_base = w_base * alpha_i[i]
+    c = np.ones(num_users, np.float32) if cred_u is None else np.asarray(cred_u, np.float32)
+    w_cred = c[u] * w_base
+    return u, i, w_base.astype(np.float32), w_cred.astype(np.float32)
+
+
+def j_values(edges_2xE, num_users, num_items, cred_u=None):
+    """lightgcn_cu.py:383-397. Returns (u, i, w_item_from_user, w_user_from_item, deg_i):
+    M_ui[i,u] (item<-user) = c_u/denom, M_iu[u,i] (user<-item) = 1/denom."""
+    u = edges_2xE[0].astype(np.int64)
+    i = edges_2xE[1].astype(np.int64)
+    deg_u = np.bincount(u, minlength=num_users).astype(np.float32)
+    deg_i = np.bincount(i, minlength=num_items).astype(np.float32)
+    denom = np.sqrt(np.maximum(deg_u[u] * deg_i[i], 1e-12)).astype(np.float32)
+    c = np.ones(num_users, np.float32) if cred_u is None else np.asarray(cred_u, np.float32)
+    w_ui = (c[u] / denom).astype(np.float32)
+    w_iu = (1.0 / denom).astype(np.float32)
+    return u, i, w_ui, w_iu, deg_i
+
+
+def sym_values(edges_2xE, num_users, num_items):
+    """lightgcn.py:352-372 after coalesce: returns scipy CSR [N,N] float64 of
+    the fp32 values v * dinv[r] * dinv[c] with v = multiplicity."""
+    u = edges_2xE[0].astype(np.int64)
+    it = edges_2xE[1].astype(np.int64) + num_users
+    N = num_users + num_items
+    row = np.concatenate([u, it])
+    col = np.concatenate([it, u])
+    A = sp.coo_matrix((np.ones(row.size, np.float32), (row, col)), shape=(N, N)).tocsr()
+    A.sum_duplicates()
+    deg = np.asarray(A.sum(axis=1)).ravel().astype(np.float32)
+    with np.errstate(divide="ignore"):
+        dinv = np.power(deg, np.float32(-0.5)).astype(np.float32)
+    dinv[np.isinf(dinv)] = 0.0
+    coo = A.tocoo()
+    v = (coo.data.astype(np.float32) * dinv[coo.row] * dinv[coo.col]).astype(np.float32)
+    return sp.csr_matrix((v.astype(np.float64), (coo.row, coo.col)), shape=(N, N))
+
+
+def csr64(rows, cols, vals, shape) -> sp.csr_matrix:
+    """Coalesced (duplicates summed) float64 matrix of fp32 values."""
+    m = sp.coo_matrix((np.asarray(vals, np.float64), (rows, cols)), shape=shape).tocsr()
+    m.sum_duplicates()
+    return m
+
+
+def gs_mats(edges_2xE, U, I, cred_u=None, method_a=False):
+    u, i, w_ui, w_iu = gs_values(edges_2xE, U, I, cred_u, method_a)
+    return csr64(u, i, w_ui, (U, I)), csr64(i, u, w_iu, (I, U))   # M_ui, M_iu
+
+
+def j_mats(edges_2xE, U, I, cred_u=None):
+    u, i, w_ui, w_iu, deg_i = j_values(edges_2xE, U, I, cred_u)
+    return csr64(i, u, w_ui, (I, U)), csr64(u, i, w_iu, (U, I)), deg_i  # M_ui[I,U], M_iu[U,I]
+
+
+# ---------------------------------------------------------------------------
+# Propagation (float64)
+# ---------------------------------------------------------------------------
+def propagate_gs(M_ui, M_iu, u0, i0, K):
+    """Version-2/lighgcn_cu_pop.py:472-490. Returns (u_final, i_final, us, is_)."""
+    u, i = np.asarray(u0, np.float64), np.asarray(i0, np.float64)
+    us, is_ = [u], [i]
+    for _ in range(K):
+        i = M_iu @ u
+        u = M_ui @ i
+        us.append(u)
+        is_.append(i)
+    return np.mean(us, 0), np.mean(is_, 0), us, is_
+
+
+def propagate_j(M_item_from_user, M_user_from_item, u0, i0, K):
+    """lightgcn_cu.py:420-448 (M_ui [I,U] item<-user, M_iu [U,I]; u' uses is_[-1])."""
+    us = [np.asarray(u0, np.float64)]
+    is_ = [np.asarray(i0, np.float64)]
+    for _ in range(K):
+        e_i = M_item_from_user @ us[-1]
+        e_u = M_user_from_item @ is_[-1]
+        us.append(e_u)
+        is_.append(e_i)
+    return np.mean(us, 0), np.mean(is_, 0), us, is_
+
+
+def propagate_sym(A, x0, K):
+    """lightgcn.py:318-325."""
+    x = np.asarray(x0, np.float64)
+    xs = [x]
+    for _ in range(K):
+        x = A @ x
+        xs.append(x)
+    return np.mean(xs, 0), xs
+
+
+def backward_gs(M_ui, M_iu, gU, gI, K):
+    """Adjoint of propagate_gs: grads of (u0, i0) from dL/du_final, dL/di_final."""
+    gl = 1.0 / (K + 1)
+    gU, gI = np.asarray(gU, np.float64) * gl, np.asarray(gI, np.float64) * gl
+    Gu = gU.copy()
+    for _ in range(K):
+        Gi = gI + M_ui.T @ Gu
+        Gu = gU + M_iu.T @ Gi
+    return Gu, gI.copy()
+
+
+def backward_j(M_item_from_user, M_user_from_item, gU, gI, K):
+    gl = 1.0 / (K + 1)
+    gU, gI = np.asarray(gU, np.float64) * gl, np.asarray(gI, np.float64) * gl
+    Gu, Gi = gU.copy(), gI.copy()
+    for _ in range(K):
+        Gu, Gi = gU + M_item_from_user.T @ Gi, gI + M_user_from_item.T @ Gu
+    return Gu, Gi
+
+
+def backward_sym(A, g, K):
+    gl = 1.0 / (K + 1)
+    g = np.asarray(g, np.float64) * gl
+    G = g.copy()
+    for _ in range(K):
+        G = g + A.T @ G
+    return G
+
+
+# ---------------------------------------------------------------------------
+# BPR (+reg, +fair) and its gradients (float64)
+# ---------------------------------------------------------------------------
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def bpr_loss(uf, itf, ue, ie, users, pos, neg, reg, pop=None, lambda_fair=0.0):
+    """Version-2/lighgcn_cu_pop.py:495-508 (+ lightgcn_cu.py:641-648 fair term).
+    Returns (loss, grads dict with dense g_uf, g_if, g_ue, g_ie)."""
+    uf, itf = np.asarray(uf, np.float64), np.asarray(itf, np.float64)
+    ue, ie = np.asarray(ue, np.float64), np.asarray(ie, np.float64)
+    users, pos, neg = (np.asarray(a, np.int64) for a in (users, pos, neg))
+    B = users.size
+    u, p, n = uf[users], itf[pos], itf[neg]
+    sp_, sn = (u * p).sum(1), (u * n).sum(1)
+    x = sp_ - sn
+    sig = _sigmoid(x)
+    loss_bpr = -np.log(sig + 1e-12).mean()
+    r = ((ue[users] ** 2).sum(1) + (ie[pos] ** 2).sum(1) + (ie[neg] ** 2).sum(1)).mean()
+    fair = 0.0 if pop is None else (np.asarray(pop, np.float64)[pos] * sp_).mean()
+    loss = loss_bpr + reg * r + lambda_fair * fair
+    gx = -(sig * (1.0 - sig)) / (sig + 1e-12) / B
+    gpos = gx + (0.0 if pop is None else lambda_fair * np.asarray(pop, np.float64)[pos] / B)
+    gneg = -gx
+    g_uf = np.zeros_like(uf)
+    g_if = np.zeros_like(itf)
+    np.add.at(g_uf, users, gpos[:, None] * p + gneg[:, None] * n)
+    np.add.at(g_if, pos, gpos[:, None] * u)
+    np.add.at(g_if, neg, gneg[:, None] * u)
+    g_ue = np.zeros_like(ue)
+    g_ie = np.zeros_like(ie)
+    np.add.at(g_ue, users, 2.0 * reg / B * ue[users])
+    np.add.at(g_ie, pos, 2.0 * reg / B * ie[pos])
+    np.add.at(g_ie, neg, 2.0 * reg / B * ie[neg])
+    return float(loss), dict(g_uf=g_uf, g_if=g_if, g_ue=g_ue, g_ie=g_ie,
+                             parts=np.stack([-np.log(sig + 1e-12),
+                                             (ue[users] ** 2).sum(1) + (ie[pos] ** 2).sum(1)
+                                             + (ie[neg] ** 2).sum(1),
+                                             np.zeros(B) if pop is None else
+                                             np.asarray(pop, np.float64)[pos] * sp_], 1))
+
+
+def adam_step(p, g, m, v, step, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8):
+    """torch.optim.Adam (amsgrad=False, weight_decay=0) in float64."""
+    p, g, m, v = (np.asarray(a, np.float64).copy() for a in (p, g, m, v))
+    m = m + (1 - beta1) * (g - m)
+    v = beta2 * v + (1 - beta2) * g * g
+    bc1 = 1 - beta1 ** step
+    bc2s = np.sqrt(1 - beta2 ** step)
+    p = p - (lr / bc1) * m / (np.sqrt(v) / bc2s + eps)
+    return p, m, v
+
+
+def xavier_uniform(rows, cols, rng):
+    """torch.nn.init.xavier_uniform_ bound for an [rows, cols] weight."""
+    a = np.sqrt(6.0 / (rows + cols))
+    return rng.uniform(-a, a, size=(rows, cols)).astype(np.float32)

@@ -1,0 +1,34 @@
+"""CPU: the oracle still reproduces the committed golden fixture."""
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_oracle_reproduces_golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    fresh = mg.build()
+    gold = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
+    assert set(gold.files) == set(fresh)
+    for k in gold.files:
+        a, b = gold[k], fresh[k]
+        if a.dtype.kind in "iu":
+            np.testing.assert_array_equal(a, b, err_msg=k)
+        else:
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7, err_msg=k)
+
+
+def test_golden_edges_have_duplicates_and_isolated_rows():
+    g = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
+    U, I, E, DUP = (int(x) for x in g["meta"][:4])
+    e = g["edges"]
+    assert e.shape == (2, E + DUP)
+    keys = e[0].astype(np.int64) * I + e[1]
+    assert np.unique(keys).size < keys.size            # duplicate pairs present
+    assert (np.bincount(e[1], minlength=I) == 0).sum() >= 8   # isolated items
+    assert (np.bincount(e[0], minlength=U) == 0).sum() >= 8   # isolated users

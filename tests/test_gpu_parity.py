@@ -1,0 +1,484 @@
+"""GPU parity tests: the HIP path (libbbgr.so through the C ABI) against the
+oracle and the committed golden fixture.
+
+Tolerance (BASELINE.md "Parity"; fp32 kernels vs float64 truth): per output
+table, normwise relative error <= 1e-5 AND max-abs error <= 1e-5 * max|ref|.
+Integer/index outputs (CSR, plan, sampler invariants) are exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from bbgr import _lib  # noqa: E402
+from bbgr.graph import BipartiteGraph, Csr  # noqa: E402
+from bbgr.synthetic import synthetic_credibility, synthetic_edges  # noqa: E402
+from oracle import ref_numpy as R  # noqa: E402
+from oracle import ref_torch as T  # noqa: E402
+
+DEV = "cuda"
+TOL = 1e-5
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def assert_parity(got, ref, what, tol=TOL):
+    got = got.detach().double().cpu().numpy() if isinstance(got, torch.Tensor) else got
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    nrm = np.linalg.norm(ref)
+    err = np.linalg.norm(got - ref)
+    assert err <= tol * max(nrm, 1e-30), f"{what}: normwise rel err {err / max(nrm, 1e-30):.3e}"
+    mx = np.abs(ref).max() if ref.size else 0.0
+    assert np.abs(got - ref).max() <= tol * max(mx, 1e-30), f"{what}: max-abs err"
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return dict(np.load(os.path.join(HERE, "golden", "golden_small.npz")))
+
+
+def t(a, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(a)).to(DEV, dtype)
+
+
+# ---------------------------------------------------------------------------
+# CSR build + plan
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dup", [0, 50])
+def test_csr_build_bit_exact(dup):
+    U, I = 500, 300
+    e = synthetic_edges(U - 5, I - 5, 6000, 3, items="zipf", duplicates=dup)
+    c = Csr(e[0], e[1], U, I, DEV)
+    indptr, indices = R.edges_to_user_csr(e, U)
+    np.testing.assert_array_equal(c.indptr.cpu().numpy(), indptr)
+    np.testing.assert_array_equal(c.indices[: c.nnz].cpu().numpy(), indices)
+
+
+def test_csr_empty_and_single():
+    c = Csr(np.zeros(0, np.int32), np.zeros(0, np.int32), 7, 3, DEV)
+    assert c.indptr.cpu().tolist() == [0] * 8
+    c = Csr([6], [2], 7, 3, DEV)
+    assert c.indptr.cpu().tolist() == [0] * 7 + [1] and c.indices[:1].item() == 2
+
+
+def test_plan_chunks_cover_long_rows():
+    e = synthetic_edges(2000, 100, 40000, 5, items="zipf")
+    c = Csr(e[1], e[0], 100, 2000, DEV, long_threshold=64, chunk_edges=128)
+    deg = np.bincount(e[1], minlength=100)
+    chunks = c.chunks[: 4 * c.n_chunks].view(-1, 4).cpu().numpy()
+    covered = np.zeros(100, np.int64)
+    for row, b, en, slot in chunks:
+        covered[row] += en - b
+        assert en - b <= 128
+    np.testing.assert_array_equal(covered[deg > 64], deg[deg > 64])
+    assert (covered[deg <= 64] == 0).all()
+    assert c.n_split == int(((deg > 64) & (deg > 128)).sum())
+
+
+# ---------------------------------------------------------------------------
+# Single fused SpMM vs scipy float64, all weight modes and dims
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("thr", [256, 8])
+def test_spmm_modes(d, mode, thr):
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(d + mode + thr)
+    R_, C_ = 400, 350
+    e = synthetic_edges(C_ - 3, R_ - 3, 9000, 7, items="zipf", duplicates=20)
+    rows, cols = e[1], e[0]                     # item rows (skewed)
+    vals = rng.uniform(0.1, 1.0, rows.size).astype(np.float32)
+    cs = rng.uniform(0.5, 2.0, C_).astype(np.float32)
+    c = Csr(rows, cols, R_, C_, DEV, edge_values=t(vals) if mode == 1 else None,
+            long_threshold=thr, chunk_edges=32)
+    prod = Product(c, c.values if mode == 1 else None, t(cs) if mode == 2 else None, None, {})
+    x = rng.uniform(-1, 1, (C_, d)).astype(np.float32)
+    w = vals if mode == 1 else (cs[cols] if mode == 2 else np.ones(rows.size, np.float32))
+    Tm = R.csr64(rows, cols, w, (R_, C_)) @ x.astype(np.float64)
+    ys = rng.uniform(0.5, 1.5, R_).astype(np.float32)
+    add = rng.normal(size=(R_, d)).astype(np.float32)
+    adds = rng.uniform(0.5, 1.5, R_).astype(np.float32)
+    acc_in = rng.normal(size=(R_, d)).astype(np.float32)
+    accs = rng.uniform(0.5, 1.5, R_).astype(np.float32)
+    y = torch.empty(R_, d, device=DEV)
+    acc = torch.empty(R_, d, device=DEV)
+    spmm(prod, t(x), True, y=y, y_scale=t(ys), y_scale_s=0.75, add=t(add), add_scale=t(adds),
+         add_scale_s=0.5, acc_in=t(acc_in), acc_out=acc, acc_scale=t(accs), acc_scale_s=1.25,
+         gamma=0.25)
+    want_y = 0.75 * ys[:, None] * Tm + 0.5 * adds[:, None] * add
+    want_acc = 0.25 * (acc_in + 1.25 * accs[:, None] * Tm)
+    assert_parity(y, want_y, "y")
+    assert_parity(acc, want_acc, "acc")
+
+
+def test_spmm_deterministic():
+    from bbgr.propagate import Product, spmm
+    e = synthetic_edges(3000, 500, 60000, 9, items="zipf")
+    c = Csr(e[1], e[0], 500, 3000, DEV, long_threshold=32, chunk_edges=64)
+    prod = Product(c, None, None, None, {})
+    x = torch.randn(3000, 64, device=DEV)
+    y1, y2 = torch.empty(500, 64, device=DEV), torch.empty(500, 64, device=DEV)
+    spmm(prod, x, False, y=y1)
+    spmm(prod, x, False, y=y2)
+    assert torch.equal(y1, y2)
+
+
+def test_spmm_unsupported_dim_raises():
+    from bbgr.propagate import Product, spmm
+    c = Csr([0], [0], 1, 1, DEV)
+    with pytest.raises(_lib.BbgrError, match="UNSUPPORTED"):
+        spmm(Product(c, None, None, None, {}), torch.zeros(1, 48, device=DEV), False,
+             y=torch.zeros(1, 48, device=DEV))
+
+
+# ---------------------------------------------------------------------------
+# Drop-in modules vs golden (forward + autograd backward)
+# ---------------------------------------------------------------------------
+def _load(model, g):
+    with torch.no_grad():
+        if hasattr(model, "emb"):
+            model.emb.weight.copy_(t(np.concatenate([g["u0"], g["i0"]])))
+        else:
+            model.user_emb.weight.copy_(t(g["u0"]))
+            model.item_emb.weight.copy_(t(g["i0"]))
+
+
+def test_v2_lightgcn_forward_backward_vs_golden(gold):
+    from bbgr.lightgcn_cu_pop import LightGCN, build_message_passing_mats
+    U, I, E, DUP, D, K, B = (int(x) for x in gold["meta"])
+    M_ui, M_iu = build_message_passing_mats(gold["edges"], U, I, t(gold["cred"]), DEV)
+    assert tuple(M_ui.shape) == (U, I) and tuple(M_iu.shape) == (I, U)
+    m = LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    assert set(m.state_dict()) == {"user_emb.weight", "item_emb.weight"}
+    _load(m, gold)
+    uf, itf = m.get_user_item_emb()
+    assert_parity(uf, gold["gs_uf"], "gs u_final")
+    assert_parity(itf, gold["gs_if"], "gs i_final")
+    ((uf * t(gold["gU"])).sum() + (itf * t(gold["gI"])).sum()).backward()
+    assert_parity(m.user_emb.weight.grad, gold["gs_gu0"], "gs grad u0")
+    assert_parity(m.item_emb.weight.grad, gold["gs_gi0"], "gs grad i0")
+
+
+def test_method_a_forward_vs_golden(gold):
+    from bbgr.lightgcn_cu_pop_long_tail_exposure import LightGCN, build_message_passing_mats
+    U, I, E, DUP, D, K, B = (int(x) for x in gold["meta"])
+    M_ui, M_iu = build_message_passing_mats(gold["edges"], U, I, t(gold["cred"]), DEV)
+    m = LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    _load(m, gold)
+    uf, itf = m.propagate()
+    assert_parity(uf, gold["ma_uf"], "method-A u_final")
+    assert_parity(itf, gold["ma_if"], "method-A i_final")
+
+
+def test_cred_lightgcn_jacobi_vs_golden(gold):
+    from bbgr.lightgcn_cu import CredLightGCN, build_cred_weighted_mats
+    U, I, E, DUP, D, K, B = (int(x) for x in gold["meta"])
+    M_ui, M_iu, deg_i = build_cred_weighted_mats(gold["edges"], U, I, gold["cred"], DEV)
+    assert tuple(M_ui.shape) == (I, U) and tuple(M_iu.shape) == (U, I)
+    np.testing.assert_array_equal(deg_i, np.bincount(gold["edges"][1], minlength=I))
+    m = CredLightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    _load(m, gold)
+    uf, itf = m.final_embeddings()
+    assert_parity(uf, gold["j_uf"], "J u_final")
+    assert_parity(itf, gold["j_if"], "J i_final")
+    ((uf * t(gold["gU"])).sum() + (itf * t(gold["gI"])).sum()).backward()
+    assert_parity(m.user_emb.weight.grad, gold["j_gu0"], "J grad u0")
+    assert_parity(m.item_emb.weight.grad, gold["j_gi0"], "J grad i0")
+    # unfused per-layer path gives the same means
+    us, is_ = m.propagate_all_layers()
+    assert_parity(torch.stack(us).mean(0), gold["j_uf"], "J per-layer mean u")
+    assert_parity(torch.stack(is_).mean(0), gold["j_if"], "J per-layer mean i")
+
+
+def test_plain_lightgcn_sym_vs_golden(gold):
+    from bbgr.lightgcn import LightGCN, build_norm_adj
+    U, I, E, DUP, D, K, B = (int(x) for x in gold["meta"])
+    A = build_norm_adj(gold["edges"], U, I, DEV)
+    m = LightGCN(U, I, D, K, A).to(DEV)
+    assert set(m.state_dict()) == {"emb.weight"}
+    _load(m, gold)
+    xf = m.propagate()
+    assert_parity(xf, gold["sym_xf"], "sym x_final")
+    (xf * t(np.concatenate([gold["gU"], gold["gI"]]))).sum().backward()
+    assert_parity(m.emb.weight.grad, gold["sym_gx"], "sym grad")
+    uf, itf = m.get_user_item_emb()
+    assert uf.shape == (U, D) and itf.shape == (I, D)
+
+
+def test_torch_sparse_operators_are_accepted(gold):
+    """LightGCN fed the reference's own COO tensors (generic explicit-value path)."""
+    from bbgr.lightgcn import LightGCN as PlainLightGCN
+    from bbgr.lightgcn_cu_pop import LightGCN
+    U, I, E, DUP, D, K, B = (int(x) for x in gold["meta"])
+    M_ui, M_iu = T.gs_operators(gold["edges"], U, I, gold["cred"], device=DEV)
+    m = LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    _load(m, gold)
+    uf, itf = m.propagate()
+    assert_parity(uf, gold["gs_uf"], "coo gs u_final")
+    assert_parity(itf, gold["gs_if"], "coo gs i_final")
+    ((uf * t(gold["gU"])).sum() + (itf * t(gold["gI"])).sum()).backward()
+    assert_parity(m.user_emb.weight.grad, gold["gs_gu0"], "coo gs grad u0")
+    A = T.sym_operator(gold["edges"], U, I, device=DEV)
+    pm = PlainLightGCN(U, I, D, K, A).to(DEV)
+    _load(pm, gold)
+    xf = pm.propagate()
+    assert_parity(xf, gold["sym_xf"], "coo sym x_final")
+    (xf * t(np.concatenate([gold["gU"], gold["gI"]]))).sum().backward()
+    assert_parity(pm.emb.weight.grad, gold["sym_gx"], "coo sym grad")
+
+
+def test_operator_to_torch_sparse_matches_reference_values(gold):
+    from bbgr.lightgcn_cu_pop import build_message_passing_mats
+    U, I = int(gold["meta"][0]), int(gold["meta"][1])
+    M_ui, M_iu = build_message_passing_mats(gold["edges"], U, I, t(gold["cred"]), DEV)
+    R_ui, R_iu = R.gs_mats(gold["edges"], U, I, gold["cred"])
+    assert_parity(M_ui.to_torch_sparse().to_dense(), R_ui.toarray(), "M_ui values")
+    assert_parity(M_iu.to_torch_sparse().to_dense(), R_iu.toarray(), "M_iu values")
+    x = np.random.default_rng(0).normal(size=(U, 64)).astype(np.float32)
+    assert_parity(M_iu @ t(x), R_iu @ x.astype(np.float64), "M_iu @ x")
+
+
+# ---------------------------------------------------------------------------
+# BPR, Adam
+# ---------------------------------------------------------------------------
+def test_bpr_loss_and_grads_vs_golden(gold):
+    from bbgr.bpr import bpr_loss
+    uf = t(gold["gs_uf"]).requires_grad_()
+    itf = t(gold["gs_if"]).requires_grad_()
+    ue = t(gold["u0"]).requires_grad_()
+    ie = t(gold["i0"]).requires_grad_()
+    loss = bpr_loss(t(gold["users"], torch.int64), t(gold["pos"], torch.int64),
+                    t(gold["neg"], torch.int64), uf, itf, ue, ie, 1e-4, pop=t(gold["pop"]),
+                    lambda_fair=0.05)
+    assert abs(float(loss) - float(gold["bpr_loss"])) <= TOL * abs(float(gold["bpr_loss"]))
+    loss.backward()
+    assert_parity(uf.grad, gold["bpr_g_uf"], "bpr g_uf")
+    assert_parity(itf.grad, gold["bpr_g_if"], "bpr g_if")
+    assert_parity(ue.grad, gold["bpr_g_ue"], "bpr g_ue")
+    assert_parity(ie.grad, gold["bpr_g_ie"], "bpr g_ie")
+
+
+def test_bpr_ln2_at_zero_embeddings():
+    from bbgr.bpr import bpr_loss_value
+    z = torch.zeros(10, 64, device=DEV)
+    idx = torch.arange(8, device=DEV)
+    loss = bpr_loss_value(idx, idx, idx + 1, z, z, z, z, 1e-4)
+    assert abs(float(loss) - np.log(2.0)) < 1e-6
+
+
+def test_fused_adam_vs_golden_and_torch(gold):
+    from bbgr.optim import FusedAdam, adam_step
+    p = t(gold["u0"]).clone()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    adam_step(p, t(gold["gU"]), m, v, 1, 1e-3)
+    assert_parity(p, gold["adam_p1"], "adam step 1", tol=1e-6)
+    a = torch.nn.Parameter(t(gold["u0"]).clone())
+    b = torch.nn.Parameter(t(gold["u0"]).clone())
+    oa, ob = FusedAdam([a], lr=1e-3), torch.optim.Adam([b], lr=1e-3)
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        g = t(rng.normal(size=a.shape))
+        a.grad, b.grad = g.clone(), g.clone()
+        oa.step()
+        ob.step()
+    assert_parity(a.detach(), b.detach().double().cpu().numpy(), "FusedAdam vs torch Adam",
+                  tol=1e-6)
+
+
+# ---------------------------------------------------------------------------
+# Samplers
+# ---------------------------------------------------------------------------
+def _graph(U=2000, I=800, E=30000, seed=3):
+    e = synthetic_edges(U, I, E, seed, items="zipf")
+    return e, BipartiteGraph(e, U, I, DEV)
+
+
+def test_sampler_invariants_and_determinism():
+    from bbgr.sampler import PopMixSampler
+    e, g = _graph()
+    indptr, indices = R.edges_to_user_csr(e, 2000)
+    s = PopMixSampler(g.user_csr, g.item_csr, 800, mix_pop=0.7, gamma=0.75, max_tries=50, seed=42)
+    users = torch.arange(2000, device=DEV)
+    pos, neg = s.sample(users, counter=5)
+    p, n = pos.cpu().numpy(), neg.cpu().numpy()
+    for u in range(2000):
+        assert R.user_has_item(indptr, indices, u, p[u])
+        assert not R.user_has_item(indptr, indices, u, n[u])
+    pos2, neg2 = s.sample(users, counter=5)
+    assert torch.equal(pos, pos2) and torch.equal(neg, neg2)
+    pos3, neg3 = s.sample(users, counter=6)
+    assert not torch.equal(neg, neg3)
+    assert int(s.fail_count.item()) == 0
+
+
+def test_sampler_popularity_distribution_chi2():
+    """mix_pop = 1 and a tiny graph (rejections rare): negatives follow pop_prob."""
+    from bbgr.sampler import PopMixSampler
+    U, I = 4000, 50
+    e = synthetic_edges(U, I, U, 8, items="zipf")        # one edge per user
+    g = BipartiteGraph(e, U, I, DEV)
+    s = PopMixSampler(g.user_csr, g.item_csr, I, mix_pop=1.0, gamma=0.75, max_tries=50, seed=1)
+    counts = np.zeros(I)
+    users = torch.arange(U, device=DEV)
+    for c in range(50):
+        _, neg = s.sample(users, counter=c)
+        counts += np.bincount(neg.cpu().numpy(), minlength=I)
+    pp = R.pop_prob(e, I)
+    # exact expectation with one rejected item per user: renormalise per user
+    indptr, indices = R.edges_to_user_csr(e, U)
+    exp = np.zeros(I)
+    for u in range(U):
+        q = pp.copy()
+        q[indices[indptr[u]:indptr[u + 1]]] = 0
+        exp += q / q.sum()
+    exp *= 50
+    chi2 = ((counts - exp) ** 2 / exp).sum()
+    assert chi2 < 2.0 * I, chi2          # dof = 49; generous bound
+
+
+def test_sampler_full_row_user_flags_failure():
+    from bbgr.sampler import PopMixSampler
+    e = np.array([[0, 0, 0, 1], [0, 1, 2, 0]], np.int32)   # user 0 holds every item
+    g = BipartiteGraph(e, 2, 3, DEV)
+    s = PopMixSampler(g.user_csr, g.item_csr, 3, mix_pop=0.0, gamma=None, max_tries=5)
+    pos, neg = s.sample(torch.tensor([0, 1], device=DEV))
+    assert neg[0].item() == -1 and int(s.fail_count.item()) == 1
+    assert neg[1].item() in (1, 2)
+
+
+def test_shuffle_and_nonempty_rows():
+    from bbgr.sampler import nonempty_rows, shuffle
+    e = np.array([[0, 2, 2, 5], [0, 1, 2, 0]], np.int32)
+    g = BipartiteGraph(e, 7, 3, DEV)
+    assert nonempty_rows(g.user_csr).cpu().tolist() == [0, 2, 5]
+    v = torch.arange(100000, device=DEV)
+    p1 = shuffle(v, 42, 1)
+    assert torch.equal(torch.sort(p1).values, v) and not torch.equal(p1, v)
+    assert torch.equal(p1, shuffle(v, 42, 1)) and not torch.equal(p1, shuffle(v, 42, 2))
+
+
+# ---------------------------------------------------------------------------
+# Fused training step vs the float64 oracle step on identical triples
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair", "method_a"])
+def test_fused_trainer_step_vs_oracle(gold, variant):
+    from bbgr.trainer import FusedTrainer
+    U, I, E, DUP, D, K, B = (int(x) for x in gold["meta"])
+    e, cred = gold["edges"], gold["cred"]
+    g = BipartiteGraph(e, U, I, DEV)
+    lam = 0.05 if variant == "cu_fair" else 0.0
+    tr = FusedTrainer(g, variant, cred=cred, emb_dim=D, num_layers=K, batch_size=B,
+                      lambda_fair=lam, u0=gold["u0"], i0=gold["i0"])
+    deg_u = np.bincount(e[0], minlength=U)
+    uu = np.unique(gold["users"])
+    users = t(uu[deg_u[uu] > 0], torch.int64)       # train users have >= 1 positive
+    loss = tr.step(users)
+    pos, neg = tr.pos[: users.numel()].cpu().numpy(), tr.neg[: users.numel()].cpu().numpy()
+    uu = users.cpu().numpy()
+    # oracle step on the same triples
+    if variant == "cu_fair":
+        A, Bm, deg_i = R.j_mats(e, U, I, cred)
+        uf, itf, _, _ = R.propagate_j(A, Bm, gold["u0"], gold["i0"], K)
+        pop = deg_i / max(deg_i.max(), 1.0)
+    else:
+        A, Bm = R.gs_mats(e, U, I, cred, method_a=(variant == "method_a"))
+        uf, itf, _, _ = R.propagate_gs(A, Bm, gold["u0"], gold["i0"], K)
+        pop = None
+    want_loss, gr = R.bpr_loss(uf, itf, gold["u0"], gold["i0"], uu, pos, neg, 1e-4, pop, lam)
+    if variant == "cu_fair":
+        gu0, gi0 = R.backward_j(A, Bm, gr["g_uf"], gr["g_if"], K)
+    else:
+        gu0, gi0 = R.backward_gs(A, Bm, gr["g_uf"], gr["g_if"], K)
+    gu0, gi0 = gu0 + gr["g_ue"], gi0 + gr["g_ie"]
+    assert abs(float(loss) - want_loss) <= TOL * want_loss
+    z = np.zeros_like
+    pu, _, _ = R.adam_step(gold["u0"], gu0, z(gu0), z(gu0), 1)
+    pi, _, _ = R.adam_step(gold["i0"], gi0, z(gi0), z(gi0), 1)
+    # Adam's first step moves each weight by ~lr*sign(g): compare the update itself
+    assert_parity(tr.user_w - t(gold["u0"]), pu - gold["u0"], "user update", tol=1e-3)
+    assert_parity(tr.item_w - t(gold["i0"]), pi - gold["i0"], "item update", tol=1e-3)
+    assert tr.g_uf.abs().sum().item() == 0 and tr.g_if.abs().sum().item() == 0
+
+
+def test_dropin_training_step_matches_reference_torch_step(gold):
+    """One step of the drop-in module + torch Adam == the fp32 torch restatement."""
+    from bbgr.lightgcn_cu_pop import LightGCN, build_message_passing_mats
+    U, I, E, DUP, D, K, B = (int(x) for x in gold["meta"])
+    e, cred = gold["edges"], gold["cred"]
+    users = torch.as_tensor(np.unique(gold["users"]))
+    pos = torch.as_tensor(gold["pos"][: users.numel()])
+    neg = torch.as_tensor(gold["neg"][: users.numel()])
+    M_ui, M_iu = build_message_passing_mats(e, U, I, t(cred), DEV)
+    m = LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    _load(m, gold)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    ue, ie = m.get_user_item_emb()
+    loss = m.bpr_loss(users.to(DEV), pos.to(DEV), neg.to(DEV), ue, ie, 1e-4)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    Tui, Tiu = T.gs_operators(e, U, I, cred)
+    ref = T.GSModel(U, I, D, K, Tui, Tiu, gold["u0"], gold["i0"])
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    rloss = T.train_step(ref, ropt, users, pos, neg, 1e-4)
+    assert abs(float(loss) - rloss) <= 1e-5 * rloss
+    du = (m.user_emb.weight.detach().cpu() - torch.as_tensor(gold["u0"])).double().numpy()
+    rdu = (ref.user_emb.weight.detach() - torch.as_tensor(gold["u0"])).double().numpy()
+    assert_parity(du, rdu, "drop-in user update vs torch step", tol=1e-3)
+
+
+# ---------------------------------------------------------------------------
+# Larger sizes: C2 parity, size-independent properties
+# ---------------------------------------------------------------------------
+def test_c2_forward_parity_and_adjoint():
+    from bbgr.synthetic import CONFIGS, config_edges
+    from bbgr.propagate import ORDER_GS, OperatorPair, backward, forward
+    c = CONFIGS["C2"]
+    U, I, d, K = c["num_users"], c["num_items"], c["emb_dim"], c["num_layers"]
+    e = config_edges("C2")
+    cred = synthetic_credibility(U, 2)
+    g = BipartiteGraph(e, U, I, DEV)
+    pair = OperatorPair.factored(g, g.scales(_lib.OP_GS, t(cred)))
+    rng = np.random.default_rng(2)
+    u0 = rng.uniform(-1, 1, (U, d)).astype(np.float32)
+    i0 = rng.uniform(-1, 1, (I, d)).astype(np.float32)
+    uf, itf = forward(pair, t(u0), t(i0), K, ORDER_GS)
+    M_ui, M_iu = R.gs_mats(e, U, I, cred)
+    ruf, ritf, _, _ = R.propagate_gs(M_ui, M_iu, u0, i0, K)
+    assert_parity(uf, ruf, "C2 u_final")
+    assert_parity(itf, ritf, "C2 i_final")
+    gU = rng.normal(size=(U, d)).astype(np.float32)
+    gI = rng.normal(size=(I, d)).astype(np.float32)
+    gu0, gi0 = backward(pair, t(gU), t(gI), K, ORDER_GS)
+    lhs = (uf.double() * t(gU).double()).sum() + (itf.double() * t(gI).double()).sum()
+    rhs = (t(u0).double() * gu0.double()).sum() + (t(i0).double() * gi0.double()).sum()
+    assert abs(float(lhs - rhs)) <= 1e-5 * abs(float(lhs))
+
+
+@pytest.mark.slow
+def test_c4_size_adjoint_and_linearity():
+    """Full BASELINE C4 size: <F(x), g> == <x, F^T(g)> and F(2x) == 2 F(x)."""
+    from bbgr.synthetic import CONFIGS, config_edges
+    from bbgr.propagate import ORDER_GS, OperatorPair, backward, forward
+    c = CONFIGS["C4"]
+    U, I, d, K = c["num_users"], c["num_items"], c["emb_dim"], c["num_layers"]
+    e = config_edges("C4")
+    g = BipartiteGraph(e, U, I, DEV)
+    del e
+    pair = OperatorPair.factored(g, g.scales(_lib.OP_GS, None))
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    u0 = torch.rand(U, d, device=DEV, generator=gen) * 2 - 1
+    i0 = torch.rand(I, d, device=DEV, generator=gen) * 2 - 1
+    uf, itf = forward(pair, u0, i0, K, ORDER_GS)
+    uf2, itf2 = forward(pair, 2 * u0, 2 * i0, K, ORDER_GS)
+    assert torch.equal(uf2, 2 * uf) and torch.equal(itf2, 2 * itf)   # exact: power-of-2 scale
+    gU = torch.randn(U, d, device=DEV, generator=gen)
+    gI = torch.randn(I, d, device=DEV, generator=gen)
+    gu0, gi0 = backward(pair, gU, gI, K, ORDER_GS)
+    lhs = (uf.double() * gU.double()).sum() + (itf.double() * gI.double()).sum()
+    rhs = (u0.double() * gu0.double()).sum() + (i0.double() * gi0.double()).sum()
+    assert abs(float(lhs - rhs)) <= 1e-5 * float(
+        (uf.double().abs() * gU.double().abs()).sum() + (itf.double().abs() * gI.double().abs()).sum())

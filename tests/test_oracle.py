@@ -1,0 +1,221 @@
+"""CPU tests of the oracle (the checker): hand-derived known answers, the two
+independent restatements against each other, and algebraic properties.
+
+The reference ships no tests or fixtures and importing it was
+refused, so the known answers below are derived by hand from the
+reference source lines cited in oracle/ref_numpy.py.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_numpy as R
+from oracle import ref_torch as T
+
+S2 = 1.0 / math.sqrt(2.0)
+
+
+def test_kat_gs_operator_and_one_layer():
+    # U=2, I=2, edges (0,0),(0,1),(1,1): deg_u=[2,1], deg_i=[1,2]
+    e = np.array([[0, 0, 1], [0, 1, 1]], np.int32)
+    cred = np.array([1.0, 0.5], np.float32)
+    M_ui, M_iu = R.gs_mats(e, 2, 2, cred)
+    np.testing.assert_allclose(M_ui.toarray(), [[S2, 0.5], [0.0, S2]], rtol=1e-7)
+    np.testing.assert_allclose(M_iu.toarray(), [[S2, 0.0], [0.5, 0.5 * S2]], rtol=1e-7)
+    u0, i0 = np.array([[1.0], [2.0]]), np.array([[3.0], [4.0]])
+    uf, itf, us, is_ = R.propagate_gs(M_ui, M_iu, u0, i0, 1)
+    i1 = np.array([S2, 0.5 + S2])
+    u1 = np.array([S2 * S2 + 0.5 * (0.5 + S2), S2 * (0.5 + S2)])
+    np.testing.assert_allclose(is_[1].ravel(), i1, rtol=1e-7)
+    np.testing.assert_allclose(us[1].ravel(), u1, rtol=1e-7)   # GS: u1 uses the NEW i1
+    np.testing.assert_allclose(uf.ravel(), (np.array([1.0, 2.0]) + u1) / 2, rtol=1e-7)
+    np.testing.assert_allclose(itf.ravel(), (np.array([3.0, 4.0]) + i1) / 2, rtol=1e-7)
+
+
+def test_kat_jacobi_uses_old_item_table():
+    e = np.array([[0, 0, 1], [0, 1, 1]], np.int32)
+    cred = np.array([1.0, 0.5], np.float32)
+    M_item_from_user, M_user_from_item, deg_i = R.j_mats(e, 2, 2, cred)
+    np.testing.assert_allclose(deg_i, [1.0, 2.0])
+    # Eq 3.23: c_u / sqrt(deg_u deg_i); Eq 3.24: 1/sqrt(deg_u deg_i)
+    np.testing.assert_allclose(M_item_from_user.toarray(), [[S2, 0.0], [0.5, 0.5 * S2]],
+                               rtol=1e-7)
+    np.testing.assert_allclose(M_user_from_item.toarray(), [[S2, 0.5], [0.0, S2]], rtol=1e-7)
+    u0, i0 = np.array([[1.0], [2.0]]), np.array([[3.0], [4.0]])
+    uf, itf, us, is_ = R.propagate_j(M_item_from_user, M_user_from_item, u0, i0, 1)
+    np.testing.assert_allclose(us[1].ravel(), [3 * S2 + 2.0, 4 * S2], rtol=1e-7)  # from i0
+
+
+def test_kat_duplicate_edge_is_summed():
+    # (0,0) twice + (1,0): deg_u = [2,1], deg_i = [3] (bincount counts the repeat);
+    # coalesce sums -> M_ui[0,0] = 2 * (1/sqrt2 * 1/sqrt3), M_ui[1,0] = 1/sqrt3
+    e = np.array([[0, 0, 1], [0, 0, 0]], np.int32)
+    want = [[2.0 / math.sqrt(6.0)], [1.0 / math.sqrt(3.0)]]
+    M_ui, M_iu = R.gs_mats(e, 2, 1)
+    np.testing.assert_allclose(M_ui.toarray(), want, rtol=1e-7)
+    Mt_ui, Mt_iu = T.gs_operators(e, 2, 1)
+    np.testing.assert_allclose(Mt_ui.to_dense().numpy(), want, rtol=1e-6)
+
+
+def test_kat_isolated_item_keeps_only_layer0():
+    e = np.array([[0], [1]], np.int32)  # U=1, I=3; items 0 and 2 isolated
+    M_ui, M_iu = R.gs_mats(e, 1, 3)
+    u0, i0 = np.array([[1.0]]), np.array([[5.0], [6.0], [7.0]])
+    uf, itf, _, _ = R.propagate_gs(M_ui, M_iu, u0, i0, 3)
+    assert itf[0, 0] == pytest.approx(5.0 / 4) and itf[2, 0] == pytest.approx(7.0 / 4)
+
+
+def test_kat_symmetric_two_nodes():
+    e = np.array([[0], [0]], np.int32)  # N=2, A = [[0,1],[1,0]], deg = 1
+    A = R.sym_values(e, 1, 1)
+    np.testing.assert_allclose(A.toarray(), [[0, 1], [1, 0]])
+    xf, _ = R.propagate_sym(A, np.array([[1.0], [2.0]]), 2)
+    np.testing.assert_allclose(xf.ravel(), [4 / 3, 5 / 3], rtol=1e-12)
+    At = T.sym_operator(e, 1, 1)
+    np.testing.assert_allclose(At.to_dense().numpy(), [[0, 1], [1, 0]])
+
+
+def test_kat_sym_isolated_node_inf_to_zero():
+    e = np.array([[0], [0]], np.int32)  # U=2: user 1 isolated -> deg^-1/2 = inf -> 0
+    A = R.sym_values(e, 2, 1)
+    assert A.shape == (3, 3) and A[1].nnz == 0
+
+
+def test_kat_method_a_alpha():
+    e = np.array([[0, 1, 2], [0, 0, 1]], np.int32)  # deg_i = [2, 1]
+    u, i, w_ui, w_iu = R.gs_values(e, 3, 2, None, method_a=True)
+    alpha0 = 1.0 / math.log1p(2.0)
+    alpha1 = 1.0 / math.log1p(1.0)
+    np.testing.assert_allclose(w_ui, [S2 * alpha0, S2 * alpha0, 1.0 * alpha1], rtol=1e-6)
+
+
+def test_kat_ln2_loss_at_zero_embeddings():
+    B, d = 8, 4
+    z_u, z_i = np.zeros((3, d)), np.zeros((5, d))
+    users = np.arange(B) % 3
+    pos, neg = np.arange(B) % 5, (np.arange(B) + 1) % 5
+    loss, _ = R.bpr_loss(z_u, z_i, z_u, z_i, users, pos, neg, reg=1e-4)
+    assert loss == pytest.approx(math.log(2.0), abs=1e-11)
+
+
+def _random_case(seed=0, U=60, I=40, E=400, d=8, dup=10):
+    from bbgr.synthetic import synthetic_edges
+    e = synthetic_edges(U, I, E, seed, items="zipf", duplicates=dup)
+    rng = np.random.default_rng(seed)
+    cred = rng.uniform(0, 1, U).astype(np.float32)
+    u0 = rng.uniform(-1, 1, (U, d)).astype(np.float32)
+    i0 = rng.uniform(-1, 1, (I, d)).astype(np.float32)
+    return e, cred, u0, i0
+
+
+def nrel(a, b):
+    return np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("method_a", [False, True])
+def test_numpy_vs_torch_gs(method_a):
+    e, cred, u0, i0 = _random_case(1)
+    M_ui, M_iu = R.gs_mats(e, 60, 40, cred, method_a)
+    uf, itf, _, _ = R.propagate_gs(M_ui, M_iu, u0, i0, 3)
+    Tui, Tiu = T.gs_operators(e, 60, 40, cred, method_a)
+    tuf, titf = T.propagate_gs(Tui, Tiu, torch.tensor(u0), torch.tensor(i0), 3)
+    assert nrel(tuf.numpy(), uf) < 1e-6 and nrel(titf.numpy(), itf) < 1e-6
+
+
+def test_numpy_vs_torch_jacobi_and_sym():
+    e, cred, u0, i0 = _random_case(2)
+    A, B_, _ = R.j_mats(e, 60, 40, cred)
+    uf, itf, _, _ = R.propagate_j(A, B_, u0, i0, 3)
+    TA, TB = T.j_operators(e, 60, 40, cred)
+    tuf, titf = T.propagate_j(TA, TB, torch.tensor(u0), torch.tensor(i0), 3)
+    assert nrel(tuf.numpy(), uf) < 1e-6 and nrel(titf.numpy(), itf) < 1e-6
+    S = R.sym_values(e, 60, 40)
+    x0 = np.concatenate([u0, i0])
+    xf, _ = R.propagate_sym(S, x0, 3)
+    txf = T.propagate_sym(T.sym_operator(e, 60, 40), torch.tensor(x0), 3)
+    assert nrel(txf.numpy(), xf) < 1e-6
+
+
+def test_backward_gs_matches_torch_autograd():
+    e, cred, u0, i0 = _random_case(3)
+    M_ui, M_iu = R.gs_mats(e, 60, 40, cred)
+    rng = np.random.default_rng(5)
+    gU, gI = rng.normal(size=u0.shape), rng.normal(size=i0.shape)
+    gu0, gi0 = R.backward_gs(M_ui, M_iu, gU, gI, 3)
+    Tui, Tiu = T.gs_operators(e, 60, 40, cred)
+    tu = torch.tensor(u0, dtype=torch.float64, requires_grad=True)
+    ti = torch.tensor(i0, dtype=torch.float64, requires_grad=True)
+    tuf, titf = T.propagate_gs(Tui.double(), Tiu.double(), tu, ti, 3)
+    ((tuf * torch.tensor(gU)).sum() + (titf * torch.tensor(gI)).sum()).backward()
+    assert nrel(tu.grad.numpy(), gu0) < 1e-12 and nrel(ti.grad.numpy(), gi0) < 1e-12
+
+
+def test_backward_jacobi_and_sym_adjoint():
+    e, cred, u0, i0 = _random_case(4)
+    A, B_, _ = R.j_mats(e, 60, 40, cred)
+    rng = np.random.default_rng(6)
+    gU, gI = rng.normal(size=u0.shape), rng.normal(size=i0.shape)
+    gu0, gi0 = R.backward_j(A, B_, gU, gI, 3)
+    uf, itf, _, _ = R.propagate_j(A, B_, u0, i0, 3)
+    # propagation is linear: <final, g> == <x0, grad_x0>
+    lhs = (uf * gU).sum() + (itf * gI).sum()
+    rhs = (u0 * gu0).sum() + (i0 * gi0).sum()
+    assert lhs == pytest.approx(rhs, rel=1e-10)
+    S = R.sym_values(e, 60, 40)
+    x0 = np.concatenate([u0, i0]).astype(np.float64)
+    g = rng.normal(size=x0.shape)
+    xf, _ = R.propagate_sym(S, x0, 3)
+    assert (xf * g).sum() == pytest.approx((x0 * R.backward_sym(S, g, 3)).sum(), rel=1e-10)
+
+
+def test_bpr_grads_match_torch_autograd():
+    rng = np.random.default_rng(7)
+    U, I, d, B = 30, 20, 8, 64
+    uf, itf, ue, ie = (rng.normal(size=s) for s in ((U, d), (I, d), (U, d), (I, d)))
+    users, pos, neg = rng.integers(0, U, B), rng.integers(0, I, B), rng.integers(0, I, B)
+    pop = rng.uniform(0, 1, I)
+    loss, g = R.bpr_loss(uf, itf, ue, ie, users, pos, neg, 1e-2, pop, 0.3)
+    t = [torch.tensor(a, requires_grad=True) for a in (uf, itf, ue, ie)]
+    tl = T.bpr(*t, torch.tensor(users), torch.tensor(pos), torch.tensor(neg), 1e-2,
+               torch.tensor(pop), 0.3)
+    tl.backward()
+    assert float(tl.detach()) == pytest.approx(loss, rel=1e-12)
+    for k, tt in zip(("g_uf", "g_if", "g_ue", "g_ie"), t):
+        assert nrel(tt.grad.numpy(), g[k]) < 1e-10
+
+
+def test_adam_matches_torch():
+    rng = np.random.default_rng(8)
+    p0 = rng.normal(size=(16, 4))
+    tp = torch.nn.Parameter(torch.tensor(p0))
+    opt = torch.optim.Adam([tp], lr=1e-3)
+    p, m, v = p0.copy(), np.zeros_like(p0), np.zeros_like(p0)
+    for step in range(1, 4):
+        g = rng.normal(size=p0.shape)
+        tp.grad = torch.tensor(g)
+        opt.step()
+        p, m, v = R.adam_step(p, g, m, v, step)
+    assert nrel(tp.detach().numpy(), p) < 1e-12
+
+
+def test_reference_style_sampler_never_returns_positive():
+    e, _, _, _ = _random_case(9, U=50, I=30, E=600, dup=0)
+    indptr, indices = R.edges_to_user_csr(e, 50)
+    pp = R.pop_prob(e, 30)
+    assert pp.sum() == pytest.approx(1.0, abs=1e-9)
+    rng = np.random.default_rng(42)
+    # the reference loops forever for a user holding every item; skip those
+    users = np.flatnonzero(np.diff(indptr) < 30)
+    used, pos, neg = R.sample_batch_reference_style(indptr, indices, users, 30, rng, pp)
+    for u, p, n in zip(used, pos, neg):
+        assert R.user_has_item(indptr, indices, u, p)
+        assert not R.user_has_item(indptr, indices, u, n)
+
+
+def test_edges_to_user_csr_sorted_rows():
+    e = np.array([[2, 0, 2, 1, 0], [3, 1, 0, 2, 0]], np.int32)
+    indptr, indices = R.edges_to_user_csr(e, 4)
+    assert indptr.tolist() == [0, 2, 3, 5, 5]
+    assert indices.tolist() == [0, 1, 2, 0, 3]
