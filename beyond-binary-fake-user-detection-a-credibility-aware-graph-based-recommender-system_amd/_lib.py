@@ -109,6 +109,7 @@ _SIGNATURES = {
     "bbgr_operator_scales": ([c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P], c_int32),
     "bbgr_spmm": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(SpmmArgs), _P], c_int32),
+    "bbgr_epilogue": ([c_int32, _P, c_int64, ctypes.POINTER(SpmmArgs), _P], c_int32),
     "bbgr_bpr": ([ctypes.POINTER(BprArgs), _P], c_int32),
     "bbgr_bpr_reduce": ([c_int64, _P, c_float, c_float, _P, _P], c_int32),
     "bbgr_adam": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,

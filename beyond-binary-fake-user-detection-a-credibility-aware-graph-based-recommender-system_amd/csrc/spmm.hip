@@ -236,6 +236,20 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(SpmmParams P) {
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float *t,
+                                                       long ldt) {
+  constexpr int V = D / 64;
+  const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  if (row >= P.n_rows) return;
+  const float4 *src = reinterpret_cast<const float4 *>(t + row * ldt) + lane;
+  float4 T[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) T[k] = src[16 * k];
+  epilogue<D>(P, (int)row, lane, T);
+}
+
 template <int D, int WMODE>
 static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
   const long short_blocks = ((long)P.n_rows + 15) / 16;
@@ -272,6 +286,50 @@ static bool ld_ok(const float *p, long ld, int d) {
 }  // namespace bbgr
 
 using namespace bbgr;
+
+static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
+  P.y = a->y;
+  P.ldy = a->ldy;
+  P.y_scale = a->y_scale;
+  P.y_scale_s = a->y_scale_s;
+  P.add = a->add;
+  P.ldadd = a->ldadd;
+  P.add_scale = a->add_scale;
+  P.add_scale_s = a->add_scale_s;
+  P.acc_in = a->acc_in;
+  P.ldacc_in = a->ldacc_in;
+  P.acc_out = a->acc_out;
+  P.ldacc_out = a->ldacc_out;
+  P.acc_scale = a->acc_scale;
+  P.acc_scale_s = a->acc_scale_s;
+  P.gamma = a->gamma;
+}
+
+extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
+                             const bbgr_spmm_args *a, bbgr_stream_t stream) {
+  BBGR_REQUIRE(a && n_rows >= 0, "bbgr_epilogue: bad args");
+  const int d = a->d;
+  if (d != 64 && d != 128 && d != 256) {
+    set_error("bbgr_epilogue: embedding dim %d unsupported (64, 128, 256)", d);
+    return BBGR_ERR_UNSUPPORTED;
+  }
+  if (n_rows == 0) return BBGR_OK;
+  BBGR_REQUIRE(t && ld_ok(t, ldt, d) && ld_ok(a->y, a->ldy, d) && ld_ok(a->add, a->ldadd, d) &&
+                   ld_ok(a->acc_in, a->ldacc_in, d) && ld_ok(a->acc_out, a->ldacc_out, d),
+               "bbgr_epilogue: tables must be 16-byte aligned with ld >= d, ld % 4 == 0");
+  SpmmParams P = {};
+  P.n_rows = n_rows;
+  fill_epilogue(P, a);
+  const unsigned grid = (unsigned)(((long)n_rows + 15) / 16);
+  hipStream_t st = as_stream(stream);
+  switch (d) {
+    case 64: hipLaunchKernelGGL(epilogue_kernel<64>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
+    case 128: hipLaunchKernelGGL(epilogue_kernel<128>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
+    default: hipLaunchKernelGGL(epilogue_kernel<256>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
+  }
+  BBGR_LAUNCHED("epilogue_kernel");
+  return BBGR_OK;
+}
 
 extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
                          bbgr_stream_t stream) {
@@ -311,21 +369,7 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   P.edge_val = a->edge_val;
   P.col_scale = a->col_scale;
   P.col_scale_s = a->col_scale_s;
-  P.y = a->y;
-  P.ldy = a->ldy;
-  P.y_scale = a->y_scale;
-  P.y_scale_s = a->y_scale_s;
-  P.add = a->add;
-  P.ldadd = a->ldadd;
-  P.add_scale = a->add_scale;
-  P.add_scale_s = a->add_scale_s;
-  P.acc_in = a->acc_in;
-  P.ldacc_in = a->ldacc_in;
-  P.acc_out = a->acc_out;
-  P.ldacc_out = a->ldacc_out;
-  P.acc_scale = a->acc_scale;
-  P.acc_scale_s = a->acc_scale_s;
-  P.gamma = a->gamma;
+  fill_epilogue(P, a);
   P.partial = a->partial;
   hipStream_t st = as_stream(stream);
   switch (d) {

@@ -160,6 +160,36 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d, ev0, ev1))
 
 
+def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,
+             add_scale=None, add_scale_s: float = 1.0, acc_in=None, acc_out=None,
+             acc_scale=None, acc_scale_s: float = 1.0, gamma: float = 1.0) -> None:
+    """bbgr_epilogue: the SpMM epilogue applied to a dense table of row sums."""
+    a = _lib.SpmmArgs()
+    a.d = t.shape[1]
+    a.y, a.ldy = ptr(y), ld(y)
+    a.y_scale, a.y_scale_s = ptr(y_scale), y_scale_s
+    a.add, a.ldadd = ptr(add), ld(add)
+    a.add_scale, a.add_scale_s = ptr(add_scale), add_scale_s
+    a.acc_in, a.ldacc_in = ptr(acc_in), ld(acc_in)
+    a.acc_out, a.ldacc_out = ptr(acc_out), ld(acc_out)
+    a.acc_scale, a.acc_scale_s = ptr(acc_scale), acc_scale_s
+    a.gamma = gamma
+    call("bbgr_epilogue", t.shape[0], ptr(t), ld(t), ctypes.byref(a), stream_handle())
+
+
+def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw) -> None:
+    """Item-row product. With a `reduce` hook (user-row sharding), the SpMM writes
+    this rank's raw partial row sums, `reduce` sums them over ranks in place
+    (RCCL all-reduce), and the epilogue runs on the complete sums."""
+    if reduce is None:
+        spmm(prod, x, first, **kw)
+        return
+    t = new("partial", prod.csr.n_rows)
+    spmm(prod, x, first, y=t)
+    reduce(t)
+    epilogue(t, **kw)
+
+
 def _check_table(name, t, rows, d=None):
     if t.dtype != torch.float32:
         raise TypeError(f"{name} must be float32, got {t.dtype}")
@@ -186,8 +216,9 @@ def _buffers(ws: dict | None, device, d: int):
 
 def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
             order: str = ORDER_GS, out_u: torch.Tensor | None = None,
-            out_i: torch.Tensor | None = None, ws: dict | None = None):
-    """Final (layer-mean) user and item tables. u0 [U,d], i0 [I,d] fp32."""
+            out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None):
+    """Final (layer-mean) user and item tables. u0 [U,d], i0 [I,d] fp32.
+    `reduce(t)`: in-place sum over ranks of item-row partial sums (sharded mode)."""
     U, I = pair.num_users, pair.num_items
     d = u0.shape[1]
     _check_table("user table", u0, U, d)
@@ -206,9 +237,9 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(1, K + 1):
             g = gl if k == K else 1.0
-            spmm(FI, u0 if k == 1 else bufU, k == 1, y=bufI, y_scale=pair.feed_fwd_iu,
-                 acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
-                 acc_scale=FI.out_scale, gamma=g)
+            _item_product(FI, u0 if k == 1 else bufU, k == 1, reduce, new, y=bufI,
+                          y_scale=pair.feed_fwd_iu, acc_in=i0 if k == 1 else acc_i,
+                          acc_out=acc_i, acc_scale=FI.out_scale, gamma=g)
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
                  acc_scale=FU.out_scale, gamma=g)
@@ -218,10 +249,10 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
         for k in range(1, K + 1):
             g = gl if k == K else 1.0
             nxt = 1 - cur
-            spmm(FI, u0 if k == 1 else bufU[cur], k == 1,
-                 y=bufI[nxt] if k < K else None, y_scale=pair.feed_fwd_iu,
-                 acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
-                 acc_scale=FI.out_scale, gamma=g)
+            _item_product(FI, u0 if k == 1 else bufU[cur], k == 1, reduce, new,
+                          y=bufI[nxt] if k < K else None, y_scale=pair.feed_fwd_iu,
+                          acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
+                          acc_scale=FI.out_scale, gamma=g)
             spmm(FU, i0 if k == 1 else bufI[cur], k == 1,
                  y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
@@ -235,7 +266,7 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
 def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
              order: str = ORDER_GS, out_u: torch.Tensor | None = None,
              out_i: torch.Tensor | None = None, ws: dict | None = None,
-             grad_i0_dense: bool = True):
+             grad_i0_dense: bool = True, reduce=None):
     """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final)."""
     U, I = pair.num_users, pair.num_items
     d = gU.shape[1]
@@ -255,9 +286,9 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(K, 0, -1):
             first = k == K
-            spmm(BI, gU if first else bufU, first, y=bufI, y_scale=pair.feed_bwd_iu,
-                 y_scale_s=gl if first else 1.0,
-                 add=gI, add_scale=BU.in_scale, add_scale_s=gl)
+            _item_product(BI, gU if first else bufU, first, reduce, new, y=bufI,
+                          y_scale=pair.feed_bwd_iu, y_scale_s=gl if first else 1.0,
+                          add=gI, add_scale=BU.in_scale, add_scale_s=gl)
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
                      add=gU, add_scale=BI.in_scale, add_scale_s=gl)
@@ -278,13 +309,14 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
             if k > 1:
                 spmm(BU, xu, first, y=bufU[nxt], y_scale=pair.feed_bwd_ui, y_scale_s=ys,
                      add=gU, add_scale=BI.in_scale, add_scale_s=gl)
-                spmm(BI, xi, first, y=bufI[nxt], y_scale=pair.feed_bwd_iu, y_scale_s=ys,
-                     add=gI, add_scale=BU.in_scale, add_scale_s=gl)
+                _item_product(BI, xi, first, reduce, new, y=bufI[nxt],
+                              y_scale=pair.feed_bwd_iu, y_scale_s=ys,
+                              add=gI, add_scale=BU.in_scale, add_scale_s=gl)
             else:
                 spmm(BU, xu, first, y=gu0, y_scale=BU.out_scale, y_scale_s=ys,
                      add=gU, add_scale=None, add_scale_s=gl)
-                spmm(BI, xi, first, y=gi0, y_scale=BI.out_scale, y_scale_s=ys,
-                     add=gI, add_scale=None, add_scale_s=gl)
+                _item_product(BI, xi, first, reduce, new, y=gi0, y_scale=BI.out_scale,
+                              y_scale_s=ys, add=gI, add_scale=None, add_scale_s=gl)
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")

@@ -122,10 +122,15 @@ class FusedTrainer:
              ptr(self.loss), st)
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  out_i=self.g_i0, ws=self.ws)
-        # ego L2 term goes straight to the weight grads (Version-2:503-507)
-        a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
-                     g_ue=self.g_u0, g_ie=self.g_i0)
-        call("bbgr_bpr", ctypes.byref(a), st)
+        # ego L2 term goes straight to the weight grads (Version-2:503-507):
+        # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
+        alpha = 2.0 * self.reg / B
+        call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
+             ptr(self.g_u0), ld(self.g_u0), self.d, st)
+        call("bbgr_rows_axpy", B, ptr(pos), alpha, ptr(self.item_w), ld(self.item_w),
+             ptr(self.g_i0), ld(self.g_i0), self.d, st)
+        call("bbgr_rows_axpy", B, ptr(neg), alpha, ptr(self.item_w), ld(self.item_w),
+             ptr(self.g_i0), ld(self.g_i0), self.d, st)
         self.step_count += 1
         adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
         adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)

@@ -182,6 +182,13 @@ typedef struct {
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
               bbgr_stream_t stream);
 
+/* The SpMM epilogue alone, with T read from a dense table t[n_rows, ldt]
+ * (args->x / weight fields ignored). Used after the RCCL all-reduce of
+ * per-rank item partial sums in the user-row-sharded multi-GPU step, where
+ * the epilogue cannot run before the sum is complete. */
+int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
+                  const bbgr_spmm_args *args, bbgr_stream_t stream);
+
 /* ------------------------------------------------------------------------- */
 /* Fused BPR loss: gather -> dot -> log-sigmoid -> (+reg, +fair) -> grads     */
 /*   Replaces LightGCN.bpr_loss, Version-2/lighgcn_cu_pop.py:495-508          */

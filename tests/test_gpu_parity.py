@@ -253,7 +253,7 @@ def test_bpr_loss_and_grads_vs_golden(gold):
     loss = bpr_loss(t(gold["users"], torch.int64), t(gold["pos"], torch.int64),
                     t(gold["neg"], torch.int64), uf, itf, ue, ie, 1e-4, pop=t(gold["pop"]),
                     lambda_fair=0.05)
-    assert abs(float(loss) - float(gold["bpr_loss"])) <= TOL * abs(float(gold["bpr_loss"]))
+    assert abs(float(loss.detach()) - float(gold["bpr_loss"])) <= TOL * abs(float(gold["bpr_loss"]))
     loss.backward()
     assert_parity(uf.grad, gold["bpr_g_uf"], "bpr g_uf")
     assert_parity(itf.grad, gold["bpr_g_if"], "bpr g_if")
@@ -394,12 +394,18 @@ def test_fused_trainer_step_vs_oracle(gold, variant):
         gu0, gi0 = R.backward_gs(A, Bm, gr["g_uf"], gr["g_if"], K)
     gu0, gi0 = gu0 + gr["g_ue"], gi0 + gr["g_ie"]
     assert abs(float(loss) - want_loss) <= TOL * want_loss
+    # the weight gradients the step fed to Adam: the parity claim (1e-5)
+    assert_parity(tr.g_u0, gu0, "grad u0 (propagated + ego L2)")
+    assert_parity(tr.g_i0, gi0, "grad i0 (propagated + ego L2)")
+    # Adam's first step is ~ -lr*sign(g): elements with |g| ~ eps amplify ulp-level
+    # gradient differences, so the update itself is compared normwise only.
     z = np.zeros_like
     pu, _, _ = R.adam_step(gold["u0"], gu0, z(gu0), z(gu0), 1)
     pi, _, _ = R.adam_step(gold["i0"], gi0, z(gi0), z(gi0), 1)
-    # Adam's first step moves each weight by ~lr*sign(g): compare the update itself
-    assert_parity(tr.user_w - t(gold["u0"]), pu - gold["u0"], "user update", tol=1e-3)
-    assert_parity(tr.item_w - t(gold["i0"]), pi - gold["i0"], "item update", tol=1e-3)
+    for got, want, name in ((tr.user_w - t(gold["u0"]), pu - gold["u0"], "user update"),
+                            (tr.item_w - t(gold["i0"]), pi - gold["i0"], "item update")):
+        got = got.double().cpu().numpy()
+        assert np.linalg.norm(got - want) <= 1e-4 * np.linalg.norm(want), name
     assert tr.g_uf.abs().sum().item() == 0 and tr.g_if.abs().sum().item() == 0
 
 
@@ -427,7 +433,8 @@ def test_dropin_training_step_matches_reference_torch_step(gold):
     assert abs(float(loss) - rloss) <= 1e-5 * rloss
     du = (m.user_emb.weight.detach().cpu() - torch.as_tensor(gold["u0"])).double().numpy()
     rdu = (ref.user_emb.weight.detach() - torch.as_tensor(gold["u0"])).double().numpy()
-    assert_parity(du, rdu, "drop-in user update vs torch step", tol=1e-3)
+    # Adam step 1 ~ -lr*sign(g): normwise comparison (see the trainer test)
+    assert np.linalg.norm(du - rdu) <= 1e-4 * np.linalg.norm(rdu)
 
 
 # ---------------------------------------------------------------------------
