@@ -40,6 +40,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic():
+    """Per-launch HBM bytes of spmm_kernel from the latest committed rocprofv3
+    PMC passes (tools/profile_box.sh + tools/summarize_profile.py)."""
+    p = os.path.join(ROOT, "profiles", "spmm_traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    j = json.load(open(p))
+    return j.get("hbm_bytes_per_launch_corrected"), j.get("source")
+
+
 def spmm_bytes(nnz: int, rows: int, d: int) -> int:
     return nnz * (4 + 4 + 4 * d) + rows * (4 + 4 * d)
 
@@ -168,6 +178,7 @@ def main():
                                                  "GBps": n * spmm_bytes(nnz, rows, dd) / (ms * 1e6)}
                   for (rows, nnz, dd), (n, ms) in summ.items()}
     achieved = tot_bytes / (tot_ms * 1e6) if tot_ms > 0 else 0.0   # GB/s
+    traffic, traffic_src = pmc_traffic() if (args.config == "C4" and world == 1) else (None, None)
     edges_per_step = 4 * K * E
     if rank != 0:
         if world > 1:
@@ -197,7 +208,10 @@ def main():
         "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
         "final_loss": final_loss,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": tot_bytes / max(n_launch, 1),
                      "kernel": "bbgr::spmm_kernel (+fixup)", "launches": n_launch,
                      "avg_launch_ms": tot_ms / max(n_launch, 1), "per_operator": per_kernel},
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},

@@ -108,6 +108,7 @@ _SIGNATURES = {
                              ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_operator_scales": ([c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P], c_int32),
+    "bbgr_gather_scale": ([c_int64, _P, _P, _P, _P], c_int32),
     "bbgr_spmm": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(SpmmArgs), _P], c_int32),
     "bbgr_epilogue": ([c_int32, _P, c_int64, ctypes.POINTER(SpmmArgs), _P], c_int32),
     "bbgr_bpr": ([ctypes.POINTER(BprArgs), _P], c_int32),

@@ -258,6 +258,12 @@ __global__ void shuffle_keys_kernel(long n, unsigned long long seed,
   keys[i] = ((unsigned long long)r.x << 32) | r.y;
 }
 
+__global__ void gather_scale_kernel(long nnz, const int *indices, const float *scale,
+                                    float *out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nnz) out[e] = scale[indices[e]];
+}
+
 struct NonEmpty {
   const int *indptr;
   __host__ __device__ bool operator()(const long &r) const {
@@ -544,6 +550,18 @@ extern "C" int bbgr_shuffle(int64_t n, const int64_t *in, int64_t *out,
   BBGR_HIP(hipcub::DeviceRadixSort::SortPairs(ws + 2 * a, temp, k1, k2,
                                               (const long *)in, (long *)out, (int)n,
                                               0, 64, st));
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_gather_scale(int64_t nnz, const int32_t *indices,
+                                 const float *scale, float *out,
+                                 bbgr_stream_t stream) {
+  BBGR_REQUIRE(nnz >= 0, "bbgr_gather_scale: negative nnz");
+  if (nnz == 0) return BBGR_OK;
+  BBGR_REQUIRE(indices && scale && out, "bbgr_gather_scale: null arrays");
+  hipLaunchKernelGGL(gather_scale_kernel, dim3(blocks_for(nnz)), dim3(256), 0,
+                     as_stream(stream), (long)nnz, indices, scale, out);
+  BBGR_LAUNCHED("gather_scale_kernel");
   return BBGR_OK;
 }
 

@@ -167,7 +167,7 @@ class ShardedTrainer:
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
         self._allreduce(self.g_if)                       # item grads of the global batch
-        dist.all_gather_into_tensor(self.all_items, torch.cat([pos, neg]), group=self.group)
+        _all_gather(self.all_items, torch.cat([pos, neg]), self.group)
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  out_i=self.g_i0, ws=self.ws, reduce=self._allreduce)
         alpha = 2.0 * self.reg / self.B_global            # ego L2 (Version-2:503-507)
@@ -184,6 +184,16 @@ class ShardedTrainer:
         self._allreduce(self.loss)
         self.loss.mul_(1.0 / self.world)
         return self.loss
+
+
+def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
+    """all_gather_into_tensor (RCCL); list form where the backend lacks it (gloo)."""
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, inp, group=group)
+        return
+    parts = list(out.chunk(dist.get_world_size(group)))
+    dist.all_gather(parts, inp, group=group)
+    out.copy_(torch.cat(parts))
 
 
 class _GlobalItemCsr:

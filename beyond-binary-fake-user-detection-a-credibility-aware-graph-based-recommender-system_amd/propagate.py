@@ -51,6 +51,18 @@ class Product:
     in_scale: torch.Tensor | None
     out_scale: torch.Tensor | None
     partial: dict
+    first_vals: torch.Tensor | None = None
+
+    def first_layer_values(self) -> torch.Tensor:
+        """in_scale[col] per CSR slot (built once, 4 B/edge): the first product of
+        a chain streams these instead of gathering in_scale[col] at random."""
+        if self.first_vals is None:
+            c = self.csr
+            v = torch.empty(max(c.nnz, 1), dtype=torch.float32, device=c.device)
+            call("bbgr_gather_scale", c.nnz, ptr(c.indices), ptr(self.in_scale), ptr(v),
+                 stream_handle())
+            self.first_vals = v
+        return self.first_vals
 
     def workspace(self, d: int):
         if self.csr.n_split == 0:
@@ -138,7 +150,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     if prod.vals is not None:
         a.weight_mode, a.edge_val = 1, ptr(prod.vals)
     elif first and prod.in_scale is not None:
-        a.weight_mode, a.col_scale, a.col_scale_s = 2, ptr(prod.in_scale), 1.0
+        a.weight_mode, a.edge_val = 1, ptr(prod.first_layer_values())
     else:
         a.weight_mode = 0
     a.y, a.ldy = ptr(y), ld(y)

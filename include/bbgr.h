@@ -131,6 +131,12 @@ int bbgr_operator_scales(int32_t kind, int32_t n_users, int32_t n_items,
                          float *p, float *q, float *s, float *t, float *pt,
                          float *qs, bbgr_stream_t stream);
 
+/* out[e] = scale[indices[e]] for e < nnz: a column scale expanded into CSR
+ * slot order, so a chain's first SpMM streams 4 coalesced bytes per edge
+ * (weight_mode 1) instead of gathering scale[col] at random (weight_mode 2). */
+int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
+                      float *out, bbgr_stream_t stream);
+
 /* ------------------------------------------------------------------------- */
 /* Fused CSR-SpMM (the hot kernel)                                            */
 /*   Replaces torch.sparse.mm at Version-2/lighgcn_cu_pop.py:483-484,         */

@@ -1,0 +1,97 @@
+"""Summarise a tools/profile_box.sh run into profiles/<tag>_*.
+
+    python tools/summarize_profile.py r01
+
+Inputs : gpurun_out/prof_<tag>/{trace,fetch,write}/run_*.csv (rocprofv3)
+Outputs: profiles/<tag>_kernel_stats.csv   (rocprofv3 --stats summary, verbatim)
+         profiles/<tag>_summary.json/.md   (per-kernel avg time, PMC bytes)
+         profiles/spmm_traffic.json        (read by bench.py: roofline.traffic)
+
+HBM bytes per the MI355X guide (MI355X_MICROARCH.md §HBM, cdna_hip_programming
+§7): FETCH_SIZE and WRITE_SIZE in KiB from separate passes; on gfx950
+FETCH_SIZE reports 1/2 of the bytes of a wide coalesced stream, so
+hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. The 2x read correction is
+calibrated for 16-B-per-lane streams (checked here on adam_kernel, whose
+bytes are known); for the SpMM's 256-B row gathers it is applied as the
+guide prescribes and the raw counters are kept beside it. Infinity-Cache
+(MALL) hits are counted by FETCH_SIZE, so the figure bounds HBM traffic
+from above.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag: str):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    stats = {r["Name"]: r for r in csv.DictReader(
+        open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
+
+    def pmc(kind):
+        d = collections.defaultdict(list)
+        for r in csv.DictReader(open(os.path.join(src, kind, "run_counter_collection.csv"))):
+            d[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+        return d
+
+    fetch, write = pmc("fetch"), pmc("write")
+    # per-dispatch durations by (kernel, grid) from the trace pass
+    dur = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+        g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        dur[(r["Kernel_Name"], g)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    kernels = {}
+    for key in sorted(set(fetch) | set(dur)):
+        name, grid = key
+        f, w, t = fetch.get(key, []), write.get(key, []), dur.get(key, [])
+        e = {"kernel": name, "grid": grid, "dispatches": len(t),
+             "avg_us": (sum(t) / len(t) / 1e3) if t else None}
+        if f and w:
+            fk, wk = sum(f) / len(f), sum(w) / len(w)
+            e.update(FETCH_SIZE_KiB=fk, WRITE_SIZE_KiB=wk,
+                     hbm_bytes_corrected=(2 * fk + wk) * 1024,
+                     hbm_bytes_raw=(fk + wk) * 1024)
+            if e["avg_us"]:
+                e["hbm_GBps_corrected"] = e["hbm_bytes_corrected"] / (e["avg_us"] * 1e3)
+        kernels[f"{name}@{grid}"] = e
+    summary = {"tag": tag, "stats": {k: {"calls": int(v["Calls"]),
+                                         "avg_us": float(v["AverageNs"]) / 1e3,
+                                         "pct": float(v["Percentage"])}
+                                     for k, v in stats.items()},
+               "kernels": kernels}
+    json.dump(summary, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
+    spmm = [e for e in kernels.values()
+            if e["kernel"] == "spmm_kernel" and "hbm_bytes_corrected" in e]
+    if spmm:
+        n = sum(e["dispatches"] for e in spmm)
+        avg = sum(e["hbm_bytes_corrected"] * e["dispatches"] for e in spmm) / n
+        json.dump({"tag": tag, "kernel": "spmm_kernel",
+                   "hbm_bytes_per_launch_corrected": avg,
+                   "per_grid": {e["grid"]: e["hbm_bytes_corrected"] for e in spmm},
+                   "source": f"profiles/{tag}_summary.json"},
+                  open(os.path.join(dst, "spmm_traffic.json"), "w"), indent=1)
+    with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
+        fh.write(f"# rocprofv3 summary {tag}\n\n| kernel | calls | avg us | % |\n|---|---|---|---|\n")
+        for k, v in sorted(summary["stats"].items(), key=lambda kv: -kv[1]["pct"])[:15]:
+            fh.write(f"| {k} | {v['calls']} | {v['avg_us']:.1f} | {v['pct']:.2f} |\n")
+        fh.write("\n| kernel@grid | dispatches | avg us | FETCH KiB | WRITE KiB | HBM GB (2F+W) | GB/s |\n"
+                 "|---|---|---|---|---|---|---|\n")
+        for k, e in kernels.items():
+            if "hbm_bytes_corrected" in e:
+                fh.write(f"| {k} | {e['dispatches']} | {e['avg_us'] or 0:.1f} | "
+                         f"{e['FETCH_SIZE_KiB']:.0f} | {e['WRITE_SIZE_KiB']:.0f} | "
+                         f"{e['hbm_bytes_corrected'] / 1e9:.3f} | "
+                         f"{e.get('hbm_GBps_corrected', 0):.0f} |\n")
+    print(open(os.path.join(dst, f"{tag}_summary.md")).read())
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
