@@ -115,6 +115,8 @@ def main():
     ap.add_argument("--variant", default="v2_pop")
     ap.add_argument("--cred", default="beta", choices=["beta", "ones"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dense", action="store_true",
+                    help="disable exact frontier sparsity (every SpMM over the full CSR)")
     args = ap.parse_args()
     cfg_name_global = args.config
     cfg = CONFIGS[args.config]
@@ -123,10 +125,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    local = local % max(torch.cuda.device_count(), 1)   # ranks may share a GPU (gloo rehearsal)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        # RCCL ("nccl") in production; BBGR_DIST_BACKEND=gloo lets two ranks
+        # share one GPU to rehearse the multi-rank path on a 1-GPU box.
+        backend = os.environ.get("BBGR_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
 
     U, I, d, K = cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"]
     B = cfg["batch"]
@@ -142,7 +151,7 @@ def main():
         from bbgr.trainer import FusedTrainer
         graph = BipartiteGraph(edges, U, I, dev)
         trainer = FusedTrainer(graph, args.variant, cred=cred, emb_dim=d, num_layers=K,
-                               batch_size=B)
+                               batch_size=B, frontier=not args.dense)
     else:
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
@@ -170,7 +179,8 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss)
-    summ = timer.summary()
+    summ = timer.summary()                 # full-CSR launches: the roofline kernel
+    summ_m = timer.summary(masked=True)    # frontier-masked launches (bytes data-dependent)
     tot_bytes = sum(n * spmm_bytes(nnz, rows, dd) for (rows, nnz, dd), (n, ms) in summ.items())
     tot_ms = sum(ms for (n, ms) in summ.values())
     n_launch = sum(n for (n, ms) in summ.values())
@@ -178,6 +188,8 @@ def main():
                                                  "GBps": n * spmm_bytes(nnz, rows, dd) / (ms * 1e6)}
                   for (rows, nnz, dd), (n, ms) in summ.items()}
     achieved = tot_bytes / (tot_ms * 1e6) if tot_ms > 0 else 0.0   # GB/s
+    masked_ms = sum(ms for (n, ms) in summ_m.values())
+    masked_n = sum(n for (n, ms) in summ_m.values())
     traffic, traffic_src = pmc_traffic() if (args.config == "C4" and world == 1) else (None, None)
     edges_per_step = 4 * K * E
     if rank != 0:
@@ -206,6 +218,12 @@ def main():
                    "num_layers": K, "global_batch": B, "parallelism": f"user-rows x{world}"},
         "bpr_steps_per_s": args.steps / elapsed,
         "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
+        "frontier": {"enabled": world == 1 and not args.dense,
+                     "masked_launches_per_step": masked_n / args.steps,
+                     "masked_ms_per_step": masked_ms / args.steps,
+                     "full_launches_per_step": n_launch / args.steps,
+                     "note": "value counts the reference step's 4*K*E edge traversals; "
+                             "masked launches skip exact-zero / unread rows"},
         "final_loss": final_loss,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -71,6 +71,8 @@ class SpmmArgs(ctypes.Structure):
         ("acc_scale", c_void_p), ("acc_scale_s", c_float),
         ("gamma", c_float),
         ("partial", c_void_p),
+        ("src_mask", c_void_p),
+        ("row_mask", c_void_p),
     ]
 
 
@@ -115,6 +117,8 @@ _SIGNATURES = {
     "bbgr_bpr_reduce": ([c_int64, _P, c_float, c_float, _P, _P], c_int32),
     "bbgr_adam": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
                    c_float, c_float, c_float, _P], c_int32),
+    "bbgr_mark_rows": ([c_int64, _P, ctypes.c_uint8, _P, _P], c_int32),
+    "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
     "bbgr_rows_zero": ([c_int64, _P, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_rows_axpy": ([c_int64, _P, c_float, _P, c_int64, _P, c_int64, c_int32, _P],
                        c_int32),

@@ -52,6 +52,8 @@ struct SpmmParams {
   float acc_scale_s;
   float gamma;
   float *partial;
+  const unsigned char *src_mask;
+  const unsigned char *row_mask;
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -73,19 +75,26 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
   constexpr int U = 16 / V;  // source rows in flight per group per batch
   for (int e0 = eb; e0 < ee; e0 += 16) {
     const int n = min(16, ee - e0);
-    int my = 0;
+    int my = -1;
     float mw = 0.f;
     if (lane < n) {
       my = P.indices[e0 + lane];
-      if (WMODE == 1) mw = P.edge_val[e0 + lane];
-      if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
+      if (P.src_mask && !P.src_mask[my]) my = -1;   // exact-zero source row
+      if (my >= 0) {
+        if (WMODE == 1) mw = P.edge_val[e0 + lane];
+        if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
+      }
+    }
+    if (P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
+      const unsigned long long live = __ballot(my >= 0);
+      if (((live >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
     }
     for (int j0 = 0; j0 < n; j0 += U) {
       float4 v[U][V];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         const int c = __shfl(my, j0 + j, 16);
-        if (j0 + j < n) {
+        if (j0 + j < n && c >= 0) {
           const float4 *src =
               reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + lane;
 #pragma unroll
@@ -179,6 +188,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
   if ((int)blockIdx.x < P.n_chunks) {
     // ---- one chunk of a long row: whole workgroup --------------------------
     const int4 ch = P.chunks[blockIdx.x];  // row, e_begin, e_end, slot
+    if (P.row_mask && !P.row_mask[ch.x]) return;   // whole workgroup, uniform
     const int len = ch.z - ch.y;
     const int per = (((len + 15) >> 4) + 15) & ~15;  // multiple of 16
     const int gb = ch.y + g * per;
@@ -206,6 +216,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
   const int eb = P.indptr[row];
   const int ee = P.indptr[row + 1];
   if (ee - eb > P.long_threshold) return;  // owned by chunk blocks
+  if (P.row_mask && !P.row_mask[row]) return;
   gather_range<D, WMODE>(P, eb, ee, lane, acc);
   epilogue<D>(P, (int)row, lane, acc);
 }
@@ -218,6 +229,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(SpmmParams P) {
   const int g = threadIdx.x >> 4;
   const int lane = threadIdx.x & 15;
   const int4 sp = P.split[blockIdx.x];  // row, slot_begin, n_slots
+  if (P.row_mask && !P.row_mask[sp.x]) return;
   float4 acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -371,6 +383,8 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   P.col_scale_s = a->col_scale_s;
   fill_epilogue(P, a);
   P.partial = a->partial;
+  P.src_mask = a->src_mask;
+  P.row_mask = a->row_mask;
   hipStream_t st = as_stream(stream);
   switch (d) {
     case 64: return dispatch_wmode<64>(P, a->weight_mode, csr->n_split, st);

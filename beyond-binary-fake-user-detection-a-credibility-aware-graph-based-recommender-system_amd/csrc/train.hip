@@ -220,16 +220,33 @@ __global__ void adam_tail_kernel(long n, long start, float *p, const float *g,
 __global__ void rows_zero_kernel(long n, const long *idx, float *t, long ld,
                                  int d) {
   const long k = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
-  if (k >= n) return;
+  if (k >= n || idx[k] < 0) return;
   float *row = t + idx[k] * ld;
   for (int c = threadIdx.x & 15; c < d; c += 16) row[c] = 0.f;
+}
+
+__global__ void mark_rows_kernel(long n, const long *idx, unsigned char v,
+                                 unsigned char *mask) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n && idx[k] >= 0) mask[idx[k]] = v;   // -1 = sampler "no item"
+}
+
+// one 16-lane group per listed row; duplicate writes store the same value
+__global__ void mark_neighbors_kernel(long n, const long *rows, const int *indptr,
+                                      const int *indices, unsigned char v,
+                                      unsigned char *mask) {
+  const long k = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (k >= n || rows[k] < 0) return;
+  const long r = rows[k];
+  for (int e = indptr[r] + (threadIdx.x & 15); e < indptr[r + 1]; e += 16)
+    mask[indices[e]] = v;
 }
 
 __global__ void rows_axpy_kernel(long n, const long *idx, float alpha,
                                  const float *src, long lds, float *dst, long ldd,
                                  int d) {
   const long k = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
-  if (k >= n) return;
+  if (k >= n || idx[k] < 0) return;
   const long r = idx[k];
   for (int c = threadIdx.x & 15; c < d; c += 16)
     atomicAdd(dst + r * ldd + c, alpha * src[r * lds + c]);
@@ -342,6 +359,30 @@ extern "C" int bbgr_rows_zero(int64_t n, const int64_t *idx, float *table,
   hipLaunchKernelGGL(rows_zero_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
                      as_stream(stream), (long)n, (const long *)idx, table, (long)ld, d);
   BBGR_LAUNCHED("rows_zero_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value,
+                              uint8_t *mask, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_mark_rows: negative n");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx && mask, "bbgr_mark_rows: null arrays");
+  hipLaunchKernelGGL(mark_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)idx, value, mask);
+  BBGR_LAUNCHED("mark_rows_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_mark_neighbors(int64_t n, const int64_t *rows,
+                                   const int32_t *indptr, const int32_t *indices,
+                                   uint8_t value, uint8_t *mask, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_mark_neighbors: negative n");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(rows && indptr && indices && mask, "bbgr_mark_neighbors: null arrays");
+  hipLaunchKernelGGL(mark_neighbors_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)rows, indptr, indices, value,
+                     mask);
+  BBGR_LAUNCHED("mark_neighbors_kernel");
   return BBGR_OK;
 }
 

@@ -118,12 +118,16 @@ class SpmmTimer:
     launching stream; used by bench.py inside the timed region."""
 
     def __init__(self):
-        self.records = []   # (n_rows, nnz, d, start_event, end_event)
+        self.records = []   # (n_rows, nnz, d, masked, start_event, end_event)
 
-    def summary(self):
+    def summary(self, masked: bool = False):
+        """{(rows, nnz, d): (launches, total ms)} over full (masked=False) or
+        frontier-masked (masked=True) launches."""
         torch.cuda.synchronize()
         out = {}
-        for rows, nnz, d, a, b in self.records:
+        for rows, nnz, d, m, a, b in self.records:
+            if m != masked:
+                continue
             k = (rows, nnz, d)
             n, ms = out.get(k, (0, 0.0))
             out[k] = (n + 1, ms + a.elapsed_time(b))
@@ -141,7 +145,7 @@ def set_spmm_timer(t: SpmmTimer | None) -> None:
 def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          y_scale_s: float = 1.0, add=None, add_scale=None, add_scale_s: float = 1.0,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
-         gamma: float = 1.0) -> None:
+         gamma: float = 1.0, src_mask=None, row_mask=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
@@ -162,6 +166,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     a.acc_scale, a.acc_scale_s = ptr(acc_scale), acc_scale_s
     a.gamma = gamma
     a.partial = ptr(prod.workspace(d))
+    a.src_mask, a.row_mask = ptr(src_mask), ptr(row_mask)
     if _timer is None:
         call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
         return
@@ -169,7 +174,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     ev0.record()
     call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
     ev1.record()
-    _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d, ev0, ev1))
+    _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d,
+                           src_mask is not None or row_mask is not None, ev0, ev1))
 
 
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,
@@ -196,8 +202,9 @@ def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw
     if reduce is None:
         spmm(prod, x, first, **kw)
         return
+    masks = {k: kw.pop(k) for k in ("src_mask", "row_mask") if k in kw}
     t = new("partial", prod.csr.n_rows)
-    spmm(prod, x, first, y=t)
+    spmm(prod, x, first, y=t, **masks)
     reduce(t)
     epilogue(t, **kw)
 
@@ -228,9 +235,16 @@ def _buffers(ws: dict | None, device, d: int):
 
 def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
             order: str = ORDER_GS, out_u: torch.Tensor | None = None,
-            out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None):
+            out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None,
+            final_rows=None):
     """Final (layer-mean) user and item tables. u0 [U,d], i0 [I,d] fp32.
-    `reduce(t)`: in-place sum over ranks of item-row partial sums (sharded mode)."""
+    `reduce(t)`: in-place sum over ranks of item-row partial sums (sharded mode).
+    `final_rows=(user_mask, item_mask)`: only the flagged rows of the final
+    tables are needed (a training step reads batch rows only). The last layer
+    then computes only those rows; the item mask must cover every item the
+    flagged users' last-layer rows read (GS: N(batch users) and the batch
+    items; Jacobi: the batch items). Flagged rows are bitwise identical to a
+    full pass; the others are left stale."""
     U, I = pair.num_users, pair.num_items
     d = u0.shape[1]
     _check_table("user table", u0, U, d)
@@ -245,30 +259,34 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
     gl = 1.0 / (K + 1)
     FI, FU = pair.fwd_item, pair.fwd_user
     new = _buffers(ws, u0.device, d)
+    mu, mi = final_rows if final_rows is not None else (None, None)
     if order == ORDER_GS:
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(1, K + 1):
             g = gl if k == K else 1.0
+            last = k == K
             _item_product(FI, u0 if k == 1 else bufU, k == 1, reduce, new, y=bufI,
                           y_scale=pair.feed_fwd_iu, acc_in=i0 if k == 1 else acc_i,
-                          acc_out=acc_i, acc_scale=FI.out_scale, gamma=g)
+                          acc_out=acc_i, acc_scale=FI.out_scale, gamma=g,
+                          row_mask=mi if last else None)
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
-                 acc_scale=FU.out_scale, gamma=g)
+                 acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None)
     elif order == ORDER_J:
         bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
         cur = 0
         for k in range(1, K + 1):
             g = gl if k == K else 1.0
             nxt = 1 - cur
+            last = k == K
             _item_product(FI, u0 if k == 1 else bufU[cur], k == 1, reduce, new,
                           y=bufI[nxt] if k < K else None, y_scale=pair.feed_fwd_iu,
                           acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
-                          acc_scale=FI.out_scale, gamma=g)
+                          acc_scale=FI.out_scale, gamma=g, row_mask=mi if last else None)
             spmm(FU, i0 if k == 1 else bufI[cur], k == 1,
                  y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
-                 acc_scale=FU.out_scale, gamma=g)
+                 acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None)
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")
@@ -278,8 +296,13 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
 def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
              order: str = ORDER_GS, out_u: torch.Tensor | None = None,
              out_i: torch.Tensor | None = None, ws: dict | None = None,
-             grad_i0_dense: bool = True, reduce=None):
-    """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final)."""
+             grad_i0_dense: bool = True, reduce=None, grad_support=None):
+    """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final).
+    `grad_support=(user_mask, item_mask)`: gU is zero outside the flagged users
+    and, for GS, the first item product's output is zero outside the flagged
+    items (GS: batch items and N(batch users); Jacobi: gI's own support). The
+    first products of the chain then skip the exact-zero source rows; results
+    are bitwise identical to the dense chain (the skipped terms are +0.0)."""
     U, I = pair.num_users, pair.num_items
     d = gU.shape[1]
     _check_table("user grad", gU, U, d)
@@ -294,19 +317,22 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
     gl = 1.0 / (K + 1)
     BI, BU = pair.bwd_item, pair.bwd_user
     new = _buffers(ws, gU.device, d)
+    su, si = grad_support if grad_support is not None else (None, None)
     if order == ORDER_GS:
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(K, 0, -1):
             first = k == K
             _item_product(BI, gU if first else bufU, first, reduce, new, y=bufI,
                           y_scale=pair.feed_bwd_iu, y_scale_s=gl if first else 1.0,
-                          add=gI, add_scale=BU.in_scale, add_scale_s=gl)
+                          add=gI, add_scale=BU.in_scale, add_scale_s=gl,
+                          src_mask=su if first else None)
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
-                     add=gU, add_scale=BI.in_scale, add_scale_s=gl)
+                     add=gU, add_scale=BI.in_scale, add_scale_s=gl,
+                     src_mask=si if first else None)
             else:
                 spmm(BU, bufI, False, y=gu0, y_scale=BU.out_scale,
-                     add=gU, add_scale=None, add_scale_s=gl)
+                     add=gU, add_scale=None, add_scale_s=gl, src_mask=si if first else None)
         if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
             torch.mul(gI, gl, out=gi0)
     elif order == ORDER_J:
@@ -318,17 +344,20 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
             ys = gl if first else 1.0
             xu = gI if first else bufI[cur]   # input of BU (item table)
             xi = gU if first else bufU[cur]   # input of BI (user table)
+            mu_ = si if first else None     # BU reads gI (items), BI reads gU (users)
+            mi_ = su if first else None
             if k > 1:
                 spmm(BU, xu, first, y=bufU[nxt], y_scale=pair.feed_bwd_ui, y_scale_s=ys,
-                     add=gU, add_scale=BI.in_scale, add_scale_s=gl)
+                     add=gU, add_scale=BI.in_scale, add_scale_s=gl, src_mask=mu_)
                 _item_product(BI, xi, first, reduce, new, y=bufI[nxt],
                               y_scale=pair.feed_bwd_iu, y_scale_s=ys,
-                              add=gI, add_scale=BU.in_scale, add_scale_s=gl)
+                              add=gI, add_scale=BU.in_scale, add_scale_s=gl, src_mask=mi_)
             else:
                 spmm(BU, xu, first, y=gu0, y_scale=BU.out_scale, y_scale_s=ys,
-                     add=gU, add_scale=None, add_scale_s=gl)
+                     add=gU, add_scale=None, add_scale_s=gl, src_mask=mu_)
                 _item_product(BI, xi, first, reduce, new, y=gi0, y_scale=BI.out_scale,
-                              y_scale_s=ys, add=gI, add_scale=None, add_scale_s=gl)
+                              y_scale_s=ys, add=gI, add_scale=None, add_scale_s=gl,
+                              src_mask=mi_)
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")

@@ -42,7 +42,8 @@ class FusedTrainer:
                  emb_dim: int = 64, num_layers: int = 3, lr: float = 1e-3,
                  reg: float = 1e-4, batch_size: int = 4096, neg_mix_pop: float | None = None,
                  neg_pop_gamma: float = 0.75, neg_max_tries: int = 50,
-                 lambda_fair: float = 0.0, seed: int = 42, u0=None, i0=None):
+                 lambda_fair: float = 0.0, seed: int = 42, u0=None, i0=None,
+                 frontier: bool = True):
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}; one of {sorted(VARIANTS)}")
@@ -95,6 +96,14 @@ class FusedTrainer:
         self.perm = None
         self.pos = torch.empty(batch_size, dtype=torch.int64, device=dev)
         self.neg = torch.empty(batch_size, dtype=torch.int64, device=dev)
+        # Exact frontier sparsity: a step reads the final tables only at batch
+        # rows, and its loss gradient is non-zero only there. Masks (1 byte per
+        # node) restrict the last forward layer to the rows it feeds and let the
+        # first backward products skip exact-zero source rows. Loss, gradients
+        # and updates are bitwise identical to the dense step (tested).
+        self.frontier = frontier
+        self.mask_u = torch.zeros(self.U, dtype=torch.uint8, device=dev)
+        self.mask_i = torch.zeros(self.I, dtype=torch.uint8, device=dev)
 
     # -- batching ---------------------------------------------------------------
     def next_users(self) -> torch.Tensor:
@@ -112,8 +121,10 @@ class FusedTrainer:
         users = self.next_users() if users is None else users.to(torch.int64).contiguous()
         B = users.numel()
         pos, neg = self.sampler.sample(users, self.pos[:B], self.neg[:B])
-        self.forward()
         st = stream_handle()
+        masks = self._set_masks(users, pos, neg, 1) if self.frontier else None
+        forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
+                out_i=self.itf, ws=self.ws, final_rows=masks)
         a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
                      self.pop, self.lambda_fair, parts=self.parts[: 3 * B],
                      g_uf=self.g_uf, g_if=self.g_if)
@@ -121,7 +132,7 @@ class FusedTrainer:
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
-                 out_i=self.g_i0, ws=self.ws)
+                 out_i=self.g_i0, ws=self.ws, grad_support=masks)
         # ego L2 term goes straight to the weight grads (Version-2:503-507):
         # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
         alpha = 2.0 * self.reg / B
@@ -138,8 +149,23 @@ class FusedTrainer:
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
         call("bbgr_rows_zero", B, ptr(pos), ptr(self.g_if), ld(self.g_if), self.d, st)
         call("bbgr_rows_zero", B, ptr(neg), ptr(self.g_if), ld(self.g_if), self.d, st)
+        if masks is not None:
+            self._set_masks(users, pos, neg, 0)
         return self.loss
 
+    def _set_masks(self, users, pos, neg, value: int):
+        """mask_u = batch users; mask_i = batch items (+ N(batch users) for GS,
+        whose last user layer reads the NEW item layer)."""
+        st = stream_handle()
+        B = users.numel()
+        call("bbgr_mark_rows", B, ptr(users), value, ptr(self.mask_u), st)
+        call("bbgr_mark_rows", B, ptr(pos), value, ptr(self.mask_i), st)
+        call("bbgr_mark_rows", B, ptr(neg), value, ptr(self.mask_i), st)
+        if self.order == ORDER_GS:
+            uc = self.graph.user_csr
+            call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), value,
+                 ptr(self.mask_i), st)
+        return self.mask_u, self.mask_i
     def forward(self):
         return forward(self.pair, self.user_w, self.item_w, self.K, self.order,
                        out_u=self.uf, out_i=self.itf, ws=self.ws)

@@ -158,6 +158,10 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /* Tables are fp32 row-major with leading dimension ld* (floats, multiple of  */
 /* 4, 16-byte aligned base). d in {64, 128, 256}.                             */
 /* partial: workspace of (csr->n_chunks * d) floats when csr->n_split > 0.    */
+/* src_mask (nullable, [n_cols] bytes): edges whose column is 0 in the mask    */
+/*   are skipped — exact when x is zero on those rows (sparse gradients).     */
+/* row_mask (nullable, [n_rows] bytes): rows that are 0 are not computed and  */
+/*   not written (only the flagged rows of the outputs are needed).           */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -183,6 +187,8 @@ typedef struct {
   float acc_scale_s;
   float gamma;
   float *partial;
+  const uint8_t *src_mask;
+  const uint8_t *row_mask;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -260,6 +266,7 @@ int bbgr_adam(int64_t n, float *param, const float *grad, float *exp_avg,
 /* ------------------------------------------------------------------------- */
 /* Row utilities for the fused training step                                  */
 /* ------------------------------------------------------------------------- */
+/* Row utilities skip negative indices (the sampler's -1 "no item").        */
 /* table[idx[k], :d] = 0 for k < n (restores all-zero gradient tables). */
 int bbgr_rows_zero(int64_t n, const int64_t *idx, float *table, int64_t ld,
                    int32_t d, bbgr_stream_t stream);
@@ -267,6 +274,15 @@ int bbgr_rows_zero(int64_t n, const int64_t *idx, float *table, int64_t ld,
 int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha, const float *src,
                    int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
                    bbgr_stream_t stream);
+
+/* mask[idx[k]] = value for k < n. */
+int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value, uint8_t *mask,
+                   bbgr_stream_t stream);
+/* For each listed row r = rows[k]: mask[indices[e]] = value for every edge e of
+ * row r (the neighbourhood frontier of a batch). */
+int bbgr_mark_neighbors(int64_t n, const int64_t *rows, const int32_t *indptr,
+                        const int32_t *indices, uint8_t value, uint8_t *mask,
+                        bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Negative / positive sampling                                               */

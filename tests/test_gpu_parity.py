@@ -489,3 +489,61 @@ def test_c4_size_adjoint_and_linearity():
     rhs = (u0.double() * gu0.double()).sum() + (i0.double() * gi0.double()).sum()
     assert abs(float(lhs - rhs)) <= 1e-5 * float(
         (uf.double().abs() * gU.double().abs()).sum() + (itf.double().abs() * gI.double().abs()).sum())
+
+
+# ---------------------------------------------------------------------------
+# Frontier masks (exact sparsity)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("thr", [256, 8])
+def test_spmm_src_and_row_masks(thr):
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(thr)
+    R_, C_, d = 400, 350, 64
+    e = synthetic_edges(C_, R_, 9000, 4, items="zipf")
+    rows, cols = e[1], e[0]
+    c = Csr(rows, cols, R_, C_, DEV, long_threshold=thr, chunk_edges=32)
+    prod = Product(c, None, None, None, {})
+    x = rng.uniform(-1, 1, (C_, d)).astype(np.float32)
+    smask = (rng.random(C_) < 0.1).astype(np.uint8)
+    rmask = (rng.random(R_) < 0.3).astype(np.uint8)
+    y = torch.full((R_, d), 7.0, device=DEV)
+    xm = x * smask[:, None]          # the dense equivalent: x is zero off the mask
+    spmm(prod, t(xm), False, y=y, src_mask=t(smask, torch.uint8))
+    want = R.csr64(rows, cols, np.ones(rows.size), (R_, C_)) @ xm.astype(np.float64)
+    assert_parity(y, want, "src-masked y")
+    y2 = torch.full((R_, d), 7.0, device=DEV)
+    spmm(prod, t(x), False, y=y2, row_mask=t(rmask, torch.uint8))
+    full = R.csr64(rows, cols, np.ones(rows.size), (R_, C_)) @ x.astype(np.float64)
+    got = y2.cpu().numpy()
+    assert_parity(got[rmask == 1], full[rmask == 1], "row-masked y")
+    assert (got[rmask == 0] == 7.0).all()          # unflagged rows untouched
+
+
+@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair"])
+def test_frontier_step_matches_dense_step(variant):
+    """Frontier-masked training step == dense step (C2 graph, long rows split)."""
+    from bbgr.synthetic import CONFIGS, config_edges
+    from bbgr.trainer import FusedTrainer
+    c = CONFIGS["C2"]
+    U, I = c["num_users"], c["num_items"]
+    e = config_edges("C2")
+    cred = synthetic_credibility(U, 2)
+    g = BipartiteGraph(e, U, I, DEV)
+    rng = np.random.default_rng(0)
+    u0 = rng.uniform(-0.05, 0.05, (U, 64)).astype(np.float32)
+    i0 = rng.uniform(-0.05, 0.05, (I, 64)).astype(np.float32)
+    kw = dict(cred=cred, emb_dim=64, num_layers=3, batch_size=4096, u0=u0, i0=i0,
+              lambda_fair=0.05 if variant == "cu_fair" else 0.0)
+    dense = FusedTrainer(g, variant, frontier=False, **kw)
+    front = FusedTrainer(g, variant, frontier=True, **kw)
+    for _ in range(3):
+        users = dense.next_users()
+        front.next_users()
+        ld_, lf = float(dense.step(users)), float(front.step(users))
+        assert torch.equal(dense.pos, front.pos) and torch.equal(dense.neg, front.neg)
+        assert abs(ld_ - lf) <= 1e-6 * abs(ld_)
+        for a, b, what in ((dense.g_u0, front.g_u0, "grad u0"), (dense.g_i0, front.g_i0, "grad i0")):
+            err = (a.double() - b.double()).norm() / a.double().norm()
+            assert err <= 1e-6, (what, float(err))
+    # masks are left clean for the next step
+    assert int(front.mask_u.sum()) == 0 and int(front.mask_i.sum()) == 0
