@@ -73,6 +73,8 @@ class SpmmArgs(ctypes.Structure):
         ("partial", c_void_p),
         ("src_mask", c_void_p),
         ("row_mask", c_void_p),
+        ("acc_mask", c_void_p),
+        ("add_mask", c_void_p),
     ]
 
 

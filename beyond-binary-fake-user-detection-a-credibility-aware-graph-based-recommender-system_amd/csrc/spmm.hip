@@ -54,6 +54,8 @@ struct SpmmParams {
   float *partial;
   const unsigned char *src_mask;
   const unsigned char *row_mask;
+  const unsigned char *acc_mask;
+  const unsigned char *add_mask;
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -126,7 +128,7 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
   if (P.y) {
     const float ys = (P.y_scale ? P.y_scale[row] : 1.f) * P.y_scale_s;
     float4 *dst = reinterpret_cast<float4 *>(P.y + (long)row * P.ldy) + lane;
-    if (P.add) {
+    if (P.add && (!P.add_mask || P.add_mask[row])) {
       const float as = (P.add_scale ? P.add_scale[row] : 1.f) * P.add_scale_s;
       const float4 *ad =
           reinterpret_cast<const float4 *>(P.add + (long)row * P.ldadd) + lane;
@@ -138,7 +140,7 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
       for (int k = 0; k < V; ++k) dst[16 * k] = f4_mul(ys, T[k]);
     }
   }
-  if (P.acc_out) {
+  if (P.acc_out && (!P.acc_mask || P.acc_mask[row])) {
     const float cs = (P.acc_scale ? P.acc_scale[row] : 1.f) * P.acc_scale_s;
     float4 *dst =
         reinterpret_cast<float4 *>(P.acc_out + (long)row * P.ldacc_out) + lane;
@@ -315,6 +317,8 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.acc_scale = a->acc_scale;
   P.acc_scale_s = a->acc_scale_s;
   P.gamma = a->gamma;
+  P.acc_mask = a->acc_mask;
+  P.add_mask = a->add_mask;
 }
 
 extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,

@@ -145,7 +145,8 @@ def set_spmm_timer(t: SpmmTimer | None) -> None:
 def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          y_scale_s: float = 1.0, add=None, add_scale=None, add_scale_s: float = 1.0,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
-         gamma: float = 1.0, src_mask=None, row_mask=None) -> None:
+         gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
+         add_mask=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
@@ -167,6 +168,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     a.gamma = gamma
     a.partial = ptr(prod.workspace(d))
     a.src_mask, a.row_mask = ptr(src_mask), ptr(row_mask)
+    a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
     if _timer is None:
         call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
         return
@@ -180,7 +182,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
 
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,
              add_scale=None, add_scale_s: float = 1.0, acc_in=None, acc_out=None,
-             acc_scale=None, acc_scale_s: float = 1.0, gamma: float = 1.0) -> None:
+             acc_scale=None, acc_scale_s: float = 1.0, gamma: float = 1.0, acc_mask=None,
+             add_mask=None) -> None:
     """bbgr_epilogue: the SpMM epilogue applied to a dense table of row sums."""
     a = _lib.SpmmArgs()
     a.d = t.shape[1]
@@ -192,6 +195,7 @@ def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, a
     a.acc_out, a.ldacc_out = ptr(acc_out), ld(acc_out)
     a.acc_scale, a.acc_scale_s = ptr(acc_scale), acc_scale_s
     a.gamma = gamma
+    a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
     call("bbgr_epilogue", t.shape[0], ptr(t), ld(t), ctypes.byref(a), stream_handle())
 
 
@@ -268,10 +272,11 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
             _item_product(FI, u0 if k == 1 else bufU, k == 1, reduce, new, y=bufI,
                           y_scale=pair.feed_fwd_iu, acc_in=i0 if k == 1 else acc_i,
                           acc_out=acc_i, acc_scale=FI.out_scale, gamma=g,
-                          row_mask=mi if last else None)
+                          row_mask=mi if last else None, acc_mask=mi)
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
-                 acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None)
+                 acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
+                 acc_mask=mu)
     elif order == ORDER_J:
         bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
         cur = 0
@@ -282,11 +287,13 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
             _item_product(FI, u0 if k == 1 else bufU[cur], k == 1, reduce, new,
                           y=bufI[nxt] if k < K else None, y_scale=pair.feed_fwd_iu,
                           acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
-                          acc_scale=FI.out_scale, gamma=g, row_mask=mi if last else None)
+                          acc_scale=FI.out_scale, gamma=g, row_mask=mi if last else None,
+                          acc_mask=mi)
             spmm(FU, i0 if k == 1 else bufI[cur], k == 1,
                  y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
-                 acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None)
+                 acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
+                 acc_mask=mu)
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")
@@ -324,15 +331,15 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
             first = k == K
             _item_product(BI, gU if first else bufU, first, reduce, new, y=bufI,
                           y_scale=pair.feed_bwd_iu, y_scale_s=gl if first else 1.0,
-                          add=gI, add_scale=BU.in_scale, add_scale_s=gl,
+                          add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
                           src_mask=su if first else None)
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
-                     add=gU, add_scale=BI.in_scale, add_scale_s=gl,
+                     add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl,
                      src_mask=si if first else None)
             else:
                 spmm(BU, bufI, False, y=gu0, y_scale=BU.out_scale,
-                     add=gU, add_scale=None, add_scale_s=gl, src_mask=si if first else None)
+                     add=gU, add_mask=su, add_scale=None, add_scale_s=gl, src_mask=si if first else None)
         if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
             torch.mul(gI, gl, out=gi0)
     elif order == ORDER_J:
@@ -348,15 +355,15 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
             mi_ = su if first else None
             if k > 1:
                 spmm(BU, xu, first, y=bufU[nxt], y_scale=pair.feed_bwd_ui, y_scale_s=ys,
-                     add=gU, add_scale=BI.in_scale, add_scale_s=gl, src_mask=mu_)
+                     add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl, src_mask=mu_)
                 _item_product(BI, xi, first, reduce, new, y=bufI[nxt],
                               y_scale=pair.feed_bwd_iu, y_scale_s=ys,
-                              add=gI, add_scale=BU.in_scale, add_scale_s=gl, src_mask=mi_)
+                              add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl, src_mask=mi_)
             else:
                 spmm(BU, xu, first, y=gu0, y_scale=BU.out_scale, y_scale_s=ys,
-                     add=gU, add_scale=None, add_scale_s=gl, src_mask=mu_)
+                     add=gU, add_mask=su, add_scale=None, add_scale_s=gl, src_mask=mu_)
                 _item_product(BI, xi, first, reduce, new, y=gi0, y_scale=BI.out_scale,
-                              y_scale_s=ys, add=gI, add_scale=None, add_scale_s=gl,
+                              y_scale_s=ys, add=gI, add_mask=si, add_scale=None, add_scale_s=gl,
                               src_mask=mi_)
             cur = nxt
     else:

@@ -162,6 +162,9 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   are skipped — exact when x is zero on those rows (sparse gradients).     */
 /* row_mask (nullable, [n_rows] bytes): rows that are 0 are not computed and  */
 /*   not written (only the flagged rows of the outputs are needed).           */
+/* acc_mask (nullable, [n_rows]): acc_in/acc_out touched only on flagged rows */
+/* add_mask (nullable, [n_rows]): add[r] read only on flagged rows (treated   */
+/*   as 0 elsewhere — exact when add is zero off the mask).                   */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -189,6 +192,8 @@ typedef struct {
   float *partial;
   const uint8_t *src_mask;
   const uint8_t *row_mask;
+  const uint8_t *acc_mask;
+  const uint8_t *add_mask;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
