@@ -75,6 +75,8 @@ class SpmmArgs(ctypes.Structure):
         ("row_mask", c_void_p),
         ("acc_mask", c_void_p),
         ("add_mask", c_void_p),
+        ("row_list", c_void_p),
+        ("n_row_list", c_int64),
     ]
 
 

@@ -56,6 +56,8 @@ struct SpmmParams {
   const unsigned char *row_mask;
   const unsigned char *acc_mask;
   const unsigned char *add_mask;
+  const long *row_list;
+  long n_row_list;
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -70,7 +72,7 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 }
 
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
-template <int D, int WMODE>
+template <int D, int WMODE, bool MASKED>
 __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
                                              int lane, float4 (&acc)[D / 64]) {
   constexpr int V = D / 64;
@@ -81,13 +83,13 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     float mw = 0.f;
     if (lane < n) {
       my = P.indices[e0 + lane];
-      if (P.src_mask && !P.src_mask[my]) my = -1;   // exact-zero source row
+      if (MASKED && P.src_mask && !P.src_mask[my]) my = -1;   // exact-zero source row
       if (my >= 0) {
         if (WMODE == 1) mw = P.edge_val[e0 + lane];
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
       }
     }
-    if (P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
+    if (MASKED && P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
       const unsigned long long live = __ballot(my >= 0);
       if (((live >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
     }
@@ -96,7 +98,7 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         const int c = __shfl(my, j0 + j, 16);
-        if (j0 + j < n && c >= 0) {
+        if (j0 + j < n && (!MASKED || c >= 0)) {
           const float4 *src =
               reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + lane;
 #pragma unroll
@@ -177,8 +179,8 @@ __device__ __forceinline__ void block_reduce16(float4 *red, int g, int lane,
   __syncthreads();
 }
 
-template <int D, int WMODE>
-__global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
+template <int D, int WMODE, bool MASKED>
+__device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   constexpr int V = D / 64;
   __shared__ float4 red[16 * (D / 4)];
   const int g = threadIdx.x >> 4;
@@ -190,12 +192,13 @@ __global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
   if ((int)blockIdx.x < P.n_chunks) {
     // ---- one chunk of a long row: whole workgroup --------------------------
     const int4 ch = P.chunks[blockIdx.x];  // row, e_begin, e_end, slot
-    if (P.row_mask && !P.row_mask[ch.x]) return;   // whole workgroup, uniform
+    if (MASKED && P.row_mask && !P.row_mask[ch.x]) return;   // whole workgroup, uniform
+    if (MASKED && P.row_list && !P.row_mask) return;         // list mode: short rows only
     const int len = ch.z - ch.y;
     const int per = (((len + 15) >> 4) + 15) & ~15;  // multiple of 16
     const int gb = ch.y + g * per;
     const int ge = min(ch.z, gb + per);
-    if (gb < ge) gather_range<D, WMODE>(P, gb, ge, lane, acc);
+    if (gb < ge) gather_range<D, WMODE, MASKED>(P, gb, ge, lane, acc);
     block_reduce16<D>(red, g, lane, acc);
     if (g == 0) {
       float4 T[V];
@@ -213,14 +216,31 @@ __global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
   }
 
   // ---- short rows: one 16-lane group per row ------------------------------
-  const long row = (long)(blockIdx.x - P.n_chunks) * 16 + g;
+  long row = (long)(blockIdx.x - P.n_chunks) * 16 + g;
+  if (MASKED && P.row_list) {
+    if (row >= P.n_row_list) return;
+    row = P.row_list[row];
+    if (row < 0) return;
+  }
   if (row >= P.n_rows) return;
   const int eb = P.indptr[row];
   const int ee = P.indptr[row + 1];
   if (ee - eb > P.long_threshold) return;  // owned by chunk blocks
-  if (P.row_mask && !P.row_mask[row]) return;
-  gather_range<D, WMODE>(P, eb, ee, lane, acc);
+  if (MASKED && !P.row_list && P.row_mask && !P.row_mask[row]) return;
+  gather_range<D, WMODE, MASKED>(P, eb, ee, lane, acc);
   epilogue<D>(P, (int)row, lane, acc);
+}
+
+// Full-CSR launches (the roofline kernel) and masked / row-list launches are
+// distinct symbols so that profiles separate them.
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, false>(P);
+}
+
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) void spmm_masked_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, true>(P);
 }
 
 // Rows split into >1 chunk: sum chunk partials in chunk order, then epilogue.
@@ -266,11 +286,18 @@ __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float
 
 template <int D, int WMODE>
 static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
-  const long short_blocks = ((long)P.n_rows + 15) / 16;
+  const bool masked = P.src_mask || P.row_mask || P.row_list;
+  const long short_rows = P.row_list ? P.n_row_list : (long)P.n_rows;
+  const long short_blocks = (short_rows + 15) / 16;
   const long grid = (long)P.n_chunks + short_blocks;
   if (grid > 0) {
-    hipLaunchKernelGGL((spmm_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
-                       0, st, P);
+    if (masked) {
+      hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
+                         0, st, P);
+    } else {
+      hipLaunchKernelGGL((spmm_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
+                         0, st, P);
+    }
     BBGR_LAUNCHED("spmm_kernel");
   }
   if (n_split > 0) {
@@ -389,6 +416,9 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   P.partial = a->partial;
   P.src_mask = a->src_mask;
   P.row_mask = a->row_mask;
+  P.row_list = (const long *)a->row_list;
+  P.n_row_list = a->n_row_list;
+  BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_spmm: negative n_row_list");
   hipStream_t st = as_stream(stream);
   switch (d) {
     case 64: return dispatch_wmode<64>(P, a->weight_mode, csr->n_split, st);

@@ -146,7 +146,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          y_scale_s: float = 1.0, add=None, add_scale=None, add_scale_s: float = 1.0,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
-         add_mask=None) -> None:
+         add_mask=None, row_list=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
@@ -169,6 +169,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     a.partial = ptr(prod.workspace(d))
     a.src_mask, a.row_mask = ptr(src_mask), ptr(row_mask)
     a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
+    if row_list is not None:
+        a.row_list, a.n_row_list = ptr(row_list), row_list.numel()
     if _timer is None:
         call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
         return
@@ -177,7 +179,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
     ev1.record()
     _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d,
-                           src_mask is not None or row_mask is not None, ev0, ev1))
+                           src_mask is not None or row_mask is not None or row_list is not None,
+                           ev0, ev1))
 
 
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,
@@ -243,7 +246,7 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
             final_rows=None):
     """Final (layer-mean) user and item tables. u0 [U,d], i0 [I,d] fp32.
     `reduce(t)`: in-place sum over ranks of item-row partial sums (sharded mode).
-    `final_rows=(user_mask, item_mask)`: only the flagged rows of the final
+    `final_rows=(user_mask, item_mask[, user_list])`: only the flagged rows of the final
     tables are needed (a training step reads batch rows only). The last layer
     then computes only those rows; the item mask must cover every item the
     flagged users' last-layer rows read (GS: N(batch users) and the batch
@@ -263,7 +266,7 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
     gl = 1.0 / (K + 1)
     FI, FU = pair.fwd_item, pair.fwd_user
     new = _buffers(ws, u0.device, d)
-    mu, mi = final_rows if final_rows is not None else (None, None)
+    mu, mi, ulist = (tuple(final_rows) + (None,))[:3] if final_rows is not None else (None,) * 3
     if order == ORDER_GS:
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(1, K + 1):
@@ -276,7 +279,7 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
                  acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
-                 acc_mask=mu)
+                 acc_mask=mu, row_list=ulist if last else None)
     elif order == ORDER_J:
         bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
         cur = 0
@@ -293,7 +296,7 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
                  y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
                  acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
-                 acc_mask=mu)
+                 acc_mask=mu, row_list=ulist if last else None)
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")

@@ -124,7 +124,8 @@ class FusedTrainer:
         st = stream_handle()
         masks = self._set_masks(users, pos, neg, 1) if self.frontier else None
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
-                out_i=self.itf, ws=self.ws, final_rows=masks)
+                out_i=self.itf, ws=self.ws,
+                final_rows=None if masks is None else (masks[0], masks[1], users))
         a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
                      self.pop, self.lambda_fair, parts=self.parts[: 3 * B],
                      g_uf=self.g_uf, g_if=self.g_if)

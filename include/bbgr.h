@@ -165,6 +165,10 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /* acc_mask (nullable, [n_rows]): acc_in/acc_out touched only on flagged rows */
 /* add_mask (nullable, [n_rows]): add[r] read only on flagged rows (treated   */
 /*   as 0 elsewhere — exact when add is zero off the mask).                   */
+/* row_list (nullable, int64 [n_row_list]): compute only these rows (short    */
+/*   rows on a grid sized by the list; long rows still need row_mask set for  */
+/*   their chunk workgroups). Launches with any mask or list run as           */
+/*   `spmm_masked_kernel`, full-CSR launches as `spmm_kernel`.                */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -194,6 +198,8 @@ typedef struct {
   const uint8_t *row_mask;
   const uint8_t *acc_mask;
   const uint8_t *add_mask;
+  const int64_t *row_list;
+  int64_t n_row_list;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
