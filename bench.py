@@ -31,7 +31,8 @@ sys.path.insert(0, ROOT)
 
 import bbgr  # noqa: E402,F401
 from bbgr import propagate as P  # noqa: E402
-from bbgr.synthetic import CONFIGS, CONFIG_SEED, config_edges, synthetic_credibility  # noqa: E402
+from bbgr.synthetic import (CONFIGS, CONFIG_SEED, config_edges, shard_edges_weak,  # noqa: E402
+                            synthetic_credibility)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -117,6 +118,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true",
                     help="disable exact frontier sparsity (every SpMM over the full CSR)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = every rank owns a full config-sized user shard over the "
+                         "shared items; strong = one config graph cut into N user ranges")
     args = ap.parse_args()
     cfg_name_global = args.config
     cfg = CONFIGS[args.config]
@@ -139,12 +143,14 @@ def main():
 
     U, I, d, K = cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"]
     B = cfg["batch"]
+    weak = world > 1 and args.scaling == "weak"
     t0 = time.perf_counter()
-    edges = config_edges(args.config)
-    E = edges.shape[1]
-    cred = synthetic_credibility(U, CONFIG_SEED[args.config], args.cred)
+    seed = CONFIG_SEED[args.config]
+    edges = shard_edges_weak(args.config, rank) if weak else config_edges(args.config)
+    cred = synthetic_credibility(U, seed + 7919 * rank if weak else seed, args.cred)
+    E = edges.shape[1] * (world if weak else 1)          # edges of the whole job's graph
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} E={E} d={d} K={K} B={B} "
-        f"generated in {time.perf_counter() - t0:.1f}s")
+        f"scaling={'weak' if weak else 'strong'} generated in {time.perf_counter() - t0:.1f}s")
 
     if world == 1:
         from bbgr.graph import BipartiteGraph
@@ -152,10 +158,18 @@ def main():
         graph = BipartiteGraph(edges, U, I, dev)
         trainer = FusedTrainer(graph, args.variant, cred=cred, emb_dim=d, num_layers=K,
                                batch_size=B, frontier=not args.dense)
-    else:
+    elif weak:
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
-                                 num_layers=K, batch_size=B, device=dev)
+                                 num_layers=K, batch_size=B, device=dev, user_offset=rank * U,
+                                 frontier=not args.dense)
+    else:
+        from bbgr.distributed import ShardedTrainer
+        trainer = ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
+                                                   emb_dim=d, num_layers=K, batch_size=B,
+                                                   device=dev, frontier=not args.dense)
+    if world > 1:
+        del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: setup done, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
 
@@ -209,13 +223,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Zipf-0.8 items, geometric user degrees; xavier init; Beta cred)",
-        "config": {"workload": f"{args.config} BPR training step ({args.variant})",
-                   "num_users": U, "num_items": I, "num_edges": E, "emb_dim": d,
-                   "num_layers": K, "global_batch": B, "parallelism": f"user-rows x{world}"},
+        "config": {"workload": f"{args.config} BPR training step ({args.variant})"
+                               + (f", {world} x {args.config} user shards" if weak else ""),
+                   "num_users": U * (world if weak else 1), "num_items": I, "num_edges": E,
+                   "emb_dim": d, "num_layers": K,
+                   "global_batch": B * (world if weak else 1),
+                   "parallelism": f"user-rows x{world}"},
         "bpr_steps_per_s": args.steps / elapsed,
         "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
         "frontier": {"enabled": world == 1 and not args.dense,

@@ -77,6 +77,8 @@ class SpmmArgs(ctypes.Structure):
         ("add_mask", c_void_p),
         ("row_list", c_void_p),
         ("n_row_list", c_int64),
+        ("use_range", c_int32),
+        ("range", c_int32 * 6),
     ]
 
 

@@ -58,6 +58,8 @@ struct SpmmParams {
   const unsigned char *add_mask;
   const long *row_list;
   long n_row_list;
+  int row_begin, row_end;      // short rows computed: [row_begin, row_end)
+  int chunk_begin;             // first long-row chunk of this launch
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -191,7 +193,7 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
 
   if ((int)blockIdx.x < P.n_chunks) {
     // ---- one chunk of a long row: whole workgroup --------------------------
-    const int4 ch = P.chunks[blockIdx.x];  // row, e_begin, e_end, slot
+    const int4 ch = P.chunks[P.chunk_begin + blockIdx.x];  // row, e_begin, e_end, slot
     if (MASKED && P.row_mask && !P.row_mask[ch.x]) return;   // whole workgroup, uniform
     if (MASKED && P.row_list && !P.row_mask) return;         // list mode: short rows only
     const int len = ch.z - ch.y;
@@ -216,11 +218,13 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   }
 
   // ---- short rows: one 16-lane group per row ------------------------------
-  long row = (long)(blockIdx.x - P.n_chunks) * 16 + g;
+  long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * 16 + g;
   if (MASKED && P.row_list) {
     if (row >= P.n_row_list) return;
     row = P.row_list[row];
     if (row < 0) return;
+  } else if (row >= P.row_end) {
+    return;
   }
   if (row >= P.n_rows) return;
   const int eb = P.indptr[row];
@@ -277,6 +281,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float
   const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
   if (row >= P.n_rows) return;
+  if (P.row_mask && !P.row_mask[row]) return;
   const float4 *src = reinterpret_cast<const float4 *>(t + row * ldt) + lane;
   float4 T[V];
 #pragma unroll
@@ -287,7 +292,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float
 template <int D, int WMODE>
 static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
   const bool masked = P.src_mask || P.row_mask || P.row_list;
-  const long short_rows = P.row_list ? P.n_row_list : (long)P.n_rows;
+  const long short_rows = P.row_list ? P.n_row_list : (long)(P.row_end - P.row_begin);
   const long short_blocks = (short_rows + 15) / 16;
   const long grid = (long)P.n_chunks + short_blocks;
   if (grid > 0) {
@@ -363,6 +368,7 @@ extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
   SpmmParams P = {};
   P.n_rows = n_rows;
   fill_epilogue(P, a);
+  P.row_mask = a->row_mask;
   const unsigned grid = (unsigned)(((long)n_rows + 15) / 16);
   hipStream_t st = as_stream(stream);
   switch (d) {
@@ -418,11 +424,29 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   P.row_mask = a->row_mask;
   P.row_list = (const long *)a->row_list;
   P.n_row_list = a->n_row_list;
+  int n_split = csr->n_split;
+  P.row_begin = 0;
+  P.row_end = csr->n_rows;
+  P.chunk_begin = 0;
+  if (a->use_range) {
+    const int *r = a->range;
+    BBGR_REQUIRE(r[0] >= 0 && r[0] <= r[1] && r[1] <= csr->n_rows && r[2] >= 0 &&
+                     r[2] <= r[3] && r[3] <= csr->n_chunks && r[4] >= 0 && r[4] <= r[5] &&
+                     r[5] <= csr->n_split,
+                 "bbgr_spmm: range out of bounds");
+    BBGR_REQUIRE(!a->row_list, "bbgr_spmm: range and row_list are exclusive");
+    P.row_begin = r[0];
+    P.row_end = r[1];
+    P.chunk_begin = r[2];
+    P.n_chunks = r[3] - r[2];
+    P.split = reinterpret_cast<const int4 *>(csr->split) + r[4];
+    n_split = r[5] - r[4];
+  }
   BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_spmm: negative n_row_list");
   hipStream_t st = as_stream(stream);
   switch (d) {
-    case 64: return dispatch_wmode<64>(P, a->weight_mode, csr->n_split, st);
-    case 128: return dispatch_wmode<128>(P, a->weight_mode, csr->n_split, st);
-    default: return dispatch_wmode<256>(P, a->weight_mode, csr->n_split, st);
+    case 64: return dispatch_wmode<64>(P, a->weight_mode, n_split, st);
+    case 128: return dispatch_wmode<128>(P, a->weight_mode, n_split, st);
+    default: return dispatch_wmode<256>(P, a->weight_mode, n_split, st);
   }
 }

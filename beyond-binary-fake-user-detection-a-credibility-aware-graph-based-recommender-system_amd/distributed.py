@@ -2,21 +2,31 @@
 
 SURVEY §8(e). The reference is single-device; this is the build's scale-out:
 
-  * users are cut into `world` contiguous, edge-balanced ranges; rank g owns
-    its users' rows, ALL their edges (user-row CSR slice + the item-row CSR
-    restricted to those users), their embedding rows and Adam state.
-    Item tables and item Adam state are replicated.
-  * per layer and direction one exchange: each rank's item-row SpMM writes raw
-    partial row sums over ITS users, an in-place all-reduce (sum) completes
-    them, then the fused epilogue (layer mean, next-layer feed scale, backward
-    addend) runs on the full sums. User-row SpMMs are purely local.
-  * BPR: each rank samples batch/world of its own users; item gradient
-    contributions are all-reduced once per step; the ego-L2 item term is
-    applied from the all-gathered (pos, neg) indices on every rank (identical
-    values, so replicas stay bitwise identical). The loss is the mean over ranks.
+  * rank g owns a contiguous range of users: their rows, ALL their edges
+    (user-row CSR slice + the item-row CSR restricted to those users), their
+    embedding rows and Adam state. Item tables and item Adam state are
+    replicated on every rank.
+  * per layer and direction ONE exchange: each rank's item-row SpMM writes raw
+    partial row sums over ITS users; an in-place all-reduce(SUM) completes them;
+    the fused epilogue (layer mean, next-layer feed scale, backward addend)
+    then runs on the full sums. User-row SpMMs are purely local.
+  * the exchange is pipelined: the item rows are cut into edge-balanced
+    ranges; range c's all-reduce (async, RCCL's stream) overlaps range c+1's
+    SpMM on the compute stream.
+  * BPR: each rank samples its own users; item gradients are all-reduced once
+    per step; the ego-L2 item term is applied from the all-gathered (pos, neg)
+    indices on every rank (identical values, so replicas stay bitwise
+    identical); the loss is the mean over ranks.
+  * frontier sparsity as on one GPU, with the ITEM masks made global by one
+    all-reduce of a byte mask per step (every rank must compute every row any
+    rank needs before the exchange).
 
-Item degrees (and therefore every item scale) are global: the per-rank item
-degree counts are all-reduced at setup.
+Two ways to build the shards:
+  ShardedTrainer.from_global_edges(edges, U, I, ...)   strong scaling: one
+      graph cut into edge-balanced user ranges (global batch split over ranks)
+  ShardedTrainer(local_edges, U_local, I, ...)         weak scaling: each rank
+      brings its own user shard (local user ids) over the shared item set
+Global item degrees (hence every item scale) come from an all-reduce.
 """
 from __future__ import annotations
 
@@ -31,7 +41,7 @@ from ._lib import OP_SYM, call, ld, ptr, stream_handle
 from .bpr import bpr_args
 from .graph import BipartiteGraph, Scales
 from .optim import adam_step
-from .propagate import OperatorPair, backward, forward
+from .propagate import ORDER_GS, OperatorPair, backward, epilogue, forward, spmm
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .trainer import VARIANTS
 
@@ -64,13 +74,55 @@ def global_item_indptr(local_item_degrees: torch.Tensor, group=None) -> torch.Te
     return indptr.to(torch.int32)
 
 
+def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
+    """all_gather_into_tensor (RCCL); list form where the backend lacks it (gloo)."""
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, inp, group=group)
+        return
+    parts = list(out.chunk(dist.get_world_size(group)))
+    dist.all_gather(parts, inp, group=group)
+    out.copy_(torch.cat(parts))
+
+
+class ItemExchange:
+    """The per-layer exchange of item partial sums (propagate's `reduce` hook).
+
+    item_product(): the SpMM runs over `parts` edge-balanced item-row ranges;
+    each range's partial sums are all-reduced asynchronously as soon as they
+    are written, overlapping the next range's SpMM; the epilogue runs once all
+    ranges are summed."""
+
+    def __init__(self, group=None, parts: int = 4):
+        self.group, self.parts = group, max(1, int(parts))
+
+    def __call__(self, t: torch.Tensor) -> None:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def item_product(self, prod, x, first, new, kw) -> None:
+        src_mask = kw.pop("src_mask", None)
+        row_mask = kw.pop("row_mask", None)
+        t = new("partial", prod.csr.n_rows)
+        works = []
+        for rg in prod.csr.row_ranges(self.parts):
+            spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, rng=rg)
+            works.append(dist.all_reduce(t[rg[0]:rg[1]], op=dist.ReduceOp.SUM,
+                                         group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        epilogue(t, row_mask=row_mask, **kw)
+
+
 class ShardedTrainer:
-    def __init__(self, edges: np.ndarray, num_users: int, num_items: int,
+    def __init__(self, local_edges: np.ndarray, num_local_users: int, num_items: int,
                  variant: str = "v2_pop", cred=None, emb_dim: int = 64, num_layers: int = 3,
                  lr: float = 1e-3, reg: float = 1e-4, batch_size: int = 8192,
                  neg_mix_pop: float | None = None, neg_pop_gamma: float = 0.75,
                  neg_max_tries: int = 50, lambda_fair: float = 0.0, seed: int = 42,
-                 device=None, group=None, u0=None, i0=None):
+                 device=None, group=None, u0=None, i0=None, user_offset: int = 0,
+                 frontier: bool = True, exchange_parts: int = 4):
+        """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
+        this rank's users; i0: the full (replicated) item table; batch_size:
+        users per step on THIS rank."""
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}")
@@ -80,41 +132,40 @@ class ShardedTrainer:
         self.rank = dist.get_rank(group)
         dev = torch.device(device) if device is not None else torch.device("cuda")
         self.device = dev
-        self.U, self.I, self.d, self.K = num_users, num_items, emb_dim, num_layers
+        self.U_local, self.I, self.d, self.K = num_local_users, num_items, emb_dim, num_layers
+        self.lo, self.hi = user_offset, user_offset + num_local_users
         self.order, self.lr, self.reg = order, lr, reg
         self.lambda_fair = lambda_fair
-        self.B_local = max(1, batch_size // self.world)
+        self.B_local = max(1, int(batch_size))
         self.B_global = self.B_local * self.world
+        self.exchange = ItemExchange(group, exchange_parts)
 
-        deg_u = np.bincount(edges[0].astype(np.int64), minlength=num_users)
-        self.bounds = partition_users(deg_u, self.world)
-        lo, hi = int(self.bounds[self.rank]), int(self.bounds[self.rank + 1])
-        self.lo, self.hi, self.U_local = lo, hi, hi - lo
-        local = shard_edges(edges, lo, hi)
-        self.graph = BipartiteGraph(local, self.U_local, num_items, dev)
-        # global item degrees -> scales
+        self.graph = BipartiteGraph(local_edges, num_local_users, num_items, dev)
         indptr_i = global_item_indptr(self.graph.item_csr.degrees(), group)
         cred_t = None
         if cred is not None and kind != OP_SYM:
-            cred_t = torch.as_tensor(np.asarray(cred, np.float32)[lo:hi]).to(dev).contiguous()
+            cred_t = torch.as_tensor(np.asarray(cred, np.float32)).to(dev).contiguous()
         self.scales = _scales(kind, self.graph, indptr_i, cred_t)
         self.pair = OperatorPair.factored(self.graph, self.scales)
 
         f32 = dict(dtype=torch.float32, device=dev)
-        if u0 is None:   # the same global init on every rank; keep my rows
-            g = torch.Generator(device="cpu").manual_seed(seed)
-            au = (6.0 / (num_users + emb_dim)) ** 0.5
+        if u0 is None:   # rank-local stream for users, shared stream for items
+            gu = torch.Generator(device="cpu").manual_seed(seed + 104729 * (self.rank + 1))
+            gi = torch.Generator(device="cpu").manual_seed(seed)
+            au = (6.0 / (num_local_users * self.world + emb_dim)) ** 0.5
             ai = (6.0 / (num_items + emb_dim)) ** 0.5
-            u0 = (torch.rand(num_users, emb_dim, generator=g) * 2 - 1) * au
-            i0 = (torch.rand(num_items, emb_dim, generator=g) * 2 - 1) * ai
-        self.user_w = torch.as_tensor(u0, dtype=torch.float32)[lo:hi].to(dev).contiguous()
+            u0 = (torch.rand(num_local_users, emb_dim, generator=gu) * 2 - 1) * au
+            i0 = (torch.rand(num_items, emb_dim, generator=gi) * 2 - 1) * ai
+        self.user_w = torch.as_tensor(u0, dtype=torch.float32).to(dev).contiguous()
         self.item_w = torch.as_tensor(i0, dtype=torch.float32).to(dev).contiguous()
+        if self.user_w.shape != (num_local_users, emb_dim) or self.item_w.shape != (num_items, emb_dim):
+            raise ValueError("initial tables have the wrong shape")
         z = lambda n: torch.zeros(n, emb_dim, **f32)  # noqa: E731
-        self.m_u, self.v_u = z(self.U_local), z(self.U_local)
+        self.m_u, self.v_u = z(num_local_users), z(num_local_users)
         self.m_i, self.v_i = z(num_items), z(num_items)
-        self.uf, self.itf = z(self.U_local), z(num_items)
-        self.g_uf, self.g_if = z(self.U_local), z(num_items)
-        self.g_u0, self.g_i0 = z(self.U_local), z(num_items)
+        self.uf, self.itf = z(num_local_users), z(num_items)
+        self.g_uf, self.g_if = z(num_local_users), z(num_items)
+        self.g_u0, self.g_i0 = z(num_local_users), z(num_items)
         self.parts = torch.empty(3 * self.B_local, **f32)
         self.loss = torch.zeros((), **f32)
         self.dloss = torch.full((), 1.0 / self.world, **f32)   # mean over the global batch
@@ -135,11 +186,36 @@ class ShardedTrainer:
         self.pos = torch.empty(self.B_local, dtype=torch.int64, device=dev)
         self.neg = torch.empty(self.B_local, dtype=torch.int64, device=dev)
         self.all_items = torch.empty(2 * self.B_global, dtype=torch.int64, device=dev)
+        self.frontier = frontier
+        self.mask_u = torch.zeros(num_local_users, dtype=torch.uint8, device=dev)
+        self.mask_i = torch.zeros(num_items, dtype=torch.uint8, device=dev)
 
-    # -- collectives ---------------------------------------------------------
-    def _allreduce(self, t: torch.Tensor) -> None:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+    @classmethod
+    def from_global_edges(cls, edges: np.ndarray, num_users: int, num_items: int,
+                          variant: str = "v2_pop", cred=None, batch_size: int = 8192,
+                          u0=None, i0=None, group=None, seed: int = 42, **kw):
+        """Strong scaling: cut ONE graph into edge-balanced user ranges; the
+        global batch is split over the ranks."""
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        deg_u = np.bincount(edges[0].astype(np.int64), minlength=num_users)
+        bounds = partition_users(deg_u, world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        emb_dim = kw.get("emb_dim", 64)
+        if u0 is None:   # the same global init on every rank; keep my rows
+            g = torch.Generator(device="cpu").manual_seed(seed)
+            au = (6.0 / (num_users + emb_dim)) ** 0.5
+            ai = (6.0 / (num_items + emb_dim)) ** 0.5
+            u0 = (torch.rand(num_users, emb_dim, generator=g) * 2 - 1) * au
+            i0 = (torch.rand(num_items, emb_dim, generator=g) * 2 - 1) * ai
+        u0 = u0[lo:hi]
+        c = None if cred is None else np.asarray(cred, np.float32)[lo:hi]
+        tr = cls(shard_edges(edges, lo, hi), hi - lo, num_items, variant, cred=c,
+                 batch_size=max(1, batch_size // world), u0=u0, i0=i0, group=group,
+                 seed=seed, user_offset=lo, **kw)
+        tr.bounds = bounds
+        return tr
 
+    # -- batching ------------------------------------------------------------
     def next_users(self) -> torch.Tensor:
         n = self.train_users.numel()
         if self.perm is None or self.cursor >= n:
@@ -153,23 +229,40 @@ class ShardedTrainer:
             users = torch.cat([users, self.perm[: self.B_local - users.numel()]])
         return users
 
+    def _masks(self, users, pos, neg):
+        """mask_u: my batch users. mask_i: every rank's batch items (+ every
+        rank's N(batch users) for GS), made global by a byte all-reduce."""
+        st = stream_handle()
+        B = users.numel()
+        call("bbgr_mark_rows", B, ptr(users), 1, ptr(self.mask_u), st)
+        call("bbgr_mark_rows", B, ptr(pos), 1, ptr(self.mask_i), st)
+        call("bbgr_mark_rows", B, ptr(neg), 1, ptr(self.mask_i), st)
+        if self.order == ORDER_GS:
+            uc = self.graph.user_csr
+            call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), 1,
+                 ptr(self.mask_i), st)
+        dist.all_reduce(self.mask_i, op=dist.ReduceOp.SUM, group=self.group)  # <= world: no wrap
+        return self.mask_u, self.mask_i
+
     def step(self) -> torch.Tensor:
         users = self.next_users()
         B = users.numel()
         pos, neg = self.sampler.sample(users, self.pos[:B], self.neg[:B])
         st = stream_handle()
+        masks = self._masks(users, pos, neg) if self.frontier else None
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
-                out_i=self.itf, ws=self.ws, reduce=self._allreduce)
+                out_i=self.itf, ws=self.ws, reduce=self.exchange,
+                final_rows=None if masks is None else (masks[0], masks[1], users))
         a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
                      self.pop, self.lambda_fair, parts=self.parts[: 3 * B], dloss=self.dloss,
                      g_uf=self.g_uf, g_if=self.g_if)
         call("bbgr_bpr", ctypes.byref(a), st)
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
-        self._allreduce(self.g_if)                       # item grads of the global batch
+        self.exchange(self.g_if)                          # item grads of the global batch
         _all_gather(self.all_items, torch.cat([pos, neg]), self.group)
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
-                 out_i=self.g_i0, ws=self.ws, reduce=self._allreduce)
+                 out_i=self.g_i0, ws=self.ws, reduce=self.exchange, grad_support=masks)
         alpha = 2.0 * self.reg / self.B_global            # ego L2 (Version-2:503-507)
         call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
              ptr(self.g_u0), ld(self.g_u0), self.d, st)
@@ -181,19 +274,12 @@ class ShardedTrainer:
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
         call("bbgr_rows_zero", self.all_items.numel(), ptr(self.all_items), ptr(self.g_if),
              ld(self.g_if), self.d, st)
-        self._allreduce(self.loss)
+        if masks is not None:
+            call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), st)
+            self.mask_i.zero_()
+        dist.all_reduce(self.loss, op=dist.ReduceOp.SUM, group=self.group)
         self.loss.mul_(1.0 / self.world)
         return self.loss
-
-
-def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
-    """all_gather_into_tensor (RCCL); list form where the backend lacks it (gloo)."""
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, inp, group=group)
-        return
-    parts = list(out.chunk(dist.get_world_size(group)))
-    dist.all_gather(parts, inp, group=group)
-    out.copy_(torch.cat(parts))
 
 
 class _GlobalItemCsr:

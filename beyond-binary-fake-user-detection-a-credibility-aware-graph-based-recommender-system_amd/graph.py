@@ -118,6 +118,32 @@ class Csr:
             s.chunks, s.split = ptr(self.chunks), ptr(self.split)
         return s
 
+    def row_ranges(self, parts: int) -> list:
+        """Split rows into `parts` contiguous ranges of ~equal edge counts, each as
+        (row0, row1, chunk0, chunk1, split0, split1) for bbgr_spmm's range mode.
+        One host copy of indptr / plan at first use (setup-time)."""
+        key = int(parts)
+        cache = self.__dict__.setdefault("_ranges", {})
+        if key in cache:
+            return cache[key]
+        indptr = self.indptr.cpu().numpy().astype(np.int64)
+        ch_rows = self.chunks[: 4 * self.n_chunks].view(-1, 4)[:, 0].cpu().numpy()
+        sp_rows = self.split[: 4 * self.n_split].view(-1, 4)[:, 0].cpu().numpy()
+        targets = [self.nnz * k // parts for k in range(parts + 1)]
+        bounds = np.searchsorted(indptr, targets, side="left")
+        bounds[0], bounds[-1] = 0, self.n_rows
+        bounds = np.maximum.accumulate(np.minimum(bounds, self.n_rows))
+        out = []
+        for k in range(parts):
+            r0, r1 = int(bounds[k]), int(bounds[k + 1])
+            if r1 <= r0:
+                continue
+            c0, c1 = np.searchsorted(ch_rows, [r0, r1], side="left")
+            s0, s1 = np.searchsorted(sp_rows, [r0, r1], side="left")
+            out.append((r0, r1, int(c0), int(c1), int(s0), int(s1)))
+        cache[key] = out
+        return out
+
     def partial_workspace(self, d: int) -> torch.Tensor | None:
         if self.n_split == 0:
             return None

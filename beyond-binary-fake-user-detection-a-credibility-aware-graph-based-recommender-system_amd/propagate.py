@@ -146,7 +146,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          y_scale_s: float = 1.0, add=None, add_scale=None, add_scale_s: float = 1.0,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
-         add_mask=None, row_list=None) -> None:
+         add_mask=None, row_list=None, rng=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
@@ -171,6 +171,10 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
     if row_list is not None:
         a.row_list, a.n_row_list = ptr(row_list), row_list.numel()
+    if rng is not None:   # (row0, row1, chunk0, chunk1, split0, split1): Csr.row_ranges
+        a.use_range = 1
+        for k in range(6):
+            a.range[k] = rng[k]
     if _timer is None:
         call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
         return
@@ -186,7 +190,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,
              add_scale=None, add_scale_s: float = 1.0, acc_in=None, acc_out=None,
              acc_scale=None, acc_scale_s: float = 1.0, gamma: float = 1.0, acc_mask=None,
-             add_mask=None) -> None:
+             add_mask=None, row_mask=None) -> None:
     """bbgr_epilogue: the SpMM epilogue applied to a dense table of row sums."""
     a = _lib.SpmmArgs()
     a.d = t.shape[1]
@@ -199,6 +203,7 @@ def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, a
     a.acc_scale, a.acc_scale_s = ptr(acc_scale), acc_scale_s
     a.gamma = gamma
     a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
+    a.row_mask = ptr(row_mask)
     call("bbgr_epilogue", t.shape[0], ptr(t), ld(t), ctypes.byref(a), stream_handle())
 
 
@@ -209,11 +214,15 @@ def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw
     if reduce is None:
         spmm(prod, x, first, **kw)
         return
-    masks = {k: kw.pop(k) for k in ("src_mask", "row_mask") if k in kw}
+    if hasattr(reduce, "item_product"):   # chunked / overlapped exchange
+        reduce.item_product(prod, x, first, new, kw)
+        return
+    src_mask = kw.pop("src_mask", None)
+    row_mask = kw.pop("row_mask", None)
     t = new("partial", prod.csr.n_rows)
-    spmm(prod, x, first, y=t, **masks)
+    spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask)
     reduce(t)
-    epilogue(t, **kw)
+    epilogue(t, row_mask=row_mask, **kw)
 
 
 def _check_table(name, t, rows, d=None):

@@ -31,11 +31,13 @@ CONFIGS = {
 CONFIG_SEED = {"C1": 1, "C2": 2, "C3": 3, "C4": 4, "C5": 5}
 
 
-def _zipf_sampler(num_items: int, s: float, rng: np.random.Generator):
+def _zipf_sampler(num_items: int, s: float, rng: np.random.Generator, item_seed: int):
     w = np.power(np.arange(1, num_items + 1, dtype=np.float64), -s)
     cdf = np.cumsum(w)
     cdf /= cdf[-1]
-    relabel = rng.permutation(num_items).astype(np.int64)
+    # popularity rank -> item id relabelling: its own stream, so shards drawn
+    # with different seeds but one item_seed agree on which items are popular
+    relabel = np.random.default_rng([item_seed, 0xA11CE]).permutation(num_items).astype(np.int64)
 
     def draw(n: int) -> np.ndarray:
         r = np.searchsorted(cdf, rng.random(n), side="right")
@@ -47,9 +49,10 @@ def _zipf_sampler(num_items: int, s: float, rng: np.random.Generator):
 
 def synthetic_edges(num_users: int, num_items: int, num_edges: int, seed: int,
                     items: str = "zipf", zipf_s: float = 0.8,
-                    duplicates: int = 0) -> np.ndarray:
+                    duplicates: int = 0, item_seed: int | None = None) -> np.ndarray:
     """int32 [2, E] unique (u, i) pairs (+ `duplicates` repeated pairs appended,
-    for the coalesce-equivalence parity cases)."""
+    for the coalesce-equivalence parity cases). `item_seed` (default: seed) fixes
+    the item popularity order independently of the edge draws."""
     rng = np.random.default_rng(seed)
     U, I, E = int(num_users), int(num_items), int(num_edges)
     if E > U * I:
@@ -74,7 +77,7 @@ def synthetic_edges(num_users: int, num_items: int, num_edges: int, seed: int,
                 np.subtract.at(deg, pick, 1)
                 np.maximum(deg, 1 if E >= U else 0, out=deg)
             diff = E - int(deg.sum())
-        draw = _zipf_sampler(I, zipf_s, rng)
+        draw = _zipf_sampler(I, zipf_s, rng, seed if item_seed is None else item_seed)
         users = np.repeat(np.arange(U, dtype=np.int64), deg)
         keys = users * I + draw(E)
         keys.sort()
@@ -111,6 +114,16 @@ def config_edges(name: str, duplicates: int = 0) -> np.ndarray:
     c = CONFIGS[name]
     return synthetic_edges(c["num_users"], c["num_items"], c["num_edges"], CONFIG_SEED[name],
                            items=c["items"], duplicates=duplicates)
+
+
+def shard_edges_weak(name: str, rank: int) -> np.ndarray:
+    """Weak scaling: rank r owns a full config-sized user shard (its own users,
+    local ids) over the SAME item set and item popularity; rank 0's shard is
+    exactly config_edges(name)."""
+    c = CONFIGS[name]
+    return synthetic_edges(c["num_users"], c["num_items"], c["num_edges"],
+                           CONFIG_SEED[name] + 7919 * rank, items=c["items"],
+                           item_seed=CONFIG_SEED[name])
 
 
 def synthetic_credibility(num_users: int, seed: int, kind: str = "beta") -> np.ndarray:

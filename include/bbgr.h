@@ -169,6 +169,11 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   rows on a grid sized by the list; long rows still need row_mask set for  */
 /*   their chunk workgroups). Launches with any mask or list run as           */
 /*   `spmm_masked_kernel`, full-CSR launches as `spmm_kernel`.                */
+/* use_range != 0: compute only rows [range[0], range[1]), whose long-row     */
+/*   chunks are [range[2], range[3]) and split rows [range[4], range[5]) of   */
+/*   the plan (all three are row-ordered, so a row range maps to contiguous   */
+/*   chunk / split ranges). Lets the sharded step all-reduce item partial     */
+/*   sums chunk by chunk, overlapped with the next chunk's SpMM.              */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -200,13 +205,15 @@ typedef struct {
   const uint8_t *add_mask;
   const int64_t *row_list;
   int64_t n_row_list;
+  int32_t use_range;
+  int32_t range[6];
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
               bbgr_stream_t stream);
 
 /* The SpMM epilogue alone, with T read from a dense table t[n_rows, ldt]
- * (args->x / weight fields ignored). Used after the RCCL all-reduce of
+ * (args->x / weight fields ignored; row_mask, acc_mask, add_mask honoured). Used after the RCCL all-reduce of
  * per-rank item partial sums in the user-row-sharded multi-GPU step, where
  * the epilogue cannot run before the sum is complete. */
 int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,

@@ -1,6 +1,9 @@
 """Worker for tests/test_gpu_distributed.py (launched by torch.distributed.run):
-two gloo ranks share cuda:0 and run ShardedTrainer steps; each rank dumps its
-state for the parent test to check against the oracle."""
+two gloo ranks share cuda:0 and run one ShardedTrainer step; each rank dumps
+its state for the parent test to check against the oracle.
+
+mode "strong": one global graph (the golden fixture) cut into user ranges.
+mode "weak":   each rank builds its own user shard over the shared items."""
 import os
 import sys
 
@@ -12,18 +15,34 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr.distributed import ShardedTrainer  # noqa: E402
+from bbgr.synthetic import synthetic_edges  # noqa: E402
+
+WEAK_U, WEAK_I, WEAK_E = 200, 150, 2500
 
 
 def main():
-    out_dir, variant = sys.argv[1], sys.argv[2]
-    g = np.load(os.path.join(ROOT, "tests", "golden", "golden_small.npz"))
-    U, I, E, DUP, D, K, B = (int(x) for x in g["meta"])
+    out_dir, variant, mode = sys.argv[1], sys.argv[2], sys.argv[3]
+    frontier = len(sys.argv) < 5 or sys.argv[4] != "dense"
     dist.init_process_group("gloo")
     rank = dist.get_rank()
     torch.cuda.set_device(0)
-    tr = ShardedTrainer(g["edges"], U, I, variant, cred=g["cred"], emb_dim=D, num_layers=K,
-                        batch_size=64, device="cuda:0", u0=g["u0"], i0=g["i0"],
-                        lambda_fair=0.05 if variant == "cu_fair" else 0.0)
+    lam = 0.05 if variant == "cu_fair" else 0.0
+    if mode == "strong":
+        g = np.load(os.path.join(ROOT, "tests", "golden", "golden_small.npz"))
+        U, I, E, DUP, D, K, B = (int(x) for x in g["meta"])
+        tr = ShardedTrainer.from_global_edges(
+            g["edges"], U, I, variant, cred=g["cred"], emb_dim=D, num_layers=K, batch_size=64,
+            device="cuda:0", u0=g["u0"], i0=g["i0"], lambda_fair=lam, frontier=frontier,
+            exchange_parts=3)
+    else:
+        e = synthetic_edges(WEAK_U, WEAK_I, WEAK_E, 100 + rank, items="zipf", item_seed=100)
+        rng = np.random.default_rng(5)
+        u0 = rng.uniform(-1, 1, (2 * WEAK_U, 64)).astype(np.float32)[rank * WEAK_U:(rank + 1) * WEAK_U]
+        i0 = rng.uniform(-1, 1, (WEAK_I, 64)).astype(np.float32)
+        np.save(os.path.join(out_dir, f"edges{rank}.npy"), e)
+        tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3, batch_size=32,
+                            device="cuda:0", u0=u0, i0=i0, lambda_fair=lam,
+                            user_offset=rank * WEAK_U, frontier=frontier, exchange_parts=2)
     loss = float(tr.step())
     users = tr.perm[: tr.B_local]          # the first step takes the head of epoch 1
     torch.cuda.synchronize()

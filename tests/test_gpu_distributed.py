@@ -23,19 +23,33 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair"])
-def test_sharded_step_two_ranks_vs_oracle(tmp_path, variant):
+@pytest.mark.parametrize("variant,mode,frontier", [
+    ("v2_pop", "strong", "frontier"), ("cu_fair", "strong", "frontier"),
+    ("v2_pop", "strong", "dense"), ("v2_pop", "weak", "frontier"), ("cu_fair", "weak", "frontier")])
+def test_sharded_step_two_ranks_vs_oracle(tmp_path, variant, mode, frontier):
     from oracle import ref_numpy as R
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant]
+           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, mode, frontier]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     ranks = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(2)]
-    g = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
-    U, I, E, DUP, D, K, B = (int(x) for x in g["meta"])
-    e, cred, u0, i0 = g["edges"], g["cred"], g["u0"], g["i0"]
+    if mode == "strong":
+        g = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
+        U, I, E, DUP, D, K, B = (int(x) for x in g["meta"])
+        e, cred, u0, i0 = g["edges"], g["cred"], g["u0"], g["i0"]
+    else:   # the union of the two shards is the global graph
+        sys.path.insert(0, HERE)
+        from dist_worker import WEAK_I, WEAK_U
+        parts = [np.load(tmp_path / f"edges{k}.npy") for k in range(2)]
+        parts[1] = parts[1] + np.array([[WEAK_U], [0]], np.int32)
+        e = np.concatenate(parts, 1)
+        U, I, K = 2 * WEAK_U, WEAK_I, 3
+        cred = None
+        rng = np.random.default_rng(5)
+        u0 = rng.uniform(-1, 1, (U, 64)).astype(np.float32)
+        i0 = rng.uniform(-1, 1, (I, 64)).astype(np.float32)
     # replicas of the item side are bitwise identical across ranks
     np.testing.assert_array_equal(ranks[0]["item_w"], ranks[1]["item_w"])
     np.testing.assert_array_equal(ranks[0]["g_i0"], ranks[1]["g_i0"])
@@ -62,8 +76,14 @@ def test_sharded_step_two_ranks_vs_oracle(tmp_path, variant):
         err = np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)
         assert err <= tol, f"{what}: {err:.3e}"
 
-    close(np.concatenate([r["uf"] for r in ranks]), uf, "u_final")
-    close(ranks[0]["itf"], itf, "i_final")
+    if frontier == "dense":   # frontier mode leaves non-batch final rows stale
+        close(np.concatenate([r["uf"] for r in ranks]), uf, "u_final")
+        close(ranks[0]["itf"], itf, "i_final")
+    else:
+        bu = users
+        close(np.concatenate([r["uf"] for r in ranks])[bu], uf[bu], "u_final @ batch")
+        bi = np.concatenate([pos, neg])
+        close(ranks[0]["itf"][bi], itf[bi], "i_final @ batch")
     close(np.concatenate([r["g_u0"] for r in ranks]), gu0, "grad u0")
     close(ranks[0]["g_i0"], gi0, "grad i0")
     assert abs(ranks[0]["loss"] - loss) <= 1e-5 * loss
