@@ -94,6 +94,7 @@ class ItemExchange:
 
     def __init__(self, group=None, parts: int = 4):
         self.group, self.parts = group, max(1, int(parts))
+        self.balance_indptr = None   # global item indptr: identical cuts on every rank
 
     def __call__(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
@@ -103,7 +104,7 @@ class ItemExchange:
         row_mask = kw.pop("row_mask", None)
         t = new("partial", prod.csr.n_rows)
         works = []
-        for rg in prod.csr.row_ranges(self.parts):
+        for rg in prod.csr.row_ranges(self.parts, self.balance_indptr):
             spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, rng=rg)
             works.append(dist.all_reduce(t[rg[0]:rg[1]], op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True))
@@ -142,6 +143,7 @@ class ShardedTrainer:
 
         self.graph = BipartiteGraph(local_edges, num_local_users, num_items, dev)
         indptr_i = global_item_indptr(self.graph.item_csr.degrees(), group)
+        self.exchange.balance_indptr = indptr_i
         cred_t = None
         if cred is not None and kind != OP_SYM:
             cred_t = torch.as_tensor(np.asarray(cred, np.float32)).to(dev).contiguous()

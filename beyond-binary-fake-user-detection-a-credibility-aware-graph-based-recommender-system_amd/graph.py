@@ -118,18 +118,22 @@ class Csr:
             s.chunks, s.split = ptr(self.chunks), ptr(self.split)
         return s
 
-    def row_ranges(self, parts: int) -> list:
+    def row_ranges(self, parts: int, balance_indptr: torch.Tensor | None = None) -> list:
         """Split rows into `parts` contiguous ranges of ~equal edge counts, each as
         (row0, row1, chunk0, chunk1, split0, split1) for bbgr_spmm's range mode.
+        `balance_indptr` (default: this CSR's) sets the row boundaries — sharded
+        ranks pass the GLOBAL item indptr so every rank cuts at the same rows.
         One host copy of indptr / plan at first use (setup-time)."""
-        key = int(parts)
+        key = (int(parts), None if balance_indptr is None else balance_indptr.data_ptr())
         cache = self.__dict__.setdefault("_ranges", {})
         if key in cache:
             return cache[key]
-        indptr = self.indptr.cpu().numpy().astype(np.int64)
+        src = self.indptr if balance_indptr is None else balance_indptr
+        indptr = src.cpu().numpy().astype(np.int64)
+        total = int(indptr[-1])
         ch_rows = self.chunks[: 4 * self.n_chunks].view(-1, 4)[:, 0].cpu().numpy()
         sp_rows = self.split[: 4 * self.n_split].view(-1, 4)[:, 0].cpu().numpy()
-        targets = [self.nnz * k // parts for k in range(parts + 1)]
+        targets = [total * k // parts for k in range(parts + 1)]
         bounds = np.searchsorted(indptr, targets, side="left")
         bounds[0], bounds[-1] = 0, self.n_rows
         bounds = np.maximum.accumulate(np.minimum(bounds, self.n_rows))
