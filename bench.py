@@ -106,8 +106,18 @@ def cpu_baseline(edges, cfg, batch, sample_users=256):
 cfg_name_global = "C4"
 
 
+def _quiet_stdout():
+    """Route fd 1 to stderr (collective libraries print banners on stdout) and
+    return a writer for the real stdout: the JSON line is its only content."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(saved, "w")
+
+
 def main():
     global cfg_name_global
+    out_stream = _quiet_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -251,7 +261,7 @@ def main():
                      "avg_launch_ms": tot_ms / max(n_launch, 1), "per_operator": per_kernel},
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},
     }
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=out_stream, flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
