@@ -37,6 +37,9 @@ DEFAULT_CHUNK_EDGES = 2048
 
 
 def _as_device_i32(x, device) -> torch.Tensor:
+    if isinstance(x, np.ndarray) and x.dtype == np.int32 and x.ndim == 1:
+        from .ingest import to_device_i32    # chunked, works on memory maps
+        return to_device_i32(x, device)
     if isinstance(x, np.ndarray):
         t = torch.from_numpy(np.ascontiguousarray(x.astype(np.int32, copy=False)))
     else:
@@ -181,14 +184,18 @@ class BipartiteGraph:
                  long_threshold: int = DEFAULT_LONG_THRESHOLD,
                  chunk_edges: int = DEFAULT_CHUNK_EDGES):
         device = torch.device(device)
-        if isinstance(train_edges_2xE, torch.Tensor):
-            e = train_edges_2xE
+        if isinstance(train_edges_2xE, tuple):        # graph.py's (u2i_src, u2i_dst)
+            src, dst = train_edges_2xE
         else:
-            e = np.asarray(train_edges_2xE)
-        if e.shape[0] != 2:
-            raise ValueError("train_edges must have shape [2, E]")
-        u = _as_device_i32(e[0], device)
-        i = _as_device_i32(e[1], device)
+            e = train_edges_2xE if isinstance(train_edges_2xE, torch.Tensor) \
+                else np.asarray(train_edges_2xE)
+            if e.shape[0] != 2:
+                raise ValueError("train_edges must have shape [2, E]")
+            src, dst = e[0], e[1]
+        if len(src) != len(dst):
+            raise ValueError("source and destination arrays differ in length")
+        u = _as_device_i32(src, device)
+        i = _as_device_i32(dst, device)
         self.num_users, self.num_items = int(num_users), int(num_items)
         self.nnz = int(u.numel())
         self.device = device

@@ -547,3 +547,19 @@ def test_frontier_step_matches_dense_step(variant):
             assert err <= 1e-6, (what, float(err))
     # masks are left clean for the next step
     assert int(front.mask_u.sum()) == 0 and int(front.mask_i.sum()) == 0
+
+
+def test_graph_from_memmaps_matches_array(tmp_path):
+    from bbgr import ingest
+    e = synthetic_edges(500, 300, 6000, 12, items="zipf")
+    np.save(tmp_path / "train_edges.npy", e)
+    for name, arr in (("u2i_src.mmap", e[0]), ("u2i_dst.mmap", e[1])):
+        m = np.memmap(tmp_path / name, dtype=np.int32, mode="w+", shape=arr.shape)
+        m[:] = arr
+        m.flush()
+    g1 = BipartiteGraph(e, 500, 300, DEV)
+    g2 = BipartiteGraph(ingest.load_edges_npy(tmp_path / "train_edges.npy"), 500, 300, DEV)
+    g3 = BipartiteGraph(ingest.load_u2i_memmap(tmp_path), 500, 300, DEV)
+    for g in (g2, g3):
+        assert torch.equal(g.user_csr.indptr, g1.user_csr.indptr)
+        assert torch.equal(g.item_csr.indices, g1.item_csr.indices)
