@@ -101,6 +101,22 @@ class BprArgs(ctypes.Structure):
     ]
 
 
+class EvalArgs(ctypes.Structure):
+    _fields_ = [
+        ("n_users", c_int64), ("users", c_void_p),
+        ("te_indptr", c_void_p), ("te_indices", c_void_p),
+        ("tr_indptr", c_void_p), ("tr_indices", c_void_p),
+        ("uf", c_void_p), ("lduf", c_int64), ("itf", c_void_p), ("ldif", c_int64),
+        ("d", c_int32), ("n_items", c_int32), ("n_neg", c_int32), ("k_max", c_int32),
+        ("n_k", c_int32), ("ks", c_int32 * 8),
+        ("seed", c_uint64), ("counter", c_uint64),
+        ("item_pop", c_void_p), ("self_info_denom", c_float), ("group", c_void_p),
+        ("pos_rank", c_void_p), ("topk", c_void_p), ("cand_out", c_void_p),
+        ("fail_count", c_void_p), ("stats", c_void_p), ("covered", c_void_p),
+        ("sums", c_void_p),
+    ]
+
+
 _P = c_void_p
 _SIGNATURES = {
     "bbgr_abi_version": ([], c_int32),
@@ -134,6 +150,7 @@ _SIGNATURES = {
                      c_uint64, _P, _P, _P, _P], c_int32),
     "bbgr_shuffle": ([c_int64, _P, _P, c_uint64, c_uint64, _P,
                       ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_eval_sampled": ([ctypes.POINTER(EvalArgs), _P], c_int32),
     "bbgr_nonempty_rows": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P],
                            c_int32),
 }

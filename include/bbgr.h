@@ -342,6 +342,56 @@ int bbgr_nonempty_rows(int32_t n_rows, const int32_t *indptr, int64_t *out,
                        int64_t *count, void *workspace, size_t *workspace_bytes,
                        bbgr_stream_t stream);
 
+/* ------------------------------------------------------------------------- */
+/* Sampled evaluation                                    */
+/*   Replaces evaluate_sampled, Version-2/lighgcn_cu_pop.py:536-650 (+        */
+/*   metrics_at_k :514-531, novelty_stats_for_items :390-405): for each       */
+/*   evaluated user, pos uniform from the test row, n_neg negatives uniform   */
+/*   from [0, n_items) rejecting test and train items (duplicates allowed),   */
+/*   1+n_neg candidates scored <uf[u], itf[c]> and ranked descending with     */
+/*   ties broken by candidate order (pos first). Users without test items get */
+/*   pos_rank = -1 and are not counted.                                       */
+/* Outputs: pos_rank[n_users], topk[n_users*k_max] (-1 padded), optional     */
+/* cand_out[n_users*(1+n_neg)], and sums[n_k*11] per K =                      */
+/*   {sum P, sum R, sum NDCG, sum avg log(pop+1), sum avg self-info,          */
+/*    sum R over high-cred users, sum R over low-cred users, #high, #low,     */
+/*    #evaluated users, #distinct top-K items (coverage numerator)}.          */
+/* Workspace: stats[n_users*n_k*6] floats, covered[n_k*n_items] bytes.        */
+/* group[b]: bit0 = top-pct credibility user, bit1 = bottom-pct (nullable).   */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int64_t n_users;
+  const int64_t *users;
+  const int32_t *te_indptr;
+  const int32_t *te_indices;
+  const int32_t *tr_indptr;
+  const int32_t *tr_indices;
+  const float *uf;
+  int64_t lduf;
+  const float *itf;
+  int64_t ldif;
+  int32_t d;
+  int32_t n_items;
+  int32_t n_neg;
+  int32_t k_max;
+  int32_t n_k;
+  int32_t ks[8];
+  uint64_t seed;
+  uint64_t counter;
+  const float *item_pop;
+  float self_info_denom; /* total_train_interactions + n_items */
+  const uint8_t *group;
+  int32_t *pos_rank;
+  int32_t *topk;
+  int32_t *cand_out;
+  int32_t *fail_count;
+  float *stats;
+  uint8_t *covered;
+  float *sums;
+} bbgr_eval_args;
+
+int bbgr_eval_sampled(const bbgr_eval_args *args, bbgr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

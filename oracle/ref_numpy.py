@@ -290,3 +290,66 @@ def xavier_uniform(rows, cols, rng):
     """torch.nn.init.xavier_uniform_ bound for an [rows, cols] weight."""
     a = np.sqrt(6.0 / (rows + cols))
     return rng.uniform(-a, a, size=(rows, cols)).astype(np.float32)
+
+
+# ---------------------------------------------------------------------------
+# Sampled evaluation given the candidates (Version-2/lighgcn_cu_pop.py:514-650)
+# ---------------------------------------------------------------------------
+def metrics_at_k(ranked_items, gt_set, K):
+    """Version-2/lighgcn_cu_pop.py:514-531."""
+    import math
+    topk = ranked_items[:K]
+    hits = [1 if x in gt_set else 0 for x in topk]
+    hit_count = sum(hits)
+    precision = hit_count / K
+    recall = hit_count / max(len(gt_set), 1)
+    dcg = sum(1.0 / math.log2(idx + 2) for idx, h in enumerate(hits) if h)
+    ideal = min(len(gt_set), K)
+    idcg = sum(1.0 / math.log2(i + 2) for i in range(ideal))
+    return precision, recall, (dcg / idcg) if idcg > 0 else 0.0
+
+
+def evaluate_sampled_given(users, cands, uf, itf, item_pop, total_train, num_items, cred,
+                           groups_high, groups_low, Ks=(10, 20)):
+    """The reference's per-user loop (Version-2:574-650) on FIXED candidates
+    (cands[b] = [pos, neg_1..]), float64 scores, ranking by descending score
+    with ties in candidate order."""
+    uf, itf = np.asarray(uf, np.float64), np.asarray(itf, np.float64)
+    item_pop = np.asarray(item_pop, np.float64)
+    sums = {K: dict(p=0.0, r=0.0, n=0.0, lp=0.0, si=0.0) for K in Ks}
+    rec = {K: set() for K in Ks}
+    grp = {K: dict(hr=0.0, lr=0.0, hn=0, ln=0) for K in Ks}
+    high, low = set(map(int, groups_high)), set(map(int, groups_low))
+    cred_sum = 0.0
+    for u, cand in zip(users, cands):
+        cand = np.asarray(cand, np.int64)
+        scores = itf[cand] @ uf[int(u)]
+        ranked = cand[np.argsort(-scores, kind="stable")]
+        cred_sum += float(cred[int(u)])
+        for K in Ks:
+            topk = ranked[:K]
+            p, r, nd = metrics_at_k(ranked, {int(cand[0])}, K)
+            sums[K]["p"] += p
+            sums[K]["r"] += r
+            sums[K]["n"] += nd
+            rec[K].update(map(int, topk.tolist()))
+            pops = item_pop[topk]
+            sums[K]["lp"] += float(np.log(pops + 1.0).mean())
+            sums[K]["si"] += float((-np.log2((pops + 1.0) / (total_train + num_items))).mean())
+            if int(u) in high:
+                grp[K]["hr"] += r
+                grp[K]["hn"] += 1
+            if int(u) in low:
+                grp[K]["lr"] += r
+                grp[K]["ln"] += 1
+    n = len(users)
+    out = {}
+    for K in Ks:
+        out[K] = dict(precision=sums[K]["p"] / n, recall=sums[K]["r"] / n, ndcg=sums[K]["n"] / n,
+                      item_coverage=len(rec[K]) / num_items,
+                      avg_log_popularity=sums[K]["lp"] / n,
+                      avg_self_information=sums[K]["si"] / n, cred_utility=cred_sum / n,
+                      high_cred_recall=grp[K]["hr"] / max(grp[K]["hn"], 1),
+                      low_cred_recall=grp[K]["lr"] / max(grp[K]["ln"], 1),
+                      high_users=grp[K]["hn"], low_users=grp[K]["ln"])
+    return out

@@ -219,3 +219,24 @@ def test_edges_to_user_csr_sorted_rows():
     indptr, indices = R.edges_to_user_csr(e, 4)
     assert indptr.tolist() == [0, 2, 3, 5, 5]
     assert indices.tolist() == [0, 1, 2, 0, 3]
+
+
+def test_metrics_at_k_known_answers():
+    import math
+    p, r, n = R.metrics_at_k([5, 3, 9, 1], {3}, 2)
+    assert (p, r) == (0.5, 1.0) and n == pytest.approx(1 / math.log2(3))
+    p, r, n = R.metrics_at_k([5, 3, 9, 1], {7}, 4)
+    assert (p, r, n) == (0.0, 0.0, 0.0)
+    p, r, n = R.metrics_at_k([3, 5], {3, 5, 8}, 2)
+    assert p == 1.0 and r == pytest.approx(2 / 3) and n == pytest.approx(1.0)
+
+
+def test_evaluate_sampled_given_hand_case():
+    uf = np.array([[1.0, 0.0]])
+    itf = np.array([[0.9, 0], [0.5, 0], [1.0, 0], [0.1, 0]])
+    # cand = [pos=0, 1, 2, 3]; scores .9 .5 1 .1 -> ranked 2,0,1,3: pos at rank 1
+    res = R.evaluate_sampled_given([0], [[0, 1, 2, 3]], uf, itf, np.array([0, 1, 2, 3]),
+                                   10, 4, np.array([0.5]), [0], [], Ks=(1, 2))
+    assert res[1]["recall"] == 0.0 and res[2]["recall"] == 1.0
+    assert res[2]["ndcg"] == pytest.approx(1 / np.log2(3))
+    assert res[2]["item_coverage"] == 0.5 and res[2]["high_cred_recall"] == 1.0
