@@ -111,9 +111,8 @@ class EvalArgs(ctypes.Structure):
         ("n_k", c_int32), ("ks", c_int32 * 8),
         ("seed", c_uint64), ("counter", c_uint64),
         ("item_pop", c_void_p), ("self_info_denom", c_float), ("group", c_void_p),
-        ("pos_rank", c_void_p), ("topk", c_void_p), ("cand_out", c_void_p),
-        ("fail_count", c_void_p), ("stats", c_void_p), ("covered", c_void_p),
-        ("sums", c_void_p),
+        ("pos_rank", c_void_p), ("topk", c_void_p), ("topk_score", c_void_p),
+        ("cand_out", c_void_p), ("fail_count", c_void_p), ("sums", c_void_p),
     ]
 
 
@@ -150,7 +149,9 @@ _SIGNATURES = {
                      c_uint64, _P, _P, _P, _P], c_int32),
     "bbgr_shuffle": ([c_int64, _P, _P, c_uint64, c_uint64, _P,
                       ctypes.POINTER(c_size_t), _P], c_int32),
-    "bbgr_eval_sampled": ([ctypes.POINTER(EvalArgs), _P], c_int32),
+    "bbgr_eval_sampled": ([ctypes.POINTER(EvalArgs), _P, ctypes.POINTER(c_size_t), _P],
+                          c_int32),
+    "bbgr_eval_full": ([ctypes.POINTER(EvalArgs), _P, ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_nonempty_rows": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P],
                            c_int32),
 }

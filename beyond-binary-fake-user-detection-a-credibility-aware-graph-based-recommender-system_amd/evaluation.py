@@ -1,5 +1,5 @@
-"""GPU sampled evaluation: drop-in for evaluate_sampled
-(Version-2/lighgcn_cu_pop.py:536-650), SURVEY §8(f) row 1.
+"""GPU evaluation: drop-ins for evaluate_sampled (Version-2/lighgcn_cu_pop.py:
+536-650) and evaluate_full_ranking (:652-752), SURVEY §8(f) row 1.
 
 The reference loops over test users in Python (one torch scoring call and one
 device->host copy per user). Here one launch scores every evaluated user's
@@ -11,7 +11,7 @@ rejected if in the test row or the train row, duplicates allowed; ranking
 descending by score; P/R/NDCG@K with gt = {pos}; coverage = distinct top-K
 items / I; novelty over the top-K (avg log(pop+1), avg -log2((pop+1)/(T+I)));
 cred_utility = mean credibility of evaluated users; high/low groups = top /
-bottom `pct` of evaluated users by credibility (make_cred_groups :408-426).
+bottom `pct` of evaluated users by credibility (make_cred_groups :405-422).
 Differences (documented, distributional): the RNG is Philox, not numpy's
 PCG64 stream; exact score ties rank in candidate order (pos first) where the
 reference's quicksort argsort leaves the order unspecified; group membership
@@ -46,6 +46,63 @@ def cred_groups(users: torch.Tensor, cred: torch.Tensor, pct: float) -> torch.Te
     return flags
 
 
+def _tables(user_emb, item_emb, item_pop, cred, dev):
+    uf = user_emb.detach().to(torch.float32).contiguous()
+    itf = item_emb.detach().to(torch.float32).contiguous()
+    pop = torch.as_tensor(np.asarray(item_pop, np.float32) if not isinstance(item_pop, torch.Tensor)
+                          else item_pop).to(dev, torch.float32).contiguous()
+    cred_t = torch.as_tensor(np.asarray(cred, np.float32) if not isinstance(cred, torch.Tensor)
+                             else cred).to(dev, torch.float32).contiguous()
+    return uf, itf, pop, cred_t
+
+
+def _args(users, train_csr, test_csr, uf, itf, num_items, Ks, pop, total_train, groups, sums):
+    a = _lib.EvalArgs()
+    a.n_users, a.users = users.numel(), ptr(users)
+    a.te_indptr, a.te_indices = ptr(test_csr.indptr), ptr(test_csr.indices)
+    a.tr_indptr, a.tr_indices = ptr(train_csr.indptr), ptr(train_csr.indices)
+    a.uf, a.lduf, a.itf, a.ldif = ptr(uf), ld(uf), ptr(itf), ld(itf)
+    a.d, a.n_items, a.k_max, a.n_k = uf.shape[1], num_items, max(Ks), len(Ks)
+    for q, k in enumerate(Ks):
+        a.ks[q] = k
+    a.item_pop, a.self_info_denom = ptr(pop), float(total_train + num_items)
+    a.group, a.sums = ptr(groups), ptr(sums)
+    return a
+
+
+def _run(fn, a, dev):
+    n = ctypes.c_size_t(0)
+    call(fn, ctypes.byref(a), None, ctypes.byref(n), stream_handle())
+    ws = torch.empty(max(n.value, 1), dtype=torch.uint8, device=dev)
+    call(fn, ctypes.byref(a), ptr(ws), ctypes.byref(n), stream_handle())
+    return ws
+
+
+def _results(sums, Ks, num_items, cred_utility, mode, extra):
+    s = sums.view(len(Ks), NOUT).cpu().numpy()
+    results = {}
+    for q, K in enumerate(Ks):
+        p, r, nd, lp, si, hr, lr, hn, lnn, ne, cov = s[q]
+        nd_ = max(ne, 1.0)
+        results[K] = {
+            "precision": p / nd_, "recall": r / nd_, "ndcg": nd / nd_,
+            "item_coverage": cov / max(num_items, 1),
+            "avg_log_popularity": lp / nd_, "avg_self_information": si / nd_,
+            "cred_utility": cred_utility,
+            "high_cred_recall": hr / max(hn, 1.0), "low_cred_recall": lr / max(lnn, 1.0),
+            "high_users": int(hn), "low_users": int(lnn),
+            "users_eval": int(ne), "mode": mode, **extra,
+        }
+    return results
+
+
+def _eval_users(test_csr):
+    users = nonempty_rows(test_csr)
+    if users.numel() == 0:
+        raise RuntimeError("No users with test interactions. Check your split or threshold.")
+    return users
+
+
 def evaluate_sampled(user_emb: torch.Tensor, item_emb: torch.Tensor, train_csr: Csr,
                      test_csr: Csr, num_items: int, item_pop, total_train_interactions: int,
                      cred, Ks=(10, 20), sampled_negatives: int = 99,
@@ -54,58 +111,57 @@ def evaluate_sampled(user_emb: torch.Tensor, item_emb: torch.Tensor, train_csr: 
     """Reference-shaped results {K: {...}} for the sampled protocol."""
     _lib.require_gpu(user_emb)
     dev = user_emb.device
-    users = nonempty_rows(test_csr)
-    if users.numel() == 0:
-        raise RuntimeError("No users with test interactions. Check your split or threshold.")
+    users = _eval_users(test_csr)
     n = users.numel()
     Ks = tuple(int(k) for k in Ks)
-    k_max, n_k, nc = max(Ks), len(Ks), 1 + int(sampled_negatives)
-    uf = user_emb.detach().to(torch.float32).contiguous()
-    itf = item_emb.detach().to(torch.float32).contiguous()
-    pop = torch.as_tensor(np.asarray(item_pop, np.float32) if not isinstance(item_pop, torch.Tensor)
-                          else item_pop).to(dev, torch.float32).contiguous()
-    cred_t = torch.as_tensor(np.asarray(cred, np.float32) if not isinstance(cred, torch.Tensor)
-                             else cred).to(dev, torch.float32).contiguous()
+    nc = 1 + int(sampled_negatives)
+    uf, itf, pop, cred_t = _tables(user_emb, item_emb, item_pop, cred, dev)
     groups = cred_groups(users, cred_t, cred_group_pct)
     i32 = dict(dtype=torch.int32, device=dev)
     pos_rank = torch.empty(n, **i32)
-    topk = torch.empty(n * k_max, **i32)
+    topk = torch.empty(n * max(Ks), **i32)
     cand = torch.empty(n * nc, **i32) if return_raw else None
     fails = torch.zeros(1, **i32)
-    stats = torch.empty(n * n_k * 6, dtype=torch.float32, device=dev)
-    covered = torch.empty(n_k * num_items, dtype=torch.uint8, device=dev)
-    sums = torch.empty(n_k * NOUT, dtype=torch.float32, device=dev)
-    a = _lib.EvalArgs()
-    a.n_users, a.users = n, ptr(users)
-    a.te_indptr, a.te_indices = ptr(test_csr.indptr), ptr(test_csr.indices)
-    a.tr_indptr, a.tr_indices = ptr(train_csr.indptr), ptr(train_csr.indices)
-    a.uf, a.lduf, a.itf, a.ldif = ptr(uf), ld(uf), ptr(itf), ld(itf)
-    a.d, a.n_items, a.n_neg, a.k_max, a.n_k = uf.shape[1], num_items, nc - 1, k_max, n_k
-    for q, k in enumerate(Ks):
-        a.ks[q] = k
-    a.seed, a.counter = int(seed), int(counter)
-    a.item_pop, a.self_info_denom = ptr(pop), float(total_train_interactions + num_items)
-    a.group = ptr(groups)
+    sums = torch.empty(len(Ks) * NOUT, dtype=torch.float64, device=dev)
+    a = _args(users, train_csr, test_csr, uf, itf, num_items, Ks, pop,
+              total_train_interactions, groups, sums)
+    a.n_neg, a.seed, a.counter = nc - 1, int(seed), int(counter)
     a.pos_rank, a.topk, a.cand_out, a.fail_count = ptr(pos_rank), ptr(topk), ptr(cand), ptr(fails)
-    a.stats, a.covered, a.sums = ptr(stats), ptr(covered), ptr(sums)
-    call("bbgr_eval_sampled", ctypes.byref(a), stream_handle())
-    s = sums.view(n_k, NOUT).double().cpu().numpy()
-    cred_utility = float(cred_t[users].double().mean())
-    results = {}
-    for q, K in enumerate(Ks):
-        p, r, nd, lp, si, hr, lr, hn, lnn, ne, cov = s[q]
-        ne = max(ne, 1.0)
-        results[K] = {
-            "precision": p / ne, "recall": r / ne, "ndcg": nd / ne,
-            "item_coverage": cov / max(num_items, 1),
-            "avg_log_popularity": lp / ne, "avg_self_information": si / ne,
-            "cred_utility": cred_utility,
-            "high_cred_recall": hr / max(hn, 1.0), "low_cred_recall": lr / max(lnn, 1.0),
-            "high_users": int(hn), "low_users": int(lnn),
-            "users_eval": int(s[q][9]), "mode": "sampled(1pos+neg)",
-            "negatives": int(sampled_negatives),
-        }
+    _run("bbgr_eval_sampled", a, dev)
+    results = _results(sums, Ks, num_items, float(cred_t[users].double().mean()),
+                       "sampled(1pos+neg)", {"negatives": int(sampled_negatives)})
     if return_raw:
-        results["_raw"] = dict(users=users, pos_rank=pos_rank, topk=topk.view(n, k_max),
+        results["_raw"] = dict(users=users, pos_rank=pos_rank, topk=topk.view(n, max(Ks)),
                                cand=cand.view(n, nc), groups=groups, fails=int(fails.item()))
+    return results
+
+
+def evaluate_full(user_emb: torch.Tensor, item_emb: torch.Tensor, train_csr: Csr,
+                  test_csr: Csr, num_items: int, item_pop, total_train_interactions: int,
+                  cred, Ks=(10, 20), cred_group_pct: float = 0.20, return_raw: bool = False):
+    """Drop-in for evaluate_full_ranking (Version-2/lighgcn_cu_pop.py:652-752).
+
+    One bbgr_eval_full call scores every (evaluated user, item) pair with fp32
+    MFMA, masks train items to -1e9 and keeps the top-max(Ks) per user in
+    registers (no U x I score matrix is ever written), then reduces the
+    metrics. Ranking ties (unspecified in the reference's torch.argsort) go
+    to the lower item id."""
+    _lib.require_gpu(user_emb)
+    dev = user_emb.device
+    users = _eval_users(test_csr)
+    n = users.numel()
+    Ks = tuple(int(k) for k in Ks)
+    uf, itf, pop, cred_t = _tables(user_emb, item_emb, item_pop, cred, dev)
+    groups = cred_groups(users, cred_t, cred_group_pct)
+    topk = torch.empty(n * max(Ks), dtype=torch.int32, device=dev)
+    topk_score = torch.empty(n * max(Ks), dtype=torch.float32, device=dev) if return_raw else None
+    sums = torch.empty(len(Ks) * NOUT, dtype=torch.float64, device=dev)
+    a = _args(users, train_csr, test_csr, uf, itf, num_items, Ks, pop,
+              total_train_interactions, groups, sums)
+    a.topk, a.topk_score = ptr(topk), ptr(topk_score)
+    _run("bbgr_eval_full", a, dev)
+    results = _results(sums, Ks, num_items, float(cred_t[users].double().mean()), "full", {})
+    if return_raw:
+        results["_raw"] = dict(users=users, topk=topk.view(n, max(Ks)),
+                               topk_score=topk_score.view(n, max(Ks)), groups=groups)
     return results

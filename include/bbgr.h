@@ -343,21 +343,28 @@ int bbgr_nonempty_rows(int32_t n_rows, const int32_t *indptr, int64_t *out,
                        bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
-/* Sampled evaluation                                    */
-/*   Replaces evaluate_sampled, Version-2/lighgcn_cu_pop.py:536-650 (+        */
-/*   metrics_at_k :514-531, novelty_stats_for_items :390-405): for each       */
-/*   evaluated user, pos uniform from the test row, n_neg negatives uniform   */
-/*   from [0, n_items) rejecting test and train items (duplicates allowed),   */
-/*   1+n_neg candidates scored <uf[u], itf[c]> and ranked descending with     */
-/*   ties broken by candidate order (pos first). Users without test items get */
-/*   pos_rank = -1 and are not counted.                                       */
-/* Outputs: pos_rank[n_users], topk[n_users*k_max] (-1 padded), optional     */
-/* cand_out[n_users*(1+n_neg)], and sums[n_k*11] per K =                      */
+/* Evaluation                                            */
+/*   bbgr_eval_sampled replaces evaluate_sampled,                             */
+/*   Version-2/lighgcn_cu_pop.py:536-650; bbgr_eval_full replaces             */
+/*   evaluate_full_ranking, :652-752 (both + metrics_at_k :514-531,           */
+/*   novelty_stats_for_items :390-405).                                       */
+/* users[n_users]: the evaluated users (rows of the test CSR that are not     */
+/* empty, ascending). group[b]: bit0 = top-pct credibility user, bit1 =       */
+/* bottom-pct (make_cred_groups :405-422; nullable).                          */
+/* Sampled: pos uniform from the test row, n_neg negatives uniform from       */
+/*   [0, n_items) rejecting test and train items (duplicates allowed),        */
+/*   1+n_neg candidates scored <uf[u], itf[c]> and ranked descending, ties    */
+/*   in candidate order (pos first). Writes pos_rank[n_users],                */
+/*   topk[n_users*k_max] (-1 padded), optional cand_out[n_users*(1+n_neg)].   */
+/* Full: every item scored <uf[u], itf[i]> with fp32 MFMA (one fmaf chain    */
+/*   per score, components in the order 0, d/2, 1, d/2+1, ...), train items   */
+/*   set to -1e9, ranked by (score desc, item asc); topk[n_users*k_max] and   */
+/*   optional topk_score[n_users*k_max]. k_max <= 32, d in {64, 128}.         */
+/* Both write sums[n_k*11] (double) per K =                                   */
 /*   {sum P, sum R, sum NDCG, sum avg log(pop+1), sum avg self-info,          */
 /*    sum R over high-cred users, sum R over low-cred users, #high, #low,     */
-/*    #evaluated users, #distinct top-K items (coverage numerator)}.          */
-/* Workspace: stats[n_users*n_k*6] floats, covered[n_k*n_items] bytes.        */
-/* group[b]: bit0 = top-pct credibility user, bit1 = bottom-pct (nullable).   */
+/*    #evaluated users, #distinct top-K items (coverage numerator)},          */
+/* reduced in a fixed order (bitwise reproducible).                           */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int64_t n_users;
@@ -372,25 +379,27 @@ typedef struct {
   int64_t ldif;
   int32_t d;
   int32_t n_items;
-  int32_t n_neg;
+  int32_t n_neg;           /* sampled only */
   int32_t k_max;
   int32_t n_k;
   int32_t ks[8];
-  uint64_t seed;
-  uint64_t counter;
+  uint64_t seed;           /* sampled only */
+  uint64_t counter;        /* sampled only */
   const float *item_pop;
-  float self_info_denom; /* total_train_interactions + n_items */
+  float self_info_denom;   /* total_train_interactions + n_items */
   const uint8_t *group;
-  int32_t *pos_rank;
+  int32_t *pos_rank;       /* sampled only */
   int32_t *topk;
-  int32_t *cand_out;
-  int32_t *fail_count;
-  float *stats;
-  uint8_t *covered;
-  float *sums;
+  float *topk_score;       /* full only, nullable */
+  int32_t *cand_out;       /* sampled only, nullable */
+  int32_t *fail_count;     /* sampled only, nullable */
+  double *sums;
 } bbgr_eval_args;
 
-int bbgr_eval_sampled(const bbgr_eval_args *args, bbgr_stream_t stream);
+int bbgr_eval_sampled(const bbgr_eval_args *args, void *workspace, size_t *workspace_bytes,
+                      bbgr_stream_t stream);
+int bbgr_eval_full(const bbgr_eval_args *args, void *workspace, size_t *workspace_bytes,
+                   bbgr_stream_t stream);
 
 #ifdef __cplusplus
 }

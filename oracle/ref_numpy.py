@@ -353,3 +353,98 @@ def evaluate_sampled_given(users, cands, uf, itf, item_pop, total_train, num_ite
                       low_cred_recall=grp[K]["lr"] / max(grp[K]["ln"], 1),
                       high_users=grp[K]["hn"], low_users=grp[K]["ln"])
     return out
+
+
+def make_cred_groups(users, cred, pct):
+    """Version-2/lighgcn_cu_pop.py:405-422 (argsort ascending; top / bottom k)."""
+    users = np.asarray(users, np.int64)
+    if users.size == 0:
+        return np.array([], np.int64), np.array([], np.int64)
+    k = max(int(round(users.size * pct)), 1)
+    order = np.argsort(np.asarray(cred)[users])
+    return users[order[-k:]], users[order[:k]]
+
+
+def evaluate_sampled_reference_style(tr_ptr, tr_idx, te_ptr, te_idx, uf, itf, num_items, item_pop,
+                                     total_train, cred, Ks=(10, 20), n_neg=99, pct=0.2, seed=1041,
+                                     users=None):
+    """The whole reference loop (Version-2:536-650) including its numpy
+    sampling stream (default_rng(seed); pos via integers(0, len(gt)); negatives
+    by rejection on gt_set and user_has_item). `users` restricts the loop to a
+    subset (the CPU-baseline sample); returns (results, candidates)."""
+    rng = np.random.default_rng(seed)
+    if users is None:
+        users = np.where(np.diff(te_ptr) > 0)[0].astype(np.int64)
+    cands = []
+    for u in users:
+        gt = te_idx[te_ptr[u]:te_ptr[u + 1]]
+        gt_set = set(map(int, gt.tolist()))
+        pos = int(gt[rng.integers(0, len(gt))])
+        negs = []
+        while len(negs) < n_neg:
+            j = int(rng.integers(0, num_items))
+            if j in gt_set or user_has_item(tr_ptr, tr_idx, int(u), j):
+                continue
+            negs.append(j)
+        cands.append([pos] + negs)
+    high, low = make_cred_groups(users, cred, pct)
+    res = evaluate_sampled_given(users, np.asarray(cands, np.int64).reshape(len(users), 1 + n_neg),
+                                 uf, itf, item_pop, total_train, num_items, cred, high, low, Ks)
+    return res, cands
+
+
+def evaluate_given_topk(users, topk, te_ptr, te_idx, item_pop, total_train, num_items, cred,
+                        groups_high, groups_low, Ks=(10, 20), mode="full"):
+    """The reference's metric loop (Version-2:690-752 full / :600-650 sampled)
+    on FIXED ranked lists topk[b] (>= max(Ks) items, -1 padded); gt = the
+    user's test row (full ranking)."""
+    item_pop = np.asarray(item_pop, np.float64)
+    sums = {K: dict(p=0.0, r=0.0, n=0.0, lp=0.0, si=0.0) for K in Ks}
+    rec = {K: set() for K in Ks}
+    grp = {K: dict(hr=0.0, lr=0.0, hn=0, ln=0) for K in Ks}
+    high, low = set(map(int, groups_high)), set(map(int, groups_low))
+    cred_sum = 0.0
+    for u, ranked in zip(users, topk):
+        gt = set(map(int, te_idx[te_ptr[u]:te_ptr[u + 1]].tolist()))
+        ranked = np.asarray([x for x in ranked if x >= 0], np.int64)
+        cred_sum += float(cred[int(u)])
+        for K in Ks:
+            top = ranked[:K]
+            p, r, nd = metrics_at_k(ranked, gt, K)
+            sums[K]["p"] += p
+            sums[K]["r"] += r
+            sums[K]["n"] += nd
+            rec[K].update(map(int, top.tolist()))
+            if top.size:
+                pops = item_pop[top]
+                sums[K]["lp"] += float(np.log(pops + 1.0).mean())
+                sums[K]["si"] += float((-np.log2((pops + 1.0) / (total_train + num_items))).mean())
+            if int(u) in high:
+                grp[K]["hr"] += r
+                grp[K]["hn"] += 1
+            if int(u) in low:
+                grp[K]["lr"] += r
+                grp[K]["ln"] += 1
+    n = len(users)
+    return {K: dict(precision=sums[K]["p"] / n, recall=sums[K]["r"] / n, ndcg=sums[K]["n"] / n,
+                    item_coverage=len(rec[K]) / num_items,
+                    avg_log_popularity=sums[K]["lp"] / n,
+                    avg_self_information=sums[K]["si"] / n, cred_utility=cred_sum / n,
+                    high_cred_recall=grp[K]["hr"] / max(grp[K]["hn"], 1),
+                    low_cred_recall=grp[K]["lr"] / max(grp[K]["ln"], 1),
+                    high_users=grp[K]["hn"], low_users=grp[K]["ln"]) for K in Ks}
+
+
+def full_ranking_reference_style(users, tr_ptr, tr_idx, uf, itf, k):
+    """The reference's per-user full ranking (Version-2:690-706): fp32 scores
+    over every item, train items at -1e9, argsort descending (stable here:
+    ties by item id), top-k. Returns [n, k] int64."""
+    itf = np.asarray(itf, np.float32)
+    out = np.empty((len(users), k), np.int64)
+    for b, u in enumerate(users):
+        scores = (np.asarray(uf[int(u)], np.float32)[None, :] * itf).sum(axis=1)
+        tr = tr_idx[tr_ptr[u]:tr_ptr[u + 1]]
+        if tr.size:
+            scores[tr] = np.float32(-1e9)
+        out[b] = np.argsort(-scores, kind="stable")[:k]
+    return out

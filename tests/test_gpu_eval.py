@@ -85,3 +85,74 @@ def test_eval_known_ranking():
                            np.zeros(I), 1, np.ones(U), Ks=(1, 10))
     assert res[1]["recall"] == 1.0 and res[1]["precision"] == 1.0 and res[1]["ndcg"] == 1.0
     assert res[10]["precision"] == pytest.approx(0.1)
+
+
+def _full_case(U, I, E, d, seed, heavy_user=False):
+    tr, te = _split(U, I, E, seed)
+    if heavy_user:   # user 0 has trained all but 5 items: its top-20 ends in -1e9 entries
+        keep = tr[0] != 0
+        tr = np.concatenate([tr[:, keep], np.stack([np.zeros(I - 5, np.int32),
+                                                    np.arange(5, I, dtype=np.int32)])], axis=1)
+        te = np.concatenate([te[:, te[0] != 0], np.array([[0], [1]], np.int32)], axis=1)
+    rng = np.random.default_rng(seed + 1)
+    uf = rng.normal(size=(U, d)).astype(np.float32)
+    itf = rng.normal(size=(I, d)).astype(np.float32)
+    return tr, te, uf, itf
+
+
+@pytest.mark.parametrize("d,U,I,Ks", [(64, 2000, 1500, (10, 20)), (64, 700, 4099, (5, 32)),
+                                      (128, 300, 777, (16,)), (64, 130, 60, (20,))])
+def test_eval_full_bitexact_vs_c_oracle(d, U, I, Ks):
+    """bbgr_eval_full top-K ids AND scores are bit-identical to the C oracle's
+    fma chain (oracle/csrc/eval_full.c); metrics equal the reference's metric
+    loop (oracle evaluate_given_topk) on those lists. Covers item splits,
+    ragged user / item tiles, KM = 16/24/32, d = 128, n_items < 128."""
+    from bbgr.evaluation import evaluate_full
+    from oracle import native as N
+    tr, te, uf, itf = _full_case(U, I, 20 * U, d, 11, heavy_user=True)
+    trc, tec = Csr(tr[0], tr[1], U, I, DEV), Csr(te[0], te[1], U, I, DEV)
+    pop = np.bincount(tr[1], minlength=I)
+    cred = synthetic_credibility(U, 4)
+    res = evaluate_full(torch.tensor(uf, device=DEV), torch.tensor(itf, device=DEV), trc, tec, I,
+                        pop, int(tr.shape[1]), cred, Ks=Ks, return_raw=True)
+    raw = res.pop("_raw")
+    users = raw["users"].cpu().numpy()
+    topk = raw["topk"].cpu().numpy()
+    score = raw["topk_score"].cpu().numpy()
+    tr_ptr, tr_idx = R.edges_to_user_csr(tr, U)
+    te_ptr, te_idx = R.edges_to_user_csr(te, U)
+    o_items, o_scores = N.full_topk(users, tr_ptr, tr_idx, uf, itf, max(Ks))
+    o_items = np.where(np.isneginf(o_scores), -1, o_items)
+    np.testing.assert_array_equal(topk, o_items)
+    np.testing.assert_array_equal(score.view(np.uint32), o_scores.view(np.uint32))
+    flags = raw["groups"].cpu().numpy()
+    ref = R.evaluate_given_topk(users, o_items, te_ptr, te_idx, pop, int(tr.shape[1]), I, cred,
+                                users[flags & 1 > 0], users[flags & 2 > 0], Ks=Ks)
+    for K in Ks:
+        for k in ref[K]:
+            assert res[K][k] == pytest.approx(ref[K][k], rel=1e-9, abs=1e-12), (K, k)
+        assert res[K]["mode"] == "full" and res[K]["users_eval"] == users.size
+
+
+def test_eval_full_matches_reference_ranking():
+    """Against the reference's own ranking expression (numpy fp32 product-sum,
+    -1e9 mask, argsort): identical lists except near-ties of fp32 noise."""
+    from bbgr.evaluation import evaluate_full
+    U, I, d = 500, 2000, 64
+    tr, te, uf, itf = _full_case(U, I, 8000, d, 21)
+    trc, tec = Csr(tr[0], tr[1], U, I, DEV), Csr(te[0], te[1], U, I, DEV)
+    res = evaluate_full(torch.tensor(uf, device=DEV), torch.tensor(itf, device=DEV), trc, tec, I,
+                        np.bincount(tr[1], minlength=I), int(tr.shape[1]), np.ones(U), Ks=(20,),
+                        return_raw=True)
+    raw = res.pop("_raw")
+    users = raw["users"].cpu().numpy()
+    topk = raw["topk"].cpu().numpy()
+    tr_ptr, tr_idx = R.edges_to_user_csr(tr, U)
+    ref = R.full_ranking_reference_style(users, tr_ptr, tr_idx, uf, itf, 20)
+    same = (topk == ref).all(axis=1)
+    assert same.mean() >= 0.97
+    s64 = uf.astype(np.float64) @ itf.T.astype(np.float64)
+    for b in np.where(~same)[0]:
+        u = users[b]
+        a, r = np.sort(s64[u, topk[b]])[::-1], np.sort(s64[u, ref[b]])[::-1]
+        np.testing.assert_allclose(a, r, rtol=1e-5, atol=1e-5)

@@ -41,7 +41,8 @@ def _c_sizeof(struct_name: str) -> int:
 
 @pytest.mark.parametrize("cname,pyty", [("bbgr_csr", _lib.CsrStruct),
                                         ("bbgr_spmm_args", _lib.SpmmArgs),
-                                        ("bbgr_bpr_args", _lib.BprArgs)])
+                                        ("bbgr_bpr_args", _lib.BprArgs),
+                                        ("bbgr_eval_args", _lib.EvalArgs)])
 def test_struct_layout_matches_header(cname, pyty):
     assert _c_sizeof(cname) == ctypes.sizeof(pyty)
 
@@ -63,3 +64,23 @@ def test_gpu_required_is_loud():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.require_gpu()
+
+
+def test_eval_workspace_query_without_gpu():
+    """Size queries (workspace=NULL) are host-only: covered bytes + chunk
+    partials (+ the per-lane top-K lists for full ranking)."""
+    a = _lib.EvalArgs()
+    a.n_users, a.n_items, a.d, a.k_max, a.n_k, a.n_neg = 10000, 5000, 64, 20, 2, 99
+    a.ks[0], a.ks[1] = 10, 20
+    a.lduf = a.ldif = 64
+    a.users = a.te_indptr = a.te_indices = a.tr_indptr = a.tr_indices = 16
+    a.uf = a.itf = a.topk = a.item_pop = a.sums = 16
+    n = ctypes.c_size_t(0)
+    _lib.call("bbgr_eval_sampled", ctypes.byref(a), None, ctypes.byref(n), None)
+    assert n.value >= 2 * 5000 + 8 * 2 * 3 * 10
+    m = ctypes.c_size_t(0)
+    _lib.call("bbgr_eval_full", ctypes.byref(a), None, ctypes.byref(m), None)
+    assert m.value >= n.value + 10000 * 2 * 24 * 8
+    a.k_max = 40
+    with pytest.raises(_lib.BbgrError, match="k_max <= 32"):
+        _lib.call("bbgr_eval_full", ctypes.byref(a), None, ctypes.byref(m), None)

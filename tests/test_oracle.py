@@ -240,3 +240,70 @@ def test_evaluate_sampled_given_hand_case():
     assert res[1]["recall"] == 0.0 and res[2]["recall"] == 1.0
     assert res[2]["ndcg"] == pytest.approx(1 / np.log2(3))
     assert res[2]["item_coverage"] == 0.5 and res[2]["high_cred_recall"] == 1.0
+
+
+def test_eval_reference_style_invariants():
+    """The full reference loop restatement (Version-2:536-650): candidate
+    invariants, group sizes, and agreement with evaluate_sampled_given."""
+    from bbgr.synthetic import synthetic_edges
+    U, I, d = 300, 400, 16
+    e = synthetic_edges(U, I, 4000, 2)
+    rng = np.random.default_rng(0)
+    m = rng.random(e.shape[1]) < 0.2
+    tr, te = e[:, ~m], e[:, m]
+    trp, tri = R.edges_to_user_csr(tr, U)
+    tep, tei = R.edges_to_user_csr(te, U)
+    uf = rng.normal(size=(U, d)).astype(np.float32)
+    itf = rng.normal(size=(I, d)).astype(np.float32)
+    pop = np.bincount(tr[1], minlength=I)
+    cred = rng.random(U)
+    res, cands = R.evaluate_sampled_reference_style(trp, tri, tep, tei, uf, itf, I, pop,
+                                                    tr.shape[1], cred)
+    users = np.where(np.diff(tep) > 0)[0]
+    assert len(cands) == users.size and all(len(c) == 100 for c in cands)
+    for u, c in zip(users, cands):
+        assert R.user_has_item(tep, tei, u, c[0])
+        assert not any(R.user_has_item(tep, tei, u, j) or R.user_has_item(trp, tri, u, j)
+                       for j in c[1:])
+    k = max(int(round(users.size * 0.2)), 1)
+    assert res[10]["high_users"] == res[10]["low_users"] == k
+    hi, lo = R.make_cred_groups(users, cred, 0.2)
+    assert cred[hi].min() >= cred[lo].max()
+    again = R.evaluate_sampled_given(users, np.asarray(cands), uf, itf, pop, tr.shape[1], I,
+                                     cred, hi, lo)
+    assert again[20]["ndcg"] == res[20]["ndcg"]
+    assert 0.0 <= res[10]["recall"] <= res[20]["recall"] <= 1.0
+
+
+def test_full_ranking_c_oracle():
+    """oracle/csrc/eval_full.c: the fma-chain score agrees with float64 to fp32
+    rounding; its top-k equals the reference-style numpy ranking
+    (Version-2:690-706) except where two scores are within fp32 noise; train
+    items sink to -1e9; users with < k untrained items get -1e9 entries."""
+    from oracle import native as N
+    rng = np.random.default_rng(5)
+    U, I, d, k = 60, 300, 64, 20
+    uf = rng.normal(size=(U, d)).astype(np.float32)
+    itf = rng.normal(size=(I, d)).astype(np.float32)
+    for _ in range(20):
+        a, b = rng.normal(size=d).astype(np.float32), rng.normal(size=d).astype(np.float32)
+        exact = float(np.dot(a.astype(np.float64), b.astype(np.float64)))
+        assert abs(N.score_chain(a, b) - exact) <= 1e-6 * np.abs(a * b).sum()
+    tr = []
+    for u in range(U):
+        n = 295 if u == 0 else rng.integers(0, 15)          # user 0: only 5 untrained items
+        tr.append(np.sort(rng.choice(I, n, replace=False)))
+    ptr = np.concatenate([[0], np.cumsum([len(t) for t in tr])]).astype(np.int32)
+    idx = np.concatenate(tr).astype(np.int32)
+    users = np.arange(U)
+    items, scores = N.full_topk(users, ptr, idx, uf, itf, k)
+    ref = R.full_ranking_reference_style(users, ptr, idx, uf, itf, k)
+    same = (items == ref).all(axis=1)
+    assert same.mean() >= 0.95
+    for b in np.where(~same)[0]:                            # only near-ties may differ
+        s_ref = np.sort((uf[b] @ itf.T.astype(np.float64))[ref[b]])[::-1]
+        assert np.allclose(np.sort(scores[b])[::-1][:5], s_ref[:5], rtol=1e-5, atol=1e-5)
+    assert (scores[0, 5:] == np.float32(-1e9)).all() and not np.isin(items[0, :5], tr[0]).any()
+    for b in range(1, U):
+        assert not np.isin(items[b], tr[b]).any()
+        assert (np.diff(scores[b]) <= 0).all()
