@@ -37,7 +37,8 @@ constexpr int EVAL_NTERM = 10;       // p, r, ndcg, logpop, selfinfo, high_r, lo
 constexpr int EVAL_NOUT = 11;        // + covered count
 constexpr int EVAL_CHUNK = 4096;     // users per eval_terms workgroup (256 threads x 16)
 constexpr int ROW_CACHE = 64;        // LDS copy of test / train rows up to this length
-constexpr int FULL_USERS = 128;      // users per full-ranking workgroup (4 waves x 32)
+constexpr int FULL_THREADS = 512;    // 8 waves: 2 per SIMD hide the check path
+constexpr int FULL_USERS = 256;      // users per full-ranking workgroup (8 waves x 32)
 constexpr int FULL_TILE = 128;       // items per full-ranking LDS tile
 constexpr long FULL_BATCH = 1l << 18;  // users per full-ranking launch
 constexpr float TRAIN_MASK = -1e9f;  // Version-2:703 scores[train_items] = -1e9
@@ -216,12 +217,27 @@ __device__ __forceinline__ void topk_insert(float (&tv)[KM], int (&ti)[KM], floa
   }
 }
 
+// Items per LDS tile and per-lane candidate buffer depth, per embedding dim
+// (LDS: 2 tiles of TILE x (D+4) floats + CB x 512 float2 <= 160 KB).
+template <int D> struct FullShape {
+  static constexpr int TILE = D == 64 ? 128 : 64;
+  static constexpr int CB = 12;
+  static constexpr size_t lds_bytes() {
+    return sizeof(float) * 2 * TILE * (D + 4) + sizeof(float2) * CB * FULL_THREADS;
+  }
+};
+
 template <int D, int KM>
-__global__ __launch_bounds__(256) void eval_full_kernel(FullParams P) {
+__global__ __launch_bounds__(FULL_THREADS) void eval_full_kernel(FullParams P) {
+  constexpr int TILE = FullShape<D>::TILE;
+  constexpr int CB = FullShape<D>::CB;
+  constexpr int M = TILE / 32;        // 32-item sub-tiles (one accumulator each)
   constexpr int LDT = D + 4;          // padded LDS row (conflict-free b128 reads)
   constexpr int H = D / 2;            // components per lane half
-  constexpr int F4 = FULL_TILE * D / 4 / 256;   // float4 per thread per tile
-  extern __shared__ float tile[];     // [2][FULL_TILE][LDT]
+  constexpr int F4 = TILE * D / 4 / FULL_THREADS;   // float4 per thread per tile
+  extern __shared__ float smem[];
+  float *tile = smem;                                                  // [2][TILE][LDT]
+  float2 *cbuf = reinterpret_cast<float2 *>(smem + 2 * TILE * LDT);   // [CB][FULL_THREADS]
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, h = l >> 5;
   const long b = (long)blockIdx.x * FULL_USERS + w * 32 + r;
   const bool valid = b < P.n_users;
@@ -257,13 +273,33 @@ __global__ __launch_bounds__(256) void eval_full_kernel(FullParams P) {
     tv[j] = -INFINITY;
     ti[j] = INT_MAX;
   }
-  const int n_tiles = item_hi > item_lo ? (item_hi - item_lo + FULL_TILE - 1) / FULL_TILE : 0;
+  // Candidates whose raw score beats the (possibly stale) threshold are
+  // appended to the lane's LDS buffer in ascending item order; a flush
+  // inserts every lane's buffer at once, so the compare-swap insertion runs
+  // SIMD-parallel instead of once per passing lane.
+  int cnt = 0;
+  float thr = -INFINITY;
+  auto flush = [&]() {
+    for (int j = 0; j < cnt; ++j) {
+      const float2 c = cbuf[j * FULL_THREADS + threadIdx.x];
+      float sc = c.x;
+      const int it = __float_as_int(c.y);
+      if (sc > tv[KM - 1]) {
+        while (nt < it) nt = ++tp < tend ? P.tr_indices[tp] : INT_MAX;
+        if (nt == it) sc = TRAIN_MASK;
+        if (sc > tv[KM - 1]) topk_insert<KM>(tv, ti, sc, it);
+      }
+    }
+    cnt = 0;
+    thr = tv[KM - 1];
+  };
+  const int n_tiles = item_hi > item_lo ? (item_hi - item_lo + TILE - 1) / TILE : 0;
   float4 stage[F4];
   auto load_tile = [&](int t) {
-    const int i0 = item_lo + t * FULL_TILE;
+    const int i0 = item_lo + t * TILE;
 #pragma unroll
     for (int j = 0; j < F4; ++j) {
-      const int f = threadIdx.x + 256 * j;
+      const int f = threadIdx.x + FULL_THREADS * j;
       const int row = f / (D / 4), c4 = f % (D / 4);
       const int it = i0 + row;
       stage[j] = it < item_hi ? reinterpret_cast<const float4 *>(P.itf + (long)it * P.ldif)[c4]
@@ -271,10 +307,10 @@ __global__ __launch_bounds__(256) void eval_full_kernel(FullParams P) {
     }
   };
   auto store_tile = [&](int buf) {
-    float *T = tile + buf * FULL_TILE * LDT;
+    float *T = tile + buf * TILE * LDT;
 #pragma unroll
     for (int j = 0; j < F4; ++j) {
-      const int f = threadIdx.x + 256 * j;
+      const int f = threadIdx.x + FULL_THREADS * j;
       const int row = f / (D / 4), c4 = f % (D / 4);
       *reinterpret_cast<float4 *>(T + row * LDT + 4 * c4) = stage[j];
     }
@@ -286,55 +322,63 @@ __global__ __launch_bounds__(256) void eval_full_kernel(FullParams P) {
   __syncthreads();
   for (int t = 0; t < n_tiles; ++t) {
     if (t + 1 < n_tiles) load_tile(t + 1);
-    const float *T = tile + (t & 1) * FULL_TILE * LDT;
-    f32x16 acc[4];
+    const float *T = tile + (t & 1) * TILE * LDT;
+    f32x16 acc[M];
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < M; ++m)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
 #pragma unroll
     for (int s4 = 0; s4 < H / 4; ++s4) {
+      float4 a[M];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const float4 a =
-            *reinterpret_cast<const float4 *>(T + (m * 32 + r) * LDT + h * H + 4 * s4);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, ub[4 * s4 + 0], acc[m], 0, 0, 0);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, ub[4 * s4 + 1], acc[m], 0, 0, 0);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, ub[4 * s4 + 2], acc[m], 0, 0, 0);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, ub[4 * s4 + 3], acc[m], 0, 0, 0);
-      }
+      for (int m = 0; m < M; ++m)
+        a[m] = *reinterpret_cast<const float4 *>(T + (m * 32 + r) * LDT + h * H + 4 * s4);
+      // independent accumulators back to back
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].x, ub[4 * s4 + 0], acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].y, ub[4 * s4 + 1], acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].z, ub[4 * s4 + 2], acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].w, ub[4 * s4 + 3], acc[m], 0, 0, 0);
     }
     // acc[m][e] = score of user b, item i0 + 32m + (e&3) + 8(e>>2) + 4h
-    const int i0 = item_lo + t * FULL_TILE;
+    const int i0 = item_lo + t * TILE;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < M; ++m) {
       float mx = acc[m][0];
 #pragma unroll
       for (int e = 1; e < 16; ++e) mx = fmaxf(mx, acc[m][e]);
-      if (valid && mx > tv[KM - 1]) {
-        // slow path: the passing elements as a bit mask, then one rolled loop
-        // (register-select extraction keeps acc out of scratch)
+      if (valid && mx > thr) {
         unsigned pass = 0;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) pass |= (acc[m][e] > tv[KM - 1] ? 1u : 0u) << e;
+        for (int e = 0; e < 16; ++e) pass |= (acc[m][e] > thr ? 1u : 0u) << e;
         while (pass) {
           const int e = __builtin_ctz(pass);
           pass &= pass - 1;
-          float s = acc[m][0];
+          float sc = acc[m][0];
 #pragma unroll
-          for (int e2 = 1; e2 < 16; ++e2) s = e2 == e ? acc[m][e2] : s;
+          for (int e2 = 1; e2 < 16; ++e2) sc = e2 == e ? acc[m][e2] : sc;
           const int it = i0 + 32 * m + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (s > tv[KM - 1] && it < item_hi) {
-            while (nt < it) nt = ++tp < tend ? P.tr_indices[tp] : INT_MAX;
-            if (nt == it) s = TRAIN_MASK;
-            if (s > tv[KM - 1]) topk_insert<KM>(tv, ti, s, it);
+          if (it < item_hi) {
+            if (cnt == CB) flush();      // this lane only (early tiles: all lanes together)
+            cbuf[cnt * FULL_THREADS + threadIdx.x] = make_float2(sc, __int_as_float(it));
+            ++cnt;
           }
         }
       }
+      if (__any(cnt > CB - 4)) flush();   // batch the insertions across lanes
     }
     if (t + 1 < n_tiles) store_tile((t + 1) & 1);
     __syncthreads();
   }
+  flush();
   if (valid) {
     const long o = ((b * P.n_splits + split) * 2 + h) * KM;
 #pragma unroll
@@ -631,11 +675,11 @@ static int launch_terms(const bbgr_eval_args *a, bool full, const EvalLayout &L,
 
 template <int D, int KM>
 static int launch_full(const FullParams &P, hipStream_t st) {
-  const size_t lds = sizeof(float) * 2 * FULL_TILE * (D + 4);
+  const size_t lds = FullShape<D>::lds_bytes();
   BBGR_HIP(hipFuncSetAttribute((const void *)eval_full_kernel<D, KM>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const dim3 grid((unsigned)((P.n_users + FULL_USERS - 1) / FULL_USERS), (unsigned)P.n_splits);
-  hipLaunchKernelGGL((eval_full_kernel<D, KM>), grid, dim3(256), lds, st, P);
+  hipLaunchKernelGGL((eval_full_kernel<D, KM>), grid, dim3(FULL_THREADS), lds, st, P);
   BBGR_LAUNCHED("eval_full_kernel");
   return BBGR_OK;
 }
