@@ -55,6 +55,12 @@ def spmm_bytes(nnz: int, rows: int, d: int) -> int:
     return nnz * (4 + 4 + 4 * d) + rows * (4 + 4 * d)
 
 
+def spmm_adam_bytes(nnz: int, rows: int, d: int) -> int:
+    """Last backward product with the user Adam in its epilogue: the SpMM bytes
+    minus the gradient write, plus param / exp_avg / exp_avg_sq read + write."""
+    return spmm_bytes(nnz, rows, d) - rows * 4 * d + 6 * rows * 4 * d
+
+
 def cpu_baseline(edges, cfg, batch, sample_users=256):
     """Reference CPU path (same torch calls) on a bounded sample of the step."""
     from oracle import ref_numpy as R
@@ -203,8 +209,9 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss)
-    summ = timer.summary()                 # full-CSR launches: the roofline kernel
-    summ_m = timer.summary(masked=True)    # frontier-masked launches (bytes data-dependent)
+    summ = timer.summary("full")           # full-CSR launches: the roofline kernel
+    summ_m = timer.summary("masked")       # frontier-masked launches (bytes data-dependent)
+    summ_a = timer.summary("adam")         # last backward product + fused user Adam
     tot_bytes = sum(n * spmm_bytes(nnz, rows, dd) for (rows, nnz, dd), (n, ms) in summ.items())
     tot_ms = sum(ms for (n, ms) in summ.values())
     n_launch = sum(n for (n, ms) in summ.values())
@@ -214,6 +221,11 @@ def main():
     achieved = tot_bytes / (tot_ms * 1e6) if tot_ms > 0 else 0.0   # GB/s
     masked_ms = sum(ms for (n, ms) in summ_m.values())
     masked_n = sum(n for (n, ms) in summ_m.values())
+    adam_info = {f"rows{rows}_nnz{nnz}_d{dd}": {
+        "launches": n, "avg_ms": ms / n,
+        "algorithmic_bytes": spmm_adam_bytes(nnz, rows, dd),
+        "GBps": n * spmm_adam_bytes(nnz, rows, dd) / (ms * 1e6)}
+        for (rows, nnz, dd), (n, ms) in summ_a.items()}
     traffic, traffic_src = pmc_traffic() if (args.config == "C4" and world == 1) else (None, None)
     edges_per_step = 4 * K * E
     if rank != 0:
@@ -251,6 +263,7 @@ def main():
                      "full_launches_per_step": n_launch / args.steps,
                      "note": "value counts the reference step's 4*K*E edge traversals; "
                              "masked launches skip exact-zero / unread rows"},
+        "fused_adam_spmm": adam_info,
         "final_loss": final_loss,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

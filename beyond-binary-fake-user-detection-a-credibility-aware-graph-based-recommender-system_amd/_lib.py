@@ -79,6 +79,10 @@ class SpmmArgs(ctypes.Structure):
         ("n_row_list", c_int64),
         ("use_range", c_int32),
         ("range", c_int32 * 6),
+        ("adam_param", c_void_p), ("adam_exp_avg", c_void_p), ("adam_exp_avg_sq", c_void_p),
+        ("adam_ld", c_int64), ("adam_lr", c_float), ("adam_beta1", c_float),
+        ("adam_beta2", c_float), ("adam_eps", c_float), ("adam_weight_decay", c_float),
+        ("adam_bias_correction1", c_float), ("adam_bias_correction2_sqrt", c_float),
     ]
 
 
@@ -98,6 +102,7 @@ class BprArgs(ctypes.Structure):
         ("g_if", c_void_p), ("ldgif", c_int64),
         ("g_ue", c_void_p), ("ldgue", c_int64),
         ("g_ie", c_void_p), ("ldgie", c_int64),
+        ("contrib", c_void_p), ("ldcontrib", c_int64),
     ]
 
 
@@ -137,8 +142,10 @@ _SIGNATURES = {
     "bbgr_bpr": ([ctypes.POINTER(BprArgs), _P], c_int32),
     "bbgr_bpr_reduce": ([c_int64, _P, c_float, c_float, _P, _P], c_int32),
     "bbgr_adam": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
-                   c_float, c_float, c_float, _P], c_int32),
+                   c_float, c_float, c_float, c_float, _P], c_int32),
     "bbgr_mark_rows": ([c_int64, _P, ctypes.c_uint8, _P, _P], c_int32),
+    "bbgr_scatter_add_rows": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P,
+                               ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
     "bbgr_rows_zero": ([c_int64, _P, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_rows_axpy": ([c_int64, _P, c_float, _P, c_int64, _P, c_int64, c_int32, _P],

@@ -21,7 +21,8 @@ def _idx(t: torch.Tensor, device) -> torch.Tensor:
 
 
 def bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop=None, lambda_fair=0.0,
-             parts=None, dloss=None, g_uf=None, g_if=None, g_ue=None, g_ie=None):
+             parts=None, dloss=None, g_uf=None, g_if=None, g_ue=None, g_ie=None,
+             contrib=None):
     a = _lib.BprArgs()
     a.batch, a.d = users.numel(), uf.shape[1]
     a.n_users, a.n_items = uf.shape[0], itf.shape[0]
@@ -39,6 +40,7 @@ def bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop=None, lambda_fair=0.0,
     a.g_if, a.ldgif = ptr(g_if), ld(g_if)
     a.g_ue, a.ldgue = ptr(g_ue), ld(g_ue)
     a.g_ie, a.ldgie = ptr(g_ie), ld(g_ie)
+    a.contrib, a.ldcontrib = ptr(contrib), ld(contrib)
     return a
 
 

@@ -77,4 +77,34 @@ __device__ __forceinline__ double u01_53(uint32_t a, uint32_t b) {
   return (double)v * (1.0 / 9007199254740992.0);
 }
 
+// ---------------------------------------------------------------------------
+// torch.optim.Adam on one element (amsgrad=False, maximize=False). Shared by
+// adam_kernel and the SpMM epilogue's fused step with every rounding spelled
+// out (explicit fmaf, no contraction) so the two paths agree bit for bit.
+// ---------------------------------------------------------------------------
+struct AdamConsts {
+  float step;   // lr / bias_correction1
+  float w1;     // 1 - beta1
+  float b2;     // beta2
+  float w2;     // 1 - beta2
+  float eps;
+  float wd;     // weight_decay
+  float bc2s;   // sqrt(bias_correction2)
+};
+
+__host__ __device__ inline AdamConsts adam_consts(float lr, float b1, float b2, float eps,
+                                                  float wd, float bc1, float bc2s) {
+  return AdamConsts{lr / bc1, 1.0f - b1, b2, 1.0f - b2, eps, wd, bc2s};
+}
+
+__device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v,
+                                          const AdamConsts &c) {
+#pragma clang fp contract(off)
+  if (c.wd != 0.f) g = fmaf(c.wd, p, g);
+  m = fmaf(c.w1, g - m, m);                    // lerp(m, g, 1 - beta1)
+  v = fmaf(c.w2 * g, g, v * c.b2);             // beta2 v + (1 - beta2) g^2
+  const float denom = sqrtf(v) / c.bc2s + c.eps;
+  p = fmaf(-c.step, m / denom, p);             // p - lr/bc1 * m / denom
+}
+
 }  // namespace bbgr

@@ -60,6 +60,10 @@ struct SpmmParams {
   long n_row_list;
   int row_begin, row_end;      // short rows computed: [row_begin, row_end)
   int chunk_begin;             // first long-row chunk of this launch
+  // fused Adam on the y-row value (bbgr_spmm_args.adam_*)
+  float *adam_p, *adam_m, *adam_v;
+  long adam_ld;
+  AdamConsts adam;
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -125,24 +129,51 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
   }
 }
 
+// torch.optim.Adam on one row held by a 16-lane group: the same expression
+// order as adam_kernel (train.hip), so fused and separate steps agree bitwise.
+template <int D>
+__device__ __forceinline__ void adam_row(const SpmmParams &P, int row, int lane,
+                                         const float4 (&G)[D / 64]) {
+  constexpr int V = D / 64;
+  float4 *pp = reinterpret_cast<float4 *>(P.adam_p + (long)row * P.adam_ld) + lane;
+  float4 *pm = reinterpret_cast<float4 *>(P.adam_m + (long)row * P.adam_ld) + lane;
+  float4 *pv = reinterpret_cast<float4 *>(P.adam_v + (long)row * P.adam_ld) + lane;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    float4 p4 = pp[16 * k], m4 = pm[16 * k], v4 = pv[16 * k];
+    adam_elem(p4.x, G[k].x, m4.x, v4.x, P.adam);
+    adam_elem(p4.y, G[k].y, m4.y, v4.y, P.adam);
+    adam_elem(p4.z, G[k].z, m4.z, v4.z, P.adam);
+    adam_elem(p4.w, G[k].w, m4.w, v4.w, P.adam);
+    pp[16 * k] = p4;
+    pm[16 * k] = m4;
+    pv[16 * k] = v4;
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
                                          const float4 (&T)[D / 64]) {
   constexpr int V = D / 64;
-  if (P.y) {
+  if (P.y || P.adam_p) {
     const float ys = (P.y_scale ? P.y_scale[row] : 1.f) * P.y_scale_s;
-    float4 *dst = reinterpret_cast<float4 *>(P.y + (long)row * P.ldy) + lane;
+    float4 G[V];
     if (P.add && (!P.add_mask || P.add_mask[row])) {
       const float as = (P.add_scale ? P.add_scale[row] : 1.f) * P.add_scale_s;
       const float4 *ad =
           reinterpret_cast<const float4 *>(P.add + (long)row * P.ldadd) + lane;
 #pragma unroll
-      for (int k = 0; k < V; ++k)
-        dst[16 * k] = f4_fma(as, ad[16 * k], f4_mul(ys, T[k]));
+      for (int k = 0; k < V; ++k) G[k] = f4_fma(as, ad[16 * k], f4_mul(ys, T[k]));
     } else {
 #pragma unroll
-      for (int k = 0; k < V; ++k) dst[16 * k] = f4_mul(ys, T[k]);
+      for (int k = 0; k < V; ++k) G[k] = f4_mul(ys, T[k]);
     }
+    if (P.y) {
+      float4 *dst = reinterpret_cast<float4 *>(P.y + (long)row * P.ldy) + lane;
+#pragma unroll
+      for (int k = 0; k < V; ++k) dst[16 * k] = G[k];
+    }
+    if (P.adam_p) adam_row<D>(P, row, lane, G);
   }
   if (P.acc_out && (!P.acc_mask || P.acc_mask[row])) {
     const float cs = (P.acc_scale ? P.acc_scale[row] : 1.f) * P.acc_scale_s;
@@ -247,6 +278,13 @@ __global__ __launch_bounds__(256) void spmm_masked_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true>(P);
 }
 
+// Full-CSR launch whose epilogue applies the fused Adam step (its bytes add the
+// parameter / moment streams): a third symbol so rooflines stay per kind.
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) void spmm_adam_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, false>(P);
+}
+
 // Rows split into >1 chunk: sum chunk partials in chunk order, then epilogue.
 template <int D>
 __global__ __launch_bounds__(256) void spmm_fixup_kernel(SpmmParams P) {
@@ -298,6 +336,9 @@ static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
   if (grid > 0) {
     if (masked) {
       hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
+                         0, st, P);
+    } else if (P.adam_p) {
+      hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
                          0, st, P);
     } else {
       hipLaunchKernelGGL((spmm_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
@@ -351,6 +392,20 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.gamma = a->gamma;
   P.acc_mask = a->acc_mask;
   P.add_mask = a->add_mask;
+  P.adam_p = a->adam_param;
+  P.adam_m = a->adam_exp_avg;
+  P.adam_v = a->adam_exp_avg_sq;
+  P.adam_ld = a->adam_ld;
+  P.adam = adam_consts(a->adam_lr, a->adam_beta1, a->adam_beta2, a->adam_eps,
+                       a->adam_weight_decay, a->adam_bias_correction1,
+                       a->adam_bias_correction2_sqrt);
+}
+
+static bool adam_ok(const bbgr_spmm_args *a, int d) {
+  if (!a->adam_param) return true;
+  return a->adam_exp_avg && a->adam_exp_avg_sq && ld_ok(a->adam_param, a->adam_ld, d) &&
+         ld_ok(a->adam_exp_avg, a->adam_ld, d) && ld_ok(a->adam_exp_avg_sq, a->adam_ld, d) &&
+         a->adam_bias_correction1 > 0.f && a->adam_bias_correction2_sqrt > 0.f;
 }
 
 extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
@@ -363,7 +418,8 @@ extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
   }
   if (n_rows == 0) return BBGR_OK;
   BBGR_REQUIRE(t && ld_ok(t, ldt, d) && ld_ok(a->y, a->ldy, d) && ld_ok(a->add, a->ldadd, d) &&
-                   ld_ok(a->acc_in, a->ldacc_in, d) && ld_ok(a->acc_out, a->ldacc_out, d),
+                   ld_ok(a->acc_in, a->ldacc_in, d) && ld_ok(a->acc_out, a->ldacc_out, d) &&
+                   adam_ok(a, d),
                "bbgr_epilogue: tables must be 16-byte aligned with ld >= d, ld % 4 == 0");
   SpmmParams P = {};
   P.n_rows = n_rows;
@@ -397,6 +453,10 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
                    ld_ok(a->add, a->ldadd, d) && ld_ok(a->acc_in, a->ldacc_in, d) &&
                    ld_ok(a->acc_out, a->ldacc_out, d),
                "bbgr_spmm: tables must be 16-byte aligned with ld >= d, ld % 4 == 0");
+  BBGR_REQUIRE(adam_ok(a, d), "bbgr_spmm: fused Adam needs param/exp_avg/exp_avg_sq "
+                               "(16-byte aligned, adam_ld >= d) and bias corrections > 0");
+  BBGR_REQUIRE(!a->adam_param || !(a->src_mask || a->row_mask || a->row_list || a->use_range),
+               "bbgr_spmm: fused Adam needs every row (no masks, row list or range)");
   BBGR_REQUIRE(a->weight_mode != 1 || a->edge_val, "bbgr_spmm: weight_mode 1 needs edge_val");
   BBGR_REQUIRE(a->weight_mode != 2 || a->col_scale, "bbgr_spmm: weight_mode 2 needs col_scale");
   BBGR_REQUIRE(csr->n_chunks == 0 || csr->chunks, "bbgr_spmm: plan chunks missing");

@@ -4,6 +4,8 @@
 // Reference: LightGCN.bpr_loss  Version-2/lighgcn_cu_pop.py:495-508
 //            (lightgcn.py:333-349; lightgcn_cu.py:632-648 adds L_fair)
 //            opt.step()          Version-2/lighgcn_cu_pop.py:863 (Adam, :793)
+#include <hipcub/hipcub.hpp>
+
 #include "common.h"
 
 namespace bbgr {
@@ -19,6 +21,8 @@ struct BprParams {
   const float *dloss;
   float *g_uf, *g_if, *g_ue, *g_ie;
   long ldguf, ldgif, ldgue, ldgie;
+  float *contrib;
+  long ldc;
 };
 
 __device__ __forceinline__ float group16_sum(float v) {
@@ -61,6 +65,14 @@ __global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
       P.parts[3 * b + 0] = 0.f;
       P.parts[3 * b + 1] = 0.f;
       P.parts[3 * b + 2] = 0.f;
+    }
+    if (P.contrib) {
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          reinterpret_cast<float4 *>(P.contrib + (r * P.batch + b) * P.ldc)[lane + 16 * k] = z;
     }
     return;  // whole group leaves together
   }
@@ -108,18 +120,29 @@ __global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
       P.parts[3 * b + 2] = P.pop ? P.pop[ip] * sp : 0.f;
     }
   }
-  if (!(P.g_uf || P.g_if || P.g_ue || P.g_ie)) return;
+  if (!(P.g_uf || P.g_if || P.g_ue || P.g_ie || P.contrib)) return;
   const float G = (P.dloss ? *P.dloss : 1.0f) * P.inv_b;
   // d/dx [-log(sigmoid(x) + 1e-12)] = -sigmoid'(x) / (sigmoid(x) + 1e-12)
   const float gx = -(sig * (1.0f - sig)) / (sig + 1e-12f) * G;
   const float gpos = gx + (P.pop ? P.lambda_fair * P.pop[ip] * G : 0.f);
   const float gneg = -gx;
-  if (P.g_uf) {
+  if (P.contrib) {   // deterministic mode: per-triple rows, summed by scatter_add_rows
+    float4 *cu = reinterpret_cast<float4 *>(P.contrib + b * P.ldc) + lane;
+    float4 *cp = reinterpret_cast<float4 *>(P.contrib + (P.batch + b) * P.ldc) + lane;
+    float4 *cn = reinterpret_cast<float4 *>(P.contrib + (2 * P.batch + b) * P.ldc) + lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      cu[16 * k] = make_float4(gpos * fp[k].x + gneg * fn[k].x, gpos * fp[k].y + gneg * fn[k].y,
+                               gpos * fp[k].z + gneg * fn[k].z, gpos * fp[k].w + gneg * fn[k].w);
+      cp[16 * k] = make_float4(gpos * fu[k].x, gpos * fu[k].y, gpos * fu[k].z, gpos * fu[k].w);
+      cn[16 * k] = make_float4(gneg * fu[k].x, gneg * fu[k].y, gneg * fu[k].z, gneg * fu[k].w);
+    }
+  } else if (P.g_uf) {
     float *d = P.g_uf + u * P.ldguf + 4 * lane;
 #pragma unroll
     for (int k = 0; k < V; ++k) atomic_axpby4(d + 64 * k, gpos, fp[k], gneg, fn[k]);
   }
-  if (P.g_if) {
+  if (P.g_if && !P.contrib) {
     float *dp = P.g_if + ip * P.ldgif + 4 * lane;
     float *dn = P.g_if + in * P.ldgif + 4 * lane;
 #pragma unroll
@@ -175,46 +198,29 @@ __global__ __launch_bounds__(256) void bpr_reduce_kernel(long batch,
   }
 }
 
-// torch.optim.Adam (single-tensor/foreach math), float4 vectorised.
-__global__ __launch_bounds__(256) void adam_kernel(long n4, float4 *p,
-                                                   const float4 *g, float4 *m,
-                                                   float4 *v, float lr, float b1,
-                                                   float b2, float eps, float wd,
-                                                   float bc1, float bc2s) {
-  const float step = lr / bc1;
-  const float w1 = 1.0f - b1;
-  const float w2 = 1.0f - b2;
+// torch.optim.Adam (single-tensor/foreach math), float4 vectorised; the
+// per-element update is adam_elem (common.h), shared with the fused epilogue.
+__global__ __launch_bounds__(256) void adam_kernel(long n4, float4 *p, const float4 *g,
+                                                   float4 *m, float4 *v, AdamConsts c,
+                                                   float gs) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
-    float *pf = &pp.x, *gf = &gg.x, *mf = &mm.x, *vf = &vv.x;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float gk = gf[k];
-      if (wd != 0.f) gk = gk + wd * pf[k];
-      mf[k] = mf[k] + w1 * (gk - mf[k]);  // lerp(m, g, 1-beta1), weight < 0.5
-      vf[k] = vf[k] * b2 + w2 * gk * gk;
-      const float denom = sqrtf(vf[k]) / bc2s + eps;
-      pf[k] = pf[k] - step * (mf[k] / denom);
-    }
+    adam_elem(pp.x, gs * gg.x, mm.x, vv.x, c);
+    adam_elem(pp.y, gs * gg.y, mm.y, vv.y, c);
+    adam_elem(pp.z, gs * gg.z, mm.z, vv.z, c);
+    adam_elem(pp.w, gs * gg.w, mm.w, vv.w, c);
     p[i] = pp;
     m[i] = mm;
     v[i] = vv;
   }
 }
 
-__global__ void adam_tail_kernel(long n, long start, float *p, const float *g,
-                                 float *m, float *v, float lr, float b1, float b2,
-                                 float eps, float wd, float bc1, float bc2s) {
+__global__ void adam_tail_kernel(long n, long start, float *p, const float *g, float *m,
+                                 float *v, AdamConsts c, float gs) {
   const long i = start + (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float gk = g[i];
-  if (wd != 0.f) gk = gk + wd * p[i];
-  const float mk = m[i] + (1.0f - b1) * (gk - m[i]);
-  const float vk = v[i] * b2 + (1.0f - b2) * gk * gk;
-  m[i] = mk;
-  v[i] = vk;
-  p[i] = p[i] - (lr / bc1) * (mk / (sqrtf(vk) / bc2s + eps));
+  adam_elem(p[i], gs * g[i], m[i], v[i], c);
 }
 
 __global__ void rows_zero_kernel(long n, const long *idx, float *t, long ld,
@@ -252,9 +258,104 @@ __global__ void rows_axpy_kernel(long n, const long *idx, float alpha,
     atomicAdd(dst + r * ldd + c, alpha * src[r * lds + c]);
 }
 
+// ---- deterministic index_add_ (bbgr_scatter_add_rows) ----------------------
+__global__ void scatter_keys_kernel(long n, const long *idx, long n_dst, unsigned *keys,
+                                    int *vals) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const long r = idx[k];
+  keys[k] = (r >= 0 && r < n_dst) ? (unsigned)r : (unsigned)n_dst;   // n_dst = skip
+  vals[k] = (int)k;
+}
+
+// One 16-lane group per sorted position; the group at the start of a run of
+// equal keys sums the run's source rows in (stable) ascending-k order and adds
+// the total to the destination row once.
+template <int D>
+__global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const unsigned *keys,
+                                                               const int *vals,
+                                                               const float *src, long lds,
+                                                               float *dst, long ldd,
+                                                               unsigned skip) {
+  constexpr int V = D / 64;
+  const long s = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  if (s >= n) return;
+  const unsigned key = keys[s];
+  if (key == skip || (s > 0 && keys[s - 1] == key)) return;
+  float4 acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (long t = s; t < n && keys[t] == key; ++t) {
+    const float4 *row = reinterpret_cast<const float4 *>(src + (long)vals[t] * lds) + lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float4 x = row[16 * k];
+      acc[k] = make_float4(acc[k].x + x.x, acc[k].y + x.y, acc[k].z + x.z, acc[k].w + x.w);
+    }
+  }
+  float4 *out = reinterpret_cast<float4 *>(dst + (long)key * ldd) + lane;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const float4 o = out[16 * k];
+    out[16 * k] = make_float4(o.x + acc[k].x, o.y + acc[k].y, o.z + acc[k].z, o.w + acc[k].w);
+  }
+}
+
 }  // namespace bbgr
 
 using namespace bbgr;
+
+extern "C" int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float *src,
+                                     int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
+                                     int64_t n_dst, void *workspace, size_t *workspace_bytes,
+                                     bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n < (1ll << 31) && n_dst >= 0 && n_dst < 0xFFFFFFFFll && workspace_bytes,
+               "bbgr_scatter_add_rows: bad sizes");
+  if (d != 64 && d != 128 && d != 256) {
+    set_error("bbgr_scatter_add_rows: d = %d unsupported (64, 128, 256)", d);
+    return BBGR_ERR_UNSUPPORTED;
+  }
+  int end_bit = 1;   // keys are in [0, n_dst] (n_dst marks skipped rows)
+  while (end_bit < 32 && (1ull << end_bit) <= (unsigned long long)n_dst) ++end_bit;
+  size_t temp = 0;
+  BBGR_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (unsigned *)nullptr,
+                                              (unsigned *)nullptr, (int *)nullptr,
+                                              (int *)nullptr, (int)(n > 0 ? n : 1), 0, end_bit,
+                                              as_stream(stream)));
+  const size_t a = align_up(4 * (size_t)(n > 0 ? n : 1));
+  const size_t need = 4 * a + align_up(temp);
+  if (!workspace) {
+    *workspace_bytes = need;
+    return BBGR_OK;
+  }
+  if (*workspace_bytes < need) {
+    set_error("bbgr_scatter_add_rows: workspace %zu < %zu bytes", *workspace_bytes, need);
+    return BBGR_ERR_WORKSPACE;
+  }
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx && src && dst, "bbgr_scatter_add_rows: null arrays");
+  BBGR_REQUIRE(aligned16(src) && aligned16(dst) && ldsrc >= d && lddst >= d &&
+                   (ldsrc & 3) == 0 && (lddst & 3) == 0,
+               "bbgr_scatter_add_rows: tables must be 16-byte aligned, ld >= d, ld % 4 == 0");
+  hipStream_t st = as_stream(stream);
+  char *ws = static_cast<char *>(workspace);
+  unsigned *k1 = reinterpret_cast<unsigned *>(ws), *k2 = reinterpret_cast<unsigned *>(ws + a);
+  int *v1 = reinterpret_cast<int *>(ws + 2 * a), *v2 = reinterpret_cast<int *>(ws + 3 * a);
+  hipLaunchKernelGGL(scatter_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (long)n, (const long *)idx, (long)n_dst, k1, v1);
+  BBGR_LAUNCHED("scatter_keys_kernel");
+  BBGR_HIP(hipcub::DeviceRadixSort::SortPairs(ws + 4 * a, temp, k1, k2, v1, v2, (int)n, 0,
+                                              end_bit, st));
+  const unsigned grid = (unsigned)((n + 15) / 16);
+  switch (d) {
+    case 64: hipLaunchKernelGGL(scatter_segments_kernel<64>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
+    case 128: hipLaunchKernelGGL(scatter_segments_kernel<128>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
+    default: hipLaunchKernelGGL(scatter_segments_kernel<256>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
+  }
+  BBGR_LAUNCHED("scatter_segments_kernel");
+  return BBGR_OK;
+}
 
 extern "C" int bbgr_bpr(const bbgr_bpr_args *a, bbgr_stream_t stream) {
   BBGR_REQUIRE(a, "bbgr_bpr: null args");
@@ -291,9 +392,10 @@ extern "C" int bbgr_bpr(const bbgr_bpr_args *a, bbgr_stream_t stream) {
   P.g_if = a->g_if; P.ldgif = a->ldgif;
   P.g_ue = a->g_ue; P.ldgue = a->ldgue;
   P.g_ie = a->g_ie; P.ldgie = a->ldgie;
-  const long lds[] = {P.lduf, P.ldif, P.ldue, P.ldie, P.ldguf, P.ldgif, P.ldgue, P.ldgie};
-  const void *ptrs[] = {P.uf, P.itf, P.ue, P.ie, P.g_uf, P.g_if, P.g_ue, P.g_ie};
-  for (int k = 0; k < 8; ++k) {
+  P.contrib = a->contrib; P.ldc = a->ldcontrib;
+  const long lds[] = {P.lduf, P.ldif, P.ldue, P.ldie, P.ldguf, P.ldgif, P.ldgue, P.ldgie, P.ldc};
+  const void *ptrs[] = {P.uf, P.itf, P.ue, P.ie, P.g_uf, P.g_if, P.g_ue, P.g_ie, P.contrib};
+  for (int k = 0; k < 9; ++k) {
     if (!ptrs[k]) continue;
     BBGR_REQUIRE(aligned16(ptrs[k]) && lds[k] >= d && (lds[k] & 3) == 0,
                  "bbgr_bpr: tables must be 16-byte aligned with ld >= d, ld % 4 == 0");
@@ -321,13 +423,15 @@ extern "C" int bbgr_bpr_reduce(int64_t batch, const float *parts, float reg,
 
 extern "C" int bbgr_adam(int64_t n, float *param, const float *grad,
                          float *exp_avg, float *exp_avg_sq, float lr, float beta1,
-                         float beta2, float eps, float weight_decay,
+                         float beta2, float eps, float weight_decay, float grad_scale,
                          float bias_correction1, float bias_correction2_sqrt,
                          bbgr_stream_t stream) {
   BBGR_REQUIRE(n >= 0, "bbgr_adam: negative n");
   if (n == 0) return BBGR_OK;
   BBGR_REQUIRE(param && grad && exp_avg && exp_avg_sq, "bbgr_adam: null tensor");
   hipStream_t st = as_stream(stream);
+  const AdamConsts c = adam_consts(lr, beta1, beta2, eps, weight_decay, bias_correction1,
+                                   bias_correction2_sqrt);
   const bool vec = aligned16(param) && aligned16(grad) && aligned16(exp_avg) &&
                    aligned16(exp_avg_sq);
   const long n4 = vec ? n / 4 : 0;
@@ -336,16 +440,14 @@ extern "C" int bbgr_adam(int64_t n, float *param, const float *grad,
     if (blocks > 256 * 16) blocks = 256 * 16;
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n4,
                        (float4 *)param, (const float4 *)grad, (float4 *)exp_avg,
-                       (float4 *)exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
-                       bias_correction1, bias_correction2_sqrt);
+                       (float4 *)exp_avg_sq, c, grad_scale);
     BBGR_LAUNCHED("adam_kernel");
   }
   const long start = n4 * 4;
   if (start < n) {
     hipLaunchKernelGGL(adam_tail_kernel, dim3((unsigned)((n - start + 255) / 256)),
                        dim3(256), 0, st, (long)n, start, param, grad, exp_avg,
-                       exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
-                       bias_correction1, bias_correction2_sqrt);
+                       exp_avg_sq, c, grad_scale);
     BBGR_LAUNCHED("adam_tail_kernel");
   }
   return BBGR_OK;

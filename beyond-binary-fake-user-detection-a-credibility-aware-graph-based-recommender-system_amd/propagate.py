@@ -118,15 +118,16 @@ class SpmmTimer:
     launching stream; used by bench.py inside the timed region."""
 
     def __init__(self):
-        self.records = []   # (n_rows, nnz, d, masked, start_event, end_event)
+        self.records = []   # (n_rows, nnz, d, kind, start_event, end_event)
 
-    def summary(self, masked: bool = False):
-        """{(rows, nnz, d): (launches, total ms)} over full (masked=False) or
-        frontier-masked (masked=True) launches."""
+    def summary(self, kind: str = "full"):
+        """{(rows, nnz, d): (launches, total ms)} over one kind of launch:
+        "full" (spmm_kernel), "masked" (frontier masks / row lists,
+        spmm_masked_kernel) or "adam" (fused Adam epilogue, spmm_adam_kernel)."""
         torch.cuda.synchronize()
         out = {}
         for rows, nnz, d, m, a, b in self.records:
-            if m != masked:
+            if m != kind:
                 continue
             k = (rows, nnz, d)
             n, ms = out.get(k, (0, 0.0))
@@ -146,8 +147,9 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          y_scale_s: float = 1.0, add=None, add_scale=None, add_scale_s: float = 1.0,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
-         add_mask=None, row_list=None, rng=None) -> None:
-    """One fused SpMM launch (bbgr_spmm) on the current stream."""
+         add_mask=None, row_list=None, rng=None, adam=None) -> None:
+    """One fused SpMM launch (bbgr_spmm) on the current stream. `adam`
+    (optim.AdamRows): apply Adam to each row's y value in the epilogue."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
     a.d = d
@@ -175,6 +177,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
         a.use_range = 1
         for k in range(6):
             a.range[k] = rng[k]
+    if adam is not None:
+        adam.fill(a)
     if _timer is None:
         call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
         return
@@ -182,9 +186,9 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     ev0.record()
     call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
     ev1.record()
-    _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d,
-                           src_mask is not None or row_mask is not None or row_list is not None,
-                           ev0, ev1))
+    masked = src_mask is not None or row_mask is not None or row_list is not None
+    kind = "masked" if masked else ("adam" if adam is not None else "full")
+    _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d, kind, ev0, ev1))
 
 
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,
@@ -315,8 +319,13 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
 def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
              order: str = ORDER_GS, out_u: torch.Tensor | None = None,
              out_i: torch.Tensor | None = None, ws: dict | None = None,
-             grad_i0_dense: bool = True, reduce=None, grad_support=None):
+             grad_i0_dense: bool = True, reduce=None, grad_support=None,
+             adam_u=None, before_last=None):
     """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final).
+    GS order only: `adam_u` (optim.AdamRows) fuses the user-table Adam step into
+    the last (user-row) product, which then writes no gradient table (out_u
+    is left untouched); `before_last()` runs just before that product, after
+    every other read of gU (the trainer adds the ego-L2 rows to gU there).
     `grad_support=(user_mask, item_mask)`: gU is zero outside the flagged users
     and, for GS, the first item product's output is zero outside the flagged
     items (GS: batch items and N(batch users); Jacobi: gI's own support). The
@@ -350,8 +359,15 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
                      add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl,
                      src_mask=si if first else None)
             else:
-                spmm(BU, bufI, False, y=gu0, y_scale=BU.out_scale,
-                     add=gU, add_mask=su, add_scale=None, add_scale_s=gl, src_mask=si if first else None)
+                if before_last is not None:
+                    before_last()
+                src = si if first else None
+                fused = adam_u is not None and src is None   # fused Adam needs every row
+                spmm(BU, bufI, False, y=None if fused else gu0, y_scale=BU.out_scale,
+                     add=gU, add_mask=su, add_scale=None, add_scale_s=gl,
+                     src_mask=src, adam=adam_u if fused else None)
+                if adam_u is not None and not fused:   # K == 1: masked product, Adam apart
+                    adam_u.apply(gu0)
         if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
             torch.mul(gI, gl, out=gi0)
     elif order == ORDER_J:

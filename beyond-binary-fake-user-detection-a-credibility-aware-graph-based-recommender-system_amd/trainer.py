@@ -23,9 +23,10 @@ from . import _lib
 from ._lib import OP_GS, OP_J, OP_METHOD_A, OP_SYM, call, ld, ptr, stream_handle
 from .bpr import bpr_args
 from .graph import BipartiteGraph
-from .optim import adam_step
+from .optim import AdamRows, adam_step
 from .propagate import ORDER_GS, ORDER_J, OperatorPair, backward, forward
 from .sampler import PopMixSampler, nonempty_rows, shuffle
+from .scatter import RowScatter
 
 VARIANTS = {
     # name: (operator kind, layer order, default negative sampler mix)
@@ -43,7 +44,7 @@ class FusedTrainer:
                  reg: float = 1e-4, batch_size: int = 4096, neg_mix_pop: float | None = None,
                  neg_pop_gamma: float = 0.75, neg_max_tries: int = 50,
                  lambda_fair: float = 0.0, seed: int = 42, u0=None, i0=None,
-                 frontier: bool = True):
+                 frontier: bool = True, fuse_adam: bool = True):
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}; one of {sorted(VARIANTS)}")
@@ -94,8 +95,13 @@ class FusedTrainer:
             raise RuntimeError("No train users with interactions. Check your threshold/split.")
         self.epoch, self.cursor, self.step_count = 0, 0, 0
         self.perm = None
-        self.pos = torch.empty(batch_size, dtype=torch.int64, device=dev)
-        self.neg = torch.empty(batch_size, dtype=torch.int64, device=dev)
+        # pos and neg of a batch of B live in posneg[:B] / posneg[B:2B], so the
+        # item-gradient scatter takes one contiguous index vector
+        self.posneg = torch.empty(2 * batch_size, dtype=torch.int64, device=dev)
+        self.pos, self.neg = self.posneg[:batch_size], self.posneg[batch_size:]
+        # deterministic BPR gradient: per-triple rows, then a fixed-order scatter
+        self.contrib = torch.empty(3 * batch_size, emb_dim, **f32)
+        self.scatter = RowScatter()
         # Exact frontier sparsity: a step reads the final tables only at batch
         # rows, and its loss gradient is non-zero only there. Masks (1 byte per
         # node) restrict the last forward layer to the rows it feeds and let the
@@ -104,6 +110,12 @@ class FusedTrainer:
         self.frontier = frontier
         self.mask_u = torch.zeros(self.U, dtype=torch.uint8, device=dev)
         self.mask_i = torch.zeros(self.I, dtype=torch.uint8, device=dev)
+        # Fused optimizer (GS order): the user Adam runs inside the last backward
+        # product's epilogue and the item Adam reads gI/(K+1) straight from the
+        # sparse BPR gradient table (grad_scale), so neither weight-gradient
+        # table is written or re-read. g_u0 / g_i0 are then not materialised;
+        # fuse_adam=False keeps them (the gradient-parity tests read them).
+        self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
 
     # -- batching ---------------------------------------------------------------
     def next_users(self) -> torch.Tensor:
@@ -120,7 +132,8 @@ class FusedTrainer:
     def step(self, users: torch.Tensor | None = None) -> torch.Tensor:
         users = self.next_users() if users is None else users.to(torch.int64).contiguous()
         B = users.numel()
-        pos, neg = self.sampler.sample(users, self.pos[:B], self.neg[:B])
+        self.pos, self.neg = self.posneg[:B], self.posneg[B:2 * B]
+        pos, neg = self.sampler.sample(users, self.pos, self.neg)
         st = stream_handle()
         masks = self._set_masks(users, pos, neg, 1) if self.frontier else None
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
@@ -128,24 +141,29 @@ class FusedTrainer:
                 final_rows=None if masks is None else (masks[0], masks[1], users))
         a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
                      self.pop, self.lambda_fair, parts=self.parts[: 3 * B],
-                     g_uf=self.g_uf, g_if=self.g_if)
+                     contrib=self.contrib)
         call("bbgr_bpr", ctypes.byref(a), st)
+        self.scatter(self.g_uf, users, self.contrib[:B])
+        self.scatter(self.g_if, self.posneg[: 2 * B], self.contrib[B: 3 * B])
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
-        backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
-                 out_i=self.g_i0, ws=self.ws, grad_support=masks)
-        # ego L2 term goes straight to the weight grads (Version-2:503-507):
-        # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
         alpha = 2.0 * self.reg / B
-        call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
-             ptr(self.g_u0), ld(self.g_u0), self.d, st)
-        call("bbgr_rows_axpy", B, ptr(pos), alpha, ptr(self.item_w), ld(self.item_w),
-             ptr(self.g_i0), ld(self.g_i0), self.d, st)
-        call("bbgr_rows_axpy", B, ptr(neg), alpha, ptr(self.item_w), ld(self.item_w),
-             ptr(self.g_i0), ld(self.g_i0), self.d, st)
-        self.step_count += 1
-        adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
-        adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)
+        if self.fuse_adam:
+            self._backward_fused(users, pos, neg, masks, alpha)
+        else:
+            backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
+                     out_i=self.g_i0, ws=self.ws, grad_support=masks)
+            # ego L2 term goes straight to the weight grads (Version-2:503-507):
+            # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
+            call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
+                 ptr(self.g_u0), ld(self.g_u0), self.d, st)
+            call("bbgr_rows_axpy", B, ptr(pos), alpha, ptr(self.item_w), ld(self.item_w),
+                 ptr(self.g_i0), ld(self.g_i0), self.d, st)
+            call("bbgr_rows_axpy", B, ptr(neg), alpha, ptr(self.item_w), ld(self.item_w),
+                 ptr(self.g_i0), ld(self.g_i0), self.d, st)
+            self.step_count += 1
+            adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
+            adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)
         # restore the all-zero invariant of the sparse gradient tables
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
         call("bbgr_rows_zero", B, ptr(pos), ptr(self.g_if), ld(self.g_if), self.d, st)
@@ -153,6 +171,31 @@ class FusedTrainer:
         if masks is not None:
             self._set_masks(users, pos, neg, 0)
         return self.loss
+
+    def _backward_fused(self, users, pos, neg, masks, alpha: float) -> None:
+        """GS backward with Adam fused (see __init__). The ego-L2 rows enter
+        through the sparse tables: grad_u0 = out*T + gl*(gU + alpha/gl*u0[b])
+        and grad_i0 = gl*(gI + alpha/gl*i0[pos,neg]) (Version-2:503-507)."""
+        st = stream_handle()
+        B = users.numel()
+        gl = 1.0 / (self.K + 1)
+        a_gl = alpha / gl
+        self.step_count += 1
+        adam_u = AdamRows(self.user_w, self.m_u, self.v_u, self.step_count, self.lr)
+
+        def before_last():
+            call("bbgr_rows_axpy", B, ptr(users), a_gl, ptr(self.user_w), ld(self.user_w),
+                 ptr(self.g_uf), ld(self.g_uf), self.d, st)
+
+        backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
+                 ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
+                 before_last=before_last)
+        call("bbgr_rows_axpy", B, ptr(pos), a_gl, ptr(self.item_w), ld(self.item_w),
+             ptr(self.g_if), ld(self.g_if), self.d, st)
+        call("bbgr_rows_axpy", B, ptr(neg), a_gl, ptr(self.item_w), ld(self.item_w),
+             ptr(self.g_if), ld(self.g_if), self.d, st)
+        adam_step(self.item_w, self.g_if, self.m_i, self.v_i, self.step_count, self.lr,
+                  grad_scale=gl)
 
     def _set_masks(self, users, pos, neg, value: int):
         """mask_u = batch users; mask_i = batch items (+ N(batch users) for GS,

@@ -174,6 +174,13 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   the plan (all three are row-ordered, so a row range maps to contiguous   */
 /*   chunk / split ranges). Lets the sharded step all-reduce item partial     */
 /*   sums chunk by chunk, overlapped with the next chunk's SpMM.              */
+/* adam_param (nullable): fused optimizer step. The row value the y output    */
+/*   would receive (g = ys*T + as*add) is the gradient of that row of         */
+/*   adam_param, and bbgr_adam's update (same math, same rounding) is applied */
+/*   in place to adam_param / adam_exp_avg / adam_exp_avg_sq (row stride      */
+/*   adam_ld). y may then be NULL: the gradient table is never written nor    */
+/*   re-read (the last backward product of the training step, V2:862-863).   */
+/*   Every row of the launch must be computed (no masks / row lists).         */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -207,6 +214,17 @@ typedef struct {
   int64_t n_row_list;
   int32_t use_range;
   int32_t range[6];
+  float *adam_param;
+  float *adam_exp_avg;
+  float *adam_exp_avg_sq;
+  int64_t adam_ld;
+  float adam_lr;
+  float adam_beta1;
+  float adam_beta2;
+  float adam_eps;
+  float adam_weight_decay;
+  float adam_bias_correction1;
+  float adam_bias_correction2_sqrt;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -235,6 +253,12 @@ int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
 /*   g_uf[u] += .., g_if[p] += .., g_if[n] += ..   (dense tables, atomics)    */
 /*   g_ue[u] += 2 reg G/B ue[u], g_ie[p|n] += 2 reg G/B ie[p|n]               */
 /* Any grad pointer may be NULL to skip it. Index vectors are int64.          */
+/* contrib (nullable, [3*batch rows], ld ldcontrib): deterministic mode. The  */
+/*   g_uf / g_if terms are NOT scattered; instead row b receives the user    */
+/*   term of triple b, row batch+b its pos-item term, row 2*batch+b its      */
+/*   neg-item term (zero rows for skipped triples). bbgr_scatter_add_rows   */
+/*   then sums them per destination row in a fixed order (bitwise            */
+/*   reproducible training step).                                            */
 /* A triple with an index outside [0,n_users) / [0,n_items) (e.g. the        */
 /* sampler's -1 for a user without positives) contributes zero everywhere.   */
 /* ------------------------------------------------------------------------- */
@@ -259,6 +283,7 @@ typedef struct {
   float *g_if; int64_t ldgif;
   float *g_ue; int64_t ldgue;
   float *g_ie; int64_t ldgie;
+  float *contrib; int64_t ldcontrib;
 } bbgr_bpr_args;
 
 int bbgr_bpr(const bbgr_bpr_args *args, bbgr_stream_t stream);
@@ -275,10 +300,12 @@ int bbgr_bpr_reduce(int64_t batch, const float *parts, float reg,
 /*   bias_correction2_sqrt = sqrt(1-beta2^t) in double, as torch does.        */
 /*   m = lerp(m, g, 1-beta1); v = beta2 v + (1-beta2) g^2;                    */
 /*   p -= (lr/bc1) * m / (sqrt(v)/bc2_sqrt + eps)   (+ weight_decay*p in g)   */
+/*   with g = grad_scale * grad[i] (1.0 = plain Adam; the GS item gradient    */
+/*   gI/(K+1) is folded in this way instead of materialising it).             */
 /* ------------------------------------------------------------------------- */
 int bbgr_adam(int64_t n, float *param, const float *grad, float *exp_avg,
               float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
-              float weight_decay, float bias_correction1,
+              float weight_decay, float grad_scale, float bias_correction1,
               float bias_correction2_sqrt, bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
@@ -292,6 +319,15 @@ int bbgr_rows_zero(int64_t n, const int64_t *idx, float *table, int64_t ld,
 int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha, const float *src,
                    int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
                    bbgr_stream_t stream);
+
+/* Deterministic index_add_: dst[idx[k], :d] += src[k, :d] for k < n, with   */
+/* the addends of each destination row summed in ascending k and added once  */
+/* (stable radix sort of idx, then one segment sum per row). Negative or     */
+/* >= n_dst indices are skipped. Replaces the autograd scatter of the BPR    */
+/* gradient and Tensor.index_add_ (main.py:645-650 scatter_add).             */
+int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float *src, int64_t ldsrc,
+                          float *dst, int64_t lddst, int32_t d, int64_t n_dst,
+                          void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
 
 /* mask[idx[k]] = value for k < n. */
 int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value, uint8_t *mask,

@@ -371,7 +371,7 @@ def test_fused_trainer_step_vs_oracle(gold, variant):
     g = BipartiteGraph(e, U, I, DEV)
     lam = 0.05 if variant == "cu_fair" else 0.0
     tr = FusedTrainer(g, variant, cred=cred, emb_dim=D, num_layers=K, batch_size=B,
-                      lambda_fair=lam, u0=gold["u0"], i0=gold["i0"])
+                      lambda_fair=lam, u0=gold["u0"], i0=gold["i0"], fuse_adam=False)
     deg_u = np.bincount(e[0], minlength=U)
     uu = np.unique(gold["users"])
     users = t(uu[deg_u[uu] > 0], torch.int64)       # train users have >= 1 positive
@@ -533,7 +533,7 @@ def test_frontier_step_matches_dense_step(variant):
     u0 = rng.uniform(-0.05, 0.05, (U, 64)).astype(np.float32)
     i0 = rng.uniform(-0.05, 0.05, (I, 64)).astype(np.float32)
     kw = dict(cred=cred, emb_dim=64, num_layers=3, batch_size=4096, u0=u0, i0=i0,
-              lambda_fair=0.05 if variant == "cu_fair" else 0.0)
+              lambda_fair=0.05 if variant == "cu_fair" else 0.0, fuse_adam=False)
     dense = FusedTrainer(g, variant, frontier=False, **kw)
     front = FusedTrainer(g, variant, frontier=True, **kw)
     for _ in range(3):
@@ -547,6 +547,49 @@ def test_frontier_step_matches_dense_step(variant):
             assert err <= 1e-6, (what, float(err))
     # masks are left clean for the next step
     assert int(front.mask_u.sum()) == 0 and int(front.mask_i.sum()) == 0
+
+
+@pytest.mark.parametrize("variant,K", [("v2_pop", 3), ("method_a", 2), ("v2_pop", 1)])
+def test_fused_adam_step_matches_unfused(variant, K):
+    """Adam fused into the last backward SpMM (users) and read from the sparse
+    BPR table with grad_scale (items) == the separate gradient + Adam path:
+    bitwise on rows outside the batch, to fp32 rounding on batch rows (the
+    ego-L2 term enters as gl*(gU + a/gl*e0) instead of gl*gU + a*e0)."""
+    from bbgr.synthetic import CONFIGS, config_edges
+    from bbgr.trainer import FusedTrainer
+    c = CONFIGS["C2"]
+    U, I = c["num_users"], c["num_items"]
+    e = config_edges("C2")
+    g = BipartiteGraph(e, U, I, DEV)
+    rng = np.random.default_rng(1)
+    u0 = rng.uniform(-0.05, 0.05, (U, 64)).astype(np.float32)
+    i0 = rng.uniform(-0.05, 0.05, (I, 64)).astype(np.float32)
+    kw = dict(cred=synthetic_credibility(U, 2), emb_dim=64, num_layers=K, batch_size=4096,
+              u0=u0, i0=i0)
+    sep = FusedTrainer(g, variant, fuse_adam=False, **kw)
+    fus = FusedTrainer(g, variant, fuse_adam=True, **kw)
+    assert fus.fuse_adam and not sep.fuse_adam
+    for step in range(3):
+        users = sep.next_users()
+        fus.next_users()
+        ls, lf = float(sep.step(users)), float(fus.step(users))
+        assert torch.equal(sep.pos, fus.pos) and torch.equal(sep.neg, fus.neg)
+        assert abs(ls - lf) <= 1e-6 * abs(ls)
+        if step == 0 and K > 1:   # K == 1: masked last product + separate Adam
+            B = users.numel()
+            for a, b, rows, n, what in (
+                    (sep.user_w, fus.user_w, users, U, "user"),
+                    (sep.item_w, fus.item_w, torch.cat([sep.pos[:B], sep.neg[:B]]), I, "item")):
+                off = torch.ones(n, dtype=torch.bool, device=DEV)
+                off[rows] = False
+                assert torch.equal(a[off], b[off]), what      # bitwise off the batch
+    for a, b, init, what in ((sep.user_w, fus.user_w, u0, "user"),
+                             (sep.item_w, fus.item_w, i0, "item")):
+        err = (a.double() - b.double()).norm() / (a.double() - t(init).double()).norm()
+        assert err <= 1e-4, (what, float(err))
+    for m_s, m_f in ((sep.m_u, fus.m_u), (sep.v_u, fus.v_u), (sep.m_i, fus.m_i)):
+        assert (m_s.double() - m_f.double()).norm() <= 1e-4 * m_s.double().norm()
+    assert fus.g_uf.abs().sum().item() == 0 and fus.g_if.abs().sum().item() == 0
 
 
 def test_graph_from_memmaps_matches_array(tmp_path):
@@ -563,3 +606,44 @@ def test_graph_from_memmaps_matches_array(tmp_path):
     for g in (g2, g3):
         assert torch.equal(g.user_csr.indptr, g1.user_csr.indptr)
         assert torch.equal(g.item_csr.indices, g1.item_csr.indices)
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+def test_scatter_add_rows_matches_index_add(d):
+    """bbgr_scatter_add_rows == numpy add.at (sequential ascending order) bit
+    for bit on a zero destination; invalid indices skipped; repeatable."""
+    from bbgr.scatter import index_add_rows
+    rng = np.random.default_rng(d)
+    n, n_dst = 20000, 700
+    idx = rng.integers(-3, n_dst + 3, n)          # duplicates + out-of-range rows
+    idx[:500] = 5                                 # one long run
+    src = rng.normal(size=(n, d)).astype(np.float32)
+    want = np.zeros((n_dst, d), np.float32)
+    ok = (idx >= 0) & (idx < n_dst)
+    np.add.at(want, idx[ok], src[ok])
+    got = index_add_rows(torch.zeros(n_dst, d, device=DEV), t(idx, torch.int64), t(src))
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+    base = rng.normal(size=(n_dst, d)).astype(np.float32)
+    got2 = index_add_rows(t(base), t(idx, torch.int64), t(src)).cpu().numpy()
+    np.testing.assert_allclose(got2, base.astype(np.float64) + want, rtol=1e-5, atol=1e-4)
+    got3 = index_add_rows(t(base), t(idx, torch.int64), t(src)).cpu().numpy()
+    np.testing.assert_array_equal(got2, got3)
+    empty = index_add_rows(t(base), torch.empty(0, dtype=torch.int64, device=DEV), t(src))
+    np.testing.assert_array_equal(empty.cpu().numpy(), base)
+
+
+def test_training_step_is_bitwise_reproducible():
+    """With the deterministic BPR scatter every reduction of the fused step has
+    a fixed order: two trainers from the same state agree bit for bit."""
+    from bbgr.synthetic import CONFIGS, config_edges
+    from bbgr.trainer import FusedTrainer
+    c = CONFIGS["C2"]
+    U, I = c["num_users"], c["num_items"]
+    g = BipartiteGraph(config_edges("C2"), U, I, DEV)
+    kw = dict(cred=synthetic_credibility(U, 2), emb_dim=64, num_layers=3, batch_size=4096,
+              seed=9)
+    a, b = FusedTrainer(g, "v2_pop", **kw), FusedTrainer(g, "v2_pop", **kw)
+    for _ in range(3):
+        assert float(a.step()) == float(b.step())
+    for x, y in ((a.user_w, b.user_w), (a.item_w, b.item_w), (a.m_u, b.m_u), (a.v_i, b.v_i)):
+        assert torch.equal(x, y)

@@ -52,7 +52,8 @@ def test_invalid_arguments_rejected_without_gpu():
     L = _lib.lib()
     rc = L.bbgr_spmm(None, None, None)
     assert rc == -1 and b"null" in L.bbgr_last_error()
-    rc = L.bbgr_adam(-1, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, None)
+    rc = L.bbgr_adam(-1, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, 1.0,
+                     None)
     assert rc == -1
     with pytest.raises(_lib.BbgrError, match="BBGR_ERR_INVALID"):
         _lib.call("bbgr_bpr_reduce", 0, None, 0.0, 0.0, None, None)
