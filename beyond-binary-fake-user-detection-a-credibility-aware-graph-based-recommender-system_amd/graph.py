@@ -54,7 +54,7 @@ class Csr:
     def __init__(self, rows, cols, n_rows: int, n_cols: int, device,
                  edge_values: torch.Tensor | None = None,
                  long_threshold: int = DEFAULT_LONG_THRESHOLD,
-                 chunk_edges: int = DEFAULT_CHUNK_EDGES):
+                 chunk_edges: int = DEFAULT_CHUNK_EDGES, keep_perm: bool = False):
         _lib.require_gpu()
         device = torch.device(device)
         rows = _as_device_i32(rows, device)
@@ -72,7 +72,7 @@ class Csr:
         self.indptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=device)
         self.indices = torch.empty(max(nnz, 1), dtype=torch.int32, device=device)
         perm = (torch.empty(max(nnz, 1), dtype=torch.int32, device=device)
-                if edge_values is not None else None)
+                if edge_values is not None or keep_perm else None)
         st = stream_handle()
         ws_bytes = _lib.workspace_query(
             "bbgr_csr_build", nnz, ptr(rows), ptr(cols), self.n_rows, self.n_cols,
@@ -82,6 +82,7 @@ class Csr:
         call("bbgr_csr_build", nnz, ptr(rows), ptr(cols), self.n_rows, self.n_cols,
              ptr(self.indptr), ptr(self.indices), ptr(perm), ptr(ws), ctypes.byref(n), st)
         del ws
+        self.perm = perm if keep_perm else None   # CSR slot -> input edge id
         self.values = None
         if edge_values is not None:
             ev = torch.as_tensor(edge_values).to(device=device, dtype=torch.float32)

@@ -329,6 +329,27 @@ int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float *src, int64
                           float *dst, int64_t lddst, int32_t d, int64_t n_dst,
                           void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
 
+/* ------------------------------------------------------------------------- */
+/* Credibility-GNN edge weights, main.py:677-701:       */
+/*   CredModel.ewa_raw: w = max(beta*clamp(attr[:,col_verified],0,1) +       */
+/*                              gamma*attr[:,col_align], 0)                  */
+/*   CredModel.normalize_per_dst: w~ = w / (sum of w over the edge's dst +   */
+/*                                1e-12 (eps))                               */
+/* csr: destination-row CSR of the edges (bbgr_csr_build with perm_out);     */
+/* perm[k]: input edge id of CSR slot k. w_in (nullable, input-edge order)   */
+/* replaces the EWA formula (normalize_per_dst on given weights). Outputs    */
+/* (each nullable): w_raw and w_edge in input-edge order, w_csr in CSR order */
+/* (the edge values of the aggregation SpMM, CredModel.aggregate = bbgr_spmm */
+/* over this CSR). The csr must carry its load-balance plan; per-row sums    */
+/* follow it in a fixed order (bitwise deterministic). Workspace: per-row    */
+/* sums + chunk partials (+ raw weights when w_in and w_raw are both NULL).  */
+/* ------------------------------------------------------------------------- */
+int bbgr_ewa_normalize(const bbgr_csr *csr, const int32_t *perm, const float *w_in,
+                       const float *edge_attr, int64_t lda, int32_t col_verified,
+                       int32_t col_align, float beta, float gamma, float eps,
+                       float *w_raw, float *w_edge, float *w_csr, void *workspace,
+                       size_t *workspace_bytes, bbgr_stream_t stream);
+
 /* mask[idx[k]] = value for k < n. */
 int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value, uint8_t *mask,
                    bbgr_stream_t stream);

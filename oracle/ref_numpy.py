@@ -448,3 +448,32 @@ def full_ranking_reference_style(users, tr_ptr, tr_idx, uf, itf, k):
             scores[tr] = np.float32(-1e9)
         out[b] = np.argsort(-scores, kind="stable")[:k]
     return out
+
+
+# ---------------------------------------------------------------------------
+# Credibility GNN edge weighting + aggregation (main.py:677-691)
+# ---------------------------------------------------------------------------
+def ewa_raw(edge_attr, col_verified=0, col_align=1, beta=1.0, gamma=1.0):
+    """main.py:677-681: clamp(beta*clamp(verified,0,1) + gamma*align, min=0),
+    evaluated in fp32 as torch does."""
+    a = np.asarray(edge_attr, np.float32)
+    v = np.clip(a[:, col_verified], np.float32(0), np.float32(1))
+    w = np.float32(beta) * v + np.float32(gamma) * a[:, col_align]
+    return np.maximum(w, np.float32(0)).astype(np.float32)
+
+
+def normalize_per_dst(w, dst, num_dst, eps=1e-12):
+    """main.py:683-685 in float64: w / (sum of w over dst + eps)[dst]."""
+    w = np.asarray(w, np.float64)
+    den = np.zeros(num_dst, np.float64)
+    np.add.at(den, np.asarray(dst), w)
+    return w / (den + eps)[np.asarray(dst)]
+
+
+def aggregate(src_x, edge_index, w_tilde, num_dst):
+    """main.py:687-691 in float64: scatter_add(w_tilde * src_x[src], dst)."""
+    x = np.asarray(src_x, np.float64)
+    src, dst = np.asarray(edge_index[0]), np.asarray(edge_index[1])
+    out = np.zeros((num_dst, x.shape[1]), np.float64)
+    np.add.at(out, dst, np.asarray(w_tilde, np.float64)[:, None] * x[src])
+    return out

@@ -122,3 +122,49 @@ def train_step(model: GSModel, opt: torch.optim.Optimizer, users, pos, neg, reg)
     loss.backward()
     opt.step()
     return float(loss.item())
+
+
+class CredModelRef(torch.nn.Module):
+    """fp32 torch restatement of main.py:659-707 (CredModel) with the
+    reference's own expressions (index_add_ scatter, per-dst normalisation):
+    the CPU model the device CredModel is checked against."""
+
+    def __init__(self, user_in_dim, item_in_dim, hidden_dim, col_verified=0, col_align=1,
+                 beta=1.0, gamma=1.0):
+        super().__init__()
+        nn = torch.nn
+        self.user_proj = nn.Linear(user_in_dim, hidden_dim)
+        self.item_proj = nn.Linear(item_in_dim, hidden_dim)
+        self.item_upd = nn.Linear(hidden_dim * 2, hidden_dim)
+        self.user_upd = nn.Linear(hidden_dim * 2, hidden_dim)
+        self.out = nn.Linear(hidden_dim, 1)
+        self.cv, self.ca, self.beta, self.gamma = col_verified, col_align, beta, gamma
+
+    @staticmethod
+    def _scatter_add(src, index, dim_size):
+        out = torch.zeros((dim_size,) + src.shape[1:], dtype=src.dtype)
+        out.index_add_(0, index, src)
+        return out
+
+    def ewa_raw(self, ea):
+        w = self.beta * ea[:, self.cv].clamp(0, 1) + self.gamma * ea[:, self.ca]
+        return w.clamp(min=0.0)
+
+    def normalize_per_dst(self, w, dst, num_dst):
+        denom = self._scatter_add(w.unsqueeze(-1), dst, num_dst).squeeze(-1) + 1e-12
+        return w / denom[dst]
+
+    def aggregate(self, src_x, edge_index, w_tilde, num_dst):
+        msg = w_tilde.unsqueeze(-1) * src_x[edge_index[0]]
+        return self._scatter_add(msg, edge_index[1], num_dst)
+
+    def forward_subgraph(self, x_u, x_i, e_u2i, ea_u2i, e_i2u, ea_i2u):
+        F = torch.nn.functional
+        h_u0, h_i0 = self.user_proj(x_u), self.item_proj(x_i)
+        w1t = self.normalize_per_dst(self.ewa_raw(ea_u2i), e_u2i[1], h_i0.size(0))
+        h_i1 = F.relu(self.item_upd(torch.cat([h_i0, self.aggregate(h_u0, e_u2i, w1t,
+                                                                  h_i0.size(0))], -1)))
+        w2t = self.normalize_per_dst(self.ewa_raw(ea_i2u), e_i2u[1], h_u0.size(0))
+        h_u2 = F.relu(self.user_upd(torch.cat([h_u0, self.aggregate(h_i1, e_i2u, w2t,
+                                                                  h_u0.size(0))], -1)))
+        return torch.sigmoid(self.out(h_u2)).squeeze(-1), h_u2, h_i1, w1t

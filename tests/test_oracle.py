@@ -307,3 +307,27 @@ def test_full_ranking_c_oracle():
     for b in range(1, U):
         assert not np.isin(items[b], tr[b]).any()
         assert (np.diff(scores[b]) <= 0).all()
+
+
+def test_cred_gnn_oracle_known_answers():
+    """main.py:677-691 restated: EWA clamps, per-dst normalisation sums to 1
+    over each destination with positive weight, aggregation by hand; the numpy
+    and torch restatements agree."""
+    import torch
+    from oracle import ref_torch as T
+    ea = np.array([[1.5, 0.2, 0, 0, 0], [0.0, -0.5, 0, 0, 0], [0.5, 0.25, 0, 0, 0],
+                   [-1.0, 2.0, 0, 0, 0]], np.float32)
+    w = R.ewa_raw(ea)
+    np.testing.assert_allclose(w, [1.2, 0.0, 0.75, 2.0], rtol=1e-7)
+    ei = np.array([[0, 1, 2, 2], [0, 0, 0, 1]])
+    wt = R.normalize_per_dst(w, ei[1], 3)
+    np.testing.assert_allclose(wt, [1.2 / 1.95, 0.0, 0.75 / 1.95, 1.0], rtol=1e-6)
+    x = np.array([[1.0, 0.0], [0.0, 1.0], [2.0, 2.0]])
+    agg = R.aggregate(x, ei, wt, 3)
+    np.testing.assert_allclose(agg[0], [1.2 / 1.95 + 1.5 / 1.95, 1.5 / 1.95], rtol=1e-6)
+    np.testing.assert_allclose(agg[1], [2.0, 2.0]) and np.testing.assert_allclose(agg[2], 0.0)
+    m = T.CredModelRef(3, 3, 4)
+    tw = m.normalize_per_dst(m.ewa_raw(torch.tensor(ea)), torch.tensor(ei[1]), 3)
+    np.testing.assert_allclose(tw.numpy(), wt, rtol=1e-6)
+    ta = m.aggregate(torch.tensor(x, dtype=torch.float32), torch.tensor(ei), tw, 3)
+    np.testing.assert_allclose(ta.numpy(), agg, rtol=1e-6)
