@@ -257,10 +257,13 @@ def main():
                    "parallelism": f"user-rows x{world}"},
         "bpr_steps_per_s": args.steps / elapsed,
         "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
-        "frontier": {"enabled": world == 1 and not args.dense,
+        "frontier": {"enabled": not args.dense,
                      "masked_launches_per_step": masked_n / args.steps,
                      "masked_ms_per_step": masked_ms / args.steps,
                      "full_launches_per_step": n_launch / args.steps,
+                     "masked_sequence_ms": [
+                         {"rows": r, "nnz": z, "avg_ms": ms}
+                         for r, z, ms in timer.sequence("masked", args.steps)],
                      "note": "value counts the reference step's 4*K*E edge traversals; "
                              "masked launches skip exact-zero / unread rows"},
         "fused_adam_spmm": adam_info,

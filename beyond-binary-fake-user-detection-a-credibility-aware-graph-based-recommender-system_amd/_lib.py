@@ -164,6 +164,8 @@ _SIGNATURES = {
     "bbgr_eval_full": ([ctypes.POINTER(EvalArgs), _P, ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_nonempty_rows": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P],
                            c_int32),
+    "bbgr_mask_to_list": ([c_int64, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_rows_gather": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
 }
 
 _lib = None

@@ -271,6 +271,11 @@ struct NonEmpty {
   }
 };
 
+struct Flagged {
+  const unsigned char *mask;
+  __host__ __device__ bool operator()(const long &r) const { return mask[r] != 0; }
+};
+
 }  // namespace bbgr
 
 using namespace bbgr;
@@ -591,5 +596,35 @@ extern "C" int bbgr_nonempty_rows(int32_t n_rows, const int32_t *indptr,
   }
   BBGR_HIP(hipcub::DeviceSelect::If(workspace, temp, it, (long *)out, (long *)count,
                                     n_rows, sel, st));
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_mask_to_list(int64_t n, const uint8_t *mask, int64_t *out,
+                                 int64_t *count, void *workspace, size_t *workspace_bytes,
+                                 bbgr_stream_t stream) {
+  BBGR_REQUIRE(workspace_bytes && n >= 0 && n < (int64_t)1 << 31,
+               "bbgr_mask_to_list: bad args");
+  hipStream_t st = as_stream(stream);
+  hipcub::CountingInputIterator<long> it(0);
+  Flagged sel{mask};
+  size_t temp = 0;
+  BBGR_HIP(hipcub::DeviceSelect::If(nullptr, temp, it, (long *)nullptr, (long *)nullptr,
+                                    n > 0 ? (int)n : 1, sel, st));
+  const size_t need = align_up(temp);
+  if (!workspace) {
+    *workspace_bytes = need;
+    return BBGR_OK;
+  }
+  if (*workspace_bytes < need) {
+    set_error("bbgr_mask_to_list: workspace %zu < %zu", *workspace_bytes, need);
+    return BBGR_ERR_WORKSPACE;
+  }
+  BBGR_REQUIRE(mask && out && count, "bbgr_mask_to_list: null arrays");
+  if (n == 0) {
+    BBGR_HIP(hipMemsetAsync(count, 0, 8, st));
+    return BBGR_OK;
+  }
+  BBGR_HIP(hipcub::DeviceSelect::If(workspace, temp, it, (long *)out, (long *)count, (int)n,
+                                    sel, st));
   return BBGR_OK;
 }

@@ -316,11 +316,17 @@ template <int D>
 __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float *t,
                                                        long ldt) {
   constexpr int V = D / 64;
-  const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const long j = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
+  long row = j;
+  if (P.row_list) {   // compact input: row j of t -> output row row_list[j]
+    if (j >= P.n_row_list) return;
+    row = P.row_list[j];
+    if (row < 0) return;
+  }
   if (row >= P.n_rows) return;
   if (P.row_mask && !P.row_mask[row]) return;
-  const float4 *src = reinterpret_cast<const float4 *>(t + row * ldt) + lane;
+  const float4 *src = reinterpret_cast<const float4 *>(t + j * ldt) + lane;
   float4 T[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) T[k] = src[16 * k];
@@ -421,11 +427,16 @@ extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
                    ld_ok(a->acc_in, a->ldacc_in, d) && ld_ok(a->acc_out, a->ldacc_out, d) &&
                    adam_ok(a, d),
                "bbgr_epilogue: tables must be 16-byte aligned with ld >= d, ld % 4 == 0");
+  BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_epilogue: negative n_row_list");
   SpmmParams P = {};
   P.n_rows = n_rows;
   fill_epilogue(P, a);
   P.row_mask = a->row_mask;
-  const unsigned grid = (unsigned)(((long)n_rows + 15) / 16);
+  P.row_list = (const long *)a->row_list;
+  P.n_row_list = a->n_row_list;
+  const long n_in = a->row_list ? (long)a->n_row_list : (long)n_rows;
+  if (n_in == 0) return BBGR_OK;
+  const unsigned grid = (unsigned)((n_in + 15) / 16);
   hipStream_t st = as_stream(stream);
   switch (d) {
     case 64: hipLaunchKernelGGL(epilogue_kernel<64>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;

@@ -258,6 +258,24 @@ __global__ void rows_axpy_kernel(long n, const long *idx, float alpha,
     atomicAdd(dst + r * ldd + c, alpha * src[r * lds + c]);
 }
 
+// dst[k, :] = src[idx[k], :] (zero row for idx < 0); float4 per lane, one
+// 16-lane group per row: the compaction of frontier rows for the sparse
+// multi-GPU exchange.
+__global__ __launch_bounds__(256) void rows_gather_kernel(long n, const long *idx,
+                                                          const float4 *src, long lds4,
+                                                          float4 *dst, long ldd4, int d4) {
+  const long k = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (k >= n) return;
+  const long r = idx[k];
+  float4 *out = dst + k * ldd4;
+  if (r < 0) {
+    for (int c = threadIdx.x & 15; c < d4; c += 16) out[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const float4 *in = src + r * lds4;
+  for (int c = threadIdx.x & 15; c < d4; c += 16) out[c] = in[c];
+}
+
 // ---- deterministic index_add_ (bbgr_scatter_add_rows) ----------------------
 __global__ void scatter_keys_kernel(long n, const long *idx, long n_dst, unsigned *keys,
                                     int *vals) {
@@ -498,5 +516,22 @@ extern "C" int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha,
                      as_stream(stream), (long)n, (const long *)idx, alpha, src,
                      (long)ldsrc, dst, (long)lddst, d);
   BBGR_LAUNCHED("rows_axpy_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_rows_gather(int64_t n, const int64_t *idx, const float *src,
+                                int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
+                                bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && d > 0 && (d & 3) == 0 && ldsrc >= d && lddst >= d &&
+                   (ldsrc & 3) == 0 && (lddst & 3) == 0,
+               "bbgr_rows_gather: bad sizes (d, ld multiples of 4, ld >= d)");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx && src && dst && aligned16(src) && aligned16(dst),
+               "bbgr_rows_gather: null or unaligned arrays");
+  hipLaunchKernelGGL(rows_gather_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)idx,
+                     reinterpret_cast<const float4 *>(src), (long)ldsrc / 4,
+                     reinterpret_cast<float4 *>(dst), (long)lddst / 4, d / 4);
+  BBGR_LAUNCHED("rows_gather_kernel");
   return BBGR_OK;
 }

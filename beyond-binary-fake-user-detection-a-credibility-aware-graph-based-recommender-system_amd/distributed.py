@@ -13,13 +13,17 @@ SURVEY §8(e). The reference is single-device; this is the build's scale-out:
   * the exchange is pipelined: the item rows are cut into edge-balanced
     ranges; range c's all-reduce (async, RCCL's stream) overlaps range c+1's
     SpMM on the compute stream.
-  * BPR: each rank samples its own users; item gradients are all-reduced once
-    per step; the ego-L2 item term is applied from the all-gathered (pos, neg)
-    indices on every rank (identical values, so replicas stay bitwise
-    identical); the loss is the mean over ranks.
+  * BPR: each rank samples its own users; the item gradient of the global
+    batch is assembled on every rank from the all-gathered (pos, neg) ids and
+    per-triple gradient rows by the same fixed-order scatter (no I*d
+    all-reduce); the ego-L2 item term uses the same ids; replicas stay
+    bitwise identical; the loss is the mean over ranks.
   * frontier sparsity as on one GPU, with the ITEM masks made global by one
     all-reduce of a byte mask per step (every rank must compute every row any
-    rank needs before the exchange).
+    rank needs before the exchange); the two frontier item products exchange
+    only the frontier rows (compacted), not the whole item table.
+  * the user Adam runs fused in the last (purely local) backward product and
+    the item Adam reads the sparse item gradient, exactly as on one GPU.
 
 Two ways to build the shards:
   ShardedTrainer.from_global_edges(edges, U, I, ...)   strong scaling: one
@@ -43,7 +47,8 @@ from .graph import BipartiteGraph, Scales
 from .optim import adam_step
 from .propagate import ORDER_GS, OperatorPair, backward, epilogue, forward, spmm
 from .sampler import PopMixSampler, nonempty_rows, shuffle
-from .trainer import VARIANTS
+from .scatter import RowScatter
+from .trainer import VARIANTS, FusedTrainer
 
 
 def partition_users(deg_u: np.ndarray, world: int) -> np.ndarray:
@@ -87,22 +92,72 @@ def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
 class ItemExchange:
     """The per-layer exchange of item partial sums (propagate's `reduce` hook).
 
-    item_product(): the SpMM runs over `parts` edge-balanced item-row ranges;
-    each range's partial sums are all-reduced asynchronously as soon as they
-    are written, overlapping the next range's SpMM; the epilogue runs once all
-    ranges are summed."""
+    Dense products (every item row): the SpMM runs over `parts` edge-balanced
+    item-row ranges; each range's partial sums are all-reduced asynchronously
+    as soon as they are written, overlapping the next range's SpMM; the
+    epilogue runs once all ranges are summed.
+
+    Frontier products (a `row_mask`: the last forward item layer and the first
+    backward item product of a training step) need only the step's item
+    frontier, a GLOBAL row set identical on every rank (`set_rows`). Only
+    those rows are computed (row-list SpMM), compacted (bbgr_rows_gather),
+    all-reduced and finished by the compact epilogue: the payload is
+    |frontier|*d*4 bytes instead of I*d*4."""
 
     def __init__(self, group=None, parts: int = 4):
         self.group, self.parts = group, max(1, int(parts))
         self.balance_indptr = None   # global item indptr: identical cuts on every rank
+        self._rows = None            # (device list, device count, host count, event)
+        self._list = None
+        self._compact = None
 
     def __call__(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def set_rows(self, row_list: torch.Tensor, count_dev: torch.Tensor,
+                 count_host: torch.Tensor) -> None:
+        """The step's frontier rows: row_list[:count] (ascending, device).
+        The count's device->host copy is enqueued now; it is read (one event
+        wait, long complete by then) at the first frontier product."""
+        count_host.copy_(count_dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._rows = (row_list, count_host, ev)
+        self._list = None
+
+    def clear_rows(self) -> None:
+        self._rows, self._list = None, None
+
+    def rows(self) -> torch.Tensor | None:
+        if self._rows is None:
+            return None
+        if self._list is None:
+            lst, host, ev = self._rows
+            ev.synchronize()
+            self._list = lst[: int(host[0])]
+        return self._list
+
+    def _compact_buf(self, n: int, d: int, device) -> torch.Tensor:
+        c = self._compact
+        if c is None or c.shape[0] < n or c.shape[1] != d:
+            c = self._compact = torch.empty(max(n, 1), d, dtype=torch.float32, device=device)
+        return c[:n]
 
     def item_product(self, prod, x, first, new, kw) -> None:
         src_mask = kw.pop("src_mask", None)
         row_mask = kw.pop("row_mask", None)
         t = new("partial", prod.csr.n_rows)
+        lst = self.rows() if row_mask is not None else None
+        if lst is not None:
+            d = x.shape[1]
+            n = lst.numel()
+            spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, row_list=lst)
+            c = self._compact_buf(n, d, x.device)
+            call("bbgr_rows_gather", n, ptr(lst), ptr(t), ld(t), ptr(c), ld(c), d,
+                 stream_handle())
+            dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
+            epilogue(c, row_list=lst, n_rows=prod.csr.n_rows, **kw)
+            return
         works = []
         for rg in prod.csr.row_ranges(self.parts, self.balance_indptr):
             spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, rng=rg)
@@ -113,14 +168,27 @@ class ItemExchange:
         epilogue(t, row_mask=row_mask, **kw)
 
 
-class ShardedTrainer:
+class ShardedTrainer(FusedTrainer):
+    """FusedTrainer's step on one user shard (see the module docstring).
+
+    Per step and rank the exchanges are: one byte all-reduce of the item
+    frontier mask; 2(K-1) dense item-row all-reduces (pipelined); two
+    frontier-row all-reduces (last forward item layer, first backward item
+    product); one all-gather of the batch's (pos, neg) ids and their
+    per-triple BPR gradient rows, summed on every rank in the same fixed order
+    (bbgr_scatter_add_rows), so the item gradient — and with it the item
+    Adam step — is bitwise identical on every rank without an I*d all-reduce;
+    one scalar all-reduce of the loss. The user Adam runs fused in the last
+    (local) backward product as on one GPU."""
+
     def __init__(self, local_edges: np.ndarray, num_local_users: int, num_items: int,
                  variant: str = "v2_pop", cred=None, emb_dim: int = 64, num_layers: int = 3,
                  lr: float = 1e-3, reg: float = 1e-4, batch_size: int = 8192,
                  neg_mix_pop: float | None = None, neg_pop_gamma: float = 0.75,
                  neg_max_tries: int = 50, lambda_fair: float = 0.0, seed: int = 42,
                  device=None, group=None, u0=None, i0=None, user_offset: int = 0,
-                 frontier: bool = True, exchange_parts: int = 4):
+                 frontier: bool = True, exchange_parts: int = 4, fuse_adam: bool = True,
+                 sparse_exchange: bool = True):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
         this rank's users; i0: the full (replicated) item table; batch_size:
         users per step on THIS rank."""
@@ -133,11 +201,13 @@ class ShardedTrainer:
         self.rank = dist.get_rank(group)
         dev = torch.device(device) if device is not None else torch.device("cuda")
         self.device = dev
-        self.U_local, self.I, self.d, self.K = num_local_users, num_items, emb_dim, num_layers
+        self.variant = variant
+        self.U, self.I, self.d, self.K = num_local_users, num_items, emb_dim, num_layers
+        self.U_local = num_local_users
         self.lo, self.hi = user_offset, user_offset + num_local_users
         self.order, self.lr, self.reg = order, lr, reg
-        self.lambda_fair = lambda_fair
-        self.B_local = max(1, int(batch_size))
+        self.lambda_fair, self.seed = lambda_fair, seed
+        self.B = self.B_local = max(1, int(batch_size))
         self.B_global = self.B_local * self.world
         self.exchange = ItemExchange(group, exchange_parts)
 
@@ -166,9 +236,13 @@ class ShardedTrainer:
         self.m_u, self.v_u = z(num_local_users), z(num_local_users)
         self.m_i, self.v_i = z(num_items), z(num_items)
         self.uf, self.itf = z(num_local_users), z(num_items)
-        self.g_uf, self.g_if = z(num_local_users), z(num_items)
+        self.g_uf, self.g_if = z(num_local_users), z(num_items)   # all-zero between steps
         self.g_u0, self.g_i0 = z(num_local_users), z(num_items)
-        self.parts = torch.empty(3 * self.B_local, **f32)
+        B = self.B_local
+        self.parts = torch.empty(3 * B, **f32)
+        self.contrib = torch.empty(3 * B, emb_dim, **f32)
+        self.all_contrib = torch.empty(2 * self.B_global, emb_dim, **f32)
+        self.scatter = RowScatter()
         self.loss = torch.zeros((), **f32)
         self.dloss = torch.full((), 1.0 / self.world, **f32)   # mean over the global batch
         self.ws: dict = {}
@@ -183,14 +257,21 @@ class ShardedTrainer:
         self.train_users = nonempty_rows(self.graph.user_csr)
         if self.train_users.numel() == 0:
             raise RuntimeError(f"rank {self.rank}: no train users in its shard")
-        self.seed, self.epoch, self.cursor, self.step_count = seed, 0, 0, 0
+        self.epoch, self.cursor, self.step_count = 0, 0, 0
         self.perm = None
-        self.pos = torch.empty(self.B_local, dtype=torch.int64, device=dev)
-        self.neg = torch.empty(self.B_local, dtype=torch.int64, device=dev)
+        self.posneg = torch.empty(2 * B, dtype=torch.int64, device=dev)
+        self.pos, self.neg = self.posneg[:B], self.posneg[B:]
         self.all_items = torch.empty(2 * self.B_global, dtype=torch.int64, device=dev)
         self.frontier = frontier
         self.mask_u = torch.zeros(num_local_users, dtype=torch.uint8, device=dev)
         self.mask_i = torch.zeros(num_items, dtype=torch.uint8, device=dev)
+        self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
+        # sparse frontier exchange: the step's global item frontier as a row list
+        self.sparse_exchange = bool(sparse_exchange) and frontier
+        self.item_list = torch.empty(max(num_items, 1), dtype=torch.int64, device=dev)
+        self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.item_count_host = torch.zeros(1, dtype=torch.int64).pin_memory()
+        self._list_ws = None
 
     @classmethod
     def from_global_edges(cls, edges: np.ndarray, num_users: int, num_items: int,
@@ -233,23 +314,39 @@ class ShardedTrainer:
 
     def _masks(self, users, pos, neg):
         """mask_u: my batch users. mask_i: every rank's batch items (+ every
-        rank's N(batch users) for GS), made global by a byte all-reduce."""
+        rank's N(batch users) for GS), made global by a byte all-reduce; its
+        rows, listed, are the step's frontier for the sparse exchange."""
         st = stream_handle()
         B = users.numel()
         call("bbgr_mark_rows", B, ptr(users), 1, ptr(self.mask_u), st)
-        call("bbgr_mark_rows", B, ptr(pos), 1, ptr(self.mask_i), st)
-        call("bbgr_mark_rows", B, ptr(neg), 1, ptr(self.mask_i), st)
+        call("bbgr_mark_rows", 2 * B, ptr(self.posneg), 1, ptr(self.mask_i), st)
         if self.order == ORDER_GS:
             uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), 1,
                  ptr(self.mask_i), st)
         dist.all_reduce(self.mask_i, op=dist.ReduceOp.SUM, group=self.group)  # <= world: no wrap
+        if self.sparse_exchange:
+            self._list_rows()
         return self.mask_u, self.mask_i
+
+    def _list_rows(self) -> None:
+        st = stream_handle()
+        I = self.I
+        need = ctypes.c_size_t(0)
+        call("bbgr_mask_to_list", I, ptr(self.mask_i), ptr(self.item_list),
+             ptr(self.item_count), None, ctypes.byref(need), st)
+        if self._list_ws is None or self._list_ws.numel() < need.value:
+            self._list_ws = torch.empty(max(need.value, 1), dtype=torch.uint8,
+                                        device=self.device)
+        have = ctypes.c_size_t(self._list_ws.numel())
+        call("bbgr_mask_to_list", I, ptr(self.mask_i), ptr(self.item_list),
+             ptr(self.item_count), ptr(self._list_ws), ctypes.byref(have), st)
+        self.exchange.set_rows(self.item_list, self.item_count, self.item_count_host)
 
     def step(self) -> torch.Tensor:
         users = self.next_users()
         B = users.numel()
-        pos, neg = self.sampler.sample(users, self.pos[:B], self.neg[:B])
+        pos, neg = self.sampler.sample(users, self.pos, self.neg)
         st = stream_handle()
         masks = self._masks(users, pos, neg) if self.frontier else None
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
@@ -257,28 +354,36 @@ class ShardedTrainer:
                 final_rows=None if masks is None else (masks[0], masks[1], users))
         a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
                      self.pop, self.lambda_fair, parts=self.parts[: 3 * B], dloss=self.dloss,
-                     g_uf=self.g_uf, g_if=self.g_if)
+                     contrib=self.contrib)
         call("bbgr_bpr", ctypes.byref(a), st)
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
-        self.exchange(self.g_if)                          # item grads of the global batch
-        _all_gather(self.all_items, torch.cat([pos, neg]), self.group)
-        backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
-                 out_i=self.g_i0, ws=self.ws, reduce=self.exchange, grad_support=masks)
+        self.scatter(self.g_uf, users, self.contrib[:B])
+        # item gradient of the global batch: every rank's (pos, neg) rows and
+        # their per-triple gradient rows, summed in rank-major order
+        _all_gather(self.all_items, self.posneg, self.group)
+        _all_gather(self.all_contrib, self.contrib[B: 3 * B], self.group)
+        self.scatter(self.g_if, self.all_items, self.all_contrib)
         alpha = 2.0 * self.reg / self.B_global            # ego L2 (Version-2:503-507)
-        call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
-             ptr(self.g_u0), ld(self.g_u0), self.d, st)
-        call("bbgr_rows_axpy", self.all_items.numel(), ptr(self.all_items), alpha,
-             ptr(self.item_w), ld(self.item_w), ptr(self.g_i0), ld(self.g_i0), self.d, st)
-        self.step_count += 1
-        adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
-        adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)
+        if self.fuse_adam:
+            self._backward_fused(users, self.all_items, masks, alpha, reduce=self.exchange)
+        else:
+            backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
+                     out_i=self.g_i0, ws=self.ws, reduce=self.exchange, grad_support=masks)
+            call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
+                 ptr(self.g_u0), ld(self.g_u0), self.d, st)
+            call("bbgr_rows_axpy", self.all_items.numel(), ptr(self.all_items), alpha,
+                 ptr(self.item_w), ld(self.item_w), ptr(self.g_i0), ld(self.g_i0), self.d, st)
+            self.step_count += 1
+            adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
+            adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
         call("bbgr_rows_zero", self.all_items.numel(), ptr(self.all_items), ptr(self.g_if),
              ld(self.g_if), self.d, st)
         if masks is not None:
             call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), st)
             self.mask_i.zero_()
+        self.exchange.clear_rows()
         dist.all_reduce(self.loss, op=dist.ReduceOp.SUM, group=self.group)
         self.loss.mul_(1.0 / self.world)
         return self.loss

@@ -135,6 +135,22 @@ class SpmmTimer:
         return out
 
 
+    def sequence(self, kind: str, steps: int):
+        """Per-position average ms of one kind of launch within a step (every
+        step issues the same launch sequence): [(rows, nnz, avg_ms), ...]."""
+        torch.cuda.synchronize()
+        recs = [r for r in self.records if r[3] == kind]
+        if steps <= 0 or len(recs) % steps:
+            return []
+        per = len(recs) // steps
+        out = []
+        for j in range(per):
+            ms = sum(recs[s * per + j][4].elapsed_time(recs[s * per + j][5])
+                     for s in range(steps)) / steps
+            out.append((recs[j][0], recs[j][1], ms))
+        return out
+
+
 _timer: SpmmTimer | None = None
 
 
@@ -194,8 +210,10 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,
              add_scale=None, add_scale_s: float = 1.0, acc_in=None, acc_out=None,
              acc_scale=None, acc_scale_s: float = 1.0, gamma: float = 1.0, acc_mask=None,
-             add_mask=None, row_mask=None) -> None:
-    """bbgr_epilogue: the SpMM epilogue applied to a dense table of row sums."""
+             add_mask=None, row_mask=None, row_list=None, n_rows: int | None = None) -> None:
+    """bbgr_epilogue: the SpMM epilogue applied to a table of row sums: dense
+    (row r of t is output row r), or compact with `row_list` (row j of t is
+    output row row_list[j]; `n_rows` = the output tables' row count)."""
     a = _lib.SpmmArgs()
     a.d = t.shape[1]
     a.y, a.ldy = ptr(y), ld(y)
@@ -208,7 +226,14 @@ def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, a
     a.gamma = gamma
     a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
     a.row_mask = ptr(row_mask)
-    call("bbgr_epilogue", t.shape[0], ptr(t), ld(t), ctypes.byref(a), stream_handle())
+    if row_list is not None:
+        if n_rows is None:
+            raise ValueError("epilogue: row_list needs n_rows (the output row count)")
+        if row_list.numel() > t.shape[0]:
+            raise ValueError("epilogue: compact table has fewer rows than row_list")
+        a.row_list, a.n_row_list = ptr(row_list), row_list.numel()
+    call("bbgr_epilogue", t.shape[0] if n_rows is None else n_rows, ptr(t), ld(t),
+         ctypes.byref(a), stream_handle())
 
 
 def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw) -> None:
@@ -350,10 +375,14 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(K, 0, -1):
             first = k == K
+            # first product: Gi_K is zero off the item support (batch items and
+            # N(batch users)) and the next product reads only that support, so
+            # the other rows are neither computed nor written (row_mask)
             _item_product(BI, gU if first else bufU, first, reduce, new, y=bufI,
                           y_scale=pair.feed_bwd_iu, y_scale_s=gl if first else 1.0,
                           add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
-                          src_mask=su if first else None)
+                          src_mask=su if first else None,
+                          row_mask=si if first else None)
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
                      add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl,

@@ -149,7 +149,7 @@ class FusedTrainer:
              ptr(self.loss), st)
         alpha = 2.0 * self.reg / B
         if self.fuse_adam:
-            self._backward_fused(users, pos, neg, masks, alpha)
+            self._backward_fused(users, self.posneg[: 2 * B], masks, alpha)
         else:
             backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                      out_i=self.g_i0, ws=self.ws, grad_support=masks)
@@ -172,10 +172,13 @@ class FusedTrainer:
             self._set_masks(users, pos, neg, 0)
         return self.loss
 
-    def _backward_fused(self, users, pos, neg, masks, alpha: float) -> None:
+    def _backward_fused(self, users, item_rows, masks, alpha: float, reduce=None) -> None:
         """GS backward with Adam fused (see __init__). The ego-L2 rows enter
         through the sparse tables: grad_u0 = out*T + gl*(gU + alpha/gl*u0[b])
-        and grad_i0 = gl*(gI + alpha/gl*i0[pos,neg]) (Version-2:503-507)."""
+        and grad_i0 = gl*(gI + alpha/gl*i0[pos,neg]) (Version-2:503-507).
+        item_rows: the batch's (pos, neg) items — of every rank when sharded,
+        where `reduce` is the item exchange and gI already holds the global
+        batch's item gradient."""
         st = stream_handle()
         B = users.numel()
         gl = 1.0 / (self.K + 1)
@@ -189,11 +192,10 @@ class FusedTrainer:
 
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
-                 before_last=before_last)
-        call("bbgr_rows_axpy", B, ptr(pos), a_gl, ptr(self.item_w), ld(self.item_w),
-             ptr(self.g_if), ld(self.g_if), self.d, st)
-        call("bbgr_rows_axpy", B, ptr(neg), a_gl, ptr(self.item_w), ld(self.item_w),
-             ptr(self.g_if), ld(self.g_if), self.d, st)
+                 before_last=before_last, reduce=reduce)
+        # duplicates add the same value, so the atomic order cannot matter
+        call("bbgr_rows_axpy", item_rows.numel(), ptr(item_rows), a_gl, ptr(self.item_w),
+             ld(self.item_w), ptr(self.g_if), ld(self.g_if), self.d, st)
         adam_step(self.item_w, self.g_if, self.m_i, self.v_i, self.step_count, self.lr,
                   grad_scale=gl)
 

@@ -233,7 +233,10 @@ int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
 /* The SpMM epilogue alone, with T read from a dense table t[n_rows, ldt]
  * (args->x / weight fields ignored; row_mask, acc_mask, add_mask honoured). Used after the RCCL all-reduce of
  * per-rank item partial sums in the user-row-sharded multi-GPU step, where
- * the epilogue cannot run before the sum is complete. */
+ * the epilogue cannot run before the sum is complete.
+ * args->row_list (nullable): t is COMPACT, t[n_row_list, ldt]; its row j is
+ * the sum of output row row_list[j] (< n_rows, the output tables' row count).
+ * The sparse frontier exchange all-reduces only those rows. */
 int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
                   const bbgr_spmm_args *args, bbgr_stream_t stream);
 
@@ -320,6 +323,12 @@ int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha, const float *src,
                    int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
                    bbgr_stream_t stream);
 
+/* dst[k, :d] = src[idx[k], :d] for k < n (zero row where idx[k] < 0). d and
+ * both ld multiples of 4, tables 16-byte aligned. Compacts frontier rows for
+ * the sparse multi-GPU exchange (the inverse is bbgr_epilogue's row_list). */
+int bbgr_rows_gather(int64_t n, const int64_t *idx, const float *src, int64_t ldsrc,
+                     float *dst, int64_t lddst, int32_t d, bbgr_stream_t stream);
+
 /* Deterministic index_add_: dst[idx[k], :d] += src[k, :d] for k < n, with   */
 /* the addends of each destination row summed in ascending k and added once  */
 /* (stable radix sort of idx, then one segment sum per row). Negative or     */
@@ -398,6 +407,11 @@ int bbgr_shuffle(int64_t n, const int64_t *in, int64_t *out, uint64_t seed,
 int bbgr_nonempty_rows(int32_t n_rows, const int32_t *indptr, int64_t *out,
                        int64_t *count, void *workspace, size_t *workspace_bytes,
                        bbgr_stream_t stream);
+
+/* Rows flagged in mask[n] (any non-zero byte): out[0..*count) ascending.
+ * *count is a DEVICE int64. Same workspace protocol. */
+int bbgr_mask_to_list(int64_t n, const uint8_t *mask, int64_t *out, int64_t *count,
+                      void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Evaluation                                            */

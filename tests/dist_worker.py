@@ -23,6 +23,8 @@ WEAK_U, WEAK_I, WEAK_E = 200, 150, 2500
 def main():
     out_dir, variant, mode = sys.argv[1], sys.argv[2], sys.argv[3]
     frontier = len(sys.argv) < 5 or sys.argv[4] != "dense"
+    if mode == "fused":
+        return fused_vs_separate(out_dir, variant)
     dist.init_process_group("gloo")
     rank = dist.get_rank()
     torch.cuda.set_device(0)
@@ -33,7 +35,7 @@ def main():
         tr = ShardedTrainer.from_global_edges(
             g["edges"], U, I, variant, cred=g["cred"], emb_dim=D, num_layers=K, batch_size=64,
             device="cuda:0", u0=g["u0"], i0=g["i0"], lambda_fair=lam, frontier=frontier,
-            exchange_parts=3)
+            exchange_parts=3, fuse_adam=False)
     else:
         e = synthetic_edges(WEAK_U, WEAK_I, WEAK_E, 100 + rank, items="zipf", item_seed=100)
         rng = np.random.default_rng(5)
@@ -42,7 +44,8 @@ def main():
         np.save(os.path.join(out_dir, f"edges{rank}.npy"), e)
         tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3, batch_size=32,
                             device="cuda:0", u0=u0, i0=i0, lambda_fair=lam,
-                            user_offset=rank * WEAK_U, frontier=frontier, exchange_parts=2)
+                            user_offset=rank * WEAK_U, frontier=frontier, exchange_parts=2,
+                            fuse_adam=False)
     loss = float(tr.step())
     users = tr.perm[: tr.B_local]          # the first step takes the head of epoch 1
     torch.cuda.synchronize()
@@ -51,6 +54,35 @@ def main():
              neg=tr.neg.cpu().numpy(), g_u0=tr.g_u0.cpu().numpy(), g_i0=tr.g_i0.cpu().numpy(),
              user_w=tr.user_w.cpu().numpy(), item_w=tr.item_w.cpu().numpy(), loss=loss,
              uf=tr.uf.cpu().numpy(), itf=tr.itf.cpu().numpy())
+    dist.destroy_process_group()
+
+
+def fused_vs_separate(out_dir, variant):
+    """Three steps of four sharded trainers on the same shards and seeds:
+    separate / fused Adam x dense / sparse (frontier-row) exchange."""
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    torch.cuda.set_device(0)
+    e = synthetic_edges(WEAK_U, WEAK_I, WEAK_E, 300 + rank, items="zipf", item_seed=300)
+    rng = np.random.default_rng(9)
+    u0 = rng.uniform(-0.5, 0.5, (2 * WEAK_U, 64)).astype(np.float32)[rank * WEAK_U:(rank + 1) * WEAK_U]
+    i0 = rng.uniform(-0.5, 0.5, (WEAK_I, 64)).astype(np.float32)
+    out = {}
+    for fuse in (False, True):
+        for sparse in (False, True):
+            tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3,
+                                batch_size=32, device="cuda:0", u0=u0, i0=i0,
+                                user_offset=rank * WEAK_U, exchange_parts=2, fuse_adam=fuse,
+                                sparse_exchange=sparse)
+            losses = [float(tr.step()) for _ in range(3)]
+            tag = f"{'fused' if fuse else 'sep'}_{'sparse' if sparse else 'dense'}"
+            out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
+            out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
+            out[f"{tag}_m_i"] = tr.m_i.cpu().numpy()
+            out[f"{tag}_loss"] = np.array(losses)
+            out[f"{tag}_fused"] = np.array(tr.fuse_adam)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"fused{rank}.npz"), **out)
     dist.destroy_process_group()
 
 

@@ -87,3 +87,31 @@ def test_sharded_step_two_ranks_vs_oracle(tmp_path, variant, mode, frontier):
     close(np.concatenate([r["g_u0"] for r in ranks]), gu0, "grad u0")
     close(ranks[0]["g_i0"], gi0, "grad i0")
     assert abs(ranks[0]["loss"] - loss) <= 1e-5 * loss
+
+
+@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair"])
+def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
+    """Fused Adam (user Adam in the last backward SpMM, item Adam on the sparse
+    gradient) == separate gradient + Adam, and the frontier-row (compacted)
+    exchange == the dense item-table exchange, over three sharded steps."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, "fused"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ranks = [dict(np.load(tmp_path / f"fused{k}.npz")) for k in range(2)]
+    for rk in ranks:
+        assert bool(rk["fused_dense_fused"]) == (variant == "v2_pop")
+        for fuse in ("sep", "fused"):
+            # the compact exchange sums the same values in the same order (gloo, 2 ranks)
+            for key in ("user_w", "item_w", "m_i", "loss"):
+                np.testing.assert_array_equal(rk[f"{fuse}_sparse_{key}"],
+                                              rk[f"{fuse}_dense_{key}"])
+        for key in ("user_w", "item_w"):
+            a, b = rk[f"fused_sparse_{key}"], rk[f"sep_sparse_{key}"]
+            err = np.linalg.norm(a - b) / np.linalg.norm(b)
+            assert err < 1e-6, (key, err)
+        np.testing.assert_allclose(rk["fused_sparse_loss"], rk["sep_sparse_loss"], rtol=1e-6)
+    for key in ("sep_sparse_item_w", "fused_sparse_item_w", "fused_sparse_m_i"):
+        np.testing.assert_array_equal(ranks[0][key], ranks[1][key])   # replicas identical

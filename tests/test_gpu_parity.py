@@ -647,3 +647,54 @@ def test_training_step_is_bitwise_reproducible():
         assert float(a.step()) == float(b.step())
     for x, y in ((a.user_w, b.user_w), (a.item_w, b.item_w), (a.m_u, b.m_u), (a.v_i, b.v_i)):
         assert torch.equal(x, y)
+
+
+def test_mask_to_list_rows_gather_and_compact_epilogue():
+    """The sparse-exchange primitives: mask -> ascending row list (exact),
+    row gather (exact copy, zero rows for -1), and the compact epilogue
+    (row j of t -> output row list[j]) == the dense epilogue on those rows."""
+    import ctypes
+    from bbgr._lib import call, ld, ptr, stream_handle
+    from bbgr.propagate import epilogue
+    rng = np.random.default_rng(11)
+    n, d = 5000, 64
+    for frac in (0.0, 0.03, 1.0):
+        m = (rng.random(n) < frac).astype(np.uint8) * rng.integers(1, 4, n).astype(np.uint8)
+        mask = t(m, torch.uint8)
+        out = torch.full((n,), -7, dtype=torch.int64, device=DEV)
+        cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+        need = ctypes.c_size_t(0)
+        call("bbgr_mask_to_list", n, ptr(mask), ptr(out), ptr(cnt), None, ctypes.byref(need),
+             stream_handle())
+        ws = torch.empty(max(need.value, 1), dtype=torch.uint8, device=DEV)
+        call("bbgr_mask_to_list", n, ptr(mask), ptr(out), ptr(cnt), ptr(ws),
+             ctypes.byref(need), stream_handle())
+        want = np.flatnonzero(m)
+        assert int(cnt.item()) == want.size
+        np.testing.assert_array_equal(out[: want.size].cpu().numpy(), want)
+    src = t(rng.standard_normal((n, 68)).astype(np.float32))[:, :d]   # ld 68
+    idx = t(np.concatenate([rng.integers(0, n, 300), [-1, 0, n - 1]]), torch.int64)
+    dst = torch.full((idx.numel(), d), 5.0, device=DEV)
+    call("bbgr_rows_gather", idx.numel(), ptr(idx), ptr(src), ld(src), ptr(dst), ld(dst), d,
+         stream_handle())
+    ref = src.cpu().numpy()[idx.cpu().numpy().clip(0)]
+    ref[idx.cpu().numpy() < 0] = 0.0
+    np.testing.assert_array_equal(dst.cpu().numpy(), ref)
+    # compact epilogue vs dense epilogue restricted to the listed rows
+    rows = t(np.sort(rng.choice(n, 400, replace=False)), torch.int64)
+    T_full = t(rng.standard_normal((n, d)).astype(np.float32))
+    add = t(rng.standard_normal((n, d)).astype(np.float32))
+    acc_in = t(rng.standard_normal((n, d)).astype(np.float32))
+    ys = t(rng.random(n).astype(np.float32))
+    cs = t(rng.random(n).astype(np.float32))
+    kw = dict(y_scale=ys, add=add, add_scale_s=0.25, acc_in=acc_in, acc_scale=cs, gamma=0.5)
+    y1, a1 = torch.zeros(n, d, device=DEV), torch.zeros(n, d, device=DEV)
+    y2, a2 = torch.zeros(n, d, device=DEV), torch.zeros(n, d, device=DEV)
+    epilogue(T_full, y=y1, acc_out=a1, **kw)
+    comp = T_full[rows].contiguous()
+    epilogue(comp, y=y2, acc_out=a2, row_list=rows, n_rows=n, **kw)
+    r = rows.cpu().numpy()
+    np.testing.assert_array_equal(y2.cpu().numpy()[r], y1.cpu().numpy()[r])
+    np.testing.assert_array_equal(a2.cpu().numpy()[r], a1.cpu().numpy()[r])
+    other = np.setdiff1d(np.arange(n), r)
+    assert not y2.cpu().numpy()[other].any() and not a2.cpu().numpy()[other].any()
