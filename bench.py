@@ -261,6 +261,12 @@ def main():
                      "masked_launches_per_step": masked_n / args.steps,
                      "masked_ms_per_step": masked_ms / args.steps,
                      "full_launches_per_step": n_launch / args.steps,
+                     "full_sequence_ms": [
+                         {"rows": r, "nnz": z, "avg_ms": ms}
+                         for r, z, ms in timer.sequence("full", args.steps)],
+                     "adam_sequence_ms": [
+                         {"rows": r, "nnz": z, "avg_ms": ms}
+                         for r, z, ms in timer.sequence("adam", args.steps)],
                      "masked_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
                          for r, z, ms in timer.sequence("masked", args.steps)],

@@ -19,7 +19,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must load torch's HIP runtime before libbbgr.so)
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "lib" / "libbbgr.so"
+LIB_PATH = Path(os.environ.get("BBGR_LIB", PKG_DIR / "lib" / "libbbgr.so"))   # override: A/B builds
 HEADER_PATH = PKG_DIR.parent / "include" / "bbgr.h"
 
 BBGR_OK = 0

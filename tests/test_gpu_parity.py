@@ -698,3 +698,4 @@ def test_mask_to_list_rows_gather_and_compact_epilogue():
     np.testing.assert_array_equal(a2.cpu().numpy()[r], a1.cpu().numpy()[r])
     other = np.setdiff1d(np.arange(n), r)
     assert not y2.cpu().numpy()[other].any() and not a2.cpu().numpy()[other].any()
+
