@@ -1,5 +1,7 @@
 #!/bin/bash
-# A/B of SpMM short-row schedules on the GPU box (bench.py per variant).
+# A/B of SpMM builds on the GPU box: bench.py with the in-tree libbbgr.so
+# (base) and with each extra library given as an argument (BBGR_LIB).
+# Usage: tools/ab_spmm.sh [path/to/variant/libbbgr.so ...]
 set -o pipefail
 mkdir -p gpurun_out/ab
 timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q > gpurun_out/ab/tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/ab/tests.log; exit 1; }
@@ -9,5 +11,6 @@ run() {  # tag, env...
   echo "$tag done"
 }
 run base
-run base
+k=0
+for lib in "$@"; do k=$((k+1)); run v$k BBGR_LIB=$PWD/$lib; done
 echo ALL_OK
