@@ -31,8 +31,8 @@ sys.path.insert(0, ROOT)
 
 import bbgr  # noqa: E402,F401
 from bbgr import propagate as P  # noqa: E402
-from bbgr.synthetic import (CONFIGS, CONFIG_SEED, config_edges, shard_edges_weak,  # noqa: E402
-                            synthetic_credibility)
+from bbgr.synthetic import (CONFIGS, CONFIG_SEED, config_edges, shard_edges_strong,  # noqa: E402
+                            shard_edges_weak, synthetic_credibility)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true",
                     help="disable exact frontier sparsity (every SpMM over the full CSR)")
+    ap.add_argument("--exchange-parts", type=int, default=8,
+                    help="N>1: item-row ranges per dense exchange (all-reduce of range c "
+                         "overlaps the SpMM of range c+1)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = every rank owns a full config-sized user shard over the "
                          "shared items; strong = one config graph cut into N user ranges")
@@ -160,14 +163,27 @@ def main():
     U, I, d, K = cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"]
     B = cfg["batch"]
     weak = world > 1 and args.scaling == "weak"
+    # configs too large to draw whole on every rank (C5) are drawn per user shard
+    sharded_gen = not weak and cfg["num_edges"] > 100_000_000
     t0 = time.perf_counter()
     seed = CONFIG_SEED[args.config]
-    edges = shard_edges_weak(args.config, rank) if weak else config_edges(args.config)
-    cred = synthetic_credibility(U, seed + 7919 * rank if weak else seed, args.cred)
-    E = edges.shape[1] * (world if weak else 1)          # edges of the whole job's graph
+    lo = hi = 0
+    if weak:
+        edges = shard_edges_weak(args.config, rank)
+        cred = synthetic_credibility(U, seed + 7919 * rank, args.cred)
+        E = edges.shape[1] * world                       # edges of the whole job's graph
+    elif sharded_gen:
+        edges, lo, hi = shard_edges_strong(args.config, rank, world)
+        cred = synthetic_credibility(hi - lo, seed + 7919 * rank, args.cred)
+        E = cfg["num_edges"]
+    else:
+        edges = config_edges(args.config)
+        cred = synthetic_credibility(U, seed, args.cred)
+        E = edges.shape[1]
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} E={E} d={d} K={K} B={B} "
         f"scaling={'weak' if weak else 'strong'} generated in {time.perf_counter() - t0:.1f}s")
 
+    xp = dict(exchange_parts=args.exchange_parts)
     if world == 1:
         from bbgr.graph import BipartiteGraph
         from bbgr.trainer import FusedTrainer
@@ -178,12 +194,17 @@ def main():
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
                                  num_layers=K, batch_size=B, device=dev, user_offset=rank * U,
-                                 frontier=not args.dense)
+                                 frontier=not args.dense, **xp)
+    elif sharded_gen:
+        from bbgr.distributed import ShardedTrainer
+        trainer = ShardedTrainer(edges, hi - lo, I, args.variant, cred=cred, emb_dim=d,
+                                 num_layers=K, batch_size=max(1, B // world), device=dev,
+                                 user_offset=lo, frontier=not args.dense, **xp)
     else:
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
                                                    emb_dim=d, num_layers=K, batch_size=B,
-                                                   device=dev, frontier=not args.dense)
+                                                   device=dev, frontier=not args.dense, **xp)
     if world > 1:
         del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
     torch.cuda.synchronize()
@@ -233,7 +254,7 @@ def main():
             torch.distributed.destroy_process_group()
         return
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and world == 1 and not sharded_gen:
         log("[bench] timing the reference CPU path (bounded sample) ...")
         cpu = cpu_baseline(edges, cfg, B)
     out = {

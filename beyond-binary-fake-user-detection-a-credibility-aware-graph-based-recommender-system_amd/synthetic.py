@@ -126,6 +126,28 @@ def shard_edges_weak(name: str, rank: int) -> np.ndarray:
                            item_seed=CONFIG_SEED[name])
 
 
+def user_ranges(num_users: int, world: int) -> np.ndarray:
+    """Contiguous user ranges of (almost) equal size: bounds[world + 1]."""
+    return np.array([num_users * g // world for g in range(world + 1)], dtype=np.int64)
+
+
+def shard_edges_strong(name: str, rank: int, world: int) -> tuple[np.ndarray, int, int]:
+    """Strong scaling of a graph too large to draw on every rank (C5: 500M
+    edges): rank r draws only ITS users' edges — user range r of
+    user_ranges(U, world), edges in proportion, same degree law, same item
+    popularity order — so the union over ranks is one config-sized graph.
+    Returns (local edges int32 [2, E_r] with local user ids, lo, hi)."""
+    c = CONFIGS[name]
+    b = user_ranges(c["num_users"], world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    e_lo = c["num_edges"] * lo // c["num_users"]
+    e_hi = c["num_edges"] * hi // c["num_users"]
+    e = synthetic_edges(hi - lo, c["num_items"], e_hi - e_lo,
+                        CONFIG_SEED[name] + 7919 * rank + 104729 * world,
+                        items=c["items"], item_seed=CONFIG_SEED[name])
+    return e, lo, hi
+
+
 def synthetic_credibility(num_users: int, seed: int, kind: str = "beta") -> np.ndarray:
     if kind == "ones":
         return np.ones(num_users, dtype=np.float32)

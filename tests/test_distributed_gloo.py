@@ -95,3 +95,29 @@ def test_partition_is_contiguous_and_edge_balanced(world):
     assert sum(p.shape[1] for p in parts) == e.shape[1]
     for g, p in enumerate(parts):
         assert p[0].min() >= 0 and p[0].max() < b[g + 1] - b[g]
+
+
+def test_shard_edges_strong_partitions_a_config_graph():
+    """Per-rank drawing of a strong-scaled graph (bench.py, configs too large to
+    draw on every rank): contiguous user ranges, edges in proportion, unique
+    pairs, local ids in range, the same item popularity order on every rank."""
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bbgr  # noqa: F401
+    from bbgr.synthetic import CONFIGS, shard_edges_strong, user_ranges
+    c = CONFIGS["C2"]
+    world = 3
+    b = user_ranges(c["num_users"], world)
+    total, tops = 0, []
+    for r in range(world):
+        e, lo, hi = shard_edges_strong("C2", r, world)
+        assert (lo, hi) == (b[r], b[r + 1])
+        assert e.dtype == np.int32 and e.shape[0] == 2
+        assert e[0].min() >= 0 and e[0].max() < hi - lo
+        assert e[1].min() >= 0 and e[1].max() < c["num_items"]
+        keys = e[0].astype(np.int64) * c["num_items"] + e[1]
+        assert np.unique(keys).size == keys.size
+        total += e.shape[1]
+        tops.append(set(np.argsort(-np.bincount(e[1], minlength=c["num_items"]))[:20]))
+    assert total == c["num_edges"]
+    assert len(tops[0] & tops[1] & tops[2]) >= 10   # one popularity order
