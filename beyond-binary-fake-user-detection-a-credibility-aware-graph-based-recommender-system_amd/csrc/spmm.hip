@@ -18,6 +18,7 @@
 //     them in chunk order. Every reduction order is fixed: the result is
 //     bitwise deterministic (no atomics).
 #include <stdarg.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -59,6 +60,7 @@ struct SpmmParams {
   const long *row_list;
   long n_row_list;
   int row_begin, row_end;      // short rows computed: [row_begin, row_end)
+  int pair_rows;               // two short rows per 16-lane group (gather_pair)
   int chunk_begin;             // first long-row chunk of this launch
   // fused Adam on the y-row value (bbgr_spmm_args.adam_*)
   float *adam_p, *adam_m, *adam_v;
@@ -123,6 +125,91 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
           const float w = __shfl(mw, j0 + j, 16);
 #pragma unroll
           for (int k = 0; k < V; ++k) acc[k] = f4_fma(w, v[j][k], acc[k]);
+        }
+      }
+    }
+  }
+}
+
+// Two short rows per 16-lane group, their batches interleaved: 2*U8 source
+// rows in flight per group across two independent rows (U8 per row), so a
+// low-degree table (users, avg degree ~10) keeps twice the rows in flight
+// for the same registers. Per row the operation sequence is gather_range's
+// (edges in CSR order from zero; dead batches skipped), so results match the
+// one-row path bitwise (up to the sign of an exact zero).
+template <int D, int WMODE, bool MASKED>
+__device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int eeA, int ebB,
+                                            int eeB, int lane, float4 (&accA)[D / 64],
+                                            float4 (&accB)[D / 64]) {
+  constexpr int V = D / 64;
+  constexpr int U = 8 / V;   // per row per iteration
+  const int nA = eeA - ebA, nB = eeB - ebB;
+  const int nmax = max(nA, nB);
+  for (int o = 0; o < nmax; o += 16) {
+    int na = min(16, nA - o), nb = min(16, nB - o);
+    int myA = -1, myB = -1;
+    float mwA = 0.f, mwB = 0.f;
+    if (lane < na) {
+      myA = P.indices[ebA + o + lane];
+      if (MASKED && P.src_mask && !P.src_mask[myA]) myA = -1;
+      if (myA >= 0) {
+        if (WMODE == 1) mwA = P.edge_val[ebA + o + lane];
+        if (WMODE == 2) mwA = P.col_scale[myA] * P.col_scale_s;
+      }
+    }
+    if (lane < nb) {
+      myB = P.indices[ebB + o + lane];
+      if (MASKED && P.src_mask && !P.src_mask[myB]) myB = -1;
+      if (myB >= 0) {
+        if (WMODE == 1) mwB = P.edge_val[ebB + o + lane];
+        if (WMODE == 2) mwB = P.col_scale[myB] * P.col_scale_s;
+      }
+    }
+    if (MASKED && P.src_mask) {   // a batch with no live source adds nothing
+      const unsigned long long la = __ballot(myA >= 0), lb = __ballot(myB >= 0);
+      if (((la >> (threadIdx.x & 48)) & 0xffffull) == 0) na = 0;
+      if (((lb >> (threadIdx.x & 48)) & 0xffffull) == 0) nb = 0;
+    }
+    const int nn = max(na, nb);
+    for (int j0 = 0; j0 < nn; j0 += U) {
+      float4 vA[U][V], vB[U][V];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int cA = __shfl(myA, j0 + j, 16);
+        const int cB = __shfl(myB, j0 + j, 16);
+        if (j0 + j < na && (!MASKED || cA >= 0)) {
+          const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)cA * P.ldx) + lane;
+#pragma unroll
+          for (int k = 0; k < V; ++k) vA[j][k] = src[16 * k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < V; ++k) vA[j][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (j0 + j < nb && (!MASKED || cB >= 0)) {
+          const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)cB * P.ldx) + lane;
+#pragma unroll
+          for (int k = 0; k < V; ++k) vB[j][k] = src[16 * k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < V; ++k) vB[j][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (WMODE == 0) {
+#pragma unroll
+          for (int k = 0; k < V; ++k) {
+            accA[k] = f4_add(accA[k], vA[j][k]);
+            accB[k] = f4_add(accB[k], vB[j][k]);
+          }
+        } else {
+          const float wA = __shfl(mwA, j0 + j, 16);
+          const float wB = __shfl(mwB, j0 + j, 16);
+#pragma unroll
+          for (int k = 0; k < V; ++k) {
+            accA[k] = f4_fma(wA, vA[j][k], accA[k]);
+            accB[k] = f4_fma(wB, vB[j][k], accB[k]);
+          }
         }
       }
     }
@@ -212,7 +299,7 @@ __device__ __forceinline__ void block_reduce16(float4 *red, int g, int lane,
   __syncthreads();
 }
 
-template <int D, int WMODE, bool MASKED>
+template <int D, int WMODE, bool MASKED, bool PAIR>
 __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   constexpr int V = D / 64;
   __shared__ float4 red[16 * (D / 4)];
@@ -248,6 +335,37 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     return;
   }
 
+  if (PAIR) {   // ---- short rows, two per 16-lane group (rows j and j + 16)
+    long rr[2];
+    int eb[2], ee[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * 32 + 16 * h + g;
+      if (MASKED && P.row_list) {
+        row = row < P.n_row_list ? P.row_list[row] : -1;
+      } else if (row >= P.row_end) {
+        row = -1;
+      }
+      if (row >= P.n_rows) row = -1;
+      eb[h] = ee[h] = 0;
+      if (row >= 0) {
+        eb[h] = P.indptr[row];
+        ee[h] = P.indptr[row + 1];
+        if (ee[h] - eb[h] > P.long_threshold ||
+            (MASKED && !P.row_list && P.row_mask && !P.row_mask[row]))
+          row = -1;
+      }
+      if (row < 0) eb[h] = ee[h] = 0;
+      rr[h] = row;
+    }
+    float4 accB[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) accB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gather_pair<D, WMODE, MASKED>(P, eb[0], ee[0], eb[1], ee[1], lane, acc, accB);
+    if (rr[0] >= 0) epilogue<D>(P, (int)rr[0], lane, acc);
+    if (rr[1] >= 0) epilogue<D>(P, (int)rr[1], lane, accB);
+    return;
+  }
   // ---- short rows: one 16-lane group per row ------------------------------
   long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * 16 + g;
   if (MASKED && P.row_list) {
@@ -267,22 +385,23 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
 }
 
 // Full-CSR launches (the roofline kernel) and masked / row-list launches are
-// distinct symbols so that profiles separate them.
-template <int D, int WMODE>
+// distinct symbols so that profiles separate them. PAIR: two short rows per
+// group (low-degree tables), a separate instantiation.
+template <int D, int WMODE, bool PAIR>
 __global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
-  spmm_body<D, WMODE, false>(P);
+  spmm_body<D, WMODE, false, PAIR>(P);
 }
 
-template <int D, int WMODE>
+template <int D, int WMODE, bool PAIR>
 __global__ __launch_bounds__(256) void spmm_masked_kernel(SpmmParams P) {
-  spmm_body<D, WMODE, true>(P);
+  spmm_body<D, WMODE, true, PAIR>(P);
 }
 
 // Full-CSR launch whose epilogue applies the fused Adam step (its bytes add the
 // parameter / moment streams): a third symbol so rooflines stay per kind.
-template <int D, int WMODE>
+template <int D, int WMODE, bool PAIR>
 __global__ __launch_bounds__(256) void spmm_adam_kernel(SpmmParams P) {
-  spmm_body<D, WMODE, false>(P);
+  spmm_body<D, WMODE, false, PAIR>(P);
 }
 
 // Rows split into >1 chunk: sum chunk partials in chunk order, then epilogue.
@@ -337,18 +456,21 @@ template <int D, int WMODE>
 static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
   const bool masked = P.src_mask || P.row_mask || P.row_list;
   const long short_rows = P.row_list ? P.n_row_list : (long)(P.row_end - P.row_begin);
-  const long short_blocks = (short_rows + 15) / 16;
+  const bool pair = P.pair_rows;
+  const long per_block = pair ? 32 : 16;
+  const long short_blocks = (short_rows + per_block - 1) / per_block;
   const long grid = (long)P.n_chunks + short_blocks;
   if (grid > 0) {
+    const dim3 gd((unsigned)grid), bd(256);
     if (masked) {
-      hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
-                         0, st, P);
+      if (pair) hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE, true>), gd, bd, 0, st, P);
+      else hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE, false>), gd, bd, 0, st, P);
     } else if (P.adam_p) {
-      hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
-                         0, st, P);
+      if (pair) hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE, true>), gd, bd, 0, st, P);
+      else hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE, false>), gd, bd, 0, st, P);
     } else {
-      hipLaunchKernelGGL((spmm_kernel<D, WMODE>), dim3((unsigned)grid), dim3(256),
-                         0, st, P);
+      if (pair) hipLaunchKernelGGL((spmm_kernel<D, WMODE, true>), gd, bd, 0, st, P);
+      else hipLaunchKernelGGL((spmm_kernel<D, WMODE, false>), gd, bd, 0, st, P);
     }
     BBGR_LAUNCHED("spmm_kernel");
   }
@@ -370,6 +492,15 @@ static int dispatch_wmode(const SpmmParams &P, int wmode, int n_split,
   }
   set_error("bbgr_spmm: weight_mode %d not in {0,1,2}", wmode);
   return BBGR_ERR_INVALID;
+}
+
+// Two short rows per group for low-degree tables (average degree <= 24:
+// the user side of the bipartite graph); BBGR_SPMM_PAIR=0/1 forces it off/on
+// (A/B experiments).
+static int pair_rows(const bbgr_csr *csr) {
+  const char *env = getenv("BBGR_SPMM_PAIR");
+  if (env && *env) return atoi(env) != 0;
+  return csr->n_rows > 0 && csr->nnz <= 24L * csr->n_rows;
 }
 
 static bool ld_ok(const float *p, long ld, int d) {
@@ -514,6 +645,7 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
     n_split = r[5] - r[4];
   }
   BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_spmm: negative n_row_list");
+  P.pair_rows = pair_rows(csr);
   hipStream_t st = as_stream(stream);
   switch (d) {
     case 64: return dispatch_wmode<64>(P, a->weight_mode, n_split, st);

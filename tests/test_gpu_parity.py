@@ -699,3 +699,56 @@ def test_mask_to_list_rows_gather_and_compact_epilogue():
     other = np.setdiff1d(np.arange(n), r)
     assert not y2.cpu().numpy()[other].any() and not a2.cpu().numpy()[other].any()
 
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_spmm_pair_rows_match_single_row_path(d, mode, monkeypatch):
+    """Two short rows per 16-lane group (low-degree tables) == one row per group,
+    bitwise: empty rows, rows spanning several 16-edge batches, chunked long
+    rows, src masks, row masks, row lists, row ranges, fused Adam."""
+    from bbgr.optim import AdamRows
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(200 + d + mode)
+    Rn, Cn = 3001, 700
+    deg = rng.geometric(0.12, Rn) - 1
+    deg[rng.choice(Rn, 6, replace=False)] = [40, 300, 700, 17, 16, 33]
+    rows = np.repeat(np.arange(Rn), deg).astype(np.int32)
+    cols = rng.integers(0, Cn, rows.size).astype(np.int32)
+    vals = rng.uniform(0.1, 1.0, rows.size).astype(np.float32)
+    cs = rng.uniform(0.5, 2.0, Cn).astype(np.float32)
+    c = Csr(rows, cols, Rn, Cn, DEV, edge_values=t(vals) if mode == 1 else None,
+            long_threshold=64, chunk_edges=128)
+    prod = Product(c, c.values if mode == 1 else None, t(cs) if mode == 2 else None, None, {})
+    x = t(rng.uniform(-1, 1, (Cn, d)).astype(np.float32))
+    add = t(rng.normal(size=(Rn, d)).astype(np.float32))
+    src_mask = t((rng.random(Cn) < 0.3).astype(np.uint8), torch.uint8)
+    row_mask = t((rng.random(Rn) < 0.4).astype(np.uint8), torch.uint8)
+    row_list = torch.nonzero(row_mask).flatten()
+    p0 = t(rng.normal(size=(Rn, d)).astype(np.float32))
+
+    def run(pair, **kw):
+        monkeypatch.setenv("BBGR_SPMM_PAIR", str(pair))
+        y = torch.full((Rn, d), 7.0, device=DEV)
+        acc = torch.full((Rn, d), 7.0, device=DEV)
+        spmm(prod, x, True, y=y, y_scale_s=0.5, add=add, add_scale_s=2.0, acc_out=acc,
+             gamma=0.25, **kw)
+        torch.cuda.synchronize()
+        return y.cpu().numpy(), acc.cpu().numpy()
+
+    cases = [{}, {"src_mask": src_mask}, {"row_mask": row_mask},
+             {"row_mask": row_mask, "row_list": row_list}]
+    cases += [{"rng": rg} for rg in c.row_ranges(3)]
+    for kw in cases:
+        a, b = run(0, **kw), run(1, **kw)
+        np.testing.assert_array_equal(b[0], a[0], err_msg=f"y {list(kw)}")
+        np.testing.assert_array_equal(b[1], a[1], err_msg=f"acc {list(kw)}")
+    outs = []
+    for pair in (0, 1):   # fused Adam epilogue
+        monkeypatch.setenv("BBGR_SPMM_PAIR", str(pair))
+        p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+        spmm(prod, x, True, add=add, add_scale_s=2.0, adam=AdamRows(p, m, v, 1, 1e-3))
+        torch.cuda.synchronize()
+        outs.append((p.cpu().numpy(), m.cpu().numpy(), v.cpu().numpy()))
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(b, a)
