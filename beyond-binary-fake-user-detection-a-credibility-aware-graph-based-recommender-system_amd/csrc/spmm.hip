@@ -636,9 +636,12 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
                      r[2] <= r[3] && r[3] <= csr->n_chunks && r[4] >= 0 && r[4] <= r[5] &&
                      r[5] <= csr->n_split,
                  "bbgr_spmm: range out of bounds");
-    BBGR_REQUIRE(!a->row_list, "bbgr_spmm: range and row_list are exclusive");
-    P.row_begin = r[0];
-    P.row_end = r[1];
+    BBGR_REQUIRE(!a->row_list || a->row_mask,
+                 "bbgr_spmm: range with row_list needs row_mask (chunk rows)");
+    if (!a->row_list) {   // with a row list the short rows are the list's entries
+      P.row_begin = r[0];
+      P.row_end = r[1];
+    }
     P.chunk_begin = r[2];
     P.n_chunks = r[3] - r[2];
     P.split = reinterpret_cast<const int4 *>(csr->split) + r[4];

@@ -100,42 +100,59 @@ class ItemExchange:
     Frontier products (a `row_mask`: the last forward item layer and the first
     backward item product of a training step) need only the step's item
     frontier, a GLOBAL row set identical on every rank (`set_rows`). Only
-    those rows are computed (row-list SpMM), compacted (bbgr_rows_gather),
-    all-reduced and finished by the compact epilogue: the payload is
-    |frontier|*d*4 bytes instead of I*d*4."""
+    those rows are computed (row-list SpMM), compacted (bbgr_rows_gather) and
+    all-reduced — pipelined over the same row ranges — and the compact
+    epilogue finishes them: the payload is |frontier|*d*4 bytes instead of
+    I*d*4."""
 
     def __init__(self, group=None, parts: int = 4):
         self.group, self.parts = group, max(1, int(parts))
         self.balance_indptr = None   # global item indptr: identical cuts on every rank
-        self._rows = None            # (device list, device count, host count, event)
-        self._list = None
+        self._rows = None            # (device list, host offsets, event) of the step
+        self._offs = None
         self._compact = None
+        self._ranges = None          # (csr, ranges, device boundary rows)
 
     def __call__(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
-    def set_rows(self, row_list: torch.Tensor, count_dev: torch.Tensor,
-                 count_host: torch.Tensor) -> None:
-        """The step's frontier rows: row_list[:count] (ascending, device).
-        The count's device->host copy is enqueued now; it is read (one event
-        wait, long complete by then) at the first frontier product."""
-        count_host.copy_(count_dev, non_blocking=True)
+    def ranges(self, csr):
+        """The item CSR's row ranges (global-degree cuts) and their boundary rows."""
+        if self._ranges is None or self._ranges[0] is not csr:
+            rg = csr.row_ranges(self.parts, self.balance_indptr)
+            b = [r[0] for r in rg] + [rg[-1][1]] if rg else [0, 0]
+            self._ranges = (csr, rg, torch.tensor(b, dtype=torch.int64, device=csr.device))
+        return self._ranges[1], self._ranges[2]
+
+    def set_rows(self, csr, mask: torch.Tensor, row_list: torch.Tensor,
+                 offs_host: torch.Tensor) -> None:
+        """The step's frontier: rows flagged in `mask` (global), listed ascending
+        in `row_list` (bbgr_mask_to_list). The number of listed rows below each
+        range boundary is computed here and copied to the host without
+        blocking; it is read (one event wait, long complete by then) at the
+        first frontier product."""
+        _, bounds = self.ranges(csr)
+        cum = torch.cumsum(mask.ne(0), 0)
+        offs = torch.where(bounds > 0, cum[(bounds - 1).clamp(min=0)], torch.zeros_like(bounds))
+        host = offs_host[: bounds.numel()]
+        host.copy_(offs, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._rows = (row_list, count_host, ev)
-        self._list = None
+        self._rows = (row_list, host, ev)
+        self._offs = None
 
     def clear_rows(self) -> None:
-        self._rows, self._list = None, None
+        self._rows, self._offs = None, None
 
-    def rows(self) -> torch.Tensor | None:
+    def rows(self):
+        """(row list, [offsets into it at each range boundary]) or None."""
         if self._rows is None:
             return None
-        if self._list is None:
+        if self._offs is None:
             lst, host, ev = self._rows
             ev.synchronize()
-            self._list = lst[: int(host[0])]
-        return self._list
+            self._offs = [int(v) for v in host.tolist()]
+        return self._rows[0], self._offs
 
     def _compact_buf(self, n: int, d: int, device) -> torch.Tensor:
         c = self._compact
@@ -147,18 +164,28 @@ class ItemExchange:
         src_mask = kw.pop("src_mask", None)
         row_mask = kw.pop("row_mask", None)
         t = new("partial", prod.csr.n_rows)
-        lst = self.rows() if row_mask is not None else None
-        if lst is not None:
-            d = x.shape[1]
-            n = lst.numel()
-            spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, row_list=lst)
-            c = self._compact_buf(n, d, x.device)
-            call("bbgr_rows_gather", n, ptr(lst), ptr(t), ld(t), ptr(c), ld(c), d,
-                 stream_handle())
-            dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
-            epilogue(c, row_list=lst, n_rows=prod.csr.n_rows, **kw)
-            return
+        fr = self.rows() if row_mask is not None else None
         works = []
+        if fr is not None:
+            lst, offs = fr
+            rgs, _ = self.ranges(prod.csr)
+            d, n = x.shape[1], offs[-1]
+            c = self._compact_buf(n, d, x.device)
+            for k, rg in enumerate(rgs):
+                a, b = offs[k], offs[k + 1]
+                if b <= a:
+                    continue
+                part = lst[a:b]
+                spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask,
+                     row_list=part, rng=rg)
+                call("bbgr_rows_gather", b - a, ptr(part), ptr(t), ld(t), ptr(c[a:b]),
+                     ld(c), d, stream_handle())
+                works.append(dist.all_reduce(c[a:b], op=dist.ReduceOp.SUM,
+                                             group=self.group, async_op=True))
+            for w in works:
+                w.wait()
+            epilogue(c, row_list=lst[:n], n_rows=prod.csr.n_rows, **kw)
+            return
         for rg in prod.csr.row_ranges(self.parts, self.balance_indptr):
             spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, rng=rg)
             works.append(dist.all_reduce(t[rg[0]:rg[1]], op=dist.ReduceOp.SUM,
@@ -270,7 +297,7 @@ class ShardedTrainer(FusedTrainer):
         self.sparse_exchange = bool(sparse_exchange) and frontier
         self.item_list = torch.empty(max(num_items, 1), dtype=torch.int64, device=dev)
         self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.item_count_host = torch.zeros(1, dtype=torch.int64).pin_memory()
+        self.item_offs_host = torch.zeros(exchange_parts + 2, dtype=torch.int64).pin_memory()
         self._list_ws = None
 
     @classmethod
@@ -341,7 +368,8 @@ class ShardedTrainer(FusedTrainer):
         have = ctypes.c_size_t(self._list_ws.numel())
         call("bbgr_mask_to_list", I, ptr(self.mask_i), ptr(self.item_list),
              ptr(self.item_count), ptr(self._list_ws), ctypes.byref(have), st)
-        self.exchange.set_rows(self.item_list, self.item_count, self.item_count_host)
+        self.exchange.set_rows(self.graph.item_csr, self.mask_i, self.item_list,
+                               self.item_offs_host)
 
     def step(self) -> torch.Tensor:
         users = self.next_users()

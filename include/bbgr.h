@@ -173,7 +173,10 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   chunks are [range[2], range[3]) and split rows [range[4], range[5]) of   */
 /*   the plan (all three are row-ordered, so a row range maps to contiguous   */
 /*   chunk / split ranges). Lets the sharded step all-reduce item partial     */
-/*   sums chunk by chunk, overlapped with the next chunk's SpMM.              */
+/*   sums chunk by chunk, overlapped with the next chunk's SpMM. Combined     */
+/*   with row_list (+ row_mask): the short rows are the list's entries (the   */
+/*   caller passes the slice of its sorted list inside [range[0], range[1])) */
+/*   and the range selects the chunk / split-row sub-ranges only.             */
 /* adam_param (nullable): fused optimizer step. The row value the y output    */
 /*   would receive (g = ys*T + as*add) is the gradient of that row of         */
 /*   adam_param, and bbgr_adam's update (same math, same rounding) is applied */
