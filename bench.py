@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true",
                     help="disable exact frontier sparsity (every SpMM over the full CSR)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU trainer (torch.distributed) even at N=1: "
+                         "measures the sharded step's own overhead, collectives included")
     ap.add_argument("--exchange-parts", type=int, default=8,
                     help="N>1: item-row ranges per dense exchange (all-reduce of range c "
                          "overlaps the SpMM of range c+1)")
@@ -151,9 +154,14 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)   # ranks may share a GPU (gloo rehearsal)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    dist_mode = world > 1 or args.sharded
+    if dist_mode:
         # RCCL ("nccl") in production; BBGR_DIST_BACKEND=gloo lets two ranks
         # share one GPU to rehearse the multi-rank path on a 1-GPU box.
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29577")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         backend = os.environ.get("BBGR_DIST_BACKEND", "nccl")
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=dev)
@@ -184,7 +192,7 @@ def main():
         f"scaling={'weak' if weak else 'strong'} generated in {time.perf_counter() - t0:.1f}s")
 
     xp = dict(exchange_parts=args.exchange_parts)
-    if world == 1:
+    if not dist_mode:
         from bbgr.graph import BipartiteGraph
         from bbgr.trainer import FusedTrainer
         graph = BipartiteGraph(edges, U, I, dev)
@@ -205,7 +213,7 @@ def main():
         trainer = ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
                                                    emb_dim=d, num_layers=K, batch_size=B,
                                                    device=dev, frontier=not args.dense, **xp)
-    if world > 1:
+    if dist_mode:
         del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: setup done, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
@@ -213,7 +221,7 @@ def main():
     for _ in range(args.warmup):
         trainer.step()
     timer = P.SpmmTimer()
-    if world > 1:
+    if dist_mode:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     P.set_spmm_timer(timer)
@@ -221,11 +229,11 @@ def main():
     for _ in range(args.steps):
         loss = trainer.step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_mode:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     P.set_spmm_timer(None)
-    if world > 1:
+    if dist_mode:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -250,11 +258,11 @@ def main():
     traffic, traffic_src = pmc_traffic() if (args.config == "C4" and world == 1) else (None, None)
     edges_per_step = 4 * K * E
     if rank != 0:
-        if world > 1:
+        if dist_mode:
             torch.distributed.destroy_process_group()
         return
     cpu = None
-    if not args.no_cpu_baseline and world == 1 and not sharded_gen:
+    if not args.no_cpu_baseline and not dist_mode and not sharded_gen:
         log("[bench] timing the reference CPU path (bounded sample) ...")
         cpu = cpu_baseline(edges, cfg, B)
     out = {
@@ -275,7 +283,8 @@ def main():
                    "num_users": U * (world if weak else 1), "num_items": I, "num_edges": E,
                    "emb_dim": d, "num_layers": K,
                    "global_batch": B * (world if weak else 1),
-                   "parallelism": f"user-rows x{world}"},
+                   "parallelism": f"user-rows x{world}"
+                                  + (" (sharded trainer)" if dist_mode and world == 1 else "")},
         "bpr_steps_per_s": args.steps / elapsed,
         "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
         "frontier": {"enabled": not args.dense,
@@ -305,7 +314,7 @@ def main():
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},
     }
     print(json.dumps(out), file=out_stream, flush=True)
-    if world > 1:
+    if dist_mode:
         torch.distributed.destroy_process_group()
 
 

@@ -122,6 +122,13 @@ class Csr:
             s.chunks, s.split = ptr(self.chunks), ptr(self.split)
         return s
 
+    def range_nnz(self, r0: int, r1: int) -> int:
+        """Edges of rows [r0, r1) (host copy of indptr, made once; timing only)."""
+        h = self.__dict__.get("_indptr_host")
+        if h is None:
+            h = self.__dict__["_indptr_host"] = self.indptr.cpu().numpy().astype(np.int64)
+        return int(h[r1] - h[r0])
+
     def row_ranges(self, parts: int, balance_indptr: torch.Tensor | None = None) -> list:
         """Split rows into `parts` contiguous ranges of ~equal edge counts, each as
         (row0, row1, chunk0, chunk1, split0, split1) for bbgr_spmm's range mode.

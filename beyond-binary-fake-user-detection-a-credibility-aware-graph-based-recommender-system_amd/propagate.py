@@ -204,7 +204,10 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     ev1.record()
     masked = src_mask is not None or row_mask is not None or row_list is not None
     kind = "masked" if masked else ("adam" if adam is not None else "full")
-    _timer.records.append((prod.csr.n_rows, prod.csr.nnz, d, kind, ev0, ev1))
+    rows, nnz = prod.csr.n_rows, prod.csr.nnz
+    if rng is not None and row_list is None:   # a row range: its own rows and edges
+        rows, nnz = rng[1] - rng[0], prod.csr.range_nnz(rng[0], rng[1])
+    _timer.records.append((rows, nnz, d, kind, ev0, ev1))
 
 
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,

@@ -25,6 +25,8 @@ def main():
     frontier = len(sys.argv) < 5 or sys.argv[4] != "dense"
     if mode == "fused":
         return fused_vs_separate(out_dir, variant)
+    if mode == "rccl1":
+        return rccl_single_rank(out_dir, variant)
     dist.init_process_group("gloo")
     rank = dist.get_rank()
     torch.cuda.set_device(0)
@@ -83,6 +85,33 @@ def fused_vs_separate(out_dir, variant):
             out[f"{tag}_fused"] = np.array(tr.fuse_adam)
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"fused{rank}.npz"), **out)
+    dist.destroy_process_group()
+
+
+def rccl_single_rank(out_dir, variant):
+    """World size 1 over RCCL ("nccl"): the sharded trainer's collectives run
+    through RCCL itself (uint8 / fp32 all-reduce, async ranges, all-gather of
+    int64 and fp32) and its steps must equal the single-GPU FusedTrainer's."""
+    from bbgr.graph import BipartiteGraph
+    from bbgr.trainer import FusedTrainer
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    U, I, E = 3000, 1200, 40000
+    e = synthetic_edges(U, I, E, 77, items="zipf")
+    rng = np.random.default_rng(3)
+    u0 = rng.uniform(-0.5, 0.5, (U, 64)).astype(np.float32)
+    i0 = rng.uniform(-0.5, 0.5, (I, 64)).astype(np.float32)
+    kw = dict(emb_dim=64, num_layers=3, batch_size=256, u0=u0, i0=i0)
+    sh = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3, **kw)
+    one = FusedTrainer(BipartiteGraph(e, U, I, "cuda:0"), variant, **kw)
+    out = {}
+    for tag, tr in (("sharded", sh), ("single", one)):
+        out[f"{tag}_loss"] = np.array([float(tr.step()) for _ in range(3)])
+        out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
+        out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
+        out[f"{tag}_m_u"] = tr.m_u.cpu().numpy()
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, "rccl1.npz"), **out)
     dist.destroy_process_group()
 
 

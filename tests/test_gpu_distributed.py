@@ -115,3 +115,21 @@ def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
         np.testing.assert_allclose(rk["fused_sparse_loss"], rk["sep_sparse_loss"], rtol=1e-6)
     for key in ("sep_sparse_item_w", "fused_sparse_item_w", "fused_sparse_m_i"):
         np.testing.assert_array_equal(ranks[0][key], ranks[1][key])   # replicas identical
+
+
+@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair"])
+def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant):
+    """The sharded step with its collectives on RCCL (world size 1: the one
+    RCCL configuration a 1-GPU box can run) equals the single-GPU step."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, "rccl1"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    z = dict(np.load(tmp_path / "rccl1.npz"))
+    np.testing.assert_allclose(z["sharded_loss"], z["single_loss"], rtol=1e-6)
+    for key in ("user_w", "item_w", "m_u"):
+        a, b = z[f"sharded_{key}"], z[f"single_{key}"]
+        err = np.linalg.norm(a - b) / np.linalg.norm(b)
+        assert err < 1e-6, (key, err)
