@@ -157,11 +157,14 @@ __global__ void pop_weight_kernel(int n, const int *indptr_i, double gamma,
   w[i] = pow(deg + 1.0, gamma);
 }
 
-__global__ void cdf_normalise_kernel(int n, double *cdf) {
+// Out of place: every thread divides by the scan's last element, so the scan
+// output must stay unmodified while any block still reads it (normalising in
+// place let the block holding element n-1 overwrite it with 1.0 before other
+// blocks had read it).
+__global__ void cdf_normalise_kernel(int n, const double *scan, double *cdf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double last = cdf[n - 1];
-  cdf[i] = cdf[i] / last;
+  cdf[i] = scan[i] / scan[n - 1];
 }
 
 // ---------------------------------------------------------------------------
@@ -483,7 +486,8 @@ extern "C" int bbgr_pop_cdf(int32_t n_items, const int32_t *indptr_i,
   size_t temp = 0;
   BBGR_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, temp, (double *)nullptr,
                                             (double *)nullptr, n_items, st));
-  const size_t need = align_up(8 * (size_t)n_items) + align_up(temp);
+  const size_t a = align_up(8 * (size_t)n_items);
+  const size_t need = 2 * a + align_up(temp);
   if (!workspace) {
     *workspace_bytes = need;
     return BBGR_OK;
@@ -495,13 +499,13 @@ extern "C" int bbgr_pop_cdf(int32_t n_items, const int32_t *indptr_i,
   BBGR_REQUIRE(indptr_i && cdf, "bbgr_pop_cdf: null arrays");
   char *ws = (char *)workspace;
   double *w = (double *)ws;
+  double *scan = (double *)(ws + a);
   hipLaunchKernelGGL(pop_weight_kernel, dim3(blocks_for(n_items)), dim3(256), 0, st,
                      n_items, indptr_i, gamma, w);
   BBGR_LAUNCHED("pop_weight_kernel");
-  BBGR_HIP(hipcub::DeviceScan::InclusiveSum(ws + align_up(8 * (size_t)n_items), temp,
-                                            w, cdf, n_items, st));
+  BBGR_HIP(hipcub::DeviceScan::InclusiveSum(ws + 2 * a, temp, w, scan, n_items, st));
   hipLaunchKernelGGL(cdf_normalise_kernel, dim3(blocks_for(n_items)), dim3(256), 0,
-                     st, n_items, cdf);
+                     st, n_items, (const double *)scan, cdf);
   BBGR_LAUNCHED("cdf_normalise_kernel");
   return BBGR_OK;
 }

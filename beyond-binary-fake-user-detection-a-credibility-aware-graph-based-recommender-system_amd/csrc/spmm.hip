@@ -79,12 +79,26 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
   return make_float4(a * x.x, a * x.y, a * x.z, a * x.w);
 }
 
+// One-row-per-group tuning (A/B builds): source rows in flight per group, and
+// the occupancy target of the one-row kernels (0 = the compiler's choice).
+#define BBGR_WAVES_ATTR(n) __attribute__((amdgpu_waves_per_eu(n ? n : 1, n ? n : 10)))
+// the same, for d = 64 only (wider rows keep the compiler's choice)
+#define BBGR_WAVES_ATTR64(n) \
+  __attribute__((amdgpu_waves_per_eu(D == 64 && n ? n : 1, D == 64 && n ? n : 10)))
+#ifndef BBGR_ROW_U
+#define BBGR_ROW_U 8
+#endif
+#ifndef BBGR_ROW_WAVES
+#define BBGR_ROW_WAVES 0
+#endif
+
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
 template <int D, int WMODE, bool MASKED>
 __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
                                              int lane, float4 (&acc)[D / 64]) {
   constexpr int V = D / 64;
-  constexpr int U = 16 / V;  // source rows in flight per group per batch
+  constexpr int UR = (D == 64 ? BBGR_ROW_U : 16) / V;   // tuned at d = 64 only
+  constexpr int U = UR > 0 ? UR : 1;  // source rows in flight per group per batch
   for (int e0 = eb; e0 < ee; e0 += 16) {
     const int n = min(16, ee - e0);
     int my = -1;
@@ -131,6 +145,22 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
   }
 }
 
+// Tuning of the two-rows-per-group kernels (tools/ab_spmm.sh A/B builds):
+// source rows in flight per row and iteration, and the occupancy the
+// compiler is held to (0 = its own choice).
+#ifndef BBGR_PAIR_U
+#define BBGR_PAIR_U 4
+#endif
+#ifndef BBGR_PAIR_U_MASKED
+#define BBGR_PAIR_U_MASKED 4
+#endif
+#ifndef BBGR_PAIR_WAVES
+#define BBGR_PAIR_WAVES 8
+#endif
+#ifndef BBGR_PAIR_WAVES_MASKED
+#define BBGR_PAIR_WAVES_MASKED 8
+#endif
+
 // Two short rows per 16-lane group, their batches interleaved: 2*U8 source
 // rows in flight per group across two independent rows (U8 per row), so a
 // low-degree table (users, avg degree ~10) keeps twice the rows in flight
@@ -142,7 +172,8 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
                                             int eeB, int lane, float4 (&accA)[D / 64],
                                             float4 (&accB)[D / 64]) {
   constexpr int V = D / 64;
-  constexpr int U = 8 / V;   // per row per iteration
+  constexpr int UR = D == 64 ? (MASKED ? BBGR_PAIR_U_MASKED : BBGR_PAIR_U) / V : 8 / V;
+  constexpr int U = UR > 0 ? UR : 1;   // source rows per row and iteration
   const int nA = eeA - ebA, nB = eeB - ebB;
   const int nmax = max(nA, nB);
   for (int o = 0; o < nmax; o += 16) {
@@ -385,23 +416,42 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
 }
 
 // Full-CSR launches (the roofline kernel) and masked / row-list launches are
-// distinct symbols so that profiles separate them. PAIR: two short rows per
-// group (low-degree tables), a separate instantiation.
-template <int D, int WMODE, bool PAIR>
-__global__ __launch_bounds__(256) void spmm_kernel(SpmmParams P) {
-  spmm_body<D, WMODE, false, PAIR>(P);
+// distinct symbols so that profiles separate them. The two-rows-per-group
+// (low-degree table) forms are their own symbols too, with their own
+// occupancy target.
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES_ATTR(BBGR_ROW_WAVES) void spmm_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, false, false>(P);
 }
 
-template <int D, int WMODE, bool PAIR>
-__global__ __launch_bounds__(256) void spmm_masked_kernel(SpmmParams P) {
-  spmm_body<D, WMODE, true, PAIR>(P);
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES_ATTR64(BBGR_PAIR_WAVES) void spmm_pair_kernel(
+    SpmmParams P) {
+  spmm_body<D, WMODE, false, true>(P);
+}
+
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES_ATTR(BBGR_ROW_WAVES) void spmm_masked_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, true, false>(P);
+}
+
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES_ATTR64(BBGR_PAIR_WAVES_MASKED) void
+spmm_masked_pair_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, true, true>(P);
 }
 
 // Full-CSR launch whose epilogue applies the fused Adam step (its bytes add the
 // parameter / moment streams): a third symbol so rooflines stay per kind.
-template <int D, int WMODE, bool PAIR>
-__global__ __launch_bounds__(256) void spmm_adam_kernel(SpmmParams P) {
-  spmm_body<D, WMODE, false, PAIR>(P);
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES_ATTR(BBGR_ROW_WAVES) void spmm_adam_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, false, false>(P);
+}
+
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES_ATTR64(BBGR_PAIR_WAVES) void spmm_adam_pair_kernel(
+    SpmmParams P) {
+  spmm_body<D, WMODE, false, true>(P);
 }
 
 // Rows split into >1 chunk: sum chunk partials in chunk order, then epilogue.
@@ -463,14 +513,14 @@ static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
   if (grid > 0) {
     const dim3 gd((unsigned)grid), bd(256);
     if (masked) {
-      if (pair) hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE, true>), gd, bd, 0, st, P);
-      else hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE, false>), gd, bd, 0, st, P);
+      if (pair) hipLaunchKernelGGL((spmm_masked_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+      else hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE>), gd, bd, 0, st, P);
     } else if (P.adam_p) {
-      if (pair) hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE, true>), gd, bd, 0, st, P);
-      else hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE, false>), gd, bd, 0, st, P);
+      if (pair) hipLaunchKernelGGL((spmm_adam_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+      else hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE>), gd, bd, 0, st, P);
     } else {
-      if (pair) hipLaunchKernelGGL((spmm_kernel<D, WMODE, true>), gd, bd, 0, st, P);
-      else hipLaunchKernelGGL((spmm_kernel<D, WMODE, false>), gd, bd, 0, st, P);
+      if (pair) hipLaunchKernelGGL((spmm_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+      else hipLaunchKernelGGL((spmm_kernel<D, WMODE>), gd, bd, 0, st, P);
     }
     BBGR_LAUNCHED("spmm_kernel");
   }

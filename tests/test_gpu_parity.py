@@ -339,6 +339,23 @@ def test_sampler_popularity_distribution_chi2():
     assert chi2 < 2.0 * I, chi2          # dof = 49; generous bound
 
 
+def test_pop_cdf_matches_oracle_on_many_blocks():
+    """The pop-mix CDF (bbgr_pop_cdf) over ~1200 workgroups equals the
+    reference's normalised cumsum of pop_prob (Version-2:805-810), every
+    build (a race in an in-place normalisation once left blocks unscaled)."""
+    from bbgr.sampler import PopMixSampler
+    U, I = 20000, 300_000
+    e = synthetic_edges(U, I, 400_000, 21, items="zipf")
+    g = BipartiteGraph(e, U, I, DEV)
+    pp = R.pop_prob(e, I)
+    want = np.cumsum(pp) / np.cumsum(pp)[-1]
+    for _ in range(5):
+        s = PopMixSampler(g.user_csr, g.item_csr, I, mix_pop=0.7, gamma=0.75, seed=1)
+        got = s.cdf.cpu().numpy()
+        assert got[-1] == 1.0 and np.all(np.diff(got) >= 0)
+        np.testing.assert_allclose(got, want, rtol=1e-9, atol=0)
+
+
 def test_sampler_full_row_user_flags_failure():
     from bbgr.sampler import PopMixSampler
     e = np.array([[0, 0, 0, 1], [0, 1, 2, 0]], np.int32)   # user 0 holds every item
