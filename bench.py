@@ -309,7 +309,7 @@ def main():
                      "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3)",
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": tot_bytes / max(n_launch, 1),
-                     "kernel": "bbgr::spmm_kernel (+fixup)", "launches": n_launch,
+                     "kernel": "bbgr::spmm_kernel / spmm_pair_kernel (+fixup)", "launches": n_launch,
                      "avg_launch_ms": tot_ms / max(n_launch, 1), "per_operator": per_kernel},
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},
     }

@@ -68,14 +68,17 @@ def main(tag: str):
                                      for k, v in stats.items()},
                "kernels": kernels}
     json.dump(summary, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
+    # the full-CSR launches (bench.py's roofline kernel): one-row-per-group
+    # (item rows) and two-rows-per-group (user rows) symbols
+    full = ("spmm_kernel", "spmm_pair_kernel")
     spmm = [e for e in kernels.values()
-            if e["kernel"] == "spmm_kernel" and "hbm_bytes_corrected" in e]
+            if e["kernel"] in full and "hbm_bytes_corrected" in e]
     if spmm:
         n = sum(e["dispatches"] for e in spmm)
         avg = sum(e["hbm_bytes_corrected"] * e["dispatches"] for e in spmm) / n
-        json.dump({"tag": tag, "kernel": "spmm_kernel",
+        json.dump({"tag": tag, "kernel": "spmm_kernel + spmm_pair_kernel",
                    "hbm_bytes_per_launch_corrected": avg,
-                   "per_grid": {e["grid"]: e["hbm_bytes_corrected"] for e in spmm},
+                   "per_grid": {f'{e["kernel"]}@{e["grid"]}': e["hbm_bytes_corrected"] for e in spmm},
                    "source": f"profiles/{tag}_summary.json"},
                   open(os.path.join(dst, "spmm_traffic.json"), "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
