@@ -112,6 +112,8 @@ class ItemExchange:
         self._offs = None
         self._compact = None
         self._ranges = None          # (csr, ranges, device boundary rows)
+        self._ratios = {}            # acc_scale / y_scale vectors (linear exchange)
+        self.rank = dist.get_rank(group)
 
     def __call__(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
@@ -186,6 +188,11 @@ class ItemExchange:
                 w.wait()
             epilogue(c, row_list=lst[:n], n_rows=prod.csr.n_rows, **kw)
             return
+        y = kw.get("y")
+        if (row_mask is None and y is not None
+                and not (kw.get("add") is not None and kw.get("acc_out") is not None)):
+            self._linear_product(prod, x, first, src_mask, y, kw)
+            return
         for rg in prod.csr.row_ranges(self.parts, self.balance_indptr):
             spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, rng=rg)
             works.append(dist.all_reduce(t[rg[0]:rg[1]], op=dist.ReduceOp.SUM,
@@ -193,6 +200,45 @@ class ItemExchange:
         for w in works:
             w.wait()
         epilogue(t, row_mask=row_mask, **kw)
+
+    def _linear_product(self, prod, x, first, src_mask, y, kw) -> None:
+        """Dense product whose output y = ys*T (+ as*add) is linear in the partial
+        sums T: every rank writes its own ys*T_r straight into y (rank 0 also
+        the addend), the ranges of y are all-reduced in place, and only the
+        layer-mean accumulator (if any) needs a pass afterwards, on its masked
+        rows, with T recovered as y / ys. No partial table, no full epilogue
+        pass. Equal to the partial-sum exchange up to rounding (ys*sum vs
+        sum of ys*T_r)."""
+        ys, ys_s = kw.get("y_scale"), kw.get("y_scale_s", 1.0)
+        sk = dict(y=y, y_scale=ys, y_scale_s=ys_s)
+        if self.rank == 0 and kw.get("add") is not None:
+            sk.update(add=kw["add"], add_scale=kw.get("add_scale"),
+                      add_scale_s=kw.get("add_scale_s", 1.0), add_mask=kw.get("add_mask"))
+        works = []
+        for rg in prod.csr.row_ranges(self.parts, self.balance_indptr):
+            spmm(prod, x, first, src_mask=src_mask, rng=rg, **sk)
+            works.append(dist.all_reduce(y[rg[0]:rg[1]], op=dist.ReduceOp.SUM,
+                                         group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        if kw.get("acc_out") is not None:
+            ratio, ratio_s = self._acc_ratio(kw.get("acc_scale"), ys, ys_s)
+            epilogue(y, acc_in=kw.get("acc_in"), acc_out=kw["acc_out"], acc_scale=ratio,
+                     acc_scale_s=kw.get("acc_scale_s", 1.0) * ratio_s,
+                     gamma=kw.get("gamma", 1.0), acc_mask=kw.get("acc_mask"),
+                     row_mask=kw.get("acc_mask"))
+
+    def _acc_ratio(self, acc_scale, ys, ys_s: float):
+        """acc_scale / ys per row (0 where ys == 0: such rows have T == 0)."""
+        if ys is None:
+            return acc_scale, 1.0 / ys_s
+        key = (None if acc_scale is None else acc_scale.data_ptr(), ys.data_ptr(), ys.numel())
+        r = self._ratios.get(key)
+        if r is None:
+            num = torch.ones_like(ys) if acc_scale is None else acc_scale
+            r = torch.where(ys != 0, num / ys, torch.zeros_like(ys)).contiguous()
+            self._ratios[key] = r
+        return r, 1.0 / ys_s
 
 
 class ShardedTrainer(FusedTrainer):
