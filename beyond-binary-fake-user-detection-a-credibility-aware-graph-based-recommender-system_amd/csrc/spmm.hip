@@ -79,26 +79,82 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
   return make_float4(a * x.x, a * x.y, a * x.z, a * x.w);
 }
 
-// One-row-per-group tuning (A/B builds): source rows in flight per group, and
-// the occupancy target of the one-row kernels (0 = the compiler's choice).
-#define BBGR_WAVES_ATTR(n) __attribute__((amdgpu_waves_per_eu(n ? n : 1, n ? n : 10)))
-// the same, for d = 64 only (wider rows keep the compiler's choice)
-#define BBGR_WAVES_ATTR64(n) \
-  __attribute__((amdgpu_waves_per_eu(D == 64 && n ? n : 1, D == 64 && n ? n : 10)))
+// Per-width tuning (measured with tools/ab_spmm.sh A/B builds; every value
+// can be overridden with -D for such builds):
+//   row_u        source rows in flight per 16-lane group, one-row kernels
+//   row_waves    occupancy the one-row kernels are compiled for (0 = compiler)
+//   pair_u       source rows in flight PER ROW, two-row kernels (full / masked)
+//   pair_waves   occupancy of the two-row kernels (full / masked)
+// d = 64: more rows in flight per CU beat deeper per-row batches.
 #ifndef BBGR_ROW_U
 #define BBGR_ROW_U 8
 #endif
 #ifndef BBGR_ROW_WAVES
 #define BBGR_ROW_WAVES 0
 #endif
+#ifndef BBGR_PAIR_U
+#define BBGR_PAIR_U 4
+#endif
+#ifndef BBGR_PAIR_U_MASKED
+#define BBGR_PAIR_U_MASKED 4
+#endif
+#ifndef BBGR_PAIR_WAVES
+#define BBGR_PAIR_WAVES 8
+#endif
+#ifndef BBGR_PAIR_WAVES_MASKED
+#define BBGR_PAIR_WAVES_MASKED 8
+#endif
+// d = 128
+#ifndef BBGR_ROW_U128
+#define BBGR_ROW_U128 8
+#endif
+#ifndef BBGR_ROW_WAVES128
+#define BBGR_ROW_WAVES128 0
+#endif
+#ifndef BBGR_PAIR_U128
+#define BBGR_PAIR_U128 4
+#endif
+#ifndef BBGR_PAIR_WAVES128
+#define BBGR_PAIR_WAVES128 0
+#endif
+// d = 256
+#ifndef BBGR_ROW_U256
+#define BBGR_ROW_U256 4
+#endif
+#ifndef BBGR_ROW_WAVES256
+#define BBGR_ROW_WAVES256 0
+#endif
+#ifndef BBGR_PAIR_U256
+#define BBGR_PAIR_U256 2
+#endif
+#ifndef BBGR_PAIR_WAVES256
+#define BBGR_PAIR_WAVES256 0
+#endif
+
+template <int D> struct Tune;
+template <> struct Tune<64> {
+  static constexpr int row_u = BBGR_ROW_U, row_waves = BBGR_ROW_WAVES;
+  static constexpr int pair_u = BBGR_PAIR_U, pair_u_masked = BBGR_PAIR_U_MASKED;
+  static constexpr int pair_waves = BBGR_PAIR_WAVES, pair_waves_masked = BBGR_PAIR_WAVES_MASKED;
+};
+template <> struct Tune<128> {
+  static constexpr int row_u = BBGR_ROW_U128, row_waves = BBGR_ROW_WAVES128;
+  static constexpr int pair_u = BBGR_PAIR_U128, pair_u_masked = BBGR_PAIR_U128;
+  static constexpr int pair_waves = BBGR_PAIR_WAVES128, pair_waves_masked = BBGR_PAIR_WAVES128;
+};
+template <> struct Tune<256> {
+  static constexpr int row_u = BBGR_ROW_U256, row_waves = BBGR_ROW_WAVES256;
+  static constexpr int pair_u = BBGR_PAIR_U256, pair_u_masked = BBGR_PAIR_U256;
+  static constexpr int pair_waves = BBGR_PAIR_WAVES256, pair_waves_masked = BBGR_PAIR_WAVES256;
+};
+#define BBGR_WAVES(n) __attribute__((amdgpu_waves_per_eu((n) ? (n) : 1, (n) ? (n) : 10)))
 
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
 template <int D, int WMODE, bool MASKED>
 __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
                                              int lane, float4 (&acc)[D / 64]) {
   constexpr int V = D / 64;
-  constexpr int UR = (D == 64 ? BBGR_ROW_U : 16) / V;   // tuned at d = 64 only
-  constexpr int U = UR > 0 ? UR : 1;  // source rows in flight per group per batch
+  constexpr int U = Tune<D>::row_u;   // source rows in flight per group per batch
   for (int e0 = eb; e0 < ee; e0 += 16) {
     const int n = min(16, ee - e0);
     int my = -1;
@@ -145,22 +201,6 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
   }
 }
 
-// Tuning of the two-rows-per-group kernels (tools/ab_spmm.sh A/B builds):
-// source rows in flight per row and iteration, and the occupancy the
-// compiler is held to (0 = its own choice).
-#ifndef BBGR_PAIR_U
-#define BBGR_PAIR_U 4
-#endif
-#ifndef BBGR_PAIR_U_MASKED
-#define BBGR_PAIR_U_MASKED 4
-#endif
-#ifndef BBGR_PAIR_WAVES
-#define BBGR_PAIR_WAVES 8
-#endif
-#ifndef BBGR_PAIR_WAVES_MASKED
-#define BBGR_PAIR_WAVES_MASKED 8
-#endif
-
 // Two short rows per 16-lane group, their batches interleaved: 2*U8 source
 // rows in flight per group across two independent rows (U8 per row), so a
 // low-degree table (users, avg degree ~10) keeps twice the rows in flight
@@ -172,8 +212,7 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
                                             int eeB, int lane, float4 (&accA)[D / 64],
                                             float4 (&accB)[D / 64]) {
   constexpr int V = D / 64;
-  constexpr int UR = D == 64 ? (MASKED ? BBGR_PAIR_U_MASKED : BBGR_PAIR_U) / V : 8 / V;
-  constexpr int U = UR > 0 ? UR : 1;   // source rows per row and iteration
+  constexpr int U = MASKED ? Tune<D>::pair_u_masked : Tune<D>::pair_u;   // per row
   const int nA = eeA - ebA, nB = eeB - ebB;
   const int nmax = max(nA, nB);
   for (int o = 0; o < nmax; o += 16) {
@@ -420,23 +459,23 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
 // (low-degree table) forms are their own symbols too, with their own
 // occupancy target.
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES_ATTR(BBGR_ROW_WAVES) void spmm_kernel(SpmmParams P) {
+__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::row_waves) void spmm_kernel(SpmmParams P) {
   spmm_body<D, WMODE, false, false>(P);
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES_ATTR64(BBGR_PAIR_WAVES) void spmm_pair_kernel(
+__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves) void spmm_pair_kernel(
     SpmmParams P) {
   spmm_body<D, WMODE, false, true>(P);
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES_ATTR(BBGR_ROW_WAVES) void spmm_masked_kernel(SpmmParams P) {
+__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::row_waves) void spmm_masked_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true, false>(P);
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES_ATTR64(BBGR_PAIR_WAVES_MASKED) void
+__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves_masked) void
 spmm_masked_pair_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true, true>(P);
 }
@@ -444,12 +483,12 @@ spmm_masked_pair_kernel(SpmmParams P) {
 // Full-CSR launch whose epilogue applies the fused Adam step (its bytes add the
 // parameter / moment streams): a third symbol so rooflines stay per kind.
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES_ATTR(BBGR_ROW_WAVES) void spmm_adam_kernel(SpmmParams P) {
+__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::row_waves) void spmm_adam_kernel(SpmmParams P) {
   spmm_body<D, WMODE, false, false>(P);
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES_ATTR64(BBGR_PAIR_WAVES) void spmm_adam_pair_kernel(
+__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves) void spmm_adam_pair_kernel(
     SpmmParams P) {
   spmm_body<D, WMODE, false, true>(P);
 }
