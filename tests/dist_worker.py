@@ -41,7 +41,8 @@ def main():
     else:
         e = synthetic_edges(WEAK_U, WEAK_I, WEAK_E, 100 + rank, items="zipf", item_seed=100)
         rng = np.random.default_rng(5)
-        u0 = rng.uniform(-1, 1, (2 * WEAK_U, 64)).astype(np.float32)[rank * WEAK_U:(rank + 1) * WEAK_U]
+        world = dist.get_world_size()
+        u0 = rng.uniform(-1, 1, (world * WEAK_U, 64)).astype(np.float32)[rank * WEAK_U:(rank + 1) * WEAK_U]
         i0 = rng.uniform(-1, 1, (WEAK_I, 64)).astype(np.float32)
         np.save(os.path.join(out_dir, f"edges{rank}.npy"), e)
         tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3, batch_size=32,

@@ -1,8 +1,8 @@
 """GPU: the real ShardedTrainer (HIP kernels + torch.distributed) at world
-size 2. RCCL cannot run two ranks on one device, so the two ranks share
+sizes 2 and 3. RCCL cannot run two ranks on one device, so the ranks share
 cuda:0 over the gloo backend; the collective schedule is the one RCCL runs
 at round end on 8 GPUs. Checked against the float64 oracle on the union of
-the two ranks' batches."""
+the ranks' batches."""
 import os
 import socket
 import subprocess
@@ -23,18 +23,21 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("variant,mode,frontier", [
-    ("v2_pop", "strong", "frontier"), ("cu_fair", "strong", "frontier"),
-    ("v2_pop", "strong", "dense"), ("v2_pop", "weak", "frontier"), ("cu_fair", "weak", "frontier")])
-def test_sharded_step_two_ranks_vs_oracle(tmp_path, variant, mode, frontier):
+@pytest.mark.parametrize("variant,mode,frontier,world", [
+    ("v2_pop", "strong", "frontier", 2), ("cu_fair", "strong", "frontier", 2),
+    ("v2_pop", "strong", "dense", 2), ("v2_pop", "weak", "frontier", 2),
+    ("cu_fair", "weak", "frontier", 2), ("v2_pop", "strong", "frontier", 3),
+    ("v2_pop", "weak", "frontier", 3)])
+def test_sharded_step_vs_oracle(tmp_path, variant, mode, frontier, world):
     from oracle import ref_numpy as R
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, mode, frontier]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    ranks = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(2)]
+    ranks = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
     if mode == "strong":
         g = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
         U, I, E, DUP, D, K, B = (int(x) for x in g["meta"])
@@ -42,18 +45,20 @@ def test_sharded_step_two_ranks_vs_oracle(tmp_path, variant, mode, frontier):
     else:   # the union of the two shards is the global graph
         sys.path.insert(0, HERE)
         from dist_worker import WEAK_I, WEAK_U
-        parts = [np.load(tmp_path / f"edges{k}.npy") for k in range(2)]
-        parts[1] = parts[1] + np.array([[WEAK_U], [0]], np.int32)
+        parts = [np.load(tmp_path / f"edges{k}.npy") + np.array([[k * WEAK_U], [0]], np.int32)
+                 for k in range(world)]
         e = np.concatenate(parts, 1)
-        U, I, K = 2 * WEAK_U, WEAK_I, 3
+        U, I, K = world * WEAK_U, WEAK_I, 3
         cred = None
         rng = np.random.default_rng(5)
         u0 = rng.uniform(-1, 1, (U, 64)).astype(np.float32)
         i0 = rng.uniform(-1, 1, (I, 64)).astype(np.float32)
     # replicas of the item side are bitwise identical across ranks
-    np.testing.assert_array_equal(ranks[0]["item_w"], ranks[1]["item_w"])
-    np.testing.assert_array_equal(ranks[0]["g_i0"], ranks[1]["g_i0"])
-    assert ranks[0]["hi"] == ranks[1]["lo"] and ranks[0]["lo"] == 0 and ranks[1]["hi"] == U
+    for r in ranks[1:]:
+        np.testing.assert_array_equal(ranks[0]["item_w"], r["item_w"])
+        np.testing.assert_array_equal(ranks[0]["g_i0"], r["g_i0"])
+    assert ranks[0]["lo"] == 0 and ranks[-1]["hi"] == U
+    assert all(ranks[k]["hi"] == ranks[k + 1]["lo"] for k in range(world - 1))
     users = np.concatenate([r["users"] for r in ranks])
     pos = np.concatenate([r["pos"] for r in ranks])
     neg = np.concatenate([r["neg"] for r in ranks])
