@@ -426,6 +426,42 @@ def test_fused_trainer_step_vs_oracle(gold, variant):
     assert tr.g_uf.abs().sum().item() == 0 and tr.g_if.abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("K,d,frontier", [(0, 64, True), (1, 64, True), (4, 64, True),
+                                         (2, 128, True), (3, 256, True), (3, 128, False)])
+def test_fused_trainer_shapes_vs_oracle(K, d, frontier):
+    """The GS training step (fused Adam, frontier masks) at other depths and
+    widths: loss at 1e-5 and the Adam update normwise vs the float64 oracle."""
+    from bbgr.trainer import FusedTrainer
+    U, I = 1500, 700
+    e = synthetic_edges(U, I, 20000, 31 + K + d, items="zipf", duplicates=30)
+    cred = synthetic_credibility(U, 5)
+    rng = np.random.default_rng(K + d)
+    u0 = rng.uniform(-0.3, 0.3, (U, d)).astype(np.float32)
+    i0 = rng.uniform(-0.3, 0.3, (I, d)).astype(np.float32)
+    g = BipartiteGraph(e, U, I, DEV)
+    tr = FusedTrainer(g, "v2_pop", cred=cred, emb_dim=d, num_layers=K, batch_size=300,
+                      u0=u0, i0=i0, frontier=frontier)
+    users = tr.next_users()
+    loss = float(tr.step(users))
+    B = users.numel()
+    uu = users.cpu().numpy()
+    pos, neg = tr.pos[:B].cpu().numpy(), tr.neg[:B].cpu().numpy()
+    A, Bm = R.gs_mats(e, U, I, cred)
+    uf, itf, _, _ = R.propagate_gs(A, Bm, u0, i0, K)
+    want, gr = R.bpr_loss(uf, itf, u0, i0, uu, pos, neg, 1e-4)
+    assert abs(loss - want) <= TOL * want, (loss, want)
+    gu0, gi0 = R.backward_gs(A, Bm, gr["g_uf"], gr["g_if"], K)
+    gu0, gi0 = gu0 + gr["g_ue"], gi0 + gr["g_ie"]
+    z = np.zeros_like
+    pu, _, _ = R.adam_step(u0, gu0, z(gu0), z(gu0), 1)
+    pi, _, _ = R.adam_step(i0, gi0, z(gi0), z(gi0), 1)
+    for got, want_, name in ((tr.user_w - t(u0), pu - u0, "user update"),
+                             (tr.item_w - t(i0), pi - i0, "item update")):
+        got = got.double().cpu().numpy()
+        assert np.linalg.norm(got - want_) <= 1e-4 * np.linalg.norm(want_), name
+    assert tr.g_uf.abs().sum().item() == 0 and tr.g_if.abs().sum().item() == 0
+
+
 def test_dropin_training_step_matches_reference_torch_step(gold):
     """One step of the drop-in module + torch Adam == the fp32 torch restatement."""
     from bbgr.lightgcn_cu_pop import LightGCN, build_message_passing_mats
