@@ -140,6 +140,9 @@ def main():
     ap.add_argument("--exchange-parts", type=int, default=8,
                     help="N>1: item-row ranges per dense exchange (all-reduce of range c "
                          "overlaps the SpMM of range c+1)")
+    ap.add_argument("--vertex-order", default="degree", choices=["degree", "input"],
+                    help="number users / items by descending degree inside the graph "
+                         "(hot rows cached, cold rows streamed) or keep the input ids")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = every rank owns a full config-sized user shard over the "
                          "shared items; strong = one config graph cut into N user ranges")
@@ -191,11 +194,11 @@ def main():
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} E={E} d={d} K={K} B={B} "
         f"scaling={'weak' if weak else 'strong'} generated in {time.perf_counter() - t0:.1f}s")
 
-    xp = dict(exchange_parts=args.exchange_parts)
+    xp = dict(exchange_parts=args.exchange_parts, vertex_order=args.vertex_order)
     if not dist_mode:
         from bbgr.graph import BipartiteGraph
         from bbgr.trainer import FusedTrainer
-        graph = BipartiteGraph(edges, U, I, dev)
+        graph = BipartiteGraph(edges, U, I, dev, vertex_order=args.vertex_order)
         trainer = FusedTrainer(graph, args.variant, cred=cred, emb_dim=d, num_layers=K,
                                batch_size=B, frontier=not args.dense)
     elif weak:
@@ -274,13 +277,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "weak" if weak else "strong",
+        "scaling": args.scaling,   # N=1: weak and strong are the same run
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Zipf-0.8 items, geometric user degrees; xavier init; Beta cred)",
         "config": {"workload": f"{args.config} BPR training step ({args.variant})"
                                + (f", {world} x {args.config} user shards" if weak else ""),
                    "num_users": U * (world if weak else 1), "num_items": I, "num_edges": E,
+                   "vertex_order": args.vertex_order,
                    "emb_dim": d, "num_layers": K,
                    "global_batch": B * (world if weak else 1),
                    "parallelism": f"user-rows x{world}"
@@ -310,7 +314,12 @@ def main():
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": tot_bytes / max(n_launch, 1),
                      "kernel": "bbgr::spmm_kernel / spmm_pair_kernel (+fixup)", "launches": n_launch,
-                     "avg_launch_ms": tot_ms / max(n_launch, 1), "per_operator": per_kernel},
+                     "avg_launch_ms": tot_ms / max(n_launch, 1), "per_operator": per_kernel,
+                     "cache_assisted": achieved > HBM_PEAK_GBS,
+                     "note": "achieved = gather-model bytes (zero reuse) / launch time; above "
+                             "peak only because hot rows are served from L2 / Infinity Cache "
+                             "(degree order + streamed cold rows); `traffic` is the PMC-measured "
+                             "HBM bytes per launch"},
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},
     }
     print(json.dumps(out), file=out_stream, flush=True)

@@ -83,6 +83,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_ld", c_int64), ("adam_lr", c_float), ("adam_beta1", c_float),
         ("adam_beta2", c_float), ("adam_eps", c_float), ("adam_weight_decay", c_float),
         ("adam_bias_correction1", c_float), ("adam_bias_correction2_sqrt", c_float),
+        ("stream_from", c_int32),
     ]
 
 
@@ -137,6 +138,9 @@ _SIGNATURES = {
     "bbgr_operator_scales": ([c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P], c_int32),
     "bbgr_gather_scale": ([c_int64, _P, _P, _P, _P], c_int32),
+    "bbgr_degree_count": ([c_int64, _P, c_int32, _P, _P], c_int32),
+    "bbgr_degree_order": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_relabel": ([c_int64, _P, _P, _P, _P], c_int32),
     "bbgr_spmm": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(SpmmArgs), _P], c_int32),
     "bbgr_epilogue": ([c_int32, _P, c_int64, ctypes.POINTER(SpmmArgs), _P], c_int32),
     "bbgr_bpr": ([ctypes.POINTER(BprArgs), _P], c_int32),

@@ -267,6 +267,28 @@ __global__ void gather_scale_kernel(long nnz, const int *indices, const float *s
   if (e < nnz) out[e] = scale[indices[e]];
 }
 
+// Vertex order: degree histogram (integer atomics: exact), iota values for
+// the descending sort, inverse permutation, id relabelling.
+__global__ void degree_count_kernel(long n, const int *ids, int *deg) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) atomicAdd(deg + ids[e], 1);
+}
+
+__global__ void iota_kernel(int n, int *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = i;
+}
+
+__global__ void invert_perm_kernel(int n, const int *perm, int *rank) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) rank[perm[j]] = j;
+}
+
+__global__ void relabel_kernel(long n, const int *ids, const int *map, int *out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) out[e] = map[ids[e]];
+}
+
 struct NonEmpty {
   const int *indptr;
   __host__ __device__ bool operator()(const long &r) const {
@@ -630,5 +652,69 @@ extern "C" int bbgr_mask_to_list(int64_t n, const uint8_t *mask, int64_t *out,
   }
   BBGR_HIP(hipcub::DeviceSelect::If(workspace, temp, it, (long *)out, (long *)count, (int)n,
                                     sel, st));
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_degree_count(int64_t n_ids, const int32_t *ids, int32_t n,
+                                 int32_t *degree, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n_ids >= 0 && n >= 0, "bbgr_degree_count: negative size");
+  hipStream_t st = as_stream(stream);
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(degree && (n_ids == 0 || ids), "bbgr_degree_count: null arrays");
+  BBGR_HIP(hipMemsetAsync(degree, 0, 4 * (size_t)n, st));
+  if (n_ids == 0) return BBGR_OK;
+  hipLaunchKernelGGL(degree_count_kernel, dim3(blocks_for(n_ids)), dim3(256), 0, st,
+                     (long)n_ids, ids, degree);
+  BBGR_LAUNCHED("degree_count_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_degree_order(int32_t n, const int32_t *degree, int32_t *perm,
+                                 int32_t *rank, void *workspace, size_t *workspace_bytes,
+                                 bbgr_stream_t stream) {
+  BBGR_REQUIRE(workspace_bytes && n >= 0, "bbgr_degree_order: bad args");
+  hipStream_t st = as_stream(stream);
+  const int m = n > 0 ? n : 1;
+  size_t temp = 0;
+  BBGR_HIP(hipcub::DeviceRadixSort::SortPairsDescending(
+      nullptr, temp, (const unsigned *)nullptr, (unsigned *)nullptr, (const int *)nullptr,
+      (int *)nullptr, m, 0, 32, st));
+  const size_t off_k = 0;
+  const size_t off_v = align_up(off_k + 4 * (size_t)m);
+  const size_t off_t = align_up(off_v + 4 * (size_t)m);
+  const size_t need = align_up(off_t + temp);
+  if (!workspace) {
+    *workspace_bytes = need;
+    return BBGR_OK;
+  }
+  if (*workspace_bytes < need) {
+    set_error("bbgr_degree_order: workspace %zu < %zu", *workspace_bytes, need);
+    return BBGR_ERR_WORKSPACE;
+  }
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(degree && perm && rank, "bbgr_degree_order: null arrays");
+  char *ws = (char *)workspace;
+  unsigned *k_out = (unsigned *)(ws + off_k);
+  int *iota = (int *)(ws + off_v);
+  hipLaunchKernelGGL(iota_kernel, dim3(blocks_for(n)), dim3(256), 0, st, n, iota);
+  BBGR_LAUNCHED("iota_kernel");
+  // radix sort is stable: equal degrees keep ascending input id
+  BBGR_HIP(hipcub::DeviceRadixSort::SortPairsDescending(
+      ws + off_t, temp, (const unsigned *)degree, k_out, (const int *)iota, (int *)perm, n, 0,
+      32, st));
+  hipLaunchKernelGGL(invert_perm_kernel, dim3(blocks_for(n)), dim3(256), 0, st, n,
+                     (const int *)perm, (int *)rank);
+  BBGR_LAUNCHED("invert_perm_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_relabel(int64_t n, const int32_t *ids, const int32_t *map, int32_t *out,
+                            bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_relabel: negative size");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(ids && map && out, "bbgr_relabel: null arrays");
+  hipLaunchKernelGGL(relabel_kernel, dim3(blocks_for(n)), dim3(256), 0, as_stream(stream),
+                     (long)n, ids, map, out);
+  BBGR_LAUNCHED("relabel_kernel");
   return BBGR_OK;
 }

@@ -62,6 +62,7 @@ struct SpmmParams {
   int row_begin, row_end;      // short rows computed: [row_begin, row_end)
   int pair_rows;               // two short rows per 16-lane group (gather_pair)
   int chunk_begin;             // first long-row chunk of this launch
+  int nt_from;                 // source rows >= nt_from: streaming loads (args.stream_from)
   // fused Adam on the y-row value (bbgr_spmm_args.adam_*)
   float *adam_p, *adam_m, *adam_v;
   long adam_ld;
@@ -71,6 +72,11 @@ struct SpmmParams {
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
   return make_float4(fmaf(a, x.x, y.x), fmaf(a, x.y, y.y), fmaf(a, x.z, y.z),
                      fmaf(a, x.w, y.w));
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_nt(const float4 *p) {   // streaming (nt) load
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -179,8 +185,13 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
         if (j0 + j < n && (!MASKED || c >= 0)) {
           const float4 *src =
               reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + lane;
+          if (c >= P.nt_from) {
 #pragma unroll
-          for (int k = 0; k < V; ++k) v[j][k] = src[16 * k];
+            for (int k = 0; k < V; ++k) v[j][k] = ld_nt(src + 16 * k);
+          } else {
+#pragma unroll
+            for (int k = 0; k < V; ++k) v[j][k] = src[16 * k];
+          }
         } else {
 #pragma unroll
           for (int k = 0; k < V; ++k) v[j][k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -249,16 +260,26 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
         const int cB = __shfl(myB, j0 + j, 16);
         if (j0 + j < na && (!MASKED || cA >= 0)) {
           const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)cA * P.ldx) + lane;
+          if (cA >= P.nt_from) {
 #pragma unroll
-          for (int k = 0; k < V; ++k) vA[j][k] = src[16 * k];
+            for (int k = 0; k < V; ++k) vA[j][k] = ld_nt(src + 16 * k);
+          } else {
+#pragma unroll
+            for (int k = 0; k < V; ++k) vA[j][k] = src[16 * k];
+          }
         } else {
 #pragma unroll
           for (int k = 0; k < V; ++k) vA[j][k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         if (j0 + j < nb && (!MASKED || cB >= 0)) {
           const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)cB * P.ldx) + lane;
+          if (cB >= P.nt_from) {
 #pragma unroll
-          for (int k = 0; k < V; ++k) vB[j][k] = src[16 * k];
+            for (int k = 0; k < V; ++k) vB[j][k] = ld_nt(src + 16 * k);
+          } else {
+#pragma unroll
+            for (int k = 0; k < V; ++k) vB[j][k] = src[16 * k];
+          }
         } else {
 #pragma unroll
           for (int k = 0; k < V; ++k) vB[j][k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -738,6 +759,7 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   }
   BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_spmm: negative n_row_list");
   P.pair_rows = pair_rows(csr);
+  P.nt_from = a->stream_from > 0 ? a->stream_from : 0x7fffffff;
   hipStream_t st = as_stream(stream);
   switch (d) {
     case 64: return dispatch_wmode<64>(P, a->weight_mode, n_split, st);

@@ -48,7 +48,7 @@ from .optim import adam_step
 from .propagate import ORDER_GS, OperatorPair, backward, epilogue, forward, spmm
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .scatter import RowScatter
-from .trainer import VARIANTS, FusedTrainer
+from .trainer import VARIANTS, FusedTrainer, _internal_rows
 
 
 def partition_users(deg_u: np.ndarray, world: int) -> np.ndarray:
@@ -261,10 +261,11 @@ class ShardedTrainer(FusedTrainer):
                  neg_max_tries: int = 50, lambda_fair: float = 0.0, seed: int = 42,
                  device=None, group=None, u0=None, i0=None, user_offset: int = 0,
                  frontier: bool = True, exchange_parts: int = 4, fuse_adam: bool = True,
-                 sparse_exchange: bool = True):
+                 sparse_exchange: bool = True, vertex_order: str = "input"):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
         this rank's users; i0: the full (replicated) item table; batch_size:
-        users per step on THIS rank."""
+        users per step on THIS rank. vertex_order="degree": local users by
+        local degree, items by GLOBAL degree (identical on every rank)."""
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}")
@@ -284,12 +285,19 @@ class ShardedTrainer(FusedTrainer):
         self.B_global = self.B_local * self.world
         self.exchange = ItemExchange(group, exchange_parts)
 
-        self.graph = BipartiteGraph(local_edges, num_local_users, num_items, dev)
+        def global_degrees(deg: torch.Tensor) -> torch.Tensor:
+            g = deg.to(torch.int64)
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+            return g.to(torch.int32)
+
+        self.graph = BipartiteGraph(local_edges, num_local_users, num_items, dev,
+                                    vertex_order=vertex_order, item_degree_hook=global_degrees)
         indptr_i = global_item_indptr(self.graph.item_csr.degrees(), group)
         self.exchange.balance_indptr = indptr_i
         cred_t = None
         if cred is not None and kind != OP_SYM:
             cred_t = torch.as_tensor(np.asarray(cred, np.float32)).to(dev).contiguous()
+            cred_t = _internal_rows(self.graph.user_order, cred_t)
         self.scales = _scales(kind, self.graph, indptr_i, cred_t)
         self.pair = OperatorPair.factored(self.graph, self.scales)
 
@@ -305,6 +313,8 @@ class ShardedTrainer(FusedTrainer):
         self.item_w = torch.as_tensor(i0, dtype=torch.float32).to(dev).contiguous()
         if self.user_w.shape != (num_local_users, emb_dim) or self.item_w.shape != (num_items, emb_dim):
             raise ValueError("initial tables have the wrong shape")
+        self.user_w = _internal_rows(self.graph.user_order, self.user_w)
+        self.item_w = _internal_rows(self.graph.item_order, self.item_w)
         z = lambda n: torch.zeros(n, emb_dim, **f32)  # noqa: E731
         self.m_u, self.v_u = z(num_local_users), z(num_local_users)
         self.m_i, self.v_i = z(num_items), z(num_items)
@@ -419,6 +429,7 @@ class ShardedTrainer(FusedTrainer):
 
     def step(self) -> torch.Tensor:
         users = self.next_users()
+        self._last_users = users
         B = users.numel()
         pos, neg = self.sampler.sample(users, self.pos, self.neg)
         st = stream_handle()

@@ -34,6 +34,11 @@ from ._lib import call, ptr, stream_handle
 
 DEFAULT_LONG_THRESHOLD = 256
 DEFAULT_CHUNK_EDGES = 2048
+# Hot-row budget of a gathered table in descending-degree order: rows past it
+# are loaded non-temporal (bbgr_spmm_args.stream_from). Sized to leave room in
+# the 256 MB Infinity Cache for the streams of the launch; at most 1/8 of the
+# rows (C4: the 625k highest-degree users and 125k items stay cached).
+HOT_BYTES = 192 << 20
 
 
 def _as_device_i32(x, device) -> torch.Tensor:
@@ -159,6 +164,14 @@ class Csr:
         cache[key] = out
         return out
 
+    def stream_from(self, d: int) -> int:
+        """bbgr_spmm_args.stream_from for a gather of d-wide source rows: 0
+        unless the columns are in descending-degree order (BipartiteGraph with
+        vertex_order="degree"); then the hot prefix of the source table."""
+        if not self.__dict__.get("cols_by_degree", False):
+            return 0
+        return max(1, min(self.n_cols // 8, HOT_BYTES // (4 * d)))
+
     def partial_workspace(self, d: int) -> torch.Tensor | None:
         if self.n_split == 0:
             return None
@@ -185,12 +198,71 @@ class Scales:
     deg_i: torch.Tensor
 
 
+class VertexOrder:
+    """A renumbering of one vertex set by descending degree (bbgr_degree_order;
+    ties keep ascending id): perm[new] = input id, rank[input id] = new."""
+
+    def __init__(self, degree: torch.Tensor):
+        degree = degree.to(torch.int32).contiguous()
+        n = degree.numel()
+        dev = degree.device
+        self.perm = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        self.rank = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        st = stream_handle()
+        nb = _lib.workspace_query("bbgr_degree_order", n, ptr(degree), ptr(self.perm),
+                                  ptr(self.rank), args_after=(st,))
+        ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+        have = ctypes.c_size_t(nb)
+        call("bbgr_degree_order", n, ptr(degree), ptr(self.perm), ptr(self.rank), ptr(ws),
+             ctypes.byref(have), st)
+        self.perm, self.rank = self.perm[:n], self.rank[:n]
+        self._perm64 = self.perm.long()
+        self._rank64 = self.rank.long()
+
+    def to_internal(self, ids: torch.Tensor) -> torch.Tensor:
+        """Input ids -> internal row ids (int64)."""
+        return self._rank64[ids.to(self._rank64.device).long()]
+
+    def to_input(self, ids: torch.Tensor) -> torch.Tensor:
+        """Internal row ids -> input ids (int64)."""
+        return self._perm64[ids.to(self._perm64.device).long()]
+
+    def rows_to_internal(self, table: torch.Tensor) -> torch.Tensor:
+        """Rows indexed by input id -> rows in internal order (a copy)."""
+        return table.to(self._perm64.device)[self._perm64].contiguous()
+
+    def rows_to_input(self, table: torch.Tensor) -> torch.Tensor:
+        """Rows in internal order -> rows indexed by input id (a copy)."""
+        return table[self._rank64].contiguous()
+
+
+def _degree_count(ids: torch.Tensor, n: int) -> torch.Tensor:
+    deg = torch.empty(max(n, 1), dtype=torch.int32, device=ids.device)
+    call("bbgr_degree_count", ids.numel(), ptr(ids), n, ptr(deg), stream_handle())
+    return deg[:n]
+
+
+def _relabel(ids: torch.Tensor, order: VertexOrder) -> torch.Tensor:
+    out = torch.empty_like(ids)
+    call("bbgr_relabel", ids.numel(), ptr(ids), ptr(order.rank), ptr(out), stream_handle())
+    return out
+
+
 class BipartiteGraph:
-    """The train edges of one split as two device CSRs (user rows, item rows)."""
+    """The train edges of one split as two device CSRs (user rows, item rows).
+
+    vertex_order="degree" renumbers users and items by descending degree
+    before the build (``user_order`` / ``item_order``: VertexOrder; None in
+    input order). Every row-indexed tensor of the graph — scales, CSR rows and
+    columns, ids the sampler returns — is then in internal order; the trainers
+    map inputs and state_dict() across. `item_degree_hook(deg)` (int32 [I] ->
+    int32 [I]) replaces the local item degrees that set the item order — the
+    sharded trainer passes an all-reduce so every rank orders items alike."""
 
     def __init__(self, train_edges_2xE, num_users: int, num_items: int, device,
                  long_threshold: int = DEFAULT_LONG_THRESHOLD,
-                 chunk_edges: int = DEFAULT_CHUNK_EDGES):
+                 chunk_edges: int = DEFAULT_CHUNK_EDGES, vertex_order: str = "input",
+                 item_degree_hook=None):
         device = torch.device(device)
         if isinstance(train_edges_2xE, tuple):        # graph.py's (u2i_src, u2i_dst)
             src, dst = train_edges_2xE
@@ -207,10 +279,27 @@ class BipartiteGraph:
         self.num_users, self.num_items = int(num_users), int(num_items)
         self.nnz = int(u.numel())
         self.device = device
+        if vertex_order not in ("input", "degree"):
+            raise ValueError(f"vertex_order must be 'input' or 'degree', not {vertex_order!r}")
+        self.vertex_order = vertex_order
+        self.user_order = self.item_order = None
+        if vertex_order == "degree":
+            if self.nnz and (int(u.min()) < 0 or int(u.max()) >= self.num_users
+                             or int(i.min()) < 0 or int(i.max()) >= self.num_items):
+                raise ValueError("edge index out of range")
+            deg_i = _degree_count(i, self.num_items)
+            if item_degree_hook is not None:
+                deg_i = item_degree_hook(deg_i)
+            self.user_order = VertexOrder(_degree_count(u, self.num_users))
+            self.item_order = VertexOrder(deg_i)
+            u, i = _relabel(u, self.user_order), _relabel(i, self.item_order)
         self.user_csr = Csr(u, i, num_users, num_items, device,
                             long_threshold=long_threshold, chunk_edges=chunk_edges)
         self.item_csr = Csr(i, u, num_items, num_users, device,
                             long_threshold=long_threshold, chunk_edges=chunk_edges)
+        ordered = vertex_order == "degree"
+        self.user_csr.cols_by_degree = ordered   # gathers item rows
+        self.item_csr.cols_by_degree = ordered   # gathers user rows
         self._scales: dict = {}
 
     def scales(self, kind: int, cred: torch.Tensor | None = None) -> Scales:

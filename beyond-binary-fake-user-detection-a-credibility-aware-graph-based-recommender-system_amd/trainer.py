@@ -58,6 +58,7 @@ class FusedTrainer:
         cred_t = None
         if cred is not None and kind != OP_SYM:
             cred_t = torch.as_tensor(np.asarray(cred, np.float32)).to(dev).contiguous()
+            cred_t = _internal_rows(graph.user_order, cred_t)
         self.scales = graph.scales(kind, cred_t)
         self.pair = OperatorPair.factored(graph, self.scales)
 
@@ -72,6 +73,9 @@ class FusedTrainer:
         self.item_w = torch.as_tensor(i0, dtype=torch.float32).to(dev).contiguous()
         if self.user_w.shape != (self.U, emb_dim) or self.item_w.shape != (self.I, emb_dim):
             raise ValueError("initial tables have the wrong shape")
+        # tables are given (and generated) by input id; held in the graph's order
+        self.user_w = _internal_rows(graph.user_order, self.user_w)
+        self.item_w = _internal_rows(graph.item_order, self.item_w)
         z = lambda n: torch.zeros(n, emb_dim, **f32)  # noqa: E731
         self.m_u, self.v_u, self.m_i, self.v_i = z(self.U), z(self.U), z(self.I), z(self.I)
         self.uf = torch.empty(self.U, emb_dim, **f32)
@@ -130,7 +134,16 @@ class FusedTrainer:
 
     # -- one step ----------------------------------------------------------------
     def step(self, users: torch.Tensor | None = None) -> torch.Tensor:
-        users = self.next_users() if users is None else users.to(torch.int64).contiguous()
+        """One training step over `users` (input ids; default: the next slice of
+        the epoch permutation)."""
+        if users is None:
+            users = self.next_users()
+        else:
+            users = users.to(device=self.device, dtype=torch.int64)
+            if self.graph.user_order is not None:
+                users = self.graph.user_order.to_internal(users)
+            users = users.contiguous()
+        self._last_users = users
         B = users.numel()
         self.pos, self.neg = self.posneg[:B], self.posneg[B:2 * B]
         pos, neg = self.sampler.sample(users, self.pos, self.neg)
@@ -213,9 +226,32 @@ class FusedTrainer:
                  ptr(self.mask_i), st)
         return self.mask_u, self.mask_i
     def forward(self):
-        return forward(self.pair, self.user_w, self.item_w, self.K, self.order,
-                       out_u=self.uf, out_i=self.itf, ws=self.ws)
+        """Final (layer-mean) tables, rows by input id."""
+        uf, itf = forward(self.pair, self.user_w, self.item_w, self.K, self.order,
+                          out_u=self.uf, out_i=self.itf, ws=self.ws)
+        return _input_rows(self.graph.user_order, uf), _input_rows(self.graph.item_order, itf)
+
+    def batch(self):
+        """(users, pos, neg) of the last step, as input ids (int64)."""
+        B = self._last_users.numel()
+        users, pos, neg = self._last_users, self.posneg[:B], self.posneg[B:2 * B]
+        go, gi = self.graph.user_order, self.graph.item_order
+        if go is not None:
+            users = go.to_input(users)
+        if gi is not None:
+            pos, neg = gi.to_input(pos), gi.to_input(neg)
+        return users, pos, neg
 
     def state_dict(self) -> dict:
-        """Reference keys (Version-2:903): user_emb.weight / item_emb.weight."""
-        return {"user_emb.weight": self.user_w, "item_emb.weight": self.item_w}
+        """Reference keys (Version-2:903): user_emb.weight / item_emb.weight
+        (rows by input id)."""
+        return {"user_emb.weight": _input_rows(self.graph.user_order, self.user_w),
+                "item_emb.weight": _input_rows(self.graph.item_order, self.item_w)}
+
+
+def _internal_rows(order, t: torch.Tensor) -> torch.Tensor:
+    return t if order is None else order.rows_to_internal(t)
+
+
+def _input_rows(order, t: torch.Tensor) -> torch.Tensor:
+    return t if order is None else order.rows_to_input(t)

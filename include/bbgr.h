@@ -100,6 +100,26 @@ int bbgr_csr_plan_build(const bbgr_csr *csr, int32_t *chunks, int32_t *split,
                         bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
+/* Vertex order (a one-time relabelling before the CSR build)                 */
+/*   The reference indexes users / items in id-map order (Version-2:227-303). */
+/*   Numbering the rows of a table by descending degree packs its most        */
+/*   gathered rows into one address range: the SpMM then streams the cold     */
+/*   rows (bbgr_spmm_args.stream_from) and keeps the hot ones cached. Every   */
+/*   operator is permutation-equivariant, so the result is the same model up */
+/*   to the row order (and fp32 summation order inside a row).                */
+/* ------------------------------------------------------------------------- */
+/* degree[j] = number of e < n_ids with ids[e] == j, j < n (exact).           */
+int bbgr_degree_count(int64_t n_ids, const int32_t *ids, int32_t n, int32_t *degree,
+                      bbgr_stream_t stream);
+/* perm[new] = old id, rank[old] = new id, by descending degree; equal degrees */
+/* keep ascending id (stable). Workspace query with workspace == NULL.        */
+int bbgr_degree_order(int32_t n, const int32_t *degree, int32_t *perm, int32_t *rank,
+                      void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
+/* out[e] = map[ids[e]] for e < n (out may alias ids).                        */
+int bbgr_relabel(int64_t n, const int32_t *ids, const int32_t *map, int32_t *out,
+                 bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
 /* Operator scale vectors                                                     */
 /*   Replaces the numpy weight math of build_message_passing_mats             */
 /*   (Version-2/lighgcn_cu_pop.py:429-452), its Method-A variant              */
@@ -184,6 +204,11 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   adam_ld). y may then be NULL: the gradient table is never written nor    */
 /*   re-read (the last backward product of the training step, V2:862-863).   */
 /*   Every row of the launch must be computed (no masks / row lists).         */
+/* stream_from > 0: source rows with index >= stream_from are gathered with   */
+/*   non-temporal (streaming) loads, so they do not evict the rows below it  */
+/*   from L2 / Infinity Cache. Meant for a source table in descending-degree  */
+/*   order (bbgr_degree_order), where rows [0, stream_from) are the hot set.  */
+/*   Results are unchanged; 0 = every row loaded with the default policy.     */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -228,6 +253,7 @@ typedef struct {
   float adam_weight_decay;
   float adam_bias_correction1;
   float adam_bias_correction2_sqrt;
+  int32_t stream_from;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,

@@ -23,10 +23,11 @@ WEAK_U, WEAK_I, WEAK_E = 200, 150, 2500
 def main():
     out_dir, variant, mode = sys.argv[1], sys.argv[2], sys.argv[3]
     frontier = len(sys.argv) < 5 or sys.argv[4] != "dense"
+    order = sys.argv[5] if len(sys.argv) > 5 else "input"
     if mode == "fused":
         return fused_vs_separate(out_dir, variant)
     if mode == "rccl1":
-        return rccl_single_rank(out_dir, variant)
+        return rccl_single_rank(out_dir, variant, order)
     dist.init_process_group("gloo")
     rank = dist.get_rank()
     torch.cuda.set_device(0)
@@ -37,7 +38,7 @@ def main():
         tr = ShardedTrainer.from_global_edges(
             g["edges"], U, I, variant, cred=g["cred"], emb_dim=D, num_layers=K, batch_size=64,
             device="cuda:0", u0=g["u0"], i0=g["i0"], lambda_fair=lam, frontier=frontier,
-            exchange_parts=3, fuse_adam=False)
+            exchange_parts=3, fuse_adam=False, vertex_order=order)
     else:
         e = synthetic_edges(WEAK_U, WEAK_I, WEAK_E, 100 + rank, items="zipf", item_seed=100)
         rng = np.random.default_rng(5)
@@ -48,15 +49,20 @@ def main():
         tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3, batch_size=32,
                             device="cuda:0", u0=u0, i0=i0, lambda_fair=lam,
                             user_offset=rank * WEAK_U, frontier=frontier, exchange_parts=2,
-                            fuse_adam=False)
+                            fuse_adam=False, vertex_order=order)
     loss = float(tr.step())
-    users = tr.perm[: tr.B_local]          # the first step takes the head of epoch 1
+    users, pos, neg = tr.batch()           # input (local) ids
+    go, gi = tr.graph.user_order, tr.graph.item_order
+
+    def by_input(order, x):                # internal rows -> rows by input id
+        return (x if order is None else order.rows_to_input(x)).cpu().numpy()
+
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), lo=tr.lo, hi=tr.hi,
-             users=users.cpu().numpy() + tr.lo, pos=tr.pos.cpu().numpy(),
-             neg=tr.neg.cpu().numpy(), g_u0=tr.g_u0.cpu().numpy(), g_i0=tr.g_i0.cpu().numpy(),
-             user_w=tr.user_w.cpu().numpy(), item_w=tr.item_w.cpu().numpy(), loss=loss,
-             uf=tr.uf.cpu().numpy(), itf=tr.itf.cpu().numpy())
+             users=users.cpu().numpy() + tr.lo, pos=pos.cpu().numpy(), neg=neg.cpu().numpy(),
+             g_u0=by_input(go, tr.g_u0), g_i0=by_input(gi, tr.g_i0),
+             user_w=by_input(go, tr.user_w), item_w=by_input(gi, tr.item_w), loss=loss,
+             uf=by_input(go, tr.uf), itf=by_input(gi, tr.itf))
     dist.destroy_process_group()
 
 
@@ -89,7 +95,7 @@ def fused_vs_separate(out_dir, variant):
     dist.destroy_process_group()
 
 
-def rccl_single_rank(out_dir, variant):
+def rccl_single_rank(out_dir, variant, order="input"):
     """World size 1 over RCCL ("nccl"): the sharded trainer's collectives run
     through RCCL itself (uint8 / fp32 all-reduce, async ranges, all-gather of
     int64 and fp32) and its steps must equal the single-GPU FusedTrainer's."""
@@ -103,8 +109,9 @@ def rccl_single_rank(out_dir, variant):
     u0 = rng.uniform(-0.5, 0.5, (U, 64)).astype(np.float32)
     i0 = rng.uniform(-0.5, 0.5, (I, 64)).astype(np.float32)
     kw = dict(emb_dim=64, num_layers=3, batch_size=256, u0=u0, i0=i0)
-    sh = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3, **kw)
-    one = FusedTrainer(BipartiteGraph(e, U, I, "cuda:0"), variant, **kw)
+    sh = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
+                        vertex_order=order, **kw)
+    one = FusedTrainer(BipartiteGraph(e, U, I, "cuda:0", vertex_order=order), variant, **kw)
     out = {}
     for tag, tr in (("sharded", sh), ("single", one)):
         out[f"{tag}_loss"] = np.array([float(tr.step()) for _ in range(3)])

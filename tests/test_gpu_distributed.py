@@ -23,17 +23,21 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("variant,mode,frontier,world", [
-    ("v2_pop", "strong", "frontier", 2), ("cu_fair", "strong", "frontier", 2),
-    ("v2_pop", "strong", "dense", 2), ("v2_pop", "weak", "frontier", 2),
-    ("cu_fair", "weak", "frontier", 2), ("v2_pop", "strong", "frontier", 3),
-    ("v2_pop", "weak", "frontier", 3)])
-def test_sharded_step_vs_oracle(tmp_path, variant, mode, frontier, world):
+@pytest.mark.parametrize("variant,mode,frontier,world,order", [
+    ("v2_pop", "strong", "frontier", 2, "input"), ("cu_fair", "strong", "frontier", 2, "input"),
+    ("v2_pop", "strong", "dense", 2, "input"), ("v2_pop", "weak", "frontier", 2, "input"),
+    ("cu_fair", "weak", "frontier", 2, "input"), ("v2_pop", "strong", "frontier", 3, "input"),
+    ("v2_pop", "weak", "frontier", 3, "input"), ("v2_pop", "weak", "frontier", 2, "degree"),
+    ("v2_pop", "strong", "frontier", 3, "degree"), ("cu_fair", "weak", "dense", 2, "degree")])
+def test_sharded_step_vs_oracle(tmp_path, variant, mode, frontier, world, order):
+    """order="degree": every rank numbers its users by local degree and the
+    items by GLOBAL degree (identical on every rank); results read back by
+    input id."""
     from oracle import ref_numpy as R
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, mode, frontier]
+           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, mode, frontier, order]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -122,13 +126,15 @@ def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
         np.testing.assert_array_equal(ranks[0][key], ranks[1][key])   # replicas identical
 
 
-@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair"])
-def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant):
+@pytest.mark.parametrize("variant,order", [("v2_pop", "input"), ("cu_fair", "input"),
+                                           ("v2_pop", "degree")])
+def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, order):
     """The sharded step with its collectives on RCCL (world size 1: the one
     RCCL configuration a 1-GPU box can run) equals the single-GPU step."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, "rccl1"]
+           os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, "rccl1", "frontier",
+           order]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

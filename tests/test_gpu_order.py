@@ -1,0 +1,172 @@
+"""GPU: degree-ordered vertex numbering (BipartiteGraph(vertex_order="degree")).
+
+The order itself is integer work and must be exact (numpy's stable argsort of
+the negated degrees); the non-temporal source loads it enables must not change
+a single bit of the SpMM; a trainer on the reordered graph must be the same
+model as on the input order (parity vs the float64 oracle at 1e-5 on input
+ids, as in test_gpu_parity.py)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from bbgr.graph import BipartiteGraph, Csr, VertexOrder  # noqa: E402
+from bbgr.synthetic import synthetic_credibility, synthetic_edges  # noqa: E402
+from oracle import ref_numpy as R  # noqa: E402
+
+DEV = "cuda"
+TOL = 1e-5
+
+
+def t(a, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(a)).to(DEV, dtype)
+
+
+def rel(got, ref):
+    got = got.detach().double().cpu().numpy() if isinstance(got, torch.Tensor) else got
+    return np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)
+
+
+@pytest.mark.parametrize("n", [1, 7, 1000, 300_000])
+def test_degree_count_and_order_match_numpy(n):
+    from bbgr.graph import _degree_count, _relabel
+    rng = np.random.default_rng(n)
+    ids = rng.zipf(1.3, size=3 * n + 5).astype(np.int64) % n      # many ties, some zeros
+    ids = ids.astype(np.int32)
+    deg = _degree_count(t(ids, torch.int32), n)
+    want = np.bincount(ids, minlength=n)
+    np.testing.assert_array_equal(deg.cpu().numpy(), want)
+    o = VertexOrder(deg)
+    perm = np.argsort(-want, kind="stable")
+    np.testing.assert_array_equal(o.perm.cpu().numpy(), perm)
+    rank = np.empty(n, np.int64)
+    rank[perm] = np.arange(n)
+    np.testing.assert_array_equal(o.rank.cpu().numpy(), rank)
+    np.testing.assert_array_equal(_relabel(t(ids, torch.int32), o).cpu().numpy(), rank[ids])
+    x = t(rng.normal(size=(n, 3)))
+    assert torch.equal(o.rows_to_input(o.rows_to_internal(x)), x)
+
+
+def test_ordered_graph_csrs_are_the_relabelled_graph():
+    U, I = 900, 400
+    e = synthetic_edges(U - 3, I - 3, 12000, 4, items="zipf", duplicates=40)
+    g = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
+    ru = np.argsort(np.argsort(-np.bincount(e[0], minlength=U), kind="stable"), kind="stable")
+    ri = np.argsort(np.argsort(-np.bincount(e[1], minlength=I), kind="stable"), kind="stable")
+    e2 = np.stack([ru[e[0]], ri[e[1]]]).astype(np.int32)
+    indptr, indices = R.edges_to_user_csr(e2, U)
+    np.testing.assert_array_equal(g.user_csr.indptr.cpu().numpy(), indptr)
+    np.testing.assert_array_equal(g.user_csr.indices[: g.nnz].cpu().numpy(), indices)
+    indptr, indices = R.edges_to_user_csr(e2[::-1].copy(), I)
+    np.testing.assert_array_equal(g.item_csr.indptr.cpu().numpy(), indptr)
+    np.testing.assert_array_equal(g.item_csr.indices[: g.nnz].cpu().numpy(), indices)
+    # internal degrees are non-increasing
+    assert (np.diff(np.diff(g.user_csr.indptr.cpu().numpy())) <= 0).all()
+    assert (np.diff(np.diff(g.item_csr.indptr.cpu().numpy())) <= 0).all()
+    assert g.user_csr.stream_from(64) > 0 and g.item_csr.stream_from(256) > 0
+    assert BipartiteGraph(e, U, I, DEV).user_csr.stream_from(64) == 0
+    with pytest.raises(ValueError):
+        BipartiteGraph(e, U, I, DEV, vertex_order="random")
+    with pytest.raises(ValueError):
+        BipartiteGraph(e, U - 10, I, DEV, vertex_order="degree")
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("side", ["item_rows", "user_rows"])
+def test_stream_from_loads_leave_results_bitwise_equal(d, side):
+    """stream_from only changes the cache policy of the gathers: every output
+    bit is equal (one-row and two-row kernels, split rows, masks)."""
+    from bbgr.propagate import Product, spmm
+    U, I = 3000, 700
+    e = synthetic_edges(U, I, 30000, 11, items="zipf")
+    rows, cols, nr, nc = (e[1], e[0], I, U) if side == "item_rows" else (e[0], e[1], U, I)
+    c = Csr(rows, cols, nr, nc, DEV, long_threshold=64, chunk_edges=128)
+    prod = Product(c, None, None, None, {})
+    x = torch.randn(nc, d, device=DEV)
+    mask = (torch.rand(nc, device=DEV) < 0.3).to(torch.uint8)
+    outs = []
+    for ordered in (False, True):
+        c.cols_by_degree = ordered
+        assert (c.stream_from(d) > 0) == ordered
+        y, acc = torch.empty(nr, d, device=DEV), torch.empty(nr, d, device=DEV)
+        ym = torch.zeros(nr, d, device=DEV)
+        spmm(prod, x, False, y=y, acc_in=x[:nr] if nr <= nc else None, acc_out=acc)
+        spmm(prod, x, False, y=ym, src_mask=mask)
+        outs.append((y, acc, ym))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair", "method_a"])
+def test_ordered_trainer_step_vs_oracle(variant):
+    """A step of the trainer on the degree-ordered graph, read back by input id
+    (batch(), state_dict()), against the float64 oracle on the input graph."""
+    from bbgr.trainer import FusedTrainer
+    U, I, d, K = 1200, 500, 64, 3
+    e = synthetic_edges(U, I, 16000, 21, items="zipf", duplicates=25)
+    cred = synthetic_credibility(U, 3)
+    rng = np.random.default_rng(4)
+    u0 = rng.uniform(-0.3, 0.3, (U, d)).astype(np.float32)
+    i0 = rng.uniform(-0.3, 0.3, (I, d)).astype(np.float32)
+    lam = 0.05 if variant == "cu_fair" else 0.0
+    g = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
+    tr = FusedTrainer(g, variant, cred=cred, emb_dim=d, num_layers=K, batch_size=256,
+                      u0=u0, i0=i0, lambda_fair=lam)
+    deg_u = np.bincount(e[0], minlength=U)
+    users_in = np.flatnonzero(deg_u > 0)[::4][:256]
+    loss = float(tr.step(t(users_in, torch.int64)))
+    uu, pos, neg = (x.cpu().numpy() for x in tr.batch())
+    np.testing.assert_array_equal(uu, users_in)
+    ind, col = R.edges_to_user_csr(e, U)
+    for u, p, n in zip(uu, pos, neg):      # sampler invariants on input ids
+        row = col[ind[u]:ind[u + 1]]
+        assert p in row and n not in row
+    if variant == "cu_fair":
+        A, Bm, deg_i = R.j_mats(e, U, I, cred)
+        uf, itf, _, _ = R.propagate_j(A, Bm, u0, i0, K)
+        pop = deg_i / max(deg_i.max(), 1.0)
+    else:
+        A, Bm = R.gs_mats(e, U, I, cred, method_a=(variant == "method_a"))
+        uf, itf, _, _ = R.propagate_gs(A, Bm, u0, i0, K)
+        pop = None
+    want, gr = R.bpr_loss(uf, itf, u0, i0, uu, pos, neg, 1e-4, pop, lam)
+    assert abs(loss - want) <= TOL * want, (loss, want)
+    if variant == "cu_fair":
+        gu0, gi0 = R.backward_j(A, Bm, gr["g_uf"], gr["g_if"], K)
+    else:
+        gu0, gi0 = R.backward_gs(A, Bm, gr["g_uf"], gr["g_if"], K)
+    gu0, gi0 = gu0 + gr["g_ue"], gi0 + gr["g_ie"]
+    z = np.zeros_like
+    pu, _, _ = R.adam_step(u0, gu0, z(gu0), z(gu0), 1)
+    pi, _, _ = R.adam_step(i0, gi0, z(gi0), z(gi0), 1)
+    sd = tr.state_dict()
+    assert rel(sd["user_emb.weight"] - t(u0), pu - u0) <= 1e-4
+    assert rel(sd["item_emb.weight"] - t(i0), pi - i0) <= 1e-4
+    # the final tables of the updated model, by input id
+    pu_f, pi_f = tr.forward()
+    u1 = sd["user_emb.weight"].double().cpu().numpy()
+    i1 = sd["item_emb.weight"].double().cpu().numpy()
+    if variant == "cu_fair":
+        ruf, ritf, _, _ = R.propagate_j(A, Bm, u1, i1, K)
+    else:
+        ruf, ritf, _, _ = R.propagate_gs(A, Bm, u1, i1, K)
+    assert rel(pu_f, ruf) <= TOL and rel(pi_f, ritf) <= TOL
+
+
+def test_default_init_is_the_same_model_in_both_orders():
+    """Default (seeded xavier) tables are drawn by input id, so the ordered and
+    input-order trainers start from the same model: equal final tables by
+    input id up to fp32 summation order, and equal state_dicts bitwise."""
+    from bbgr.trainer import FusedTrainer
+    U, I, d = 2000, 900, 128
+    e = synthetic_edges(U, I, 25000, 8, items="zipf")
+    cred = synthetic_credibility(U, 8)
+    trs = [FusedTrainer(BipartiteGraph(e, U, I, DEV, vertex_order=o), "v2_pop", cred=cred,
+                        emb_dim=d, num_layers=3, batch_size=300) for o in ("input", "degree")]
+    sd = [tr.state_dict() for tr in trs]
+    for k in sd[0]:
+        assert torch.equal(sd[0][k], sd[1][k])
+    f = [tr.forward() for tr in trs]
+    for a, b in zip(f[0], f[1]):
+        assert rel(b, a.double().cpu().numpy()) <= 1e-6
