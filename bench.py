@@ -23,6 +23,12 @@ import os
 import sys
 import time
 
+# More hardware queues than HIP's default 4, so the compute stream, RCCL's stream
+# and the sharded exchange's side streams do not share (and serialise on) one
+# AQL queue. Must be set before the HIP runtime initialises.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 import numpy as np
 import torch
 
@@ -143,6 +149,11 @@ def main():
     ap.add_argument("--vertex-order", default="degree", choices=["degree", "input"],
                     help="number users / items by descending degree inside the graph "
                          "(hot rows cached, cold rows streamed) or keep the input ids")
+    ap.add_argument("--frontier-parts", type=int, default=2,
+                    help="N>1: item-row ranges per frontier (row-list) exchange")
+    ap.add_argument("--dense-check", type=int, default=5,
+                    help="after the timed steps, time this many steps with frontier sparsity "
+                         "off (reported as dense_ms_per_step; 0 = skip)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = every rank owns a full config-sized user shard over the "
                          "shared items; strong = one config graph cut into N user ranges")
@@ -167,7 +178,11 @@ def main():
         os.environ.setdefault("WORLD_SIZE", "1")
         backend = os.environ.get("BBGR_DIST_BACKEND", "nccl")
         if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=dev)
+            # high-priority RCCL stream: its kernels get CUs while the SpMM of the
+            # next item range floods the queue (range_probe: 2.07 -> 1.96 ms / product)
+            opts = torch.distributed.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            torch.distributed.init_process_group("nccl", device_id=dev, pg_options=opts)
         else:
             torch.distributed.init_process_group(backend)
 
@@ -194,7 +209,8 @@ def main():
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} E={E} d={d} K={K} B={B} "
         f"scaling={'weak' if weak else 'strong'} generated in {time.perf_counter() - t0:.1f}s")
 
-    xp = dict(exchange_parts=args.exchange_parts, vertex_order=args.vertex_order)
+    xp = dict(exchange_parts=args.exchange_parts, frontier_parts=args.frontier_parts,
+              vertex_order=args.vertex_order)
     if not dist_mode:
         from bbgr.graph import BipartiteGraph
         from bbgr.trainer import FusedTrainer
@@ -241,6 +257,28 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss)
+    dense_ms = None
+    if not args.dense and args.dense_check > 0:
+        # the same trainer with frontier sparsity off (every product over the
+        # full CSR): what the masks save, reported next to the value
+        trainer.frontier = False
+        trainer.step()
+        if dist_mode:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.dense_check):
+            trainer.step()
+        torch.cuda.synchronize()
+        if dist_mode:
+            torch.distributed.barrier()
+        dense_s = time.perf_counter() - t1
+        if dist_mode:
+            t = torch.tensor([dense_s], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            dense_s = float(t.item())
+        dense_ms = 1000.0 * dense_s / args.dense_check
+        trainer.frontier = True
     summ = timer.summary("full")           # full-CSR launches: the roofline kernel
     summ_m = timer.summary("masked")       # frontier-masked launches (bytes data-dependent)
     summ_a = timer.summary("adam")         # last backward product + fused user Adam
@@ -290,6 +328,9 @@ def main():
                    "parallelism": f"user-rows x{world}"
                                   + (" (sharded trainer)" if dist_mode and world == 1 else "")},
         "bpr_steps_per_s": args.steps / elapsed,
+        "dense_ms_per_step": dense_ms,
+        "dense_note": "same trainer, frontier sparsity off (every SpMM over the full CSR; "
+                      "loss, gradients and updates equal): timed after the main loop",
         "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
         "frontier": {"enabled": not args.dense,
                      "masked_launches_per_step": masked_n / args.steps,

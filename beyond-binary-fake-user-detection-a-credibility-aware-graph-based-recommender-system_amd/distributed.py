@@ -105,8 +105,12 @@ class ItemExchange:
     epilogue finishes them: the payload is |frontier|*d*4 bytes instead of
     I*d*4."""
 
-    def __init__(self, group=None, parts: int = 4):
+    def __init__(self, group=None, parts: int = 4, frontier_parts: int = 2):
         self.group, self.parts = group, max(1, int(parts))
+        # frontier products are short (0.2-0.9 ms at C4) and their payload small:
+        # each extra part costs a launch ramp + a collective call (~30 us) for
+        # little overlap, so they are cut coarser than the dense ones
+        self.frontier_parts = max(1, int(frontier_parts))
         self.balance_indptr = None   # global item indptr: identical cuts on every rank
         self._rows = None            # (device list, host offsets, event) of the step
         self._offs = None
@@ -119,9 +123,10 @@ class ItemExchange:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def ranges(self, csr):
-        """The item CSR's row ranges (global-degree cuts) and their boundary rows."""
+        """The item CSR's frontier row ranges (global-degree cuts) and their
+        boundary rows."""
         if self._ranges is None or self._ranges[0] is not csr:
-            rg = csr.row_ranges(self.parts, self.balance_indptr)
+            rg = csr.row_ranges(self.frontier_parts, self.balance_indptr)
             b = [r[0] for r in rg] + [rg[-1][1]] if rg else [0, 0]
             self._ranges = (csr, rg, torch.tensor(b, dtype=torch.int64, device=csr.device))
         return self._ranges[1], self._ranges[2]
@@ -261,7 +266,8 @@ class ShardedTrainer(FusedTrainer):
                  neg_max_tries: int = 50, lambda_fair: float = 0.0, seed: int = 42,
                  device=None, group=None, u0=None, i0=None, user_offset: int = 0,
                  frontier: bool = True, exchange_parts: int = 4, fuse_adam: bool = True,
-                 sparse_exchange: bool = True, vertex_order: str = "input"):
+                 sparse_exchange: bool = True, vertex_order: str = "input",
+                 frontier_parts: int = 2):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
         this rank's users; i0: the full (replicated) item table; batch_size:
         users per step on THIS rank. vertex_order="degree": local users by
@@ -283,7 +289,7 @@ class ShardedTrainer(FusedTrainer):
         self.lambda_fair, self.seed = lambda_fair, seed
         self.B = self.B_local = max(1, int(batch_size))
         self.B_global = self.B_local * self.world
-        self.exchange = ItemExchange(group, exchange_parts)
+        self.exchange = ItemExchange(group, exchange_parts, frontier_parts)
 
         def global_degrees(deg: torch.Tensor) -> torch.Tensor:
             g = deg.to(torch.int64)
@@ -353,7 +359,8 @@ class ShardedTrainer(FusedTrainer):
         self.sparse_exchange = bool(sparse_exchange) and frontier
         self.item_list = torch.empty(max(num_items, 1), dtype=torch.int64, device=dev)
         self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.item_offs_host = torch.zeros(exchange_parts + 2, dtype=torch.int64).pin_memory()
+        self.item_offs_host = torch.zeros(max(exchange_parts, frontier_parts) + 2,
+                                          dtype=torch.int64).pin_memory()
         self._list_ws = None
 
     @classmethod

@@ -123,6 +123,8 @@ class FusedTrainer:
 
     # -- batching ---------------------------------------------------------------
     def next_users(self) -> torch.Tensor:
+        """The next batch slice of the epoch permutation, as INTERNAL row ids
+        (== input ids unless the graph is degree-ordered; step() takes input ids)."""
         n = self.train_users.numel()
         if self.perm is None or self.cursor >= n:
             self.epoch += 1
