@@ -154,6 +154,9 @@ def main():
     ap.add_argument("--dense-check", type=int, default=5,
                     help="after the timed steps, time this many steps with frontier sparsity "
                          "off (reported as dense_ms_per_step; 0 = skip)")
+    ap.add_argument("--roofline-steps", type=int, default=3,
+                    help="sharded runs: steps after the timed region whose SpMM launches "
+                         "are bracketed by HIP events for the roofline")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = every rank owns a full config-sized user shard over the "
                          "shared items; strong = one config graph cut into N user ranges")
@@ -243,7 +246,15 @@ def main():
     if dist_mode:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    P.set_spmm_timer(timer)
+    # Per-launch HIP events for the roofline. On one GPU they ride inside the
+    # timed steps (cost ~0.1 ms/step). In the sharded step, events recorded
+    # between launches interleave with the collectives' cross-stream waits and
+    # cost 1.4-3 ms/step (tools/_shvar.sh: 19.4-21.1 vs 18.0-18.1 ms at N=1), so
+    # there the events are recorded over `--roofline-steps` extra steps right
+    # after the timed region instead.
+    events_in_loop = not dist_mode
+    if events_in_loop:
+        P.set_spmm_timer(timer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.step()
@@ -252,6 +263,14 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     P.set_spmm_timer(None)
+    timer_steps = args.steps
+    if not events_in_loop:
+        timer_steps = max(1, args.roofline_steps)
+        P.set_spmm_timer(timer)
+        for _ in range(timer_steps):
+            trainer.step()
+        torch.cuda.synchronize()
+        P.set_spmm_timer(None)
     if dist_mode:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -333,18 +352,18 @@ def main():
                       "loss, gradients and updates equal): timed after the main loop",
         "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
         "frontier": {"enabled": not args.dense,
-                     "masked_launches_per_step": masked_n / args.steps,
-                     "masked_ms_per_step": masked_ms / args.steps,
-                     "full_launches_per_step": n_launch / args.steps,
+                     "masked_launches_per_step": masked_n / timer_steps,
+                     "masked_ms_per_step": masked_ms / timer_steps,
+                     "full_launches_per_step": n_launch / timer_steps,
                      "full_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
-                         for r, z, ms in timer.sequence("full", args.steps)],
+                         for r, z, ms in timer.sequence("full", timer_steps)],
                      "adam_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
-                         for r, z, ms in timer.sequence("adam", args.steps)],
+                         for r, z, ms in timer.sequence("adam", timer_steps)],
                      "masked_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
-                         for r, z, ms in timer.sequence("masked", args.steps)],
+                         for r, z, ms in timer.sequence("masked", timer_steps)],
                      "note": "value counts the reference step's 4*K*E edge traversals; "
                              "masked launches skip exact-zero / unread rows"},
         "fused_adam_spmm": adam_info,
@@ -356,6 +375,8 @@ def main():
                      "algorithmic_bytes_per_launch": tot_bytes / max(n_launch, 1),
                      "kernel": "bbgr::spmm_kernel / spmm_pair_kernel (+fixup)", "launches": n_launch,
                      "avg_launch_ms": tot_ms / max(n_launch, 1), "per_operator": per_kernel,
+                     "events": "inside the timed steps" if events_in_loop else
+                               f"{timer_steps} steps after the timed region (sharded step)",
                      "cache_assisted": achieved > HBM_PEAK_GBS,
                      "note": "achieved = gather-model bytes (zero reuse) / launch time; above "
                              "peak only because hot rows are served from L2 / Infinity Cache "

@@ -83,7 +83,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_ld", c_int64), ("adam_lr", c_float), ("adam_beta1", c_float),
         ("adam_beta2", c_float), ("adam_eps", c_float), ("adam_weight_decay", c_float),
         ("adam_bias_correction1", c_float), ("adam_bias_correction2_sqrt", c_float),
-        ("stream_from", c_int32),
+        ("stream_from", c_int32), ("stream_out_from", c_int32),
     ]
 
 

@@ -63,6 +63,7 @@ struct SpmmParams {
   int pair_rows;               // two short rows per 16-lane group (gather_pair)
   int chunk_begin;             // first long-row chunk of this launch
   int nt_from;                 // source rows >= nt_from: streaming loads (args.stream_from)
+  int nt_out_from;             // output rows >= nt_out_from: streaming stores (args.stream_out_from)
   // fused Adam on the y-row value (bbgr_spmm_args.adam_*)
   float *adam_p, *adam_m, *adam_v;
   long adam_ld;
@@ -77,6 +78,14 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld_nt(const float4 *p) {   // streaming (nt) load
   const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
   return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float4 *p, float4 v) {   // streaming (nt) store
+  f4v w;
+  w.x = v.x;
+  w.y = v.y;
+  w.z = v.z;
+  w.w = v.w;
+  __builtin_nontemporal_store(w, reinterpret_cast<f4v *>(p));
 }
 __device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -318,14 +327,23 @@ __device__ __forceinline__ void adam_row(const SpmmParams &P, int row, int lane,
   float4 *pv = reinterpret_cast<float4 *>(P.adam_v + (long)row * P.adam_ld) + lane;
 #pragma unroll
   for (int k = 0; k < V; ++k) {
-    float4 p4 = pp[16 * k], m4 = pm[16 * k], v4 = pv[16 * k];
+    const bool ntm = P.nt_out_from != 0x7fffffff;   // moments: streamed once per step
+    float4 p4 = pp[16 * k];
+    float4 m4 = ntm ? ld_nt(pm + 16 * k) : pm[16 * k];
+    float4 v4 = ntm ? ld_nt(pv + 16 * k) : pv[16 * k];
     adam_elem(p4.x, G[k].x, m4.x, v4.x, P.adam);
     adam_elem(p4.y, G[k].y, m4.y, v4.y, P.adam);
     adam_elem(p4.z, G[k].z, m4.z, v4.z, P.adam);
     adam_elem(p4.w, G[k].w, m4.w, v4.w, P.adam);
-    pp[16 * k] = p4;
-    pm[16 * k] = m4;
-    pv[16 * k] = v4;
+    if (row >= P.nt_out_from) st_nt(pp + 16 * k, p4);
+    else pp[16 * k] = p4;
+    if (ntm) {
+      st_nt(pm + 16 * k, m4);
+      st_nt(pv + 16 * k, v4);
+    } else {
+      pm[16 * k] = m4;
+      pv[16 * k] = v4;
+    }
   }
 }
 
@@ -348,8 +366,13 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
     }
     if (P.y) {
       float4 *dst = reinterpret_cast<float4 *>(P.y + (long)row * P.ldy) + lane;
+      if (row >= P.nt_out_from) {
 #pragma unroll
-      for (int k = 0; k < V; ++k) dst[16 * k] = G[k];
+        for (int k = 0; k < V; ++k) st_nt(dst + 16 * k, G[k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k) dst[16 * k] = G[k];
+      }
     }
     if (P.adam_p) adam_row<D>(P, row, lane, G);
   }
@@ -671,6 +694,7 @@ extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
   BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_epilogue: negative n_row_list");
   SpmmParams P = {};
   P.n_rows = n_rows;
+  P.nt_from = P.nt_out_from = 0x7fffffff;
   fill_epilogue(P, a);
   P.row_mask = a->row_mask;
   P.row_list = (const long *)a->row_list;
@@ -760,6 +784,7 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_spmm: negative n_row_list");
   P.pair_rows = pair_rows(csr);
   P.nt_from = a->stream_from > 0 ? a->stream_from : 0x7fffffff;
+  P.nt_out_from = a->stream_out_from > 0 ? a->stream_out_from : 0x7fffffff;
   hipStream_t st = as_stream(stream);
   switch (d) {
     case 64: return dispatch_wmode<64>(P, a->weight_mode, n_split, st);

@@ -172,6 +172,14 @@ class Csr:
             return 0
         return max(1, min(self.n_cols // 8, HOT_BYTES // (4 * d)))
 
+    def stream_out_from(self, d: int) -> int:
+        """bbgr_spmm_args.stream_out_from for d-wide output rows: 0 unless the
+        rows are in descending-degree order; then the hot prefix of the output
+        table (the next product gathers it)."""
+        if not self.__dict__.get("rows_by_degree", False):
+            return 0
+        return max(1, min(self.n_rows // 8, HOT_BYTES // (4 * d)))
+
     def partial_workspace(self, d: int) -> torch.Tensor | None:
         if self.n_split == 0:
             return None
@@ -298,8 +306,8 @@ class BipartiteGraph:
         self.item_csr = Csr(i, u, num_items, num_users, device,
                             long_threshold=long_threshold, chunk_edges=chunk_edges)
         ordered = vertex_order == "degree"
-        self.user_csr.cols_by_degree = ordered   # gathers item rows
-        self.item_csr.cols_by_degree = ordered   # gathers user rows
+        for c in (self.user_csr, self.item_csr):
+            c.cols_by_degree = c.rows_by_degree = ordered
         self._scales: dict = {}
 
     def scales(self, kind: int, cred: torch.Tensor | None = None) -> Scales:

@@ -196,6 +196,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     if adam is not None:
         adam.fill(a)
     a.stream_from = prod.csr.stream_from(d)
+    a.stream_out_from = prod.csr.stream_out_from(d)
     if _timer is None:
         call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
         return

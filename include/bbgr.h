@@ -209,6 +209,10 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   from L2 / Infinity Cache. Meant for a source table in descending-degree  */
 /*   order (bbgr_degree_order), where rows [0, stream_from) are the hot set.  */
 /*   Results are unchanged; 0 = every row loaded with the default policy.     */
+/* stream_out_from > 0: output rows >= stream_out_from are stored streaming   */
+/*   (y, and the fused-Adam parameter row), and the fused Adam's moments are  */
+/*   streamed in and out: the next product gathers this table, and only its  */
+/*   hot prefix (output table in degree order) is worth keeping cached.       */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -254,6 +258,7 @@ typedef struct {
   float adam_bias_correction1;
   float adam_bias_correction2_sqrt;
   int32_t stream_from;
+  int32_t stream_out_from;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,

@@ -75,8 +75,9 @@ def test_ordered_graph_csrs_are_the_relabelled_graph():
 @pytest.mark.parametrize("d", [64, 128, 256])
 @pytest.mark.parametrize("side", ["item_rows", "user_rows"])
 def test_stream_from_loads_leave_results_bitwise_equal(d, side):
-    """stream_from only changes the cache policy of the gathers: every output
-    bit is equal (one-row and two-row kernels, split rows, masks)."""
+    """stream_from / stream_out_from only change the cache policy of the
+    gathers and stores: every output bit is equal (one-row and two-row kernels,
+    split rows, masks, the fused Adam epilogue)."""
     from bbgr.propagate import Product, spmm
     U, I = 3000, 700
     e = synthetic_edges(U, I, 30000, 11, items="zipf")
@@ -85,15 +86,19 @@ def test_stream_from_loads_leave_results_bitwise_equal(d, side):
     prod = Product(c, None, None, None, {})
     x = torch.randn(nc, d, device=DEV)
     mask = (torch.rand(nc, device=DEV) < 0.3).to(torch.uint8)
+    from bbgr.optim import AdamRows
     outs = []
+    p0 = torch.randn(nr, d, device=DEV)
     for ordered in (False, True):
-        c.cols_by_degree = ordered
-        assert (c.stream_from(d) > 0) == ordered
+        c.cols_by_degree = c.rows_by_degree = ordered
+        assert (c.stream_from(d) > 0) == ordered and (c.stream_out_from(d) > 0) == ordered
         y, acc = torch.empty(nr, d, device=DEV), torch.empty(nr, d, device=DEV)
         ym = torch.zeros(nr, d, device=DEV)
         spmm(prod, x, False, y=y, acc_in=x[:nr] if nr <= nc else None, acc_out=acc)
         spmm(prod, x, False, y=ym, src_mask=mask)
-        outs.append((y, acc, ym))
+        p, m, v = p0.clone(), torch.full_like(p0, 0.01), torch.full_like(p0, 0.02)
+        spmm(prod, x, False, adam=AdamRows(p, m, v, 3, 1e-3))    # fused Adam epilogue
+        outs.append((y, acc, ym, p, m, v))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
 
