@@ -10,8 +10,9 @@ two weighted ``index_add_`` aggregations (Eq. 3.13-3.16) — runs as:
 
 * one destination-row CSR and one source-row CSR per subgraph direction,
   built on the device (``bbgr_csr_build``, with the edge permutation);
-* ``bbgr_ewa_normalize``: raw weights, fixed-order per-destination sums and
-  the normalised weights in CSR and input order, one launch;
+* ``bbgr_ewa_normalize``: raw weights (one gather into CSR order),
+  fixed-order per-destination sums and the normalised weights in CSR and
+  input order (coalesced passes);
 * the aggregation = ``bbgr_spmm`` over the destination CSR with the
   normalised weights as edge values; its gradient w.r.t. the source features
   = ``bbgr_spmm`` over the source CSR (the transpose). No atomics: the
@@ -52,6 +53,9 @@ class EdgeSet:
         src, dst = ei[0].to(device), ei[1].to(device)
         self.by_dst = Csr(dst, src, num_dst, num_src, device, keep_perm=True)
         self.by_src = Csr(src, dst, num_src, num_dst, device, keep_perm=True)
+        # each edge's destination row (input order): w~ in input order is then
+        # one coalesced pass instead of a scatter through the CSR permutation
+        self.dst = dst.to(torch.int32).contiguous()
         self.device = device
 
     def normalize(self, w: torch.Tensor | None = None, edge_attr: torch.Tensor | None = None,
@@ -74,7 +78,7 @@ class EdgeSet:
                 attr = edge_attr.detach().to(**f32).contiguous()
                 lda = attr.shape[1]
             cs = self.by_dst.struct()
-            args = (ctypes.byref(cs), ptr(self.by_dst.perm), ptr(w_in), ptr(attr), lda,
+            args = (ctypes.byref(cs), ptr(self.by_dst.perm), ptr(self.dst), ptr(w_in), ptr(attr), lda,
                     col_verified, col_align, float(beta), float(gamma), float(eps), ptr(w_raw),
                     ptr(w_edge), ptr(w_csr))
             n = ctypes.c_size_t(0)

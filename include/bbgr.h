@@ -384,10 +384,14 @@ int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float *src, int64
 /* (each nullable): w_raw and w_edge in input-edge order, w_csr in CSR order */
 /* (the edge values of the aggregation SpMM, CredModel.aggregate = bbgr_spmm */
 /* over this CSR). The csr must carry its load-balance plan; per-row sums    */
-/* follow it in a fixed order (bitwise deterministic). Workspace: per-row    */
-/* sums + chunk partials (+ raw weights when w_in and w_raw are both NULL).  */
+/* follow it in a fixed order (bitwise deterministic). dst (nullable, input  */
+/* order): each edge's destination row; with it w_edge is written by one     */
+/* coalesced pass over the edges instead of a scatter through perm.          */
+/* Workspace: raw weights in CSR order, per-row sums, chunk partials (+ raw  */
+/* weights in input order when w_in and w_raw are both NULL).                */
 /* ------------------------------------------------------------------------- */
-int bbgr_ewa_normalize(const bbgr_csr *csr, const int32_t *perm, const float *w_in,
+int bbgr_ewa_normalize(const bbgr_csr *csr, const int32_t *perm, const int32_t *dst,
+                       const float *w_in,
                        const float *edge_attr, int64_t lda, int32_t col_verified,
                        int32_t col_align, float beta, float gamma, float eps,
                        float *w_raw, float *w_edge, float *w_csr, void *workspace,

@@ -105,3 +105,34 @@ def test_cred_model_forward_backward_vs_torch_reference(hidden):
     loss_of(outs_d, y.to(DEV)).backward()
     for (n, p_r), (_, p_d) in zip(ref.named_parameters(), dev.named_parameters()):
         _close(p_d.grad, p_r.grad.numpy(), f"grad {n}", 1e-4)
+
+
+@pytest.mark.parametrize("given_w", [False, True])
+def test_normalize_with_and_without_dst_is_bitwise_equal(given_w):
+    """bbgr_ewa_normalize writes w~ in input order either by a coalesced pass
+    over the edges (dst given, what EdgeSet does) or by the scatter through the
+    CSR permutation (dst NULL): the same values, bit for bit."""
+    import ctypes
+    from bbgr._lib import call, ptr, stream_handle
+    from bbgr.cred_gnn import EdgeSet
+    nu, ni = 700, 300
+    ei, ea = _subgraph(nu, ni, 12000, 5)
+    es = EdgeSet(torch.tensor(ei, device=DEV), nu, ni)
+    E = es.E
+    attr = torch.tensor(ea, device=DEV)
+    w_in = torch.rand(E, device=DEV) if given_w else None
+    outs = []
+    for dst in (es.dst, None):
+        w_raw, w_edge, w_csr = (torch.full((E,), -1.0, device=DEV) for _ in range(3))
+        cs = es.by_dst.struct()
+        args = (ctypes.byref(cs), ptr(es.by_dst.perm), ptr(dst), ptr(w_in),
+                ptr(None if given_w else attr), 0 if given_w else attr.shape[1], 0, 1, 1.0, 1.0,
+                1e-12, ptr(None if given_w else w_raw), ptr(w_edge), ptr(w_csr))
+        n = ctypes.c_size_t(0)
+        call("bbgr_ewa_normalize", *args, None, ctypes.byref(n), stream_handle())
+        ws = torch.empty(max(n.value, 1), dtype=torch.uint8, device=DEV)
+        call("bbgr_ewa_normalize", *args, ptr(ws), ctypes.byref(n), stream_handle())
+        outs.append((w_edge, w_csr))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    raw = w_in.cpu().numpy() if given_w else R.ewa_raw(ea)
+    _close(outs[0][0], R.normalize_per_dst(raw, ei[1], ni), "w_tilde", 1e-6)

@@ -175,3 +175,29 @@ def test_default_init_is_the_same_model_in_both_orders():
     f = [tr.forward() for tr in trs]
     for a, b in zip(f[0], f[1]):
         assert rel(b, a.double().cpu().numpy()) <= 1e-6
+
+
+def test_ordered_graph_edge_cases():
+    """No edges (identity order, empty CSRs) and isolated rows (numbered last,
+    stable by id; their rows survive the state_dict round trip)."""
+    from bbgr.trainer import FusedTrainer
+    g = BipartiteGraph(np.zeros((2, 0), np.int32), 5, 4, DEV, vertex_order="degree")
+    assert g.user_csr.nnz == 0 and g.user_csr.indptr.cpu().tolist() == [0] * 6
+    np.testing.assert_array_equal(g.user_order.perm.cpu().numpy(), np.arange(5))
+    with pytest.raises(RuntimeError):
+        FusedTrainer(g, "v2_pop", emb_dim=64, num_layers=2, batch_size=4)
+    U, I = 300, 200
+    e = synthetic_edges(U - 40, I - 30, 3000, 2, items="zipf")   # users >= 260, items >= 170 isolated
+    g = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
+    rank_u = g.user_order.rank.cpu().numpy()
+    assert (np.sort(rank_u[U - 40:]) >= U - 40).all() and (np.diff(rank_u[U - 40:]) > 0).all()
+    rng = np.random.default_rng(0)
+    u0 = rng.normal(size=(U, 64)).astype(np.float32)
+    i0 = rng.normal(size=(I, 64)).astype(np.float32)
+    tr = FusedTrainer(g, "cu_message", emb_dim=64, num_layers=2, batch_size=64, u0=u0, i0=i0)
+    sd = tr.state_dict()
+    np.testing.assert_array_equal(sd["user_emb.weight"].cpu().numpy(), u0)
+    np.testing.assert_array_equal(sd["item_emb.weight"].cpu().numpy(), i0)
+    tr.step()
+    sd = tr.state_dict()   # isolated users are never in a batch: untouched by the step
+    np.testing.assert_array_equal(sd["user_emb.weight"][U - 40:].cpu().numpy(), u0[U - 40:])
