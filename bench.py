@@ -249,7 +249,8 @@ def main():
     # Per-launch HIP events for the roofline. On one GPU they ride inside the
     # timed steps (cost ~0.1 ms/step). In the sharded step, events recorded
     # between launches interleave with the collectives' cross-stream waits and
-    # cost 1.4-3 ms/step (tools/_shvar.sh: 19.4-21.1 vs 18.0-18.1 ms at N=1), so
+    # cost 1.4-3 ms/step (15-step runs at N=1: 19.4-21.1 ms with them, 18.0-18.1
+    # without), so
     # there the events are recorded over `--roofline-steps` extra steps right
     # after the timed region instead.
     events_in_loop = not dist_mode
