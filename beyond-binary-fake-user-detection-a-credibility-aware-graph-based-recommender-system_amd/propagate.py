@@ -350,12 +350,15 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
              order: str = ORDER_GS, out_u: torch.Tensor | None = None,
              out_i: torch.Tensor | None = None, ws: dict | None = None,
              grad_i0_dense: bool = True, reduce=None, grad_support=None,
-             adam_u=None, before_last=None):
+             adam_u=None, before_last=None, adam_i=None):
     """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final).
-    GS order only: `adam_u` (optim.AdamRows) fuses the user-table Adam step into
-    the last (user-row) product, which then writes no gradient table (out_u
-    is left untouched); `before_last()` runs just before that product, after
-    every other read of gU (the trainer adds the ego-L2 rows to gU there).
+    `adam_u` (optim.AdamRows) fuses the user-table Adam step into the last
+    (user-row) product, which then writes no gradient table (out_u is left
+    untouched); `before_last()` runs just before the last products, after
+    every other read of gU / gI (the trainer adds the ego-L2 rows there).
+    Jacobi order, K >= 2, no `reduce`: `adam_i` fuses the item-table Adam into
+    the last item-row product the same way (out_i untouched). Jacobi K == 1
+    reads gU / gI as the last products' SOURCE tables: not fusable there.
     `grad_support=(user_mask, item_mask)`: gU is zero outside the flagged users
     and, for GS, the first item product's output is zero outside the flagged
     items (GS: batch items and N(batch users); Jacobi: gI's own support). The
@@ -405,6 +408,10 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
         if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
             torch.mul(gI, gl, out=gi0)
     elif order == ORDER_J:
+        if (adam_u is not None or adam_i is not None) and (K < 2 or before_last is None):
+            raise ValueError("fused Adam in the Jacobi backward needs K >= 2 and before_last")
+        if adam_i is not None and reduce is not None:
+            raise ValueError("fused item Adam needs the complete item sums (no reduce hook)")
         bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
         cur = 0
         for k in range(K, 0, -1):
@@ -422,11 +429,17 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
                               y_scale=pair.feed_bwd_iu, y_scale_s=ys,
                               add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl, src_mask=mi_)
             else:
-                spmm(BU, xu, first, y=gu0, y_scale=BU.out_scale, y_scale_s=ys,
-                     add=gU, add_mask=su, add_scale=None, add_scale_s=gl, src_mask=mu_)
-                _item_product(BI, xi, first, reduce, new, y=gi0, y_scale=BI.out_scale,
-                              y_scale_s=ys, add=gI, add_mask=si, add_scale=None, add_scale_s=gl,
-                              src_mask=mi_)
+                if before_last is not None and adam_u is not None:
+                    before_last()
+                spmm(BU, xu, first, y=None if adam_u is not None else gu0, y_scale=BU.out_scale,
+                     y_scale_s=ys, add=gU, add_mask=su, add_scale=None, add_scale_s=gl,
+                     src_mask=mu_, adam=adam_u)
+                ik = dict(y=None if adam_i is not None else gi0, y_scale=BI.out_scale,
+                          y_scale_s=ys, add=gI, add_mask=si, add_scale=None, add_scale_s=gl,
+                          src_mask=mi_)
+                if adam_i is not None:
+                    ik["adam"] = adam_i
+                _item_product(BI, xi, first, reduce, new, **ik)
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")

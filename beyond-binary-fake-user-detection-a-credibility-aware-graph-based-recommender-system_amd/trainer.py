@@ -119,7 +119,8 @@ class FusedTrainer:
         # sparse BPR gradient table (grad_scale), so neither weight-gradient
         # table is written or re-read. g_u0 / g_i0 are then not materialised;
         # fuse_adam=False keeps them (the gradient-parity tests read them).
-        self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
+        self.fuse_adam = bool(fuse_adam) and (
+            (order == ORDER_GS and num_layers >= 1) or (order == ORDER_J and num_layers >= 2))
 
     # -- batching ---------------------------------------------------------------
     def next_users(self) -> torch.Tensor:
@@ -163,7 +164,9 @@ class FusedTrainer:
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
         alpha = 2.0 * self.reg / B
-        if self.fuse_adam:
+        if self.fuse_adam and self.order == ORDER_J:
+            self._backward_fused_j(users, self.posneg[: 2 * B], masks, alpha)
+        elif self.fuse_adam:
             self._backward_fused(users, self.posneg[: 2 * B], masks, alpha)
         else:
             backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
@@ -213,6 +216,26 @@ class FusedTrainer:
              ld(self.item_w), ptr(self.g_if), ld(self.g_if), self.d, st)
         adam_step(self.item_w, self.g_if, self.m_i, self.v_i, self.step_count, self.lr,
                   grad_scale=gl)
+
+    def _backward_fused_j(self, users, item_rows, masks, alpha: float) -> None:
+        """Jacobi backward (lightgcn_cu.py / lightgcn.py order) with both Adam
+        steps fused into the last products' epilogues; the ego-L2 rows enter
+        through the sparse tables just before them, as in _backward_fused."""
+        st = stream_handle()
+        B = users.numel()
+        a_gl = alpha / (1.0 / (self.K + 1))
+        self.step_count += 1
+        adam_u = AdamRows(self.user_w, self.m_u, self.v_u, self.step_count, self.lr)
+        adam_i = AdamRows(self.item_w, self.m_i, self.v_i, self.step_count, self.lr)
+
+        def before_last():
+            call("bbgr_rows_axpy", B, ptr(users), a_gl, ptr(self.user_w), ld(self.user_w),
+                 ptr(self.g_uf), ld(self.g_uf), self.d, st)
+            call("bbgr_rows_axpy", item_rows.numel(), ptr(item_rows), a_gl, ptr(self.item_w),
+                 ld(self.item_w), ptr(self.g_if), ld(self.g_if), self.d, st)
+
+        backward(self.pair, self.g_uf, self.g_if, self.K, self.order, ws=self.ws,
+                 grad_support=masks, adam_u=adam_u, adam_i=adam_i, before_last=before_last)
 
     def _set_masks(self, users, pos, neg, value: int):
         """mask_u = batch users; mask_i = batch items (+ N(batch users) for GS,

@@ -602,7 +602,8 @@ def test_frontier_step_matches_dense_step(variant):
     assert int(front.mask_u.sum()) == 0 and int(front.mask_i.sum()) == 0
 
 
-@pytest.mark.parametrize("variant,K", [("v2_pop", 3), ("method_a", 2), ("v2_pop", 1)])
+@pytest.mark.parametrize("variant,K", [("v2_pop", 3), ("method_a", 2), ("v2_pop", 1),
+                                       ("cu_fair", 3), ("cu_fair", 2)])
 def test_fused_adam_step_matches_unfused(variant, K):
     """Adam fused into the last backward SpMM (users) and read from the sparse
     BPR table with grad_scale (items) == the separate gradient + Adam path:
@@ -621,7 +622,7 @@ def test_fused_adam_step_matches_unfused(variant, K):
               u0=u0, i0=i0)
     sep = FusedTrainer(g, variant, fuse_adam=False, **kw)
     fus = FusedTrainer(g, variant, fuse_adam=True, **kw)
-    assert fus.fuse_adam and not sep.fuse_adam
+    assert fus.fuse_adam and not sep.fuse_adam   # Jacobi: both Adams fused (K >= 2)
     for step in range(3):
         users = sep.next_users()
         fus.next_users()
