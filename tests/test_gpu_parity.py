@@ -603,7 +603,7 @@ def test_frontier_step_matches_dense_step(variant):
 
 
 @pytest.mark.parametrize("variant,K", [("v2_pop", 3), ("method_a", 2), ("v2_pop", 1),
-                                       ("cu_fair", 3), ("cu_fair", 2)])
+                                       ("cu_fair", 3), ("cu_fair", 2), ("plain", 3)])
 def test_fused_adam_step_matches_unfused(variant, K):
     """Adam fused into the last backward SpMM (users) and read from the sparse
     BPR table with grad_scale (items) == the separate gradient + Adam path:
