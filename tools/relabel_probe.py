@@ -1,9 +1,11 @@
 """Probe: does a degree-ordered vertex numbering speed up the C4 training step?
 
 The synthetic graphs number items (and users) at random, as real id spaces
-are. Relabelling rows by descending degree packs the heavily gathered rows of
-each table into a contiguous address range (fewer pages touched by the hot
-set). The step is permutation-equivariant, so only the time changes.
+are. Relabelling rows by descending degree (here on the host, before the
+graph is built with vertex_order="input") packs the heavily gathered rows of
+each table into one address range. The step is permutation-equivariant, so
+only the time changes. (The streamed-cold-row A/B of DESIGN §3 ran an earlier
+form of this probe with the stream threshold set per run.)
 
     python tools/relabel_probe.py [--steps 10] [--modes none,items,users,both]
 """
@@ -65,7 +67,6 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--modes", default="none,items,users,both")
-    ap.add_argument("--nt", default="1", help="BBGR_NT_FRAC values (cold-row streaming loads)")
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     U, I = cfg["num_users"], cfg["num_items"]
@@ -81,11 +82,8 @@ def main():
             e[0] = nu[e0[0]]
             cred = np.empty_like(cred0)
             cred[nu] = cred0
-        for nt in a.nt.split(";"):
-            os.environ["BBGR_NT_FRAC"] = nt
-            ms, seq = run(e, cfg, cred, a.steps, a.warmup)
-            print(json.dumps({"mode": mode, "nt": nt, "ms_per_step": round(ms, 3), **seq}),
-                  flush=True)
+        ms, seq = run(e, cfg, cred, a.steps, a.warmup)
+        print(json.dumps({"mode": mode, "ms_per_step": round(ms, 3), **seq}), flush=True)
 
 
 if __name__ == "__main__":
