@@ -84,11 +84,14 @@ struct EvalParams {
   int *fail_count;
 };
 
-template <int D>
+// MC: LDS candidate capacity per user (128 covers the reference's 1 + 99;
+// 256 the ABI maximum). The arrays dominate the workgroup's LDS, so the small
+// form fits 6 workgroups per CU instead of 4 (more gathers in flight).
+template <int D, int MC>
 __global__ __launch_bounds__(256) void eval_sampled_kernel(EvalParams P) {
   constexpr int V = D / 64;
-  __shared__ int cand[16][EVAL_MAX_CAND];
-  __shared__ float score[16][EVAL_MAX_CAND];
+  __shared__ int cand[16][MC];
+  __shared__ float score[16][MC];
   __shared__ int rows[16][2][ROW_CACHE];
   const int g = threadIdx.x >> 4;
   const int lane = threadIdx.x & 15;
@@ -141,17 +144,19 @@ __global__ __launch_bounds__(256) void eval_sampled_kernel(EvalParams P) {
   __syncthreads();
   const bool work = active && nte > 0;   // no early return: every thread reaches each barrier
   if (active && !work && lane == 0) P.pos_rank[b] = -1;   // no test items: not evaluated
-  // ---- scores: each lane holds float4 columns of the user row; 4 candidates
-  // in flight per group
+  // ---- scores: each lane holds float4 columns of the user row; CF candidate
+  // rows in flight per group (each score is its own dot product: the batching
+  // does not change any result)
+  constexpr int CF = D == 64 ? 8 : 4;
   float4 fu[V];
   const float4 *pu = reinterpret_cast<const float4 *>(P.uf + u * P.lduf) + lane;
 #pragma unroll
   for (int k = 0; k < V; ++k) fu[k] = work ? pu[16 * k] : make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int c0 = 0; work && c0 < nc; c0 += 4) {
-    int it[4];
-    float4 x[4][V];
+  for (int c0 = 0; work && c0 < nc; c0 += CF) {
+    int it[CF];
+    float4 x[CF][V];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < CF; ++q) {
       it[q] = c0 + q < nc ? cand[g][c0 + q] : -1;
       const float4 *pi =
           reinterpret_cast<const float4 *>(P.itf + (long)(it[q] < 0 ? 0 : it[q]) * P.ldif) + lane;
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(256) void eval_sampled_kernel(EvalParams P) {
         x[q][k] = it[q] >= 0 ? pi[16 * k] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < CF; ++q) {
       float a = 0.f;
 #pragma unroll
       for (int k = 0; k < V; ++k)
@@ -742,10 +747,20 @@ extern "C" int bbgr_eval_sampled(const bbgr_eval_args *a, void *workspace,
     P.fail_count = a->fail_count;
     BBGR_HIP(hipMemsetAsync(a->topk, 0xff, sizeof(int) * (size_t)a->n_users * a->k_max, st));
     const unsigned grid = (unsigned)((a->n_users + 15) / 16);
+    const bool small = 1 + a->n_neg <= 128;
     switch (d) {
-      case 64: hipLaunchKernelGGL(eval_sampled_kernel<64>, dim3(grid), dim3(256), 0, st, P); break;
-      case 128: hipLaunchKernelGGL(eval_sampled_kernel<128>, dim3(grid), dim3(256), 0, st, P); break;
-      default: hipLaunchKernelGGL(eval_sampled_kernel<256>, dim3(grid), dim3(256), 0, st, P); break;
+      case 64:
+        if (small) hipLaunchKernelGGL((eval_sampled_kernel<64, 128>), dim3(grid), dim3(256), 0, st, P);
+        else hipLaunchKernelGGL((eval_sampled_kernel<64, 256>), dim3(grid), dim3(256), 0, st, P);
+        break;
+      case 128:
+        if (small) hipLaunchKernelGGL((eval_sampled_kernel<128, 128>), dim3(grid), dim3(256), 0, st, P);
+        else hipLaunchKernelGGL((eval_sampled_kernel<128, 256>), dim3(grid), dim3(256), 0, st, P);
+        break;
+      default:
+        if (small) hipLaunchKernelGGL((eval_sampled_kernel<256, 128>), dim3(grid), dim3(256), 0, st, P);
+        else hipLaunchKernelGGL((eval_sampled_kernel<256, 256>), dim3(grid), dim3(256), 0, st, P);
+        break;
     }
     BBGR_LAUNCHED("eval_sampled_kernel");
   }
