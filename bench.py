@@ -210,7 +210,7 @@ def main():
         cred = synthetic_credibility(U, seed, args.cred)
         E = edges.shape[1]
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} E={E} d={d} K={K} B={B} "
-        f"scaling={'weak' if weak else 'strong'} generated in {time.perf_counter() - t0:.1f}s")
+        f"scaling={args.scaling} generated in {time.perf_counter() - t0:.1f}s")
 
     xp = dict(exchange_parts=args.exchange_parts, frontier_parts=args.frontier_parts,
               vertex_order=args.vertex_order)
