@@ -149,6 +149,9 @@ def main():
     ap.add_argument("--vertex-order", default="degree", choices=["degree", "input"],
                     help="number users / items by descending degree inside the graph "
                          "(hot rows cached, cold rows streamed) or keep the input ids")
+    ap.add_argument("--native-comm", action="store_true",
+                    help="N>1: item all-reduces through the C ABI's own RCCL communicator "
+                         "(bbgr_allreduce_items) instead of torch.distributed")
     ap.add_argument("--frontier-parts", type=int, default=2,
                     help="N>1: item-row ranges per frontier (row-list) exchange")
     ap.add_argument("--dense-check", type=int, default=5,
@@ -214,6 +217,8 @@ def main():
 
     xp = dict(exchange_parts=args.exchange_parts, frontier_parts=args.frontier_parts,
               vertex_order=args.vertex_order)
+    if args.native_comm:
+        xp["native_comm"] = True
     if not dist_mode:
         from bbgr.graph import BipartiteGraph
         from bbgr.trainer import FusedTrainer

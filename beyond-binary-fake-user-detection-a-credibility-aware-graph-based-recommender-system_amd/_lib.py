@@ -148,6 +148,10 @@ _SIGNATURES = {
     "bbgr_adam": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
                    c_float, c_float, c_float, c_float, _P], c_int32),
     "bbgr_mark_rows": ([c_int64, _P, ctypes.c_uint8, _P, _P], c_int32),
+    "bbgr_comm_unique_id": ([_P], c_int32),
+    "bbgr_comm_init": ([_P, c_int32, c_int32, _P], c_int32),
+    "bbgr_comm_destroy": ([_P], c_int32),
+    "bbgr_allreduce_items": ([_P, _P, c_int64, _P], c_int32),
     "bbgr_ewa_normalize": ([ctypes.POINTER(CsrStruct), _P, _P, _P, _P, c_int64, c_int32, c_int32,
                             c_float, c_float, c_float, _P, _P, _P, _P,
                             ctypes.POINTER(c_size_t), _P], c_int32),

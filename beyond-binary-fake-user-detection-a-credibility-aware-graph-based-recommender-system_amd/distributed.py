@@ -89,6 +89,46 @@ def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
     out.copy_(torch.cat(parts))
 
 
+class RcclItemComm:
+    """The item exchange through the C ABI's own RCCL communicator
+    (bbgr_comm_init / bbgr_allreduce_items) instead of torch.distributed's
+    collective machinery. The unique id travels once over `group`; each
+    all-reduce is enqueued on a high-priority comm stream behind the compute
+    stream's work so far, and wait() makes the compute stream wait for all of
+    them."""
+
+    def __init__(self, group=None, device=None):
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        ids = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            call("bbgr_comm_unique_id", ids)
+        t = torch.tensor(list(ids), dtype=torch.uint8)
+        if dist.get_backend(group) == "nccl":
+            t = t.to(device)
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast(t, src=src, group=group)
+        ids = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+        self.comm = ctypes.c_void_p()
+        call("bbgr_comm_init", ctypes.byref(self.comm), world, rank, ids)
+        self.stream = torch.cuda.Stream(device=device, priority=-1)
+        self.pending = False
+
+    def allreduce_async(self, t: torch.Tensor) -> None:
+        self.stream.wait_stream(torch.cuda.current_stream(t.device))
+        call("bbgr_allreduce_items", self.comm, ptr(t), t.numel(), self.stream.cuda_stream)
+        self.pending = True
+
+    def wait(self) -> None:
+        if self.pending:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+            self.pending = False
+
+    def close(self) -> None:
+        if self.comm:
+            call("bbgr_comm_destroy", self.comm)
+            self.comm = ctypes.c_void_p()
+
+
 class ItemExchange:
     """The per-layer exchange of item partial sums (propagate's `reduce` hook).
 
@@ -118,6 +158,20 @@ class ItemExchange:
         self._ranges = None          # (csr, ranges, device boundary rows)
         self._ratios = {}            # acc_scale / y_scale vectors (linear exchange)
         self.rank = dist.get_rank(group)
+        self.native: RcclItemComm | None = None   # set: bbgr_allreduce_items instead
+
+    def _allreduce_async(self, t: torch.Tensor, works: list) -> None:
+        if self.native is not None:
+            self.native.allreduce_async(t)
+        else:
+            works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group,
+                                         async_op=True))
+
+    def _wait(self, works: list) -> None:
+        for w in works:
+            w.wait()
+        if self.native is not None:
+            self.native.wait()
 
     def __call__(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
@@ -187,10 +241,8 @@ class ItemExchange:
                      row_list=part, rng=rg)
                 call("bbgr_rows_gather", b - a, ptr(part), ptr(t), ld(t), ptr(c[a:b]),
                      ld(c), d, stream_handle())
-                works.append(dist.all_reduce(c[a:b], op=dist.ReduceOp.SUM,
-                                             group=self.group, async_op=True))
-            for w in works:
-                w.wait()
+                self._allreduce_async(c[a:b], works)
+            self._wait(works)
             epilogue(c, row_list=lst[:n], n_rows=prod.csr.n_rows, **kw)
             return
         y = kw.get("y")
@@ -200,10 +252,8 @@ class ItemExchange:
             return
         for rg in self._dense_order(prod.csr):
             spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, rng=rg)
-            works.append(dist.all_reduce(t[rg[0]:rg[1]], op=dist.ReduceOp.SUM,
-                                         group=self.group, async_op=True))
-        for w in works:
-            w.wait()
+            self._allreduce_async(t[rg[0]:rg[1]], works)
+        self._wait(works)
         epilogue(t, row_mask=row_mask, **kw)
 
     def _dense_order(self, csr):
@@ -231,10 +281,8 @@ class ItemExchange:
         works = []
         for rg in self._dense_order(prod.csr):
             spmm(prod, x, first, src_mask=src_mask, rng=rg, **sk)
-            works.append(dist.all_reduce(y[rg[0]:rg[1]], op=dist.ReduceOp.SUM,
-                                         group=self.group, async_op=True))
-        for w in works:
-            w.wait()
+            self._allreduce_async(y[rg[0]:rg[1]], works)
+        self._wait(works)
         if kw.get("acc_out") is not None:
             ratio, ratio_s = self._acc_ratio(kw.get("acc_scale"), ys, ys_s)
             epilogue(y, acc_in=kw.get("acc_in"), acc_out=kw["acc_out"], acc_scale=ratio,
@@ -276,7 +324,7 @@ class ShardedTrainer(FusedTrainer):
                  device=None, group=None, u0=None, i0=None, user_offset: int = 0,
                  frontier: bool = True, exchange_parts: int = 4, fuse_adam: bool = True,
                  sparse_exchange: bool = True, vertex_order: str = "input",
-                 frontier_parts: int = 2):
+                 frontier_parts: int = 2, native_comm: bool = False):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
         this rank's users; i0: the full (replicated) item table; batch_size:
         users per step on THIS rank. vertex_order="degree": local users by
@@ -299,6 +347,8 @@ class ShardedTrainer(FusedTrainer):
         self.B = self.B_local = max(1, int(batch_size))
         self.B_global = self.B_local * self.world
         self.exchange = ItemExchange(group, exchange_parts, frontier_parts)
+        if native_comm:   # item all-reduces through bbgr_allreduce_items (own RCCL comm)
+            self.exchange.native = RcclItemComm(group, dev)
 
         def global_degrees(deg: torch.Tensor) -> torch.Tensor:
             g = deg.to(torch.int64)

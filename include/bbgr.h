@@ -407,6 +407,21 @@ int bbgr_mark_neighbors(int64_t n, const int64_t *rows, const int32_t *indptr,
                         bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
+/* Item exchange over RCCL (the sharded step's per-layer all-reduce of item   */
+/* partial sums) for callers without torch.distributed.        */
+/* RCCL is resolved at run time (librccl.so.1: the copy already loaded in the */
+/* process, else the library path). The communicator is an ncclComm_t.       */
+/* ------------------------------------------------------------------------- */
+/* id_out: 128 bytes (ncclUniqueId) to hand to every rank (rank 0 creates).  */
+int bbgr_comm_unique_id(uint8_t *id_out);
+/* Collective over nranks processes (blocks until all have joined); the      */
+/* calling thread's current HIP device is the rank's GPU.                    */
+int bbgr_comm_init(void **comm_out, int32_t nranks, int32_t rank, const uint8_t *id);
+int bbgr_comm_destroy(void *comm);
+/* In-place sum over the ranks of items[count] (fp32), stream-ordered.       */
+int bbgr_allreduce_items(void *comm, float *items, int64_t count, bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
 /* Negative / positive sampling                                               */
 /*   Replaces the per-user host loop of Version-2/lighgcn_cu_pop.py:835-849:  */
 /*   sample_pos_item (:339-343), sample_neg_item_popmix (:349-376),           */

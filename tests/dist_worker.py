@@ -112,8 +112,10 @@ def rccl_single_rank(out_dir, variant, order="input"):
     sh = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
                         vertex_order=order, **kw)
     one = FusedTrainer(BipartiteGraph(e, U, I, "cuda:0", vertex_order=order), variant, **kw)
+    nat = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
+                         vertex_order=order, native_comm=True, **kw)   # bbgr_allreduce_items
     out = {}
-    for tag, tr in (("sharded", sh), ("single", one)):
+    for tag, tr in (("sharded", sh), ("single", one), ("native", nat)):
         out[f"{tag}_loss"] = np.array([float(tr.step()) for _ in range(3)])
         out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
         out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()

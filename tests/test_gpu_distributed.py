@@ -144,3 +144,6 @@ def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, 
         a, b = z[f"sharded_{key}"], z[f"single_{key}"]
         err = np.linalg.norm(a - b) / np.linalg.norm(b)
         assert err < 1e-6, (key, err)
+        # the C ABI's own RCCL communicator (bbgr_allreduce_items) == torch's
+        np.testing.assert_array_equal(z[f"native_{key}"], z[f"sharded_{key}"])
+    np.testing.assert_array_equal(z["native_loss"], z["sharded_loss"])
