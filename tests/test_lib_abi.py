@@ -59,6 +59,20 @@ def test_invalid_arguments_rejected_without_gpu():
         _lib.call("bbgr_bpr_reduce", 0, None, 0.0, 0.0, None, None)
 
 
+def test_comm_entry_points_validate_without_gpu():
+    """The RCCL exchange ABI rejects bad handles / sizes before touching RCCL;
+    destroying a null communicator is a no-op."""
+    L = _lib.lib()
+    assert L.bbgr_allreduce_items(None, None, 16, None) == -1
+    assert L.bbgr_allreduce_items(ctypes.c_void_p(16), None, 16, None) == -1
+    assert L.bbgr_comm_init(None, 2, 0, None) == -1
+    ids = (ctypes.c_uint8 * 128)()
+    comm = ctypes.c_void_p()
+    assert L.bbgr_comm_init(ctypes.byref(comm), 2, 2, ids) == -1    # rank >= nranks
+    assert L.bbgr_comm_unique_id(None) == -1
+    assert L.bbgr_comm_destroy(None) == 0
+
+
 def test_gpu_required_is_loud():
     import torch
     if torch.cuda.is_available():
