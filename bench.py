@@ -304,7 +304,9 @@ def main():
             dense_s = float(t.item())
         dense_ms = 1000.0 * dense_s / args.dense_check
         trainer.frontier = True
-    summ = timer.summary("full")           # full-CSR launches: the roofline kernel
+    if dist_mode:
+        trainer.close()                    # the native exchange's communicator, if any
+    summ = timer.summary("full")          # full-CSR launches: the roofline kernel
     summ_m = timer.summary("masked")       # frontier-masked launches (bytes data-dependent)
     summ_a = timer.summary("adam")         # last backward product + fused user Adam
     tot_bytes = sum(n * spmm_bytes(nnz, rows, dd) for (rows, nnz, dd), (n, ms) in summ.items())

@@ -115,6 +115,7 @@ class RcclItemComm:
 
     def allreduce_async(self, t: torch.Tensor) -> None:
         self.stream.wait_stream(torch.cuda.current_stream(t.device))
+        t.record_stream(self.stream)   # the allocator must not reuse t before the sum lands
         call("bbgr_allreduce_items", self.comm, ptr(t), t.numel(), self.stream.cuda_stream)
         self.pending = True
 
@@ -446,6 +447,14 @@ class ShardedTrainer(FusedTrainer):
                  seed=seed, user_offset=lo, **kw)
         tr.bounds = bounds
         return tr
+
+    def close(self) -> None:
+        """Destroy the exchange's own RCCL communicator (native_comm), if any;
+        collective: every rank calls it before the process group goes."""
+        if self.exchange.native is not None:
+            torch.cuda.synchronize(self.device)
+            self.exchange.native.close()
+            self.exchange.native = None
 
     # -- batching ------------------------------------------------------------
     def next_users(self) -> torch.Tensor:

@@ -122,6 +122,7 @@ def rccl_single_rank(out_dir, variant, order="input"):
         out[f"{tag}_m_u"] = tr.m_u.cpu().numpy()
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, "rccl1.npz"), **out)
+    nat.close()   # bbgr_comm_destroy
     dist.destroy_process_group()
 
 
