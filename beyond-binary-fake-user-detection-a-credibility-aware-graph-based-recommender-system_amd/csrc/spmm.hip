@@ -114,10 +114,10 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 #define BBGR_PAIR_U_MASKED 4
 #endif
 #ifndef BBGR_PAIR_WAVES
-#define BBGR_PAIR_WAVES 8
+#define BBGR_PAIR_WAVES 0
 #endif
 #ifndef BBGR_PAIR_WAVES_MASKED
-#define BBGR_PAIR_WAVES_MASKED 8
+#define BBGR_PAIR_WAVES_MASKED 0
 #endif
 // d = 128
 #ifndef BBGR_ROW_U128
