@@ -147,7 +147,7 @@ _SIGNATURES = {
     "bbgr_bpr_reduce": ([c_int64, _P, c_float, c_float, _P, _P], c_int32),
     "bbgr_adam": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
                    c_float, c_float, c_float, c_float, _P], c_int32),
-    "bbgr_mark_rows": ([c_int64, _P, ctypes.c_uint8, _P, _P], c_int32),
+    "bbgr_mark_rows": ([c_int64, _P, ctypes.c_uint8, _P, c_int64, _P], c_int32),
     "bbgr_comm_unique_id": ([_P], c_int32),
     "bbgr_comm_init": ([_P, c_int32, c_int32, _P], c_int32),
     "bbgr_comm_destroy": ([_P], c_int32),
@@ -199,7 +199,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 1:
+        if handle.bbgr_abi_version() != 2:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

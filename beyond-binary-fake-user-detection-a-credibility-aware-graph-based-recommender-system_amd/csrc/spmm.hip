@@ -782,6 +782,11 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
     n_split = r[5] - r[4];
   }
   BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_spmm: negative n_row_list");
+  // chunk workgroups of a list launch compute only rows flagged in row_mask
+  // (and the fix-up sums only those): without the mask, long listed rows
+  // would be skipped and the fix-up would sum stale partials
+  BBGR_REQUIRE(!a->row_list || a->row_mask || csr->n_chunks == 0,
+               "bbgr_spmm: row_list needs row_mask when the plan has long-row chunks");
   P.pair_rows = pair_rows(csr);
   P.nt_from = a->stream_from > 0 ? a->stream_from : 0x7fffffff;
   P.nt_out_from = a->stream_out_from > 0 ? a->stream_out_from : 0x7fffffff;

@@ -232,9 +232,11 @@ __global__ void rows_zero_kernel(long n, const long *idx, float *t, long ld,
 }
 
 __global__ void mark_rows_kernel(long n, const long *idx, unsigned char v,
-                                 unsigned char *mask) {
+                                 unsigned char *mask, long n_rows) {
   const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n && idx[k] >= 0) mask[idx[k]] = v;   // -1 = sampler "no item"
+  if (k >= n) return;
+  const long r = idx[k];
+  if (r >= 0 && r < n_rows) mask[r] = v;   // -1 = sampler "no item"; out of range: skipped
 }
 
 // one 16-lane group per listed row; duplicate writes store the same value
@@ -483,12 +485,12 @@ extern "C" int bbgr_rows_zero(int64_t n, const int64_t *idx, float *table,
 }
 
 extern "C" int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value,
-                              uint8_t *mask, bbgr_stream_t stream) {
-  BBGR_REQUIRE(n >= 0, "bbgr_mark_rows: negative n");
+                              uint8_t *mask, int64_t n_rows, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n_rows >= 0, "bbgr_mark_rows: negative n / n_rows");
   if (n == 0) return BBGR_OK;
   BBGR_REQUIRE(idx && mask, "bbgr_mark_rows: null arrays");
   hipLaunchKernelGGL(mark_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), (long)n, (const long *)idx, value, mask);
+                     as_stream(stream), (long)n, (const long *)idx, value, mask, (long)n_rows);
   BBGR_LAUNCHED("mark_rows_kernel");
   return BBGR_OK;
 }

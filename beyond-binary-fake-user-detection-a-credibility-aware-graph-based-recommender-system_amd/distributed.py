@@ -295,12 +295,15 @@ class ItemExchange:
         """acc_scale / ys per row (0 where ys == 0: such rows have T == 0)."""
         if ys is None:
             return acc_scale, 1.0 / ys_s
-        key = (None if acc_scale is None else acc_scale.data_ptr(), ys.data_ptr(), ys.numel())
-        r = self._ratios.get(key)
-        if r is None:
-            num = torch.ones_like(ys) if acc_scale is None else acc_scale
-            r = torch.where(ys != 0, num / ys, torch.zeros_like(ys)).contiguous()
-            self._ratios[key] = r
+        # keyed on the scale tensors themselves (held by the entry), so a freed
+        # vector whose address is reused by a different one never matches
+        key = (id(acc_scale), id(ys))
+        hit = self._ratios.get(key)
+        if hit is not None and hit[0] is acc_scale and hit[1] is ys:
+            return hit[2], 1.0 / ys_s
+        num = torch.ones_like(ys) if acc_scale is None else acc_scale
+        r = torch.where(ys != 0, num / ys, torch.zeros_like(ys)).contiguous()
+        self._ratios[key] = (acc_scale, ys, r)
         return r, 1.0 / ys_s
 
 
@@ -345,8 +348,6 @@ class ShardedTrainer(FusedTrainer):
         self.lo, self.hi = user_offset, user_offset + num_local_users
         self.order, self.lr, self.reg = order, lr, reg
         self.lambda_fair, self.seed = lambda_fair, seed
-        self.B = self.B_local = max(1, int(batch_size))
-        self.B_global = self.B_local * self.world
         self.exchange = ItemExchange(group, exchange_parts, frontier_parts)
         if native_comm:   # item all-reduces through bbgr_allreduce_items (own RCCL comm)
             self.exchange.native = RcclItemComm(group, dev)
@@ -381,6 +382,20 @@ class ShardedTrainer(FusedTrainer):
             raise ValueError("initial tables have the wrong shape")
         self.user_w = _internal_rows(self.graph.user_order, self.user_w)
         self.item_w = _internal_rows(self.graph.item_order, self.item_w)
+        self.train_users = nonempty_rows(self.graph.user_csr)
+        if self.train_users.numel() == 0:
+            raise RuntimeError(f"rank {self.rank}: no train users in its shard")
+        # Every rank takes the same number of users per step (the all-gathers of
+        # the batch's item rows need equal shapes), and no batch may hold a user
+        # twice (the last forward user product updates acc rows in place from a
+        # row list): B_local is capped at the smallest shard's train-user count,
+        # as the reference's slice perm[start:start+B] caps a batch at the
+        # number of train users (Version-2:826-827).
+        n_min = torch.tensor([self.train_users.numel()], dtype=torch.int64,
+                             device=dev if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(n_min, op=dist.ReduceOp.MIN, group=group)
+        self.B = self.B_local = max(1, min(int(batch_size), int(n_min.item())))
+        self.B_global = self.B_local * self.world
         z = lambda n: torch.zeros(n, emb_dim, **f32)  # noqa: E731
         self.m_u, self.v_u = z(num_local_users), z(num_local_users)
         self.m_i, self.v_i = z(num_items), z(num_items)
@@ -403,9 +418,6 @@ class ShardedTrainer(FusedTrainer):
         self.sampler = PopMixSampler(self.graph.user_csr, None if mix <= 0 else _GlobalItemCsr(
             indptr_i), num_items, mix_pop=mix, gamma=neg_pop_gamma if mix > 0 else None,
             max_tries=neg_max_tries, seed=seed + 7919 * self.rank)
-        self.train_users = nonempty_rows(self.graph.user_csr)
-        if self.train_users.numel() == 0:
-            raise RuntimeError(f"rank {self.rank}: no train users in its shard")
         self.epoch, self.cursor, self.step_count = 0, 0, 0
         self.perm = None
         self.posneg = torch.empty(2 * B, dtype=torch.int64, device=dev)
@@ -466,6 +478,8 @@ class ShardedTrainer(FusedTrainer):
         users = self.perm[self.cursor: self.cursor + self.B_local]
         self.cursor += self.B_local
         if users.numel() < self.B_local:   # wrap so every rank keeps a full slice
+            # B_local <= n (see __init__): the tail perm[c:n] and the head
+            # perm[:B-(n-c)] do not overlap, so the batch has no repeated user
             self.cursor = n
             users = torch.cat([users, self.perm[: self.B_local - users.numel()]])
         return users
@@ -476,8 +490,8 @@ class ShardedTrainer(FusedTrainer):
         rows, listed, are the step's frontier for the sparse exchange."""
         st = stream_handle()
         B = users.numel()
-        call("bbgr_mark_rows", B, ptr(users), 1, ptr(self.mask_u), st)
-        call("bbgr_mark_rows", 2 * B, ptr(self.posneg), 1, ptr(self.mask_i), st)
+        call("bbgr_mark_rows", B, ptr(users), 1, ptr(self.mask_u), self.U, st)
+        call("bbgr_mark_rows", 2 * B, ptr(self.posneg), 1, ptr(self.mask_i), self.I, st)
         if self.order == ORDER_GS:
             uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), 1,
@@ -541,7 +555,7 @@ class ShardedTrainer(FusedTrainer):
         call("bbgr_rows_zero", self.all_items.numel(), ptr(self.all_items), ptr(self.g_if),
              ld(self.g_if), self.d, st)
         if masks is not None:
-            call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), st)
+            call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), self.U, st)
             self.mask_i.zero_()
         self.exchange.clear_rows()
         dist.all_reduce(self.loss, op=dist.ReduceOp.SUM, group=self.group)

@@ -139,6 +139,7 @@ class FusedTrainer:
     def step(self, users: torch.Tensor | None = None) -> torch.Tensor:
         """One training step over `users` (input ids; default: the next slice of
         the epoch permutation)."""
+        listed = users is None   # epoch-permutation slices never repeat a user
         if users is None:
             users = self.next_users()
         else:
@@ -154,7 +155,11 @@ class FusedTrainer:
         masks = self._set_masks(users, pos, neg, 1) if self.frontier else None
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
                 out_i=self.itf, ws=self.ws,
-                final_rows=None if masks is None else (masks[0], masks[1], users))
+                final_rows=None if masks is None else
+                (masks[0], masks[1], users if listed else None))
+        # (a caller's batch may repeat a user: its last user layer then runs on
+        # the de-duplicated mask instead of a row list, whose repeated rows
+        # would update the in-place accumulator twice)
         a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
                      self.pop, self.lambda_fair, parts=self.parts[: 3 * B],
                      contrib=self.contrib)
@@ -242,9 +247,9 @@ class FusedTrainer:
         whose last user layer reads the NEW item layer)."""
         st = stream_handle()
         B = users.numel()
-        call("bbgr_mark_rows", B, ptr(users), value, ptr(self.mask_u), st)
-        call("bbgr_mark_rows", B, ptr(pos), value, ptr(self.mask_i), st)
-        call("bbgr_mark_rows", B, ptr(neg), value, ptr(self.mask_i), st)
+        call("bbgr_mark_rows", B, ptr(users), value, ptr(self.mask_u), self.U, st)
+        call("bbgr_mark_rows", B, ptr(pos), value, ptr(self.mask_i), self.I, st)
+        call("bbgr_mark_rows", B, ptr(neg), value, ptr(self.mask_i), self.I, st)
         if self.order == ORDER_GS:
             uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), value,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 1
+#define BBGR_ABI_VERSION 2
 
 typedef enum {
   BBGR_OK = 0,
@@ -186,8 +186,9 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /* add_mask (nullable, [n_rows]): add[r] read only on flagged rows (treated   */
 /*   as 0 elsewhere — exact when add is zero off the mask).                   */
 /* row_list (nullable, int64 [n_row_list]): compute only these rows (short    */
-/*   rows on a grid sized by the list; long rows still need row_mask set for  */
-/*   their chunk workgroups). Launches with any mask or list run as           */
+/*   rows on a grid sized by the list; long rows need row_mask set for their  */
+/*   chunk workgroups: a row_list without row_mask is rejected when the plan  */
+/*   has chunks). Listed rows must be distinct. Launches with any mask or list run as */
 /*   `spmm_masked_kernel`, full-CSR launches as `spmm_kernel`.                */
 /* use_range != 0: compute only rows [range[0], range[1]), whose long-row     */
 /*   chunks are [range[2], range[3]) and split rows [range[4], range[5]) of   */
@@ -397,9 +398,10 @@ int bbgr_ewa_normalize(const bbgr_csr *csr, const int32_t *perm, const int32_t *
                        float *w_raw, float *w_edge, float *w_csr, void *workspace,
                        size_t *workspace_bytes, bbgr_stream_t stream);
 
-/* mask[idx[k]] = value for k < n. */
+/* mask[idx[k]] = value for k < n; indices outside [0, n_rows) (the sampler's
+ * -1, or a caller's stale tail) are skipped. */
 int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value, uint8_t *mask,
-                   bbgr_stream_t stream);
+                   int64_t n_rows, bbgr_stream_t stream);
 /* For each listed row r = rows[k]: mask[indices[e]] = value for every edge e of
  * row r (the neighbourhood frontier of a batch). */
 int bbgr_mark_neighbors(int64_t n, const int64_t *rows, const int32_t *indptr,

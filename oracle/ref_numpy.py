@@ -97,23 +97,87 @@ def sample_batch_reference_style(indptr, indices, users, num_items, rng, pop_pro
 # ---------------------------------------------------------------------------
 # Operator values (fp32, as the reference computes them)
 # ---------------------------------------------------------------------------
+def degrees(edges_2xE, num_users, num_items):
+    """fp32 (deg_u, deg_i) as the reference builders compute them: np.bincount
+    of the edge list -> float32 (Version-2/lighgcn_cu_pop.py:434-435,
+    lightgcn_cu.py:383-384). Duplicate pairs count with their multiplicity."""
+    deg_u = np.bincount(edges_2xE[0].astype(np.int64), minlength=num_users).astype(np.float32)
+    deg_i = np.bincount(edges_2xE[1].astype(np.int64), minlength=num_items).astype(np.float32)
+    return deg_u, deg_i
+
+
+def edge_weights(kind, u, i, deg_u, deg_i, cred_u=None):
+    """Per-edge fp32 operator values of the edges (u[e], i[e]) given the graph's
+    fp32 degrees — the reference's weight expressions evaluated on any subset
+    of the edges (the full-size parity tests check sampled rows only).
+    Returns (w_user_from_item, w_item_from_user):
+      "gs" / "method_a": Version-2/lighgcn_cu_pop.py:436-450 (M_ui[u,i] = w_base,
+          M_iu[i,u] = c_u * w_base); method_a also x alpha_i,
+          version_1/lightgcn_cu_pop_long_tail_exposure.py:379-392
+      "j": lightgcn_cu.py:385-397 (item<-user c_u/denom, user<-item 1/denom)
+      "sym": lightgcn.py:365-372 (deg^-1/2 on both ends, inf -> 0; one
+          entry per edge, so a duplicate pair sums to v * dinv_r * dinv_c)."""
+    u = np.asarray(u, np.int64)
+    i = np.asarray(i, np.int64)
+    c = None if cred_u is None else np.asarray(cred_u, np.float32)
+    if kind in ("gs", "method_a"):
+        inv_sqrt_u = 1.0 / np.sqrt(np.maximum(deg_u, 1.0))
+        inv_sqrt_i = 1.0 / np.sqrt(np.maximum(deg_i, 1.0))
+        w_base = inv_sqrt_u[u] * inv_sqrt_i[i]
+        if kind == "method_a":
+            alpha_i = (1.0 / np.log1p(np.maximum(deg_i, 1.0))).astype(np.float32)
+            w_base = w_base * alpha_i[i]
+        w_cred = w_base if c is None else c[u] * w_base
+        return w_base.astype(np.float32), w_cred.astype(np.float32)
+    if kind == "j":
+        denom = np.sqrt(np.maximum(deg_u[u] * deg_i[i], 1e-12)).astype(np.float32)
+        w_iu = (1.0 / denom).astype(np.float32)
+        w_ui = (np.float32(1.0) / denom if c is None else c[u] / denom).astype(np.float32)
+        return w_iu, w_ui
+    if kind == "sym":
+        with np.errstate(divide="ignore"):
+            du = np.power(deg_u, np.float32(-0.5)).astype(np.float32)
+            di = np.power(deg_i, np.float32(-0.5)).astype(np.float32)
+        du[np.isinf(du)] = 0.0
+        di[np.isinf(di)] = 0.0
+        w = (np.float32(1.0) * du[u] * di[i]).astype(np.float32)
+        return w, w
+    raise ValueError(f"unknown operator kind {kind!r}")
+
+
+def rows_product(sel_rows, rows, cols, w, x_cols):
+    """float64 y[sel_rows[k]] = sum over the edges e of that row of
+    w[e] * x_cols[e] — one sparse product evaluated on a subset of its output
+    rows (torch.sparse.mm of Version-2:483-484 / lightgcn_cu.py:431,434 /
+    lightgcn.py:323 restricted to those rows). rows[e] must be in sel_rows;
+    x_cols[e] is the source row of edge e (any float dtype). Sums in float64
+    (segment sums over the edges grouped by output row)."""
+    sel_rows = np.asarray(sel_rows, np.int64)
+    x_cols = np.asarray(x_cols)
+    srt = np.argsort(sel_rows, kind="stable")
+    slot = srt[np.searchsorted(sel_rows[srt], np.asarray(rows, np.int64))]
+    out = np.zeros((sel_rows.size, x_cols.shape[1]), np.float64)
+    if slot.size == 0:
+        return out
+    o = np.argsort(slot, kind="stable")
+    contrib = np.asarray(w, np.float64)[o, None] * x_cols[o].astype(np.float64)
+    starts = np.searchsorted(slot[o], np.arange(sel_rows.size))
+    ends = np.append(starts[1:], slot.size)
+    nz = ends > starts
+    out[nz] = np.add.reduceat(contrib, starts[nz], axis=0)
+    return out
+
+
 def gs_values(edges_2xE, num_users, num_items, cred_u=None, method_a=False):
     """Version-2/lighgcn_cu_pop.py:430-450 (method_a: version_1/
     lightgcn_cu_pop_long_tail_exposure.py:379-392).
     Returns (u, i, w_ui, w_iu): M_ui[u,i] += w_ui, M_iu[i,u] += w_iu."""
     u = edges_2xE[0].astype(np.int64)
     i = edges_2xE[1].astype(np.int64)
-    deg_u = np.bincount(u, minlength=num_users).astype(np.float32)
-    deg_i = np.bincount(i, minlength=num_items).astype(np.float32)
-    inv_sqrt_u = 1.0 / np.sqrt(np.maximum(deg_u, 1.0))
-    inv_sqrt_i = 1.0 / np.sqrt(np.maximum(deg_i, 1.0))
-    w_base = inv_sqrt_u[u] * inv_sqrt_i[i]
-    if method_a:
-        alpha_i = (1.0 / np.log1p(np.maximum(deg_i, 1.0))).astype(np.float32)
-        w_base = w_base * alpha_i[i]
-    c = np.ones(num_users, np.float32) if cred_u is None else np.asarray(cred_u, np.float32)
-    w_cred = c[u] * w_base
-    return u, i, w_base.astype(np.float32), w_cred.astype(np.float32)
+    deg_u, deg_i = degrees(edges_2xE, num_users, num_items)
+    w_base, w_cred = edge_weights("method_a" if method_a else "gs", u, i, deg_u, deg_i,
+                                  np.ones(num_users, np.float32) if cred_u is None else cred_u)
+    return u, i, w_base, w_cred
 
 
 def j_values(edges_2xE, num_users, num_items, cred_u=None):
@@ -121,12 +185,9 @@ def j_values(edges_2xE, num_users, num_items, cred_u=None):
     M_ui[i,u] (item<-user) = c_u/denom, M_iu[u,i] (user<-item) = 1/denom."""
     u = edges_2xE[0].astype(np.int64)
     i = edges_2xE[1].astype(np.int64)
-    deg_u = np.bincount(u, minlength=num_users).astype(np.float32)
-    deg_i = np.bincount(i, minlength=num_items).astype(np.float32)
-    denom = np.sqrt(np.maximum(deg_u[u] * deg_i[i], 1e-12)).astype(np.float32)
-    c = np.ones(num_users, np.float32) if cred_u is None else np.asarray(cred_u, np.float32)
-    w_ui = (c[u] / denom).astype(np.float32)
-    w_iu = (1.0 / denom).astype(np.float32)
+    deg_u, deg_i = degrees(edges_2xE, num_users, num_items)
+    w_iu, w_ui = edge_weights("j", u, i, deg_u, deg_i,
+                              np.ones(num_users, np.float32) if cred_u is None else cred_u)
     return u, i, w_ui, w_iu, deg_i
 
 

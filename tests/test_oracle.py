@@ -331,3 +331,40 @@ def test_cred_gnn_oracle_known_answers():
     np.testing.assert_allclose(tw.numpy(), wt, rtol=1e-6)
     ta = m.aggregate(torch.tensor(x, dtype=torch.float32), torch.tensor(ei), tw, 3)
     np.testing.assert_allclose(ta.numpy(), agg, rtol=1e-6)
+
+
+def test_rows_product_equals_full_product_rows():
+    """The sampled-row evaluator of the full-size parity tests equals the rows
+    of the whole float64 product (duplicates, empty rows, unsorted selection)."""
+    rng = np.random.default_rng(5)
+    rows = rng.integers(0, 60, 2000)
+    cols = rng.integers(0, 40, 2000)
+    w = rng.random(2000).astype(np.float32)
+    x = rng.normal(size=(40, 16))
+    sel = np.array([59, 3, 0, 17, 48, 12])
+    rows[rows == 12] = 13                      # row 12 has no edges
+    m = np.isin(rows, sel)
+    got = R.rows_product(sel, rows[m], cols[m], w[m], x[cols[m]])
+    want = (R.csr64(rows, cols, w, (60, 40)) @ x)[sel]
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+    assert not got[sel == 12].any()
+
+
+def test_edge_weights_match_operator_builders():
+    """edge_weights on an edge subset equals the full builders' values."""
+    e = np.array([[0, 0, 1, 2, 2, 2], [0, 1, 1, 0, 1, 3]], np.int32)
+    U, I = 4, 5
+    cred = np.array([0.5, 1.0, 0.25, 0.8], np.float32)
+    deg_u, deg_i = R.degrees(e, U, I)
+    for kind, full in (("gs", R.gs_values(e, U, I, cred)),
+                       ("method_a", R.gs_values(e, U, I, cred, method_a=True))):
+        a, b = R.edge_weights(kind, e[0], e[1], deg_u, deg_i, cred)
+        np.testing.assert_array_equal(a, full[2])
+        np.testing.assert_array_equal(b, full[3])
+    u, i, w_ui, w_iu, _ = R.j_values(e, U, I, cred)
+    a, b = R.edge_weights("j", e[0], e[1], deg_u, deg_i, cred)
+    np.testing.assert_array_equal(a, w_iu)
+    np.testing.assert_array_equal(b, w_ui)
+    S = R.sym_values(e, U, I)
+    a, _ = R.edge_weights("sym", e[0], e[1], deg_u, deg_i)
+    np.testing.assert_allclose(a, np.asarray(S[e[0], e[1] + U]).ravel(), rtol=1e-7)
