@@ -330,7 +330,7 @@ def test_c1_symmetric_path_every_layer_loss_and_grad_vs_golden(c1):
                   "C1 sym final")
     users, pos, neg = (t(c1[k], torch.int64) for k in ("users", "pos", "neg"))
     loss = model.bpr_loss(users, pos, neg, uf, itf, 1e-4)
-    assert abs(float(loss) - float(c1["sym_loss"])) <= TOL * float(c1["sym_loss"])
+    assert abs(float(loss.detach()) - float(c1["sym_loss"])) <= TOL * float(c1["sym_loss"])
     loss.backward()
     assert_parity(model.emb.weight.grad.double().cpu().numpy(), c1["sym_grad_emb"],
                   "C1 grad emb.weight")

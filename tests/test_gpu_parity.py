@@ -840,3 +840,36 @@ def test_every_layer_vs_oracle(gold, variant):
         u = M_ui.mm(i)                                             # ... users from the NEW items
         assert_parity(i, is_[k], f"{variant} item layer {k}")
         assert_parity(u, us[k], f"{variant} user layer {k}")
+
+
+def test_spmm_row_list_needs_row_mask_on_chunked_plan():
+    """a row list without a row mask on a plan with long-row chunks
+    used to skip the listed long rows and let the fix-up sum stale partials;
+    the call is now rejected (and still accepted on an unchunked plan)."""
+    from bbgr.propagate import Product, spmm
+    e = synthetic_edges(300, 50, 6000, 3, items="zipf")
+    c = Csr(e[1], e[0], 50, 300, DEV, long_threshold=8, chunk_edges=32)
+    assert c.n_chunks > 0 and c.n_split > 0
+    prod = Product(c, None, None, None, {})
+    x = torch.randn(300, 64, device=DEV)
+    y = torch.zeros(50, 64, device=DEV)
+    lst = torch.tensor([0, 1, 2], dtype=torch.int64, device=DEV)
+    with pytest.raises(_lib.BbgrError, match="INVALID"):
+        spmm(prod, x, False, y=y, row_list=lst)
+    c2 = Csr(e[1], e[0], 50, 300, DEV, long_threshold=1 << 30)
+    assert c2.n_chunks == 0
+    spmm(Product(c2, None, None, None, {}), x, False, y=y, row_list=lst)
+    want = R.csr64(e[1], e[0], np.ones(e.shape[1]), (50, 300)) @ x.double().cpu().numpy()
+    assert_parity(y[:3], want[:3], "listed rows")
+    assert not y[3:].any()
+
+
+def test_mark_rows_skips_out_of_range_indices():
+    from bbgr._lib import call, ptr, stream_handle
+    mask = torch.zeros(10, dtype=torch.uint8, device=DEV)
+    idx = torch.tensor([3, -1, 10, 12, 9], dtype=torch.int64, device=DEV)
+    guard = torch.zeros(64, dtype=torch.uint8, device=DEV)   # allocated after: canary
+    call("bbgr_mark_rows", 5, ptr(idx), 1, ptr(mask), 10, stream_handle())
+    torch.cuda.synchronize()
+    assert mask.cpu().tolist() == [0, 0, 0, 1, 0, 0, 0, 0, 0, 1]
+    assert not guard.any()
