@@ -47,16 +47,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of spmm_kernel from the latest committed rocprofv3
-    PMC passes (tools/profile_box.sh + tools/summarize_profile.py)."""
-    p = os.path.join(ROOT, "profiles", "spmm_traffic.json")
-    if not os.path.exists(p):
-        return None, None
-    j = json.load(open(p))
-    return j.get("hbm_bytes_per_launch_corrected"), j.get("source")
-
-
 def spmm_bytes(nnz: int, rows: int, d: int) -> int:
     return nnz * (4 + 4 + 4 * d) + rows * (4 + 4 * d)
 
@@ -67,51 +57,144 @@ def spmm_adam_bytes(nnz: int, rows: int, d: int) -> int:
     return spmm_bytes(nnz, rows, d) - rows * 4 * d + 6 * rows * 4 * d
 
 
-def cpu_baseline(edges, cfg, batch, sample_users=256):
-    """Reference CPU path (same torch calls) on a bounded sample of the step."""
+def _median_s(fn, reps: int = 5, warmup: int = 1):
+    """Median wall time of fn() over `reps` runs after `warmup` untimed runs.
+    fn may return its own measured seconds (a sub-interval); else the call is timed."""
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = fn()
+        ts.append(r if isinstance(r, float) else time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def _reference_step_s(cfg_name: str, reps: int = 5):
+    """Median seconds of one whole reference-style training step at a small
+    config (Version-2/lighgcn_cu_pop.py:826-866: the per-user sampler loop
+    :835-849, then propagate -> bpr_loss -> backward -> Adam :858-863)."""
+    from oracle import ref_numpy as R
+    from oracle import ref_torch as T
+    c = CONFIGS[cfg_name]
+    U, I, d, K, B = c["num_users"], c["num_items"], c["emb_dim"], c["num_layers"], c["batch"]
+    e = config_edges(cfg_name)
+    cred = synthetic_credibility(U, CONFIG_SEED[cfg_name])
+    M_ui, M_iu = T.gs_operators(e, U, I, cred)
+    torch.manual_seed(42)
+    model = T.GSModel(U, I, d, K, M_ui, M_iu)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    indptr, indices = R.edges_to_user_csr(e, U)
+    pp = R.pop_prob(e, I)
+    rng = np.random.default_rng(42)
+    train_users = np.flatnonzero(np.diff(indptr) > 0)
+    perm = rng.permutation(train_users)
+    pos_in_perm = [0]
+
+    def step():
+        lo = pos_in_perm[0] % max(len(perm) - B, 1)
+        pos_in_perm[0] += B
+        users = perm[lo:lo + B]
+        us, ps, ns = R.sample_batch_reference_style(indptr, indices, users, I, rng, pp)
+        T.train_step(model, opt, torch.as_tensor(us), torch.as_tensor(ps),
+                     torch.as_tensor(ns), 1e-4)
+
+    med, ts = _median_s(step, reps)
+    return med, ts, 4 * K * e.shape[1]
+
+
+def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
+                 whole_steps=("C2", "C1")):
+    """The reference's CPU path (oracle/ref_torch.py: the same torch calls as
+    Version-2/lighgcn_cu_pop.py:441-450, 482-489, 858-863) timed on this host,
+    SURVEY §8(d): every figure is the median of `reps` runs after one warm-up.
+
+    Bounded sample of the C4 step: each of the four products of a step is timed
+    on the rows of every `every`-th output vertex (all their edges, the FULL
+    source table gathered, so cache behaviour is the real one) and scaled by
+    E / sampled edges:
+      forward  item<-user  M_iu[items % every == 0, :] @ u
+      forward  user<-item  M_ui[users % every == 0, :] @ i
+      backward grad u      autograd of M_iu[:, users % every == 0] @ u_s
+                           (the reference's transposed product incl. its coalesce)
+      backward grad i      autograd of M_ui[:, items % every == 0] @ i_s
+    plus torch Adam over all (U+I) x d parameters and the reference's per-user
+    pop-mix sampler loop on B/every users (scaled by `every`). A whole reference
+    step is timed end to end at C2 (and C1) beside it."""
     from oracle import ref_numpy as R
     from oracle import ref_torch as T
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     cores = max(1, min(cores, os.cpu_count() or 1))
     torch.set_num_threads(cores)
-    U, I, d, K = cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"]
+    U, I, d, K, B = (cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"],
+                     cfg["batch"])
     E = edges.shape[1]
-    M_ui, M_iu = T.gs_operators(edges, U, I)            # not timed (operator build)
+    t_setup = time.perf_counter()
+    u, i, w_ui, w_iu = R.gs_values(edges, U, I, cred)
     g = torch.Generator().manual_seed(0)
-    u0 = torch.rand(U, d, generator=g) - 0.5
-    i0 = torch.rand(I, d, generator=g) - 0.5
-    t0 = time.perf_counter()
-    torch.sparse.mm(M_iu, u0)
-    t_iu = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    torch.sparse.mm(M_ui, i0)
-    t_ui = time.perf_counter() - t0
-    del M_ui, M_iu
-    # Adam over every parameter (dense, as the reference's dense grads force)
-    pu = torch.nn.Parameter(u0)
-    pi = torch.nn.Parameter(i0)
+    x_u = torch.rand(U, d, generator=g) - 0.5
+    x_i = torch.rand(I, d, generator=g) - 0.5
+    su, si = (u % every) == 0, (i % every) == 0
+    Us, Is = (U + every - 1) // every, (I + every - 1) // every
+    A_f_iu = T.coo(i[si] // every, u[si], w_iu[si], (Is, U))      # item rows sampled
+    A_f_ui = T.coo(u[su] // every, i[su], w_ui[su], (Us, I))      # user rows sampled
+    A_b_u = T.coo(i[su], u[su] // every, w_iu[su], (I, Us))       # grad-u rows sampled
+    A_b_i = T.coo(u[si], i[si] // every, w_ui[si], (U, Is))       # grad-i rows sampled
+    e_iu, e_ui = int(si.sum()), int(su.sum())
+    del u, i, w_ui, w_iu, su, si
+    t_setup = time.perf_counter() - t_setup
+
+    def bwd(A, x_s, gy):
+        xs = x_s.clone().requires_grad_()
+        y = torch.sparse.mm(A, xs)
+        t0 = time.perf_counter()
+        y.backward(gy)
+        return time.perf_counter() - t0
+
+    t_f_iu, _ = _median_s(lambda: torch.sparse.mm(A_f_iu, x_u), reps)
+    t_f_ui, _ = _median_s(lambda: torch.sparse.mm(A_f_ui, x_i), reps)
+    gi, gu = torch.rand(I, d, generator=g), torch.rand(U, d, generator=g)
+    t_b_u, _ = _median_s(lambda: bwd(A_b_u, x_u[::every].contiguous(), gi), reps)
+    t_b_i, _ = _median_s(lambda: bwd(A_b_i, x_i[::every].contiguous(), gu), reps)
+    del A_f_iu, A_f_ui, A_b_u, A_b_i, gi, gu
+    s_iu, s_ui = E / max(e_iu, 1), E / max(e_ui, 1)
+    t_prop = K * (t_f_iu * s_iu + t_f_ui * s_ui + t_b_u * s_ui + t_b_i * s_iu)
+    # torch Adam over every parameter row (the reference's dense gradients)
+    pu, pi = torch.nn.Parameter(x_u), torch.nn.Parameter(x_i)
     opt = torch.optim.Adam([pu, pi], lr=1e-3)
-    pu.grad, pi.grad = torch.zeros_like(u0), torch.zeros_like(i0)
-    t0 = time.perf_counter()
-    opt.step()
-    t_adam = time.perf_counter() - t0
-    # the reference's per-user pop-mix sampler loop on a user subset
+    pu.grad, pi.grad = torch.full_like(x_u, 1e-3), torch.full_like(x_i, 1e-3)
+    t_adam, _ = _median_s(opt.step, reps)
+    del opt, pu, pi, x_u, x_i
+    # the reference's per-user pop-mix sampler loop on B/every users
     indptr, indices = R.edges_to_user_csr(edges, U)
     pp = R.pop_prob(edges, I)
     rng = np.random.default_rng(42)
-    users = rng.choice(np.flatnonzero(np.diff(indptr) > 0), sample_users, replace=False)
-    t0 = time.perf_counter()
-    R.sample_batch_reference_style(indptr, indices, users, I, rng, pp)
-    t_samp = (time.perf_counter() - t0) * batch / sample_users
-    t_step = K * (t_iu + t_ui) * 2 + t_adam + t_samp
+    nonempty = np.flatnonzero(np.diff(indptr) > 0)
+    n_s = max(1, B // every)
+    t_samp, _ = _median_s(lambda: R.sample_batch_reference_style(
+        indptr, indices, rng.choice(nonempty, n_s, replace=False), I, rng, pp), reps)
+    t_samp *= B / n_s
+    t_step = t_prop + t_adam + t_samp
+    whole = {n: _reference_step_s(n, reps) for n in whole_steps}
     return {
         "value": 4 * K * E / t_step, "unit": "edges/s", "cores": cores, "kind": "port",
-        "sample": (f"{cfg_name_global}: one torch.sparse.mm per direction "
-                   f"(item<-user {t_iu:.2f}s, user<-item {t_ui:.2f}s) x2K for fwd+bwd, "
-                   f"torch Adam on all {U + I} rows ({t_adam:.2f}s), reference pop-mix "
-                   f"sampler loop on {sample_users} users scaled to B={batch} "
-                   f"({t_samp:.2f}s); est. {t_step:.1f}s/step"),
+        "bpr_steps_per_s": 1.0 / t_step,
+        "sample": (f"{cfg_name_global} step from sampled products (median of {reps} after 1 "
+                   f"warm-up, rows of every {every}th output vertex, scaled by edges): "
+                   f"fwd item<-user {t_f_iu * s_iu:.2f}s, fwd user<-item {t_f_ui * s_ui:.2f}s, "
+                   f"bwd grad-u {t_b_u * s_ui:.2f}s, bwd grad-i {t_b_i * s_iu:.2f}s per layer "
+                   f"(x K={K}); torch Adam on {U + I} rows {t_adam:.2f}s; reference pop-mix "
+                   f"sampler loop {t_samp:.2f}s for B={B} (timed on {n_s} users); "
+                   f"est. {t_step:.1f}s/step. Whole reference steps, median of {reps}: "
+                   + ", ".join(f"{n} {w[0]:.3f}s ({w[2] / w[0] / 1e6:.1f} M edges/s)"
+                               for n, w in whole.items())),
         "step_s": t_step,
+        "components_s": {"fwd_item_from_user": t_f_iu * s_iu, "fwd_user_from_item": t_f_ui * s_ui,
+                         "bwd_grad_u": t_b_u * s_ui, "bwd_grad_i": t_b_i * s_iu,
+                         "adam": t_adam, "sampler": t_samp},
+        "whole_step_s": {n: {"median": w[0], "runs": w[1], "edges_per_s": w[2] / w[0]}
+                         for n, w in whole.items()},
+        "setup_s": t_setup,
     }
 
 
@@ -127,6 +210,67 @@ def _quiet_stdout():
     return os.fdopen(saved, "w")
 
 
+def _allreduce(x: float, dev, op) -> float:
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=op)
+    return float(t.item())
+
+
+def _compulsory_bytes(nnz: int, rows: int, n_cols: int, d: int) -> int:
+    """every edge's index + weight once, every source row
+    once, every output row (+ indptr) once: E*8 + C*4d + R*(4 + 4d)."""
+    return nnz * 8 + n_cols * 4 * d + rows * (4 + 4 * d)
+
+
+def roofline_groups(timer, counts, steps: int, count_steps: int, n_items: int):
+    """Per launch kind and side: launches, average ms, gather-model and
+    compulsory-model bytes per launch, their GB/s and fractions of 8 TB/s.
+    Full-CSR / range launches take their bytes from the CSR; masked launches
+    from the rows / edges counted on the device over `count_steps` extra steps."""
+    out = []
+    for (kind, tr, nc, d), (n, ms, rows, nnz) in sorted(timer.groups().items()):
+        side = "item<-user" if tr == n_items else "user<-item"
+        e = {"kind": kind, "side": side, "d": d, "launches_per_step": n / steps,
+             "avg_ms": ms / n}
+        if kind == "masked":
+            c = counts.get((kind, tr, nc, d))
+            if not c:
+                continue
+            cn, crows, cvis, cgat = c
+            rows_l, vis_l, gat_l = crows / cn, cvis / cn, cgat / cn
+            e["rows_per_launch"], e["edges_visited_per_launch"] = rows_l, vis_l
+            e["edges_gathered_per_launch"] = gat_l
+            gather = vis_l * 8 + gat_l * 4 * d + rows_l * (4 + 4 * d)
+            compulsory = None
+        else:
+            rows_l, nnz_l = rows / n, nnz / n
+            gather = spmm_bytes(nnz_l, rows_l, d) if kind == "full" else \
+                spmm_adam_bytes(nnz_l, rows_l, d)
+            compulsory = _compulsory_bytes(nnz_l, rows_l, nc, d) + \
+                (0 if kind == "full" else 5 * rows_l * 4 * d)
+            e["rows_per_launch"], e["edges_per_launch"] = rows_l, nnz_l
+        e["gather_model_bytes"] = gather
+        e["gather_model_GBps"] = gather / (e["avg_ms"] * 1e6)
+        e["gather_model_frac"] = e["gather_model_GBps"] / HBM_PEAK_GBS
+        e["cache_assisted"] = e["gather_model_frac"] > 1.0
+        if compulsory is not None:
+            e["compulsory_bytes"] = compulsory
+            e["compulsory_GBps"] = compulsory / (e["avg_ms"] * 1e6)
+            e["compulsory_frac"] = e["compulsory_GBps"] / HBM_PEAK_GBS
+        out.append(e)
+    return out
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of the dominant kernel (item<-user spmm_kernel) from
+    the committed rocprofv3 PMC passes (tools/profile_box.sh +
+    tools/summarize_profile.py), with the commit and tag they were taken at."""
+    p = os.path.join(ROOT, "profiles", "spmm_traffic.json")
+    if not os.path.exists(p):
+        return None
+    return json.load(open(p))
+
+
 def main():
     global cfg_name_global
     out_stream = _quiet_stdout()
@@ -140,6 +284,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true",
                     help="disable exact frontier sparsity (every SpMM over the full CSR)")
+    ap.add_argument("--frontier", default="auto", choices=["auto", "on", "off"],
+                    help="frontier masks: auto = the trainer's size rule")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU trainer (torch.distributed) even at N=1: "
                          "measures the sharded step's own overhead, collectives included")
@@ -157,12 +303,16 @@ def main():
     ap.add_argument("--dense-check", type=int, default=5,
                     help="after the timed steps, time this many steps with frontier sparsity "
                          "off (reported as dense_ms_per_step; 0 = skip)")
+    ap.add_argument("--count-steps", type=int, default=3,
+                    help="steps after the timed region whose launches count the rows / edges "
+                         "they actually process (value = traversed edges)")
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="sharded runs: steps after the timed region whose SpMM launches "
                          "are bracketed by HIP events for the roofline")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N>1: weak = every rank owns a full config-sized user shard over the "
-                         "shared items; strong = one config graph cut into N user ranges")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="N>1: strong (default) = the config's one graph cut into N user "
+                         "ranges (the metric's |E|); weak = every rank owns a full "
+                         "config-sized user shard over the shared items")
     args = ap.parse_args()
     cfg_name_global = args.config
     cfg = CONFIGS[args.config]
@@ -171,6 +321,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    scaling = args.scaling or "strong"
     local = local % max(torch.cuda.device_count(), 1)   # ranks may share a GPU (gloo rehearsal)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -194,7 +345,7 @@ def main():
 
     U, I, d, K = cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"]
     B = cfg["batch"]
-    weak = world > 1 and args.scaling == "weak"
+    weak = world > 1 and scaling == "weak"
     # configs too large to draw whole on every rank (C5) are drawn per user shard
     sharded_gen = not weak and cfg["num_edges"] > 100_000_000
     t0 = time.perf_counter()
@@ -203,47 +354,52 @@ def main():
     if weak:
         edges = shard_edges_weak(args.config, rank)
         cred = synthetic_credibility(U, seed + 7919 * rank, args.cred)
-        E = edges.shape[1] * world                       # edges of the whole job's graph
     elif sharded_gen:
         edges, lo, hi = shard_edges_strong(args.config, rank, world)
         cred = synthetic_credibility(hi - lo, seed + 7919 * rank, args.cred)
-        E = cfg["num_edges"]
     else:
         edges = config_edges(args.config)
         cred = synthetic_credibility(U, seed, args.cred)
-        E = edges.shape[1]
-    log(f"[bench] rank {rank}: {args.config} U={U} I={I} E={E} d={d} K={K} B={B} "
-        f"scaling={args.scaling} generated in {time.perf_counter() - t0:.1f}s")
+    log(f"[bench] rank {rank}: {args.config} U={U} I={I} d={d} K={K} B={B} "
+        f"scaling={scaling} generated in {time.perf_counter() - t0:.1f}s")
 
     xp = dict(exchange_parts=args.exchange_parts, frontier_parts=args.frontier_parts,
               vertex_order=args.vertex_order)
     if args.native_comm:
         xp["native_comm"] = True
+    frontier = {"auto": "auto", "on": True, "off": False}[args.frontier]
+    if args.dense:
+        frontier = False
     if not dist_mode:
         from bbgr.graph import BipartiteGraph
         from bbgr.trainer import FusedTrainer
         graph = BipartiteGraph(edges, U, I, dev, vertex_order=args.vertex_order)
         trainer = FusedTrainer(graph, args.variant, cred=cred, emb_dim=d, num_layers=K,
-                               batch_size=B, frontier=not args.dense)
+                               batch_size=B, frontier=frontier)
     elif weak:
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
                                  num_layers=K, batch_size=B, device=dev, user_offset=rank * U,
-                                 frontier=not args.dense, **xp)
+                                 frontier=frontier, **xp)
     elif sharded_gen:
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer(edges, hi - lo, I, args.variant, cred=cred, emb_dim=d,
                                  num_layers=K, batch_size=max(1, B // world), device=dev,
-                                 user_offset=lo, frontier=not args.dense, **xp)
+                                 user_offset=lo, frontier=frontier, **xp)
     else:
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
                                                    emb_dim=d, num_layers=K, batch_size=B,
-                                                   device=dev, frontier=not args.dense, **xp)
+                                                   device=dev, frontier=frontier, **xp)
+    # edges of the whole job's graph: the sum of the ranks' shards
+    E_local = trainer.graph.item_csr.nnz
+    E = int(_allreduce(E_local, dev, torch.distributed.ReduceOp.SUM)) if dist_mode else E_local
+    U_job = U * (world if weak else 1)
     if dist_mode:
         del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
     torch.cuda.synchronize()
-    log(f"[bench] rank {rank}: setup done, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
+    log(f"[bench] rank {rank}: setup done, E={E} (local {E_local}), frontier="
+        f"{trainer.frontier}, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
 
     for _ in range(args.warmup):
         trainer.step()
@@ -254,10 +410,8 @@ def main():
     # Per-launch HIP events for the roofline. On one GPU they ride inside the
     # timed steps (cost ~0.1 ms/step). In the sharded step, events recorded
     # between launches interleave with the collectives' cross-stream waits and
-    # cost 1.4-3 ms/step (15-step runs at N=1: 19.4-21.1 ms with them, 18.0-18.1
-    # without), so
-    # there the events are recorded over `--roofline-steps` extra steps right
-    # after the timed region instead.
+    # cost 1.4-3 ms/step, so there the events are recorded over
+    # `--roofline-steps` extra steps right after the timed region instead.
     events_in_loop = not dist_mode
     if events_in_loop:
         P.set_spmm_timer(timer)
@@ -278,12 +432,25 @@ def main():
         torch.cuda.synchronize()
         P.set_spmm_timer(None)
     if dist_mode:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = _allreduce(elapsed, dev, torch.distributed.ReduceOp.MAX)
     final_loss = float(loss)
+    # rows / edges every launch actually processes (frontier masks make them
+    # data-dependent), counted on the device over extra steps
+    counter = P.SpmmTimer(count=True)
+    count_steps = max(1, args.count_steps)
+    P.set_spmm_timer(counter)
+    for _ in range(count_steps):
+        trainer.step()
+    torch.cuda.synchronize()
+    P.set_spmm_timer(None)
+    counts = counter.edge_counts()
+    gathered_step = sum(c[3] for c in counts.values()) / count_steps
+    visited_step = sum(c[2] for c in counts.values()) / count_steps
+    if dist_mode:
+        gathered_step = _allreduce(gathered_step, dev, torch.distributed.ReduceOp.SUM)
+        visited_step = _allreduce(visited_step, dev, torch.distributed.ReduceOp.SUM)
     dense_ms = None
-    if not args.dense and args.dense_check > 0:
+    if trainer.frontier and args.dense_check > 0:
         # the same trainer with frontier sparsity off (every product over the
         # full CSR): what the masks save, reported next to the value
         trainer.frontier = False
@@ -299,32 +466,24 @@ def main():
             torch.distributed.barrier()
         dense_s = time.perf_counter() - t1
         if dist_mode:
-            t = torch.tensor([dense_s], device=dev, dtype=torch.float64)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            dense_s = float(t.item())
+            dense_s = _allreduce(dense_s, dev, torch.distributed.ReduceOp.MAX)
         dense_ms = 1000.0 * dense_s / args.dense_check
         trainer.frontier = True
     if dist_mode:
         trainer.close()                    # the native exchange's communicator, if any
-    summ = timer.summary("full")          # full-CSR launches: the roofline kernel
-    summ_m = timer.summary("masked")       # frontier-masked launches (bytes data-dependent)
-    summ_a = timer.summary("adam")         # last backward product + fused user Adam
-    tot_bytes = sum(n * spmm_bytes(nnz, rows, dd) for (rows, nnz, dd), (n, ms) in summ.items())
-    tot_ms = sum(ms for (n, ms) in summ.values())
-    n_launch = sum(n for (n, ms) in summ.values())
-    per_kernel = {f"rows{rows}_nnz{nnz}_d{dd}": {"launches": n, "avg_ms": ms / n,
-                                                 "GBps": n * spmm_bytes(nnz, rows, dd) / (ms * 1e6)}
-                  for (rows, nnz, dd), (n, ms) in summ.items()}
-    achieved = tot_bytes / (tot_ms * 1e6) if tot_ms > 0 else 0.0   # GB/s
-    masked_ms = sum(ms for (n, ms) in summ_m.values())
-    masked_n = sum(n for (n, ms) in summ_m.values())
-    adam_info = {f"rows{rows}_nnz{nnz}_d{dd}": {
-        "launches": n, "avg_ms": ms / n,
-        "algorithmic_bytes": spmm_adam_bytes(nnz, rows, dd),
-        "GBps": n * spmm_adam_bytes(nnz, rows, dd) / (ms * 1e6)}
-        for (rows, nnz, dd), (n, ms) in summ_a.items()}
-    traffic, traffic_src = pmc_traffic() if (args.config == "C4" and world == 1) else (None, None)
-    edges_per_step = 4 * K * E
+    groups = roofline_groups(timer, counts, timer_steps, count_steps, I)
+    # the dominant kernel: full-CSR item<-user products (spmm_kernel)
+    dom = [g for g in groups if g["kind"] == "full" and g["side"] == "item<-user"]
+    dom_n = sum(g["launches_per_step"] for g in dom)
+    dom_ms = sum(g["avg_ms"] * g["launches_per_step"] for g in dom) / dom_n if dom_n else 0.0
+    dom_bytes = (sum(g["gather_model_bytes"] * g["launches_per_step"] for g in dom) / dom_n
+                 if dom_n else 0.0)
+    dom_comp = (sum(g["compulsory_bytes"] * g["launches_per_step"] for g in dom) / dom_n
+                if dom_n else 0.0)
+    achieved = dom_bytes / (dom_ms * 1e6) if dom_ms > 0 else 0.0   # GB/s
+    spmm_ms_step = sum(g["avg_ms"] * g["launches_per_step"] for g in groups)
+    pmc = pmc_traffic() if (args.config == "C4" and world == 1 and not dist_mode) else None
+    steps_per_s = args.steps / elapsed
     if rank != 0:
         if dist_mode:
             torch.distributed.destroy_process_group()
@@ -332,37 +491,49 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and not dist_mode and not sharded_gen:
         log("[bench] timing the reference CPU path (bounded sample) ...")
-        cpu = cpu_baseline(edges, cfg, B)
+        t_cpu = time.perf_counter()
+        cpu = cpu_baseline(edges, cfg, args.config, cred)
+        log(f"[bench] cpu baseline took {time.perf_counter() - t_cpu:.1f}s")
+    dense_equiv = 4 * K * E
     out = {
         "metric": "SpMM edges/sec + BPR steps/sec, |E|=50M d=64, 1/2/4/8 MI355X; %HBM roofline",
-        "value": edges_per_step * args.steps / elapsed,
+        "value": gathered_step * steps_per_s,
         "unit": "edges/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": args.scaling,   # N=1: weak and strong are the same run
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Zipf-0.8 items, geometric user degrees; xavier init; Beta cred)",
         "config": {"workload": f"{args.config} BPR training step ({args.variant})"
                                + (f", {world} x {args.config} user shards" if weak else ""),
-                   "num_users": U * (world if weak else 1), "num_items": I, "num_edges": E,
+                   "num_users": U_job, "num_items": I, "num_edges": E,
                    "vertex_order": args.vertex_order,
                    "emb_dim": d, "num_layers": K,
                    "global_batch": B * (world if weak else 1),
                    "parallelism": f"user-rows x{world}"
                                   + (" (sharded trainer)" if dist_mode and world == 1 else "")},
-        "bpr_steps_per_s": args.steps / elapsed,
+        "bpr_steps_per_s": steps_per_s,
+        "value_note": "value = SpMM edges actually gathered (source row read and "
+                      "multiply-added) per second, whole job: every launch's edges counted "
+                      f"on the device over {count_steps} steps after the timed region "
+                      "(full-CSR launches all E; frontier-masked launches only their rows' "
+                      "edges with a live source)",
+        "edges_gathered_per_step": gathered_step,
+        "edges_visited_per_step": visited_step,
+        "reference_equivalent_edges_per_s": dense_equiv * steps_per_s,
+        "reference_equivalent_note": "4*K*E per step (the reference's dense step: 2K "
+                                     "products forward, 2K backward) / this step time: NOT "
+                                     "edges traversed here",
         "dense_ms_per_step": dense_ms,
+        "dense_edges_per_s": (dense_equiv / (dense_ms / 1e3)) if dense_ms else None,
         "dense_note": "same trainer, frontier sparsity off (every SpMM over the full CSR; "
-                      "loss, gradients and updates equal): timed after the main loop",
-        "spmm_edges_per_s_kernel": (E * n_launch) / (tot_ms / 1e3) if tot_ms else None,
-        "frontier": {"enabled": not args.dense,
-                     "masked_launches_per_step": masked_n / timer_steps,
-                     "masked_ms_per_step": masked_ms / timer_steps,
-                     "full_launches_per_step": n_launch / timer_steps,
+                      "loss, gradients and updates equal): timed after the main loop; "
+                      "dense_edges_per_s = 4*K*E traversed per dense step",
+        "frontier": {"enabled": bool(trainer.frontier),
                      "full_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
                          for r, z, ms in timer.sequence("full", timer_steps)],
@@ -371,25 +542,29 @@ def main():
                          for r, z, ms in timer.sequence("adam", timer_steps)],
                      "masked_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
-                         for r, z, ms in timer.sequence("masked", timer_steps)],
-                     "note": "value counts the reference step's 4*K*E edge traversals; "
-                             "masked launches skip exact-zero / unread rows"},
-        "fused_adam_spmm": adam_info,
+                         for r, z, ms in timer.sequence("masked", timer_steps)]},
+        "spmm_ms_per_step": spmm_ms_step,
         "final_loss": final_loss,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3)",
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": tot_bytes / max(n_launch, 1),
-                     "kernel": "bbgr::spmm_kernel / spmm_pair_kernel (+fixup)", "launches": n_launch,
-                     "avg_launch_ms": tot_ms / max(n_launch, 1), "per_operator": per_kernel,
-                     "events": "inside the timed steps" if events_in_loop else
-                               f"{timer_steps} steps after the timed region (sharded step)",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch_corrected"),
+                     "kernel": "bbgr::spmm_kernel (+ spmm_fixup_kernel): full-CSR item<-user "
+                               "product, the largest share of step time",
+                     "algorithmic_bytes_per_launch": dom_bytes,
+                     "algorithmic_model": "gather model E*(4+4+4d) + R*(4+4d) (SURVEY §8(d))",
+                     "compulsory_bytes_per_launch": dom_comp,
+                     "compulsory_frac": (dom_comp / (dom_ms * 1e6) / HBM_PEAK_GBS) if dom_ms else None,
+                     "compulsory_model": "E*8 + C*4d + R*(4+4d), C = source rows (SURVEY §8(d)(ii))",
+                     "avg_launch_ms": dom_ms, "launches_per_step": dom_n,
+                     "events": ("HIP events on the launching stream, inside the timed steps"
+                                if events_in_loop else
+                                f"HIP events over {timer_steps} steps after the timed region"),
+                     "traffic_unit": "HBM bytes per launch, 2*FETCH_SIZE+WRITE_SIZE (rocprofv3 "
+                                     "PMC, gfx950 correction); counts Infinity-Cache hits",
+                     "traffic_source": None if pmc is None else
+                     {k: pmc.get(k) for k in ("tag", "commit", "kernel", "avg_us", "dispatches")},
                      "cache_assisted": achieved > HBM_PEAK_GBS,
-                     "note": "achieved = gather-model bytes (zero reuse) / launch time; above "
-                             "peak only because hot rows are served from L2 / Infinity Cache "
-                             "(degree order + streamed cold rows); `traffic` is the PMC-measured "
-                             "HBM bytes per launch"},
+                     "per_kernel": groups},
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},
     }
     print(json.dumps(out), file=out_stream, flush=True)

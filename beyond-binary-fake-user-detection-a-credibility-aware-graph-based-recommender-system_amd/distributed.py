@@ -48,7 +48,7 @@ from .optim import adam_step
 from .propagate import ORDER_GS, OperatorPair, backward, epilogue, forward, spmm
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .scatter import RowScatter
-from .trainer import VARIANTS, FusedTrainer, _internal_rows
+from .trainer import VARIANTS, FusedTrainer, _internal_rows, resolve_frontier
 
 
 def partition_users(deg_u: np.ndarray, world: int) -> np.ndarray:
@@ -326,7 +326,7 @@ class ShardedTrainer(FusedTrainer):
                  neg_mix_pop: float | None = None, neg_pop_gamma: float = 0.75,
                  neg_max_tries: int = 50, lambda_fair: float = 0.0, seed: int = 42,
                  device=None, group=None, u0=None, i0=None, user_offset: int = 0,
-                 frontier: bool = True, exchange_parts: int = 4, fuse_adam: bool = True,
+                 frontier="auto", exchange_parts: int = 4, fuse_adam: bool = True,
                  sparse_exchange: bool = True, vertex_order: str = "input",
                  frontier_parts: int = 2, native_comm: bool = False):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
@@ -423,12 +423,13 @@ class ShardedTrainer(FusedTrainer):
         self.posneg = torch.empty(2 * B, dtype=torch.int64, device=dev)
         self.pos, self.neg = self.posneg[:B], self.posneg[B:]
         self.all_items = torch.empty(2 * self.B_global, dtype=torch.int64, device=dev)
-        self.frontier = frontier
+        # one decision for every rank: the size rule on the GLOBAL edge count
+        self.frontier = resolve_frontier(frontier, int(indptr_i[-1]))
         self.mask_u = torch.zeros(num_local_users, dtype=torch.uint8, device=dev)
         self.mask_i = torch.zeros(num_items, dtype=torch.uint8, device=dev)
         self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
         # sparse frontier exchange: the step's global item frontier as a row list
-        self.sparse_exchange = bool(sparse_exchange) and frontier
+        self.sparse_exchange = bool(sparse_exchange) and self.frontier
         self.item_list = torch.empty(max(num_items, 1), dtype=torch.int64, device=dev)
         self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
         self.item_offs_host = torch.zeros(max(exchange_parts, frontier_parts) + 2,

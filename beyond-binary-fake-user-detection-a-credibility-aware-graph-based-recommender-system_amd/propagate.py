@@ -115,25 +115,61 @@ class OperatorPair:
 
 class SpmmTimer:
     """Brackets every bbgr_spmm launch (incl. its fix-up) with events on the
-    launching stream; used by bench.py inside the timed region."""
+    launching stream; used by bench.py inside the timed region. With
+    `count=True` it records no events and instead counts, on the device, the
+    rows and edges each launch actually processes (bench.py's traversed-edge
+    figure; run over extra steps outside the timed region)."""
 
-    def __init__(self):
-        self.records = []   # (n_rows, nnz, d, kind, start_event, end_event)
+    def __init__(self, count: bool = False):
+        self.count = count
+        # (rows, nnz, d, kind, start_event, end_event, table_rows, n_cols)
+        self.records = []
+        # (kind, table_rows, n_cols, d, rows_t, visited_t, gathered_t): device counts
+        self.counts = []
 
-    def summary(self, kind: str = "full"):
+    def summary(self, kind: str = "full", table_rows: int | None = None):
         """{(rows, nnz, d): (launches, total ms)} over one kind of launch:
         "full" (spmm_kernel), "masked" (frontier masks / row lists,
-        spmm_masked_kernel) or "adam" (fused Adam epilogue, spmm_adam_kernel)."""
+        spmm_masked_kernel) or "adam" (fused Adam epilogue, spmm_adam_kernel);
+        `table_rows` keeps only launches over a CSR with that many rows (the
+        item-row CSR: the item<-user products)."""
         torch.cuda.synchronize()
         out = {}
-        for rows, nnz, d, m, a, b in self.records:
-            if m != kind:
+        for rows, nnz, d, m, a, b, tr, _ in self.records:
+            if m != kind or (table_rows is not None and tr != table_rows):
                 continue
             k = (rows, nnz, d)
             n, ms = out.get(k, (0, 0.0))
             out[k] = (n + 1, ms + a.elapsed_time(b))
         return out
 
+    def groups(self):
+        """{(kind, table_rows, n_cols, d): [launches, total ms, rows, nnz]} over
+        every timed launch (rows / nnz summed over the launches: full-CSR and
+        range launches only; masked launches are data-dependent)."""
+        torch.cuda.synchronize()
+        out = {}
+        for rows, nnz, d, m, a, b, tr, nc in self.records:
+            g = out.setdefault((m, tr, nc, d), [0, 0.0, 0, 0])
+            g[0] += 1
+            g[1] += a.elapsed_time(b)
+            g[2] += rows
+            g[3] += nnz
+        return out
+
+    def edge_counts(self):
+        """{(kind, table_rows, n_cols, d): [launches, rows, visited, gathered]}
+        summed over the counted launches: `visited` = edges of the rows a launch
+        computes (index + weight read), `gathered` = those whose source row is
+        read and multiply-added (a src_mask skips exact-zero sources)."""
+        out = {}
+        for kind, tr, nc, d, r, v, g in self.counts:
+            e = out.setdefault((kind, tr, nc, d), [0, 0, 0, 0])
+            e[0] += 1
+            e[1] += int(r)
+            e[2] += int(v)
+            e[3] += int(g)
+        return out
 
     def sequence(self, kind: str, steps: int):
         """Per-position average ms of one kind of launch within a step (every
@@ -149,6 +185,32 @@ class SpmmTimer:
                      for s in range(steps)) / steps
             out.append((recs[j][0], recs[j][1], ms))
         return out
+
+    def count_launch(self, prod: "Product", kind: str, d: int, rng, src_mask, row_mask,
+                     row_list) -> None:
+        """Device-side count of the rows / edges one launch processes (stream-
+        ordered torch ops on the launch's own masks, read after the steps)."""
+        c = prod.csr
+        deg = c.__dict__.get("_deg64")
+        if deg is None:
+            deg = c.__dict__["_deg64"] = c.degrees().long()
+        if row_list is not None:
+            sel = torch.zeros(c.n_rows, dtype=torch.bool, device=c.device)
+            sel[row_list.long()] = True
+        else:
+            sel = (torch.ones(c.n_rows, dtype=torch.bool, device=c.device)
+                   if row_mask is None else row_mask[:c.n_rows].bool())
+            if rng is not None:
+                keep = torch.zeros_like(sel)
+                keep[rng[0]:rng[1]] = True
+                sel = sel & keep
+        visited = deg[sel].sum()
+        if src_mask is None:
+            gathered = visited
+        else:
+            live = src_mask[c.indices[:c.nnz].long()].bool()
+            gathered = (live & torch.repeat_interleave(sel, deg)).sum()
+        self.counts.append((kind, c.n_rows, c.n_cols, d, sel.sum(), visited, gathered))
 
 
 _timer: SpmmTimer | None = None
@@ -200,16 +262,20 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     if _timer is None:
         call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
         return
+    masked = src_mask is not None or row_mask is not None or row_list is not None
+    kind = "masked" if masked else ("adam" if adam is not None else "full")
+    if _timer.count:
+        call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
+        _timer.count_launch(prod, kind, d, rng, src_mask, row_mask, row_list)
+        return
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
     ev1.record()
-    masked = src_mask is not None or row_mask is not None or row_list is not None
-    kind = "masked" if masked else ("adam" if adam is not None else "full")
     rows, nnz = prod.csr.n_rows, prod.csr.nnz
     if rng is not None and row_list is None:   # a row range: its own rows and edges
         rows, nnz = rng[1] - rng[0], prod.csr.range_nnz(rng[0], rng[1])
-    _timer.records.append((rows, nnz, d, kind, ev0, ev1))
+    _timer.records.append((rows, nnz, d, kind, ev0, ev1, prod.csr.n_rows, prod.csr.n_cols))
 
 
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,

@@ -37,6 +37,21 @@ VARIANTS = {
     "plain": (OP_SYM, ORDER_J, 0.0),         # lightgcn.py
 }
 
+# frontier="auto": masks pay only on graphs whose full-CSR products take well
+# over the mask build (~0.05 ms of small launches). At C2 (1M edges) the masked
+# step measured 1.092 ms against 1.058 dense (profiles/r08_c2_bench.json); at
+# C4 (50M) 17.0 against 23.5. Below this many edges the step runs dense.
+FRONTIER_MIN_EDGES = 4_000_000
+
+
+def resolve_frontier(frontier, nnz: int) -> bool:
+    """`frontier` as given, or the size rule for "auto"."""
+    if isinstance(frontier, str):
+        if frontier != "auto":
+            raise ValueError(f"frontier must be True, False or 'auto', got {frontier!r}")
+        return nnz >= FRONTIER_MIN_EDGES
+    return bool(frontier)
+
 
 class FusedTrainer:
     def __init__(self, graph: BipartiteGraph, variant: str = "v2_pop", cred=None,
@@ -44,7 +59,7 @@ class FusedTrainer:
                  reg: float = 1e-4, batch_size: int = 4096, neg_mix_pop: float | None = None,
                  neg_pop_gamma: float = 0.75, neg_max_tries: int = 50,
                  lambda_fair: float = 0.0, seed: int = 42, u0=None, i0=None,
-                 frontier: bool = True, fuse_adam: bool = True):
+                 frontier="auto", fuse_adam: bool = True):
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}; one of {sorted(VARIANTS)}")
@@ -111,7 +126,7 @@ class FusedTrainer:
         # node) restrict the last forward layer to the rows it feeds and let the
         # first backward products skip exact-zero source rows. Loss, gradients
         # and updates are bitwise identical to the dense step (tested).
-        self.frontier = frontier
+        self.frontier = resolve_frontier(frontier, graph.item_csr.nnz)
         self.mask_u = torch.zeros(self.U, dtype=torch.uint8, device=dev)
         self.mask_i = torch.zeros(self.I, dtype=torch.uint8, device=dev)
         # Fused optimizer (GS order): the user Adam runs inside the last backward

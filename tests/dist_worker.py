@@ -81,7 +81,7 @@ def fused_vs_separate(out_dir, variant):
         for sparse in (False, True):
             tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3,
                                 batch_size=32, device="cuda:0", u0=u0, i0=i0,
-                                user_offset=rank * WEAK_U, exchange_parts=2, fuse_adam=fuse,
+                                user_offset=rank * WEAK_U, exchange_parts=2, fuse_adam=fuse, frontier=True,
                                 sparse_exchange=sparse)
             losses = [float(tr.step()) for _ in range(3)]
             tag = f"{'fused' if fuse else 'sep'}_{'sparse' if sparse else 'dense'}"
@@ -108,7 +108,7 @@ def rccl_single_rank(out_dir, variant, order="input"):
     rng = np.random.default_rng(3)
     u0 = rng.uniform(-0.5, 0.5, (U, 64)).astype(np.float32)
     i0 = rng.uniform(-0.5, 0.5, (I, 64)).astype(np.float32)
-    kw = dict(emb_dim=64, num_layers=3, batch_size=256, u0=u0, i0=i0)
+    kw = dict(emb_dim=64, num_layers=3, batch_size=256, u0=u0, i0=i0, frontier=True)
     sh = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
                         vertex_order=order, **kw)
     one = FusedTrainer(BipartiteGraph(e, U, I, "cuda:0", vertex_order=order), variant, **kw)

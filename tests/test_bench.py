@@ -1,0 +1,94 @@
+"""CPU: bench.py's accounting — the roofline groups (gather / compulsory
+models, dominant-kernel selection inputs) and the reference CPU baseline's
+sampled timing path on a small graph. No kernel launches."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+@pytest.fixture(scope="module")
+def bench():
+    argv, sys.argv = sys.argv, ["bench.py"]
+    try:
+        import bench as b
+    finally:
+        sys.argv = argv
+    return b
+
+
+class _Ev:
+    def __init__(self, t):
+        self.t = t
+
+    def elapsed_time(self, other):
+        return other.t - self.t
+
+
+class _FakeTimer:
+    """SpmmTimer.groups() over hand-made records (no torch.cuda)."""
+
+    def __init__(self, records):
+        self.records = records
+
+    def groups(self):
+        out = {}
+        for rows, nnz, d, m, a, b, tr, nc in self.records:
+            g = out.setdefault((m, tr, nc, d), [0, 0.0, 0, 0])
+            g[0] += 1
+            g[1] += a.elapsed_time(b)
+            g[2] += rows
+            g[3] += nnz
+        return out
+
+
+def test_roofline_groups_models(bench):
+    I, U, E, d = 1000, 5000, 50000, 64
+    recs = []
+    for s in range(2):   # two steps: one item and one user full launch, one masked
+        recs.append((I, E, d, "full", _Ev(0.0), _Ev(0.5), I, U))
+        recs.append((U, E, d, "full", _Ev(0.0), _Ev(0.25), U, I))
+        recs.append((U, E, d, "masked", _Ev(0.0), _Ev(0.1), U, I))
+    counts = {("masked", U, I, d): [4, 4 * 100, 4 * 1000, 4 * 600]}
+    gs = bench.roofline_groups(_FakeTimer(recs), counts, steps=2, count_steps=4, n_items=I)
+    by = {(g["kind"], g["side"]): g for g in gs}
+    item = by[("full", "item<-user")]
+    assert item["launches_per_step"] == 1 and item["avg_ms"] == pytest.approx(0.5)
+    assert item["gather_model_bytes"] == E * (8 + 4 * d) + I * (4 + 4 * d)
+    assert item["compulsory_bytes"] == E * 8 + U * 4 * d + I * (4 + 4 * d)
+    assert item["gather_model_GBps"] == pytest.approx(item["gather_model_bytes"] / 0.5e6)
+    user = by[("full", "user<-item")]
+    assert user["cache_assisted"] == (user["gather_model_frac"] > 1.0)
+    m = by[("masked", "user<-item")]
+    assert m["rows_per_launch"] == 100 and m["edges_gathered_per_launch"] == 600
+    assert m["gather_model_bytes"] == 1000 * 8 + 600 * 4 * d + 100 * (4 + 4 * d)
+
+
+def test_cpu_baseline_small_graph(bench):
+    """The sampled-product baseline runs end to end and scales each sampled
+    product by its own edge fraction; the whole-step timing uses the
+    reference-style step (sampler loop + torch autograd + Adam)."""
+    from bbgr.synthetic import synthetic_credibility, synthetic_edges
+    U, I, E = 4000, 1000, 40000
+    cfg = dict(num_users=U, num_items=I, num_edges=E, emb_dim=16, num_layers=2, batch=256)
+    e = synthetic_edges(U, I, E, seed=3, items="zipf")
+    r = bench.cpu_baseline(e, cfg, "X", synthetic_credibility(U, 3), every=4, reps=2,
+                           whole_steps=("C1",))
+    assert r["kind"] == "port" and r["unit"] == "edges/s" and r["cores"] >= 1
+    comp = r["components_s"]
+    assert all(v > 0 for v in comp.values())
+    K = 2   # the four products run once per layer
+    step = K * (comp["fwd_item_from_user"] + comp["fwd_user_from_item"] + comp["bwd_grad_u"]
+                + comp["bwd_grad_i"]) + comp["adam"] + comp["sampler"]
+    assert r["value"] == pytest.approx(4 * 2 * E / step, rel=1e-9)
+    assert r["whole_step_s"]["C1"]["median"] > 0 and len(r["whole_step_s"]["C1"]["runs"]) == 2
+
+
+def test_median_uses_returned_interval(bench):
+    t, ts = bench._median_s(lambda: 2.0, reps=3, warmup=1)
+    assert t == 2.0 and ts == [2.0, 2.0, 2.0]
+    assert np.isfinite(bench._median_s(lambda: None, reps=1)[0])

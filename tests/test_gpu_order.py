@@ -117,7 +117,7 @@ def test_ordered_trainer_step_vs_oracle(variant):
     lam = 0.05 if variant == "cu_fair" else 0.0
     g = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
     tr = FusedTrainer(g, variant, cred=cred, emb_dim=d, num_layers=K, batch_size=256,
-                      u0=u0, i0=i0, lambda_fair=lam)
+                      u0=u0, i0=i0, lambda_fair=lam, frontier=True)
     deg_u = np.bincount(e[0], minlength=U)
     users_in = np.flatnonzero(deg_u > 0)[::4][:256]
     loss = float(tr.step(t(users_in, torch.int64)))
@@ -168,7 +168,7 @@ def test_default_init_is_the_same_model_in_both_orders():
     e = synthetic_edges(U, I, 25000, 8, items="zipf")
     cred = synthetic_credibility(U, 8)
     trs = [FusedTrainer(BipartiteGraph(e, U, I, DEV, vertex_order=o), "v2_pop", cred=cred,
-                        emb_dim=d, num_layers=3, batch_size=300) for o in ("input", "degree")]
+                        emb_dim=d, num_layers=3, batch_size=300, frontier=True) for o in ("input", "degree")]
     sd = [tr.state_dict() for tr in trs]
     for k in sd[0]:
         assert torch.equal(sd[0][k], sd[1][k])
@@ -194,7 +194,8 @@ def test_ordered_graph_edge_cases():
     rng = np.random.default_rng(0)
     u0 = rng.normal(size=(U, 64)).astype(np.float32)
     i0 = rng.normal(size=(I, 64)).astype(np.float32)
-    tr = FusedTrainer(g, "cu_message", emb_dim=64, num_layers=2, batch_size=64, u0=u0, i0=i0)
+    tr = FusedTrainer(g, "cu_message", emb_dim=64, num_layers=2, batch_size=64, u0=u0, i0=i0,
+                      frontier=True)
     sd = tr.state_dict()
     np.testing.assert_array_equal(sd["user_emb.weight"].cpu().numpy(), u0)
     np.testing.assert_array_equal(sd["item_emb.weight"].cpu().numpy(), i0)

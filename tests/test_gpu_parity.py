@@ -388,7 +388,8 @@ def test_fused_trainer_step_vs_oracle(gold, variant):
     g = BipartiteGraph(e, U, I, DEV)
     lam = 0.05 if variant == "cu_fair" else 0.0
     tr = FusedTrainer(g, variant, cred=cred, emb_dim=D, num_layers=K, batch_size=B,
-                      lambda_fair=lam, u0=gold["u0"], i0=gold["i0"], fuse_adam=False)
+                      lambda_fair=lam, u0=gold["u0"], i0=gold["i0"], fuse_adam=False,
+                      frontier=True)
     deg_u = np.bincount(e[0], minlength=U)
     uu = np.unique(gold["users"])
     users = t(uu[deg_u[uu] > 0], torch.int64)       # train users have >= 1 positive
@@ -619,7 +620,7 @@ def test_fused_adam_step_matches_unfused(variant, K):
     u0 = rng.uniform(-0.05, 0.05, (U, 64)).astype(np.float32)
     i0 = rng.uniform(-0.05, 0.05, (I, 64)).astype(np.float32)
     kw = dict(cred=synthetic_credibility(U, 2), emb_dim=64, num_layers=K, batch_size=4096,
-              u0=u0, i0=i0)
+              u0=u0, i0=i0, frontier=True)
     sep = FusedTrainer(g, variant, fuse_adam=False, **kw)
     fus = FusedTrainer(g, variant, fuse_adam=True, **kw)
     assert fus.fuse_adam and not sep.fuse_adam   # Jacobi: both Adams fused (K >= 2)
@@ -695,7 +696,7 @@ def test_training_step_is_bitwise_reproducible():
     U, I = c["num_users"], c["num_items"]
     g = BipartiteGraph(config_edges("C2"), U, I, DEV)
     kw = dict(cred=synthetic_credibility(U, 2), emb_dim=64, num_layers=3, batch_size=4096,
-              seed=9)
+              seed=9, frontier=True)
     a, b = FusedTrainer(g, "v2_pop", **kw), FusedTrainer(g, "v2_pop", **kw)
     for _ in range(3):
         assert float(a.step()) == float(b.step())

@@ -68,17 +68,28 @@ def main(tag: str):
                                      for k, v in stats.items()},
                "kernels": kernels}
     json.dump(summary, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
-    # the full-CSR launches (bench.py's roofline kernel): one-row-per-group
-    # (item rows) and two-rows-per-group (user rows) symbols
-    full = ("spmm_kernel", "spmm_pair_kernel")
-    spmm = [e for e in kernels.values()
-            if e["kernel"] in full and "hbm_bytes_corrected" in e]
-    if spmm:
-        n = sum(e["dispatches"] for e in spmm)
-        avg = sum(e["hbm_bytes_corrected"] * e["dispatches"] for e in spmm) / n
-        json.dump({"tag": tag, "kernel": "spmm_kernel + spmm_pair_kernel",
+    # bench.py's roofline kernel: the full-CSR item<-user product, symbol
+    # spmm_kernel (one row per 16-lane group; the user-row products are
+    # spmm_pair_kernel, the frontier ones spmm_masked_*, the fused-Adam one
+    # spmm_adam_*). Its per-launch PMC bytes feed roofline.traffic; the commit
+    # the profile was taken at travels with it (BBGR_COMMIT, set by the caller:
+    # the GPU box has no .git).
+    dom = [e for e in kernels.values()
+           if e["kernel"] == "spmm_kernel" and "hbm_bytes_corrected" in e]
+    if dom:
+        n = sum(e["dispatches"] for e in dom)
+        avg = sum(e["hbm_bytes_corrected"] * e["dispatches"] for e in dom) / n
+        avg_us = sum(e["avg_us"] * e["dispatches"] for e in dom) / n
+        json.dump({"tag": tag, "commit": os.environ.get("BBGR_COMMIT"),
+                   "kernel": "spmm_kernel (full-CSR item<-user product)",
                    "hbm_bytes_per_launch_corrected": avg,
-                   "per_grid": {f'{e["kernel"]}@{e["grid"]}': e["hbm_bytes_corrected"] for e in spmm},
+                   "fetch_KiB_per_launch": sum(e["FETCH_SIZE_KiB"] * e["dispatches"]
+                                               for e in dom) / n,
+                   "write_KiB_per_launch": sum(e["WRITE_SIZE_KiB"] * e["dispatches"]
+                                               for e in dom) / n,
+                   "avg_us": avg_us, "dispatches": n,
+                   "per_grid": {f'{e["kernel"]}@{e["grid"]}': e["hbm_bytes_corrected"]
+                                for e in dom},
                    "source": f"profiles/{tag}_summary.json"},
                   open(os.path.join(dst, "spmm_traffic.json"), "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
