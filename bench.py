@@ -228,12 +228,13 @@ def roofline_groups(timer, counts, steps: int, count_steps: int, n_items: int):
     Full-CSR / range launches take their bytes from the CSR; masked launches
     from the rows / edges counted on the device over `count_steps` extra steps."""
     out = []
-    for (kind, tr, nc, d), (n, ms, rows, nnz) in sorted(timer.groups().items()):
+    for (kind, sig, tr, nc, d), (n, ms, rows, nnz) in sorted(timer.groups().items()):
         side = "item<-user" if tr == n_items else "user<-item"
         e = {"kind": kind, "side": side, "d": d, "launches_per_step": n / steps,
              "avg_ms": ms / n}
         if kind == "masked":
-            c = counts.get((kind, tr, nc, d))
+            e["masks"] = sig
+            c = counts.get((kind, sig, tr, nc, d))
             if not c:
                 continue
             cn, crows, cvis, cgat = c
@@ -286,6 +287,10 @@ def main():
                     help="disable exact frontier sparsity (every SpMM over the full CSR)")
     ap.add_argument("--frontier", default="auto", choices=["auto", "on", "off"],
                     help="frontier masks: auto = the trainer's size rule")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="single GPU: replay the step as one captured HIP graph "
+                         "(trainer.GraphedStep); auto = on below the frontier size rule's "
+                         "edge count (launch-bound small graphs)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU trainer (torch.distributed) even at N=1: "
                          "measures the sharded step's own overhead, collectives included")
@@ -401,8 +406,15 @@ def main():
     log(f"[bench] rank {rank}: setup done, E={E} (local {E_local}), frontier="
         f"{trainer.frontier}, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
 
+    from bbgr.trainer import FRONTIER_MIN_EDGES
+    use_graph = not dist_mode and (args.graph == "on" or (args.graph == "auto"
+                                                          and E < FRONTIER_MIN_EDGES))
+    step_fn = trainer.step
+    if use_graph:
+        from bbgr.trainer import GraphedStep
+        step_fn = GraphedStep(trainer).step
     for _ in range(args.warmup):
-        trainer.step()
+        step_fn()
     timer = P.SpmmTimer()
     if dist_mode:
         torch.distributed.barrier()
@@ -412,12 +424,14 @@ def main():
     # between launches interleave with the collectives' cross-stream waits and
     # cost 1.4-3 ms/step, so there the events are recorded over
     # `--roofline-steps` extra steps right after the timed region instead.
-    events_in_loop = not dist_mode
+    # A captured graph replays its launches without the host: its per-launch
+    # events are taken over eager steps after the timed region, as for sharded.
+    events_in_loop = not dist_mode and not use_graph
     if events_in_loop:
         P.set_spmm_timer(timer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = trainer.step()
+        loss = step_fn()
     torch.cuda.synchronize()
     if dist_mode:
         torch.distributed.barrier()
@@ -517,6 +531,7 @@ def main():
                    "parallelism": f"user-rows x{world}"
                                   + (" (sharded trainer)" if dist_mode and world == 1 else "")},
         "bpr_steps_per_s": steps_per_s,
+        "graph_replay": use_graph,
         "value_note": "value = SpMM edges actually gathered (source row read and "
                       "multiply-added) per second, whole job: every launch's edges counted "
                       f"on the device over {count_steps} steps after the timed region "
@@ -558,7 +573,9 @@ def main():
                      "avg_launch_ms": dom_ms, "launches_per_step": dom_n,
                      "events": ("HIP events on the launching stream, inside the timed steps"
                                 if events_in_loop else
-                                f"HIP events over {timer_steps} steps after the timed region"),
+                                f"HIP events over {timer_steps} eager steps after the timed "
+                                "region" + (" (timed steps are graph replays)" if use_graph
+                                            else "")),
                      "traffic_unit": "HBM bytes per launch, 2*FETCH_SIZE+WRITE_SIZE (rocprofv3 "
                                      "PMC, gfx950 correction); counts Infinity-Cache hits",
                      "traffic_source": None if pmc is None else

@@ -84,6 +84,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_beta2", c_float), ("adam_eps", c_float), ("adam_weight_decay", c_float),
         ("adam_bias_correction1", c_float), ("adam_bias_correction2_sqrt", c_float),
         ("stream_from", c_int32), ("stream_out_from", c_int32),
+        ("adam_bc_table", c_void_p), ("adam_state", c_void_p),
     ]
 
 
@@ -147,6 +148,9 @@ _SIGNATURES = {
     "bbgr_bpr_reduce": ([c_int64, _P, c_float, c_float, _P, _P], c_int32),
     "bbgr_adam": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
                    c_float, c_float, c_float, c_float, _P], c_int32),
+    "bbgr_adam_dev": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
+                       c_float, c_float, _P, _P, _P], c_int32),
+    "bbgr_step_begin": ([_P, _P], c_int32),
     "bbgr_mark_rows": ([c_int64, _P, ctypes.c_uint8, _P, c_int64, _P], c_int32),
     "bbgr_comm_unique_id": ([_P], c_int32),
     "bbgr_comm_init": ([_P, c_int32, c_int32, _P], c_int32),
@@ -165,6 +169,8 @@ _SIGNATURES = {
                      c_int32),
     "bbgr_sample": ([c_int64, _P, _P, _P, c_int32, _P, c_float, c_int32, c_uint64,
                      c_uint64, _P, _P, _P, _P], c_int32),
+    "bbgr_sample_dev": ([c_int64, _P, _P, _P, c_int32, _P, c_float, c_int32, c_uint64,
+                         _P, _P, _P, _P, _P], c_int32),
     "bbgr_shuffle": ([c_int64, _P, _P, c_uint64, c_uint64, _P,
                       ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_eval_sampled": ([ctypes.POINTER(EvalArgs), _P, ctypes.POINTER(c_size_t), _P],
@@ -199,7 +205,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 2:
+        if handle.bbgr_abi_version() != 3:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

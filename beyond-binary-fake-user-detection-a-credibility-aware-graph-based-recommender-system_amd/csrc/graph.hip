@@ -196,10 +196,12 @@ __device__ __forceinline__ int cdf_search(const double *cdf, int n, double u) {
 __global__ void sample_kernel(long batch, const long *users, const int *indptr,
                               const int *indices, int n_items, const double *cdf,
                               float mix_pop, int max_tries, unsigned long long seed,
-                              unsigned long long counter, long *pos, long *neg,
-                              int *fail_count) {
+                              unsigned long long counter0, const long *state, long *pos,
+                              long *neg, int *fail_count) {
   const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= batch) return;
+  // captured steps read this step's counter from the device step state
+  const unsigned long long counter = state ? (unsigned long long)state[1] : counter0;
   const long u = users[b];
   const int rb = indptr[u], re = indptr[u + 1];
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -532,12 +534,11 @@ extern "C" int bbgr_pop_cdf(int32_t n_items, const int32_t *indptr_i,
   return BBGR_OK;
 }
 
-extern "C" int bbgr_sample(int64_t batch, const int64_t *users,
-                           const int32_t *indptr, const int32_t *indices,
-                           int32_t n_items, const double *cdf, float mix_pop,
-                           int32_t max_tries, uint64_t seed, uint64_t counter,
-                           int64_t *pos, int64_t *neg, int32_t *fail_count,
-                           bbgr_stream_t stream) {
+static int sample_launch(int64_t batch, const int64_t *users, const int32_t *indptr,
+                         const int32_t *indices, int32_t n_items, const double *cdf,
+                         float mix_pop, int32_t max_tries, uint64_t seed, uint64_t counter,
+                         const int64_t *state, int64_t *pos, int64_t *neg,
+                         int32_t *fail_count, bbgr_stream_t stream) {
   BBGR_REQUIRE(batch >= 0 && n_items > 0 && max_tries >= 0, "bbgr_sample: bad sizes");
   if (batch == 0) return BBGR_OK;
   BBGR_REQUIRE(users && indptr && indices && pos && neg, "bbgr_sample: null arrays");
@@ -545,9 +546,30 @@ extern "C" int bbgr_sample(int64_t batch, const int64_t *users,
                      as_stream(stream), (long)batch, (const long *)users, indptr,
                      indices, n_items, cdf, mix_pop, max_tries,
                      (unsigned long long)seed, (unsigned long long)counter,
-                     (long *)pos, (long *)neg, fail_count);
+                     (const long *)state, (long *)pos, (long *)neg, fail_count);
   BBGR_LAUNCHED("sample_kernel");
   return BBGR_OK;
+}
+
+extern "C" int bbgr_sample(int64_t batch, const int64_t *users,
+                           const int32_t *indptr, const int32_t *indices,
+                           int32_t n_items, const double *cdf, float mix_pop,
+                           int32_t max_tries, uint64_t seed, uint64_t counter,
+                           int64_t *pos, int64_t *neg, int32_t *fail_count,
+                           bbgr_stream_t stream) {
+  return sample_launch(batch, users, indptr, indices, n_items, cdf, mix_pop, max_tries, seed,
+                       counter, nullptr, pos, neg, fail_count, stream);
+}
+
+extern "C" int bbgr_sample_dev(int64_t batch, const int64_t *users,
+                               const int32_t *indptr, const int32_t *indices,
+                               int32_t n_items, const double *cdf, float mix_pop,
+                               int32_t max_tries, uint64_t seed, const int64_t *state,
+                               int64_t *pos, int64_t *neg, int32_t *fail_count,
+                               bbgr_stream_t stream) {
+  BBGR_REQUIRE(state, "bbgr_sample_dev: null state");
+  return sample_launch(batch, users, indptr, indices, n_items, cdf, mix_pop, max_tries, seed,
+                       0, state, pos, neg, fail_count, stream);
 }
 
 extern "C" int bbgr_shuffle(int64_t n, const int64_t *in, int64_t *out,

@@ -64,10 +64,15 @@ struct SpmmParams {
   int chunk_begin;             // first long-row chunk of this launch
   int nt_from;                 // source rows >= nt_from: streaming loads (args.stream_from)
   int nt_out_from;             // output rows >= nt_out_from: streaming stores (args.stream_out_from)
+  int chunk_edges;             // plan chunk size (a split row has ceil(deg / chunk_edges) chunks)
+  int *arrivals;               // per-chunk arrival counters (after the partials), zero between launches
   // fused Adam on the y-row value (bbgr_spmm_args.adam_*)
   float *adam_p, *adam_m, *adam_v;
   long adam_ld;
   AdamConsts adam;
+  float adam_lr;
+  const float *adam_bc;        // device step state (nullable): bias corrections by step t
+  const long *adam_state;
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -318,10 +323,23 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
 
 // torch.optim.Adam on one row held by a 16-lane group: the same expression
 // order as adam_kernel (train.hip), so fused and separate steps agree bitwise.
+// The Adam constants of this launch: the host's, or (captured steps) the step
+// t in device memory with the bias corrections of the host-built table.
+__device__ __forceinline__ AdamConsts launch_adam_consts(const SpmmParams &P) {
+  AdamConsts c = P.adam;
+  if (P.adam_state) {
+    const long t = P.adam_state[0];
+    c.step = P.adam_lr / P.adam_bc[2 * (t - 1)];
+    c.bc2s = P.adam_bc[2 * (t - 1) + 1];
+  }
+  return c;
+}
+
 template <int D>
 __device__ __forceinline__ void adam_row(const SpmmParams &P, int row, int lane,
                                          const float4 (&G)[D / 64]) {
   constexpr int V = D / 64;
+  const AdamConsts ac = launch_adam_consts(P);
   float4 *pp = reinterpret_cast<float4 *>(P.adam_p + (long)row * P.adam_ld) + lane;
   float4 *pm = reinterpret_cast<float4 *>(P.adam_m + (long)row * P.adam_ld) + lane;
   float4 *pv = reinterpret_cast<float4 *>(P.adam_v + (long)row * P.adam_ld) + lane;
@@ -331,10 +349,10 @@ __device__ __forceinline__ void adam_row(const SpmmParams &P, int row, int lane,
     float4 p4 = pp[16 * k];
     float4 m4 = ntm ? ld_nt(pm + 16 * k) : pm[16 * k];
     float4 v4 = ntm ? ld_nt(pv + 16 * k) : pv[16 * k];
-    adam_elem(p4.x, G[k].x, m4.x, v4.x, P.adam);
-    adam_elem(p4.y, G[k].y, m4.y, v4.y, P.adam);
-    adam_elem(p4.z, G[k].z, m4.z, v4.z, P.adam);
-    adam_elem(p4.w, G[k].w, m4.w, v4.w, P.adam);
+    adam_elem(p4.x, G[k].x, m4.x, v4.x, ac);
+    adam_elem(p4.y, G[k].y, m4.y, v4.y, ac);
+    adam_elem(p4.z, G[k].z, m4.z, v4.z, ac);
+    adam_elem(p4.w, G[k].w, m4.w, v4.w, ac);
     if (row >= P.nt_out_from) st_nt(pp + 16 * k, p4);
     else pp[16 * k] = p4;
     if (ntm) {
@@ -413,6 +431,76 @@ __device__ __forceinline__ void block_reduce16(float4 *red, int g, int lane,
   __syncthreads();
 }
 
+// Fixed-order sum of a split row's chunk partials (slots base .. base+c-1):
+// group g adds slots g, g+16, ... in order, then the 16 group sums are added
+// in group order (block_reduce16); g == 0 runs the epilogue.
+template <int D>
+__device__ __forceinline__ void split_row_finish(const SpmmParams &P, int row, int base, int c,
+                                                 float4 *red, int g, int lane) {
+  constexpr int V = D / 64;
+  float4 acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sl = g; sl < c; sl += 16) {
+    const float4 *src =
+        reinterpret_cast<const float4 *>(P.partial) + (long)(base + sl) * (D / 4) + lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = f4_add(acc[k], src[16 * k]);
+  }
+  block_reduce16<D>(red, g, lane, acc);
+  if (g == 0) {
+    float4 T[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
+    epilogue<D>(P, row, lane, T);
+  }
+}
+
+// A chunk of a row cut into c > 1 chunks: publish this chunk's partial; the
+// last chunk of the row to arrive sums them all (split_row_finish) in this
+// launch. Hand-off per cdna_hip_programming.md (in-launch split reduction):
+// plain stores -> drain -> barrier -> one agent-scope release -> ticket
+// fetch_add (agent scope); the drawer of ticket c-1 takes one agent-scope
+// acquire before the workgroup reads the slots. The ticket counter lives at
+// arrivals[base] (base = the row's first chunk) and the reducer re-zeroes it.
+template <int D>
+__device__ __forceinline__ void split_row_arrive(const SpmmParams &P, int4 ch, float4 *red,
+                                                 int g, int lane) {
+  constexpr int V = D / 64;
+  if (g == 0) {
+    float4 *dst = reinterpret_cast<float4 *>(P.partial) + (long)ch.w * (D / 4) + lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) dst[16 * k] = red[lane + 16 * k];
+  }
+  // chunk j of c (plan_fill_kernel: chunk j starts at eb + floor(len*j/c)),
+  // slot = base + j
+  const int eb = P.indptr[ch.x];
+  const long len = (long)P.indptr[ch.x + 1] - eb;
+  const int c = (int)((len + P.chunk_edges - 1) / P.chunk_edges);
+  const int j = (int)(((long)(ch.y - eb) * c + len - 1) / len);
+  const int base = ch.w - j;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave has read red[] and drained its stores
+  int *flag = reinterpret_cast<int *>(red);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ticket =
+        __hip_atomic_fetch_add(P.arrivals + base, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = ticket == c - 1;
+    if (last) {
+      __hip_atomic_store(P.arrivals + base, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  const int last = flag[0];
+  __syncthreads();   // flag read before split_row_finish reuses red[]
+  if (last) split_row_finish<D>(P, ch.x, base, c, red, g, lane);
+}
+
 template <int D, int WMODE, bool MASKED, bool PAIR>
 __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   constexpr int V = D / 64;
@@ -434,18 +522,16 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     const int ge = min(ch.z, gb + per);
     if (gb < ge) gather_range<D, WMODE, MASKED>(P, gb, ge, lane, acc);
     block_reduce16<D>(red, g, lane, acc);
-    if (g == 0) {
-      float4 T[V];
+    if (ch.w < 0) {   // the row's only chunk
+      if (g == 0) {
+        float4 T[V];
 #pragma unroll
-      for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
-      if (ch.w < 0) {
+        for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
         epilogue<D>(P, ch.x, lane, T);
-      } else {
-        float4 *dst = reinterpret_cast<float4 *>(P.partial) + (long)ch.w * (D / 4) + lane;
-#pragma unroll
-        for (int k = 0; k < V; ++k) dst[16 * k] = T[k];
       }
+      return;
     }
+    split_row_arrive<D>(P, ch, red, g, lane);
     return;
   }
 
@@ -537,33 +623,6 @@ __global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves) void spmm_adam
   spmm_body<D, WMODE, false, true>(P);
 }
 
-// Rows split into >1 chunk: sum chunk partials in chunk order, then epilogue.
-template <int D>
-__global__ __launch_bounds__(256) void spmm_fixup_kernel(SpmmParams P) {
-  constexpr int V = D / 64;
-  __shared__ float4 red[16 * (D / 4)];
-  const int g = threadIdx.x >> 4;
-  const int lane = threadIdx.x & 15;
-  const int4 sp = P.split[blockIdx.x];  // row, slot_begin, n_slots
-  if (P.row_mask && !P.row_mask[sp.x]) return;
-  float4 acc[V];
-#pragma unroll
-  for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int sl = g; sl < sp.z; sl += 16) {
-    const float4 *src =
-        reinterpret_cast<const float4 *>(P.partial) + (long)(sp.y + sl) * (D / 4) + lane;
-#pragma unroll
-    for (int k = 0; k < V; ++k) acc[k] = f4_add(acc[k], src[16 * k]);
-  }
-  block_reduce16<D>(red, g, lane, acc);
-  if (g == 0) {
-    float4 T[V];
-#pragma unroll
-    for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
-    epilogue<D>(P, sp.x, lane, T);
-  }
-}
-
 template <int D>
 __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float *t,
                                                        long ldt) {
@@ -607,11 +666,7 @@ static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
     }
     BBGR_LAUNCHED("spmm_kernel");
   }
-  if (n_split > 0) {
-    hipLaunchKernelGGL((spmm_fixup_kernel<D>), dim3((unsigned)n_split),
-                       dim3(256), 0, st, P);
-    BBGR_LAUNCHED("spmm_fixup_kernel");
-  }
+  (void)n_split;   // split rows are finished in-launch (split_row_arrive)
   return BBGR_OK;
 }
 
@@ -666,16 +721,24 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.adam_m = a->adam_exp_avg;
   P.adam_v = a->adam_exp_avg_sq;
   P.adam_ld = a->adam_ld;
+  P.adam_lr = a->adam_lr;
+  P.adam_bc = a->adam_bc_table;
+  P.adam_state = (const long *)a->adam_state;
+  // with device step state the bias corrections come from the table (set
+  // per launch from state[0]); 1.0 keeps the host-side constants finite
+  const bool dev = a->adam_state != nullptr;
   P.adam = adam_consts(a->adam_lr, a->adam_beta1, a->adam_beta2, a->adam_eps,
-                       a->adam_weight_decay, a->adam_bias_correction1,
-                       a->adam_bias_correction2_sqrt);
+                       a->adam_weight_decay, dev ? 1.f : a->adam_bias_correction1,
+                       dev ? 1.f : a->adam_bias_correction2_sqrt);
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {
   if (!a->adam_param) return true;
+  const bool dev = a->adam_state != nullptr;
   return a->adam_exp_avg && a->adam_exp_avg_sq && ld_ok(a->adam_param, a->adam_ld, d) &&
          ld_ok(a->adam_exp_avg, a->adam_ld, d) && ld_ok(a->adam_exp_avg_sq, a->adam_ld, d) &&
-         a->adam_bias_correction1 > 0.f && a->adam_bias_correction2_sqrt > 0.f;
+         (dev ? a->adam_bc_table != nullptr
+              : (a->adam_bias_correction1 > 0.f && a->adam_bias_correction2_sqrt > 0.f));
 }
 
 extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
@@ -741,7 +804,7 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   BBGR_REQUIRE(csr->n_chunks == 0 || csr->long_threshold > 0,
                "bbgr_spmm: plan without long_threshold");
 
-  SpmmParams P;
+  SpmmParams P = {};
   P.n_rows = csr->n_rows;
   P.long_threshold = csr->n_chunks ? csr->long_threshold : 0x7fffffff;
   P.n_chunks = csr->n_chunks;
@@ -756,6 +819,9 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   P.col_scale_s = a->col_scale_s;
   fill_epilogue(P, a);
   P.partial = a->partial;
+  P.chunk_edges = csr->chunk_edges > 0 ? csr->chunk_edges : 2048;
+  P.arrivals = a->partial ? reinterpret_cast<int *>(a->partial + (long)csr->n_chunks * d)
+                          : nullptr;
   P.src_mask = a->src_mask;
   P.row_mask = a->row_mask;
   P.row_list = (const long *)a->row_list;

@@ -200,9 +200,23 @@ __global__ __launch_bounds__(256) void bpr_reduce_kernel(long batch,
 
 // torch.optim.Adam (single-tensor/foreach math), float4 vectorised; the
 // per-element update is adam_elem (common.h), shared with the fused epilogue.
+// Step t from device memory (captured steps): the bias corrections come from
+// the host-built table, so the constants equal the host's bit for bit.
+__device__ __forceinline__ AdamConsts device_step_consts(AdamConsts c, float lr,
+                                                         const float *bc, const long *state) {
+  if (state) {
+    const long t = state[0];
+    c.step = lr / bc[2 * (t - 1)];
+    c.bc2s = bc[2 * (t - 1) + 1];
+  }
+  return c;
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(long n4, float4 *p, const float4 *g,
-                                                   float4 *m, float4 *v, AdamConsts c,
-                                                   float gs) {
+                                                   float4 *m, float4 *v, AdamConsts c0,
+                                                   float gs, float lr, const float *bc,
+                                                   const long *state) {
+  const AdamConsts c = device_step_consts(c0, lr, bc, state);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
@@ -217,10 +231,21 @@ __global__ __launch_bounds__(256) void adam_kernel(long n4, float4 *p, const flo
 }
 
 __global__ void adam_tail_kernel(long n, long start, float *p, const float *g, float *m,
-                                 float *v, AdamConsts c, float gs) {
+                                 float *v, AdamConsts c0, float gs, float lr, const float *bc,
+                                 const long *state) {
   const long i = start + (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const AdamConsts c = device_step_consts(c0, lr, bc, state);
   adam_elem(p[i], gs * g[i], m[i], v[i], c);
+}
+
+// bbgr_step_begin: state = {t, counter, next counter}; one lane.
+__global__ void step_begin_kernel(long *state) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const long t = state[0], next = state[2];
+  state[0] = t + 1;
+  state[1] = next;
+  state[2] = next + 1;
 }
 
 __global__ void rows_zero_kernel(long n, const long *idx, float *t, long ld,
@@ -441,15 +466,11 @@ extern "C" int bbgr_bpr_reduce(int64_t batch, const float *parts, float reg,
   return BBGR_OK;
 }
 
-extern "C" int bbgr_adam(int64_t n, float *param, const float *grad,
-                         float *exp_avg, float *exp_avg_sq, float lr, float beta1,
-                         float beta2, float eps, float weight_decay, float grad_scale,
-                         float bias_correction1, float bias_correction2_sqrt,
-                         bbgr_stream_t stream) {
-  BBGR_REQUIRE(n >= 0, "bbgr_adam: negative n");
-  if (n == 0) return BBGR_OK;
-  BBGR_REQUIRE(param && grad && exp_avg && exp_avg_sq, "bbgr_adam: null tensor");
-  hipStream_t st = as_stream(stream);
+static int adam_launch(int64_t n, float *param, const float *grad, float *exp_avg,
+                       float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                       float weight_decay, float grad_scale, float bias_correction1,
+                       float bias_correction2_sqrt, const float *bc, const long *state,
+                       hipStream_t st) {
   const AdamConsts c = adam_consts(lr, beta1, beta2, eps, weight_decay, bias_correction1,
                                    bias_correction2_sqrt);
   const bool vec = aligned16(param) && aligned16(grad) && aligned16(exp_avg) &&
@@ -460,16 +481,49 @@ extern "C" int bbgr_adam(int64_t n, float *param, const float *grad,
     if (blocks > 256 * 16) blocks = 256 * 16;
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n4,
                        (float4 *)param, (const float4 *)grad, (float4 *)exp_avg,
-                       (float4 *)exp_avg_sq, c, grad_scale);
+                       (float4 *)exp_avg_sq, c, grad_scale, lr, bc, state);
     BBGR_LAUNCHED("adam_kernel");
   }
   const long start = n4 * 4;
   if (start < n) {
     hipLaunchKernelGGL(adam_tail_kernel, dim3((unsigned)((n - start + 255) / 256)),
                        dim3(256), 0, st, (long)n, start, param, grad, exp_avg,
-                       exp_avg_sq, c, grad_scale);
+                       exp_avg_sq, c, grad_scale, lr, bc, state);
     BBGR_LAUNCHED("adam_tail_kernel");
   }
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_adam(int64_t n, float *param, const float *grad,
+                         float *exp_avg, float *exp_avg_sq, float lr, float beta1,
+                         float beta2, float eps, float weight_decay, float grad_scale,
+                         float bias_correction1, float bias_correction2_sqrt,
+                         bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_adam: negative n");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(param && grad && exp_avg && exp_avg_sq, "bbgr_adam: null tensor");
+  return adam_launch(n, param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                     grad_scale, bias_correction1, bias_correction2_sqrt, nullptr, nullptr,
+                     as_stream(stream));
+}
+
+extern "C" int bbgr_adam_dev(int64_t n, float *param, const float *grad, float *exp_avg,
+                             float *exp_avg_sq, float lr, float beta1, float beta2,
+                             float eps, float weight_decay, float grad_scale,
+                             const float *bc_table, const int64_t *state,
+                             bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_adam_dev: negative n");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(param && grad && exp_avg && exp_avg_sq && bc_table && state,
+               "bbgr_adam_dev: null tensor / table / state");
+  return adam_launch(n, param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                     grad_scale, 1.f, 1.f, bc_table, (const long *)state, as_stream(stream));
+}
+
+extern "C" int bbgr_step_begin(int64_t *state, bbgr_stream_t stream) {
+  BBGR_REQUIRE(state, "bbgr_step_begin: null state");
+  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(64), 0, as_stream(stream), (long *)state);
+  BBGR_LAUNCHED("step_begin_kernel");
   return BBGR_OK;
 }
 

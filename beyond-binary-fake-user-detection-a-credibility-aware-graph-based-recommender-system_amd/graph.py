@@ -181,9 +181,12 @@ class Csr:
         return max(1, min(self.n_rows // 8, HOT_BYTES // (4 * d)))
 
     def partial_workspace(self, d: int) -> torch.Tensor | None:
+        """bbgr_spmm_args.partial: n_chunks*d floats of chunk partials, then
+        n_chunks int32 arrival counters that must start at zero (every launch
+        leaves them zero again)."""
         if self.n_split == 0:
             return None
-        return torch.empty(self.n_chunks * d, dtype=torch.float32, device=self.device)
+        return torch.zeros(self.n_chunks * (d + 1), dtype=torch.float32, device=self.device)
 
     def degrees(self) -> torch.Tensor:
         return (self.indptr[1:] - self.indptr[:-1])

@@ -10,29 +10,62 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 
 from . import _lib
 from ._lib import call, ptr, stream_handle
 
 
+def bias_corrections(n: int, beta1: float = 0.9, beta2: float = 0.999) -> np.ndarray:
+    """float32 [n, 2]: (1 - beta1^t, sqrt(1 - beta2^t)) for t = 1..n, with the
+    host path's arithmetic (libm pow and sqrt in double, then rounded to float
+    as the ctypes float argument rounds it)."""
+    t = np.arange(1, n + 1, dtype=np.float64)
+    bc = np.empty((n, 2), dtype=np.float64)
+    bc[:, 0] = 1.0 - np.power(np.float64(beta1), t)
+    bc[:, 1] = np.sqrt(1.0 - np.power(np.float64(beta2), t))
+    return bc.astype(np.float32)
+
+
+class DeviceStepState:
+    """Device-resident step scalars of a graph-captured training step
+    (include/bbgr.h, bbgr_step_begin): state = int64 {t, counter, next counter}
+    and the bias-correction table bc[t-1] = (1 - beta1^t, sqrt(1 - beta2^t)),
+    computed here in double exactly as the host path does (then float)."""
+
+    def __init__(self, device, step: int, counter: int, max_steps: int = 1 << 20,
+                 beta1: float = 0.9, beta2: float = 0.999):
+        self.max_steps = int(max_steps)
+        self.beta1, self.beta2 = beta1, beta2
+        self.state = torch.tensor([step, counter - 1, counter], dtype=torch.int64, device=device)
+        self.bc_table = torch.from_numpy(bias_corrections(self.max_steps, beta1, beta2)).to(device)
+
+    def begin(self) -> None:
+        """t += 1; this step's sampler counter = next; next += 1 (on the device)."""
+        call("bbgr_step_begin", ptr(self.state), stream_handle())
+
+
 class AdamRows:
     """Arguments of a fused Adam step applied inside an SpMM epilogue
-    (bbgr_spmm_args.adam_*): the row gradient never touches HBM."""
+    (bbgr_spmm_args.adam_*): the row gradient never touches HBM. With
+    `dev` (DeviceStepState) the step t and bias corrections are read on the
+    device (graph-captured steps)."""
 
     def __init__(self, param, exp_avg, exp_avg_sq, step: int, lr: float, beta1: float = 0.9,
-                 beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0):
+                 beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0,
+                 dev: DeviceStepState | None = None):
         self.param, self.exp_avg, self.exp_avg_sq = param, exp_avg, exp_avg_sq
         self.lr, self.beta1, self.beta2, self.eps, self.wd = lr, beta1, beta2, eps, weight_decay
         self.bc1 = 1.0 - beta1 ** step
         self.bc2s = math.sqrt(1.0 - beta2 ** step)
+        self.dev = dev
 
     def apply(self, grad: torch.Tensor) -> None:
         """The same step, unfused (bbgr_adam on a materialised gradient)."""
-        call("bbgr_adam", self.param.numel(), ptr(self.param), ptr(grad), ptr(self.exp_avg),
-             ptr(self.exp_avg_sq), float(self.lr), float(self.beta1), float(self.beta2),
-             float(self.eps), float(self.wd), 1.0, float(self.bc1), float(self.bc2s),
-             stream_handle())
+        adam_step(self.param, grad, self.exp_avg, self.exp_avg_sq, 0, self.lr, self.beta1,
+                  self.beta2, self.eps, self.wd, dev=self.dev,
+                  bc=(self.bc1, self.bc2s))
 
     def fill(self, a) -> None:
         from ._lib import ld
@@ -41,19 +74,30 @@ class AdamRows:
         a.adam_lr, a.adam_beta1, a.adam_beta2 = self.lr, self.beta1, self.beta2
         a.adam_eps, a.adam_weight_decay = self.eps, self.wd
         a.adam_bias_correction1, a.adam_bias_correction2_sqrt = self.bc1, self.bc2s
+        if self.dev is not None:
+            a.adam_bc_table, a.adam_state = ptr(self.dev.bc_table), ptr(self.dev.state)
 
 
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,
               exp_avg_sq: torch.Tensor, step: int, lr: float, beta1: float = 0.9,
               beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0,
-              grad_scale: float = 1.0) -> None:
+              grad_scale: float = 1.0, dev: DeviceStepState | None = None,
+              bc: tuple | None = None) -> None:
+    """torch.optim.Adam's step `step` on one tensor (bbgr_adam); with `dev`
+    the step and bias corrections come from the device step state instead
+    (bbgr_adam_dev; `step` is then ignored)."""
     for t in (param, grad, exp_avg, exp_avg_sq):
         if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
             raise ValueError("adam_step takes contiguous fp32 device tensors")
         if t.numel() != param.numel():
             raise ValueError("adam_step: size mismatch")
-    bc1 = 1.0 - beta1 ** step
-    bc2s = math.sqrt(1.0 - beta2 ** step)
+    if dev is not None:
+        call("bbgr_adam_dev", param.numel(), ptr(param), ptr(grad), ptr(exp_avg),
+             ptr(exp_avg_sq), float(lr), float(beta1), float(beta2), float(eps),
+             float(weight_decay), float(grad_scale), ptr(dev.bc_table), ptr(dev.state),
+             stream_handle())
+        return
+    bc1, bc2s = bc if bc is not None else (1.0 - beta1 ** step, math.sqrt(1.0 - beta2 ** step))
     call("bbgr_adam", param.numel(), ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq),
          float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
          float(grad_scale), float(bc1), float(bc2s), stream_handle())

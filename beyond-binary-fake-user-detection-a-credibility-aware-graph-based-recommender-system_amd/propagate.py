@@ -122,9 +122,9 @@ class SpmmTimer:
 
     def __init__(self, count: bool = False):
         self.count = count
-        # (rows, nnz, d, kind, start_event, end_event, table_rows, n_cols)
+        # (rows, nnz, d, kind, start_event, end_event, table_rows, n_cols, masks)
         self.records = []
-        # (kind, table_rows, n_cols, d, rows_t, visited_t, gathered_t): device counts
+        # (kind, masks, table_rows, n_cols, d, rows_t, visited_t, gathered_t): device counts
         self.counts = []
 
     def summary(self, kind: str = "full", table_rows: int | None = None):
@@ -135,7 +135,7 @@ class SpmmTimer:
         item-row CSR: the item<-user products)."""
         torch.cuda.synchronize()
         out = {}
-        for rows, nnz, d, m, a, b, tr, _ in self.records:
+        for rows, nnz, d, m, a, b, tr, _, _ in self.records:
             if m != kind or (table_rows is not None and tr != table_rows):
                 continue
             k = (rows, nnz, d)
@@ -144,13 +144,15 @@ class SpmmTimer:
         return out
 
     def groups(self):
-        """{(kind, table_rows, n_cols, d): [launches, total ms, rows, nnz]} over
-        every timed launch (rows / nnz summed over the launches: full-CSR and
-        range launches only; masked launches are data-dependent)."""
+        """{(kind, masks, table_rows, n_cols, d): [launches, total ms, rows, nnz]}
+        over every timed launch (rows / nnz summed over the launches: full-CSR and
+        range launches only; masked launches are data-dependent). `masks` names
+        the masks a launch was given ("row_list", "row", "src", "src+row"; "" for
+        unmasked), so the different frontier products stay apart."""
         torch.cuda.synchronize()
         out = {}
-        for rows, nnz, d, m, a, b, tr, nc in self.records:
-            g = out.setdefault((m, tr, nc, d), [0, 0.0, 0, 0])
+        for rows, nnz, d, m, a, b, tr, nc, sig in self.records:
+            g = out.setdefault((m, sig, tr, nc, d), [0, 0.0, 0, 0])
             g[0] += 1
             g[1] += a.elapsed_time(b)
             g[2] += rows
@@ -158,13 +160,13 @@ class SpmmTimer:
         return out
 
     def edge_counts(self):
-        """{(kind, table_rows, n_cols, d): [launches, rows, visited, gathered]}
+        """{(kind, masks, table_rows, n_cols, d): [launches, rows, visited, gathered]}
         summed over the counted launches: `visited` = edges of the rows a launch
         computes (index + weight read), `gathered` = those whose source row is
         read and multiply-added (a src_mask skips exact-zero sources)."""
         out = {}
-        for kind, tr, nc, d, r, v, g in self.counts:
-            e = out.setdefault((kind, tr, nc, d), [0, 0, 0, 0])
+        for kind, sig, tr, nc, d, r, v, g in self.counts:
+            e = out.setdefault((kind, sig, tr, nc, d), [0, 0, 0, 0])
             e[0] += 1
             e[1] += int(r)
             e[2] += int(v)
@@ -210,7 +212,14 @@ class SpmmTimer:
         else:
             live = src_mask[c.indices[:c.nnz].long()].bool()
             gathered = (live & torch.repeat_interleave(sel, deg)).sum()
-        self.counts.append((kind, c.n_rows, c.n_cols, d, sel.sum(), visited, gathered))
+        self.counts.append((kind, mask_signature(src_mask, row_mask, row_list), c.n_rows,
+                            c.n_cols, d, sel.sum(), visited, gathered))
+
+
+def mask_signature(src_mask, row_mask, row_list) -> str:
+    if row_list is not None:
+        return "row_list"
+    return "+".join(n for n, m in (("src", src_mask), ("row", row_mask)) if m is not None)
 
 
 _timer: SpmmTimer | None = None
@@ -275,7 +284,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     rows, nnz = prod.csr.n_rows, prod.csr.nnz
     if rng is not None and row_list is None:   # a row range: its own rows and edges
         rows, nnz = rng[1] - rng[0], prod.csr.range_nnz(rng[0], rng[1])
-    _timer.records.append((rows, nnz, d, kind, ev0, ev1, prod.csr.n_rows, prod.csr.n_cols))
+    _timer.records.append((rows, nnz, d, kind, ev0, ev1, prod.csr.n_rows, prod.csr.n_cols,
+                           mask_signature(src_mask, row_mask, row_list)))
 
 
 def epilogue(t: torch.Tensor, *, y=None, y_scale=None, y_scale_s: float = 1.0, add=None,

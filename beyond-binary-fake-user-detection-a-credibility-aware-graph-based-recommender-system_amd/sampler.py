@@ -57,12 +57,21 @@ class PopMixSampler:
                  ptr(self.cdf), ptr(ws), ctypes.byref(n), st)
 
     def sample(self, users: torch.Tensor, pos: torch.Tensor | None = None,
-               neg: torch.Tensor | None = None, counter: int | None = None):
-        """(pos[B], neg[B]) int64 for int64 users[B] (device)."""
+               neg: torch.Tensor | None = None, counter: int | None = None,
+               state: torch.Tensor | None = None):
+        """(pos[B], neg[B]) int64 for int64 users[B] (device). `state`: the
+        device step state (optim.DeviceStepState.state) whose [1] is this
+        step's counter (graph-captured steps); the host counter still advances."""
         users = users.to(dtype=torch.int64).contiguous()
         B = users.numel()
         pos = torch.empty(B, dtype=torch.int64, device=users.device) if pos is None else pos
         neg = torch.empty(B, dtype=torch.int64, device=users.device) if neg is None else neg
+        if state is not None:
+            self.counter += 1
+            call("bbgr_sample_dev", B, ptr(users), ptr(self.csr.indptr), ptr(self.csr.indices),
+                 self.num_items, ptr(self.cdf), self.mix_pop, self.max_tries, self.seed,
+                 ptr(state), ptr(pos), ptr(neg), ptr(self.fail_count), stream_handle())
+            return pos, neg
         c = self.counter if counter is None else int(counter)
         if counter is None:
             self.counter += 1

@@ -23,7 +23,7 @@ from . import _lib
 from ._lib import OP_GS, OP_J, OP_METHOD_A, OP_SYM, call, ld, ptr, stream_handle
 from .bpr import bpr_args
 from .graph import BipartiteGraph
-from .optim import AdamRows, adam_step
+from .optim import AdamRows, DeviceStepState, adam_step
 from .propagate import ORDER_GS, ORDER_J, OperatorPair, backward, forward
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .scatter import RowScatter
@@ -136,6 +136,17 @@ class FusedTrainer:
         # fuse_adam=False keeps them (the gradient-parity tests read them).
         self.fuse_adam = bool(fuse_adam) and (
             (order == ORDER_GS and num_layers >= 1) or (order == ORDER_J and num_layers >= 2))
+        # device-resident step scalars (Adam t, sampler counter) for graph
+        # capture; None = host scalars in the kernel arguments (eager default)
+        self.dev_state: DeviceStepState | None = None
+
+    def enable_device_state(self, max_steps: int = 1 << 20) -> None:
+        """Keep the Adam step and the sampler counter on the device from now on
+        (bbgr_step_begin), so a step captured once replays correctly. Results
+        are bitwise those of the host-scalar path."""
+        if self.dev_state is None:
+            self.dev_state = DeviceStepState(self.device, self.step_count, self.sampler.counter,
+                                             max_steps)
 
     # -- batching ---------------------------------------------------------------
     def next_users(self) -> torch.Tensor:
@@ -162,10 +173,21 @@ class FusedTrainer:
             if self.graph.user_order is not None:
                 users = self.graph.user_order.to_internal(users)
             users = users.contiguous()
+        return self._step(users, listed)
+
+    def _step(self, users: torch.Tensor, listed: bool) -> torch.Tensor:
+        """The step on internal user ids (`listed`: no repeated user). Issues
+        device work only, so it can be captured (GraphedStep)."""
+        if self.dev_state is not None:
+            if self.step_count + 1 > self.dev_state.max_steps:
+                raise RuntimeError("device step state: bias-correction table exhausted")
+            self.dev_state.begin()
         self._last_users = users
         B = users.numel()
         self.pos, self.neg = self.posneg[:B], self.posneg[B:2 * B]
-        pos, neg = self.sampler.sample(users, self.pos, self.neg)
+        pos, neg = self.sampler.sample(users, self.pos, self.neg,
+                                       state=None if self.dev_state is None
+                                       else self.dev_state.state)
         st = stream_handle()
         masks = self._set_masks(users, pos, neg, 1) if self.frontier else None
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
@@ -200,8 +222,10 @@ class FusedTrainer:
             call("bbgr_rows_axpy", B, ptr(neg), alpha, ptr(self.item_w), ld(self.item_w),
                  ptr(self.g_i0), ld(self.g_i0), self.d, st)
             self.step_count += 1
-            adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
-            adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)
+            adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr,
+                      dev=self.dev_state)
+            adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr,
+                      dev=self.dev_state)
         # restore the all-zero invariant of the sparse gradient tables
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
         call("bbgr_rows_zero", B, ptr(pos), ptr(self.g_if), ld(self.g_if), self.d, st)
@@ -222,7 +246,8 @@ class FusedTrainer:
         gl = 1.0 / (self.K + 1)
         a_gl = alpha / gl
         self.step_count += 1
-        adam_u = AdamRows(self.user_w, self.m_u, self.v_u, self.step_count, self.lr)
+        adam_u = AdamRows(self.user_w, self.m_u, self.v_u, self.step_count, self.lr,
+                          dev=self.dev_state)
 
         def before_last():
             call("bbgr_rows_axpy", B, ptr(users), a_gl, ptr(self.user_w), ld(self.user_w),
@@ -235,7 +260,7 @@ class FusedTrainer:
         call("bbgr_rows_axpy", item_rows.numel(), ptr(item_rows), a_gl, ptr(self.item_w),
              ld(self.item_w), ptr(self.g_if), ld(self.g_if), self.d, st)
         adam_step(self.item_w, self.g_if, self.m_i, self.v_i, self.step_count, self.lr,
-                  grad_scale=gl)
+                  grad_scale=gl, dev=self.dev_state)
 
     def _backward_fused_j(self, users, item_rows, masks, alpha: float) -> None:
         """Jacobi backward (lightgcn_cu.py / lightgcn.py order) with both Adam
@@ -245,8 +270,10 @@ class FusedTrainer:
         B = users.numel()
         a_gl = alpha / (1.0 / (self.K + 1))
         self.step_count += 1
-        adam_u = AdamRows(self.user_w, self.m_u, self.v_u, self.step_count, self.lr)
-        adam_i = AdamRows(self.item_w, self.m_i, self.v_i, self.step_count, self.lr)
+        adam_u = AdamRows(self.user_w, self.m_u, self.v_u, self.step_count, self.lr,
+                          dev=self.dev_state)
+        adam_i = AdamRows(self.item_w, self.m_i, self.v_i, self.step_count, self.lr,
+                          dev=self.dev_state)
 
         def before_last():
             call("bbgr_rows_axpy", B, ptr(users), a_gl, ptr(self.user_w), ld(self.user_w),
@@ -292,6 +319,51 @@ class FusedTrainer:
         (rows by input id)."""
         return {"user_emb.weight": _input_rows(self.graph.user_order, self.user_w),
                 "item_emb.weight": _input_rows(self.graph.item_order, self.item_w)}
+
+
+class GraphedStep:
+    """FusedTrainer.step captured once into a HIP graph (torch.cuda.CUDAGraph)
+    and replayed: one graph launch per step instead of ~40 kernel launches
+    (the small-graph path, where launch gaps and per-launch ramps are a
+    large share of the step: C2). The trainer keeps its Adam step and sampler
+    counter on the device (enable_device_state), the batch users are copied
+    into a fixed buffer before each replay, and every replay is bitwise the
+    eager step (tested). A short last batch of an epoch runs eagerly.
+
+    Capturing needs the step's workspaces to exist: a trainer that has not
+    stepped yet runs its first step eagerly here (a real training step)."""
+
+    def __init__(self, trainer: FusedTrainer):
+        self.tr = trainer
+        trainer.enable_device_state()
+        self.first_loss = None
+        if trainer.step_count == 0:
+            self.first_loss = trainer.step()
+        # capture records launches without running them: the buffer's content
+        # at capture time is irrelevant
+        self.users = torch.zeros(trainer.B, dtype=torch.int64, device=trainer.device)
+        host = (trainer.step_count, trainer.sampler.counter)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            trainer._step(self.users, True)
+        # capture recorded the step's launches without running them: undo the
+        # host mirrors it advanced
+        trainer.step_count, trainer.sampler.counter = host
+        torch.cuda.synchronize()
+
+    def step(self) -> torch.Tensor:
+        tr = self.tr
+        users = tr.next_users()
+        if users.numel() != tr.B:       # short tail of an epoch: eager (same device state)
+            return tr._step(users, True)
+        self.users.copy_(users)
+        self.graph.replay()
+        tr.step_count += 1
+        tr.sampler.counter += 1
+        tr._last_users = self.users
+        tr.pos, tr.neg = tr.posneg[: tr.B], tr.posneg[tr.B: 2 * tr.B]
+        return tr.loss
 
 
 def _internal_rows(order, t: torch.Tensor) -> torch.Tensor:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 2
+#define BBGR_ABI_VERSION 3
 
 typedef enum {
   BBGR_OK = 0,
@@ -214,6 +214,14 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   (y, and the fused-Adam parameter row), and the fused Adam's moments are  */
 /*   streamed in and out: the next product gathers this table, and only its  */
 /*   hot prefix (output table in degree order) is worth keeping cached.       */
+/* adam_state (nullable, with adam_bc_table): the fused Adam reads its step t */
+/*   from device memory (bbgr_step_begin's state[0]) and its bias corrections */
+/*   from adam_bc_table[2(t-1)], [2(t-1)+1] instead of the two float fields,  */
+/*   so a captured step (hipGraph) replays with the right t every time.       */
+/* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
+/*   (zero when allocated; each launch leaves them zero): the last chunk of a */
+/*   split row to arrive sums the row's partials in chunk order in the same  */
+/*   launch (no separate fix-up kernel).                                      */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
@@ -260,6 +268,8 @@ typedef struct {
   float adam_bias_correction2_sqrt;
   int32_t stream_from;
   int32_t stream_out_from;
+  const float *adam_bc_table;
+  const int64_t *adam_state;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -345,6 +355,26 @@ int bbgr_adam(int64_t n, float *param, const float *grad, float *exp_avg,
               float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
               float weight_decay, float grad_scale, float bias_correction1,
               float bias_correction2_sqrt, bbgr_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Device-resident step state (graph-captured training steps)                 */
+/*   A training step captured once into a hipGraph (torch.cuda.CUDAGraph) and */
+/*   replayed must not bake the host's per-step scalars into kernel args.     */
+/*   state[3] int64 on the device: state[0] = Adam step t, state[1] = this    */
+/*   step's sampler counter, state[2] = the next one. bbgr_step_begin (one    */
+/*   lane): t += 1; state[1] = state[2]; state[2] += 1 -- the same sequence   */
+/*   the host keeps for an eager step (counter used, then incremented).       */
+/*   bc_table[2(t-1)] = 1 - beta1^t, bc_table[2(t-1)+1] = sqrt(1 - beta2^t),  */
+/*   computed on the host in double as torch does, rounded to float: the     */
+/*   device constants are then bit-identical to the host ones.               */
+/*   bbgr_adam_dev / bbgr_sample_dev: bbgr_adam / bbgr_sample with t and the  */
+/*   counter read from state (t must not exceed the table's length).          */
+/* ------------------------------------------------------------------------- */
+int bbgr_step_begin(int64_t *state, bbgr_stream_t stream);
+int bbgr_adam_dev(int64_t n, float *param, const float *grad, float *exp_avg,
+                  float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, float grad_scale, const float *bc_table,
+                  const int64_t *state, bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Row utilities for the fused training step                                  */
@@ -450,6 +480,11 @@ int bbgr_sample(int64_t batch, const int64_t *users, const int32_t *indptr,
                 float mix_pop, int32_t max_tries, uint64_t seed,
                 uint64_t counter, int64_t *pos, int64_t *neg,
                 int32_t *fail_count, bbgr_stream_t stream);
+int bbgr_sample_dev(int64_t batch, const int64_t *users, const int32_t *indptr,
+                    const int32_t *indices, int32_t n_items, const double *cdf,
+                    float mix_pop, int32_t max_tries, uint64_t seed,
+                    const int64_t *state, int64_t *pos, int64_t *neg,
+                    int32_t *fail_count, bbgr_stream_t stream);
 
 /* out = a random permutation of in[0..n) (Philox keys + radix sort), the
  * device form of rng.shuffle(train_users) (Version-2:821). */

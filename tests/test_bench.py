@@ -37,8 +37,8 @@ class _FakeTimer:
 
     def groups(self):
         out = {}
-        for rows, nnz, d, m, a, b, tr, nc in self.records:
-            g = out.setdefault((m, tr, nc, d), [0, 0.0, 0, 0])
+        for rows, nnz, d, m, a, b, tr, nc, sig in self.records:
+            g = out.setdefault((m, sig, tr, nc, d), [0, 0.0, 0, 0])
             g[0] += 1
             g[1] += a.elapsed_time(b)
             g[2] += rows
@@ -50,10 +50,10 @@ def test_roofline_groups_models(bench):
     I, U, E, d = 1000, 5000, 50000, 64
     recs = []
     for s in range(2):   # two steps: one item and one user full launch, one masked
-        recs.append((I, E, d, "full", _Ev(0.0), _Ev(0.5), I, U))
-        recs.append((U, E, d, "full", _Ev(0.0), _Ev(0.25), U, I))
-        recs.append((U, E, d, "masked", _Ev(0.0), _Ev(0.1), U, I))
-    counts = {("masked", U, I, d): [4, 4 * 100, 4 * 1000, 4 * 600]}
+        recs.append((I, E, d, "full", _Ev(0.0), _Ev(0.5), I, U, ""))
+        recs.append((U, E, d, "full", _Ev(0.0), _Ev(0.25), U, I, ""))
+        recs.append((U, E, d, "masked", _Ev(0.0), _Ev(0.1), U, I, "src"))
+    counts = {("masked", "src", U, I, d): [4, 4 * 100, 4 * 1000, 4 * 600]}
     gs = bench.roofline_groups(_FakeTimer(recs), counts, steps=2, count_steps=4, n_items=I)
     by = {(g["kind"], g["side"]): g for g in gs}
     item = by[("full", "item<-user")]
@@ -64,7 +64,7 @@ def test_roofline_groups_models(bench):
     user = by[("full", "user<-item")]
     assert user["cache_assisted"] == (user["gather_model_frac"] > 1.0)
     m = by[("masked", "user<-item")]
-    assert m["rows_per_launch"] == 100 and m["edges_gathered_per_launch"] == 600
+    assert m["masks"] == "src" and m["rows_per_launch"] == 100 and m["edges_gathered_per_launch"] == 600
     assert m["gather_model_bytes"] == 1000 * 8 + 600 * 4 * d + 100 * (4 + 4 * d)
 
 

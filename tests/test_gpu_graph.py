@@ -1,0 +1,124 @@
+"""GPU: the graph-capturable training step.
+
+* device step state (bbgr_step_begin / bbgr_sample_dev / bbgr_adam_dev and the
+  fused Adam's adam_state): an eager step reading t and the sampler counter
+  from device memory is bitwise the host-scalar step;
+* GraphedStep (torch.cuda.CUDAGraph capture of FusedTrainer._step): replays
+  are bitwise the eager steps, across an epoch boundary and for the fused
+  GS / Jacobi Adam and the separate Adam;
+* in-launch split-row reduction: the arrival counters of the partial
+  workspace are zero again after every launch, and results are bitwise
+  stable across launches.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from bbgr.graph import BipartiteGraph  # noqa: E402
+from bbgr.synthetic import synthetic_credibility, synthetic_edges  # noqa: E402
+from bbgr.trainer import FusedTrainer, GraphedStep  # noqa: E402
+
+DEV = "cuda"
+
+
+def _graph(U=3000, I=1200, E=60000, seed=5):
+    e = synthetic_edges(U, I, E, seed=seed, items="zipf")
+    return e, BipartiteGraph(e, U, I, DEV, vertex_order="degree")
+
+
+def _state(tr):
+    return [tr.user_w, tr.item_w, tr.m_u, tr.v_u, tr.m_i, tr.v_i]
+
+
+def _assert_same(a, b):
+    for x, y in zip(_state(a), _state(b)):
+        assert torch.equal(x, y)
+    assert a.step_count == b.step_count and a.sampler.counter == b.sampler.counter
+
+
+@pytest.mark.parametrize("variant,fuse", [("v2_pop", True), ("cu_fair", True),
+                                          ("v2_pop", False)])
+def test_device_state_eager_matches_host_scalars(variant, fuse):
+    e, g = _graph()
+    kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=64, num_layers=3, batch_size=256,
+              frontier=True, fuse_adam=fuse, seed=3)
+    a, b = FusedTrainer(g, variant, **kw), FusedTrainer(g, variant, **kw)
+    b.enable_device_state()
+    for _ in range(4):
+        assert float(a.step()) == float(b.step())
+    _assert_same(a, b)
+    st = b.dev_state.state.cpu().tolist()
+    assert st == [4, 3, 4]          # t, this step's counter, next counter
+
+
+@pytest.mark.parametrize("variant,fuse,frontier", [("v2_pop", True, True),
+                                                   ("v2_pop", True, False),
+                                                   ("cu_fair", True, True),
+                                                   ("v2_pop", False, True)])
+def test_graphed_step_replays_bitwise_eager(variant, fuse, frontier):
+    """Captured once, replayed: weights, Adam moments, loss and batch are the
+    eager trainer's bit for bit, also across epoch boundaries (3000 users,
+    batch 700: the permutation is redrawn every 5th step; the short tail runs
+    eagerly)."""
+    e, g = _graph()
+    kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=64, num_layers=3, batch_size=700,
+              frontier=frontier, fuse_adam=fuse, seed=11)
+    a, b = FusedTrainer(g, variant, **kw), FusedTrainer(g, variant, **kw)
+    gs = GraphedStep(b)                        # runs b's first step eagerly
+    la = [float(a.step())]
+    lb = [float(gs.first_loss)]
+    for _ in range(11):
+        la.append(float(a.step()))
+        lb.append(float(gs.step()))
+        ua, pa, na = a.batch()
+        ub, pb, nb = b.batch()
+        assert torch.equal(ua, ub) and torch.equal(pa, pb) and torch.equal(na, nb)
+    assert la == lb
+    _assert_same(a, b)
+    assert a.epoch >= 3
+
+
+def test_graphed_step_sparse_tables_stay_zero():
+    """The replayed step restores the all-zero invariant of its sparse
+    gradient tables and masks, as the eager step does."""
+    e, g = _graph()
+    tr = FusedTrainer(g, "v2_pop", emb_dim=64, num_layers=2, batch_size=512, frontier=True)
+    gs = GraphedStep(tr)
+    for _ in range(3):
+        gs.step()
+    torch.cuda.synchronize()
+    assert float(tr.g_uf.abs().sum()) == 0.0 and float(tr.g_if.abs().sum()) == 0.0
+    assert int(tr.mask_u.sum()) == 0 and int(tr.mask_i.sum()) == 0
+
+
+def test_split_rows_finish_in_launch_and_counters_reset():
+    """Rows cut into several chunks are summed by their last-arriving chunk in
+    the same launch: the arrival counters behind the partials are zero after
+    each launch and repeated launches give bitwise identical tables."""
+    from bbgr import propagate as P
+    U, I = 4000, 300
+    e = synthetic_edges(U, I, 200000, seed=9, items="zipf")   # hub items: deg >> 2048
+    g = BipartiteGraph(e, U, I, DEV)
+    prod = P.Product(g.item_csr, None, None, None, {})
+    assert g.item_csr.n_split > 0
+    x = torch.randn(U, 64, device=DEV)
+    outs = []
+    for _ in range(3):
+        y = torch.empty(I, 64, device=DEV)
+        P.spmm(prod, x, False, y=y)
+        outs.append(y)
+        ws = prod.workspace(64)
+        cnt = ws[g.item_csr.n_chunks * 64:].view(torch.int32)
+        torch.cuda.synchronize()
+        assert int(cnt.abs().sum()) == 0
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    # the launch computes the plain sum over each row's edges (weight_mode 0,
+    # no scales): against float64
+    A = torch.zeros(I, U, dtype=torch.float64)
+    ii, uu = torch.as_tensor(e[1], dtype=torch.long), torch.as_tensor(e[0], dtype=torch.long)
+    A.index_put_((ii, uu), torch.ones(ii.numel(), dtype=torch.float64), accumulate=True)
+    ref = (A @ x.double().cpu()).numpy()
+    got = outs[0].double().cpu().numpy()
+    assert np.linalg.norm(got - ref) <= 1e-5 * np.linalg.norm(ref)
