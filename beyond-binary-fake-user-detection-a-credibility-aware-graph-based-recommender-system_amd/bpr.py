@@ -59,35 +59,14 @@ def bpr_loss_value(users, pos, neg, uf, itf, ue, ie, reg, pop=None, lambda_fair=
     return out
 
 
-class _BprFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair):
-        _lib.require_gpu(uf)
-        uf, itf, ue, ie = (t.contiguous() for t in (uf, itf, ue, ie))
-        loss = bpr_loss_value(users, pos, neg, uf, itf, ue, ie, reg, pop, lambda_fair)
-        ctx.save_for_backward(uf, itf, ue, ie, users, pos, neg)
-        ctx.reg, ctx.pop, ctx.lambda_fair = reg, pop, lambda_fair
-        return loss
-
-    @staticmethod
-    def backward(ctx, gloss):
-        uf, itf, ue, ie, users, pos, neg = ctx.saved_tensors
-        need = ctx.needs_input_grad
-        z = lambda t, n: torch.zeros_like(t) if need[n] else None  # noqa: E731
-        g_uf, g_if, g_ue, g_ie = z(uf, 0), z(itf, 1), z(ue, 2), z(ie, 3)
-        dloss = gloss.to(torch.float32).contiguous().reshape(())
-        a = bpr_args(users, pos, neg, uf, itf, ue, ie, ctx.reg, ctx.pop, ctx.lambda_fair,
-                     dloss=dloss, g_uf=g_uf, g_if=g_if, g_ue=g_ue, g_ie=g_ie)
-        call("bbgr_bpr", ctypes.byref(a), stream_handle())
-        return g_uf, g_if, g_ue, g_ie, None, None, None, None, None, None
-
-
 def bpr_loss(users, pos_items, neg_items, user_final, item_final, user_ego, item_ego,
              reg_weight: float, pop: torch.Tensor | None = None, lambda_fair: float = 0.0):
-    """Differentiable fused BPR loss (0-d tensor)."""
+    """Differentiable fused BPR loss (0-d tensor): the registered operator
+    bbgr::bpr_loss (ops.py), backward bbgr::bpr_loss_backward."""
     dev = user_final.device
     users, pos_items, neg_items = (_idx(t, dev) for t in (users, pos_items, neg_items))
     if not (users.numel() == pos_items.numel() == neg_items.numel()):
         raise ValueError("users, pos_items, neg_items must have equal length")
-    return _BprFn.apply(user_final, item_final, user_ego, item_ego, users, pos_items,
+    from . import ops
+    return ops.bpr_loss(user_final, item_final, user_ego, item_ego, users, pos_items,
                         neg_items, float(reg_weight), pop, float(lambda_fair))

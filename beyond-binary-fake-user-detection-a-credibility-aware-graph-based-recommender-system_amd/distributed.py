@@ -428,6 +428,7 @@ class ShardedTrainer(FusedTrainer):
         self.mask_u = torch.zeros(num_local_users, dtype=torch.uint8, device=dev)
         self.mask_i = torch.zeros(num_items, dtype=torch.uint8, device=dev)
         self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
+        self.dev_state = None   # host step scalars (the sharded step is not graph-captured)
         # sparse frontier exchange: the step's global item frontier as a row list
         self.sparse_exchange = bool(sparse_exchange) and self.frontier
         self.item_list = torch.empty(max(num_items, 1), dtype=torch.int64, device=dev)

@@ -31,25 +31,6 @@ def build_norm_adj(train_edges, num_users: int, num_items: int, device):
     return NormAdjOperator(OperatorPair.factored(graph, sc), graph)
 
 
-class _SymPropagateFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x0, pair, K):
-        U = pair.num_users
-        x0 = x0.contiguous()
-        out = torch.empty_like(x0)
-        _fwd(pair, x0[:U], x0[U:], K, ORDER_J, out_u=out[:U], out_i=out[U:])
-        ctx.pair, ctx.K = pair, K
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        pair, U = ctx.pair, ctx.pair.num_users
-        g = g.contiguous()
-        gx = torch.empty_like(g)
-        _bwd(pair, g[:U], g[U:], ctx.K, ORDER_J, out_u=gx[:U], out_i=gx[U:])
-        return gx, None, None
-
-
 class LightGCN(torch.nn.Module):
     def __init__(self, num_users, num_items, emb_dim, num_layers, norm_adj):
         super().__init__()
@@ -65,7 +46,9 @@ class LightGCN(torch.nn.Module):
 
     def propagate(self):
         if isinstance(self.norm_adj, NormAdjOperator):
-            return _SymPropagateFn.apply(self.emb.weight, self.norm_adj.pair, self.num_layers)
+            from . import ops
+            return ops.propagate_sym(self.emb.weight, ops.pair_key(self.norm_adj.pair),
+                                     int(self.num_layers))
         if self._square is None:
             self._square = square_from_torch_sparse(self.norm_adj, self.emb.weight.device)
         return _SquareFn.apply(self.emb.weight, self._square, self.num_layers)

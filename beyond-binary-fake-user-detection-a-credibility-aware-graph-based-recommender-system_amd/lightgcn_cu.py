@@ -97,36 +97,10 @@ class CredLightGCN(torch.nn.Module):
 
 
 def _propagate_one(pair: OperatorPair, u: torch.Tensor, i: torch.Tensor):
-    """One Jacobi layer (i' = M_ui u, u' = M_iu i) as a differentiable op."""
-    return _OneLayerFn.apply(u, i, pair)
-
-
-class _OneLayerFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, u, i, pair):
-        from .propagate import spmm
-        u, i = u.contiguous(), i.contiguous()
-        FI, FU = pair.fwd_item, pair.fwd_user
-        new_i = torch.empty(pair.num_items, u.shape[1], device=u.device)
-        new_u = torch.empty(pair.num_users, u.shape[1], device=u.device)
-        spmm(FI, u, True, y=new_i, y_scale=FI.out_scale)
-        spmm(FU, i, True, y=new_u, y_scale=FU.out_scale)
-        ctx.pair = pair
-        return new_i, new_u
-
-    @staticmethod
-    def backward(ctx, g_i, g_u):
-        from .propagate import spmm
-        pair = ctx.pair
-        BI, BU = pair.bwd_item, pair.bwd_user
-        gu = gi = None
-        if g_i is not None:   # d/du of new_i = M_iu^T g_i  (user rows)
-            gu = torch.empty(pair.num_users, g_i.shape[1], device=g_i.device)
-            spmm(BU, g_i.contiguous(), True, y=gu, y_scale=BU.out_scale)
-        if g_u is not None:   # d/di of new_u = M_ui^T g_u  (item rows)
-            gi = torch.empty(pair.num_items, g_u.shape[1], device=g_u.device)
-            spmm(BI, g_u.contiguous(), True, y=gi, y_scale=BI.out_scale)
-        return gu, gi, None
+    """One Jacobi layer (i' = M_ui u, u' = M_iu i) as a differentiable op:
+    the registered operator bbgr::jacobi_layer (ops.py)."""
+    from . import ops
+    return ops.jacobi_layer(u, i, ops.pair_key(pair))
 
 
 __all__ = ["build_cred_weighted_mats", "CredLightGCN"]

@@ -1,0 +1,252 @@
+"""The hot-path kernels as registered torch operators (torch.library).
+
+`LightGCN.propagate()` and `LightGCN.bpr_loss()` of the drop-in modules
+(Version-2/lighgcn_cu_pop.py:472-508, lightgcn_cu.py:420-463, lightgcn.py:
+318-349) call these instead of Python autograd.Functions, so the drop-in step
+(:858-863 — propagate, bpr_loss, backward, Adam) survives torch.compile
+(dynamo traces the ops through their fake kernels, AOTAutograd sees their
+registered backward) and CUDA-graph capture (the ops issue device work only,
+on torch's current stream).
+
+  bbgr::propagate(u0, i0, pair_key, num_layers, order) -> (u_final, i_final)
+  bbgr::propagate_backward(gU, gI, pair_key, num_layers, order) -> (grad_u0, grad_i0)
+  bbgr::jacobi_layer(u, i, pair_key) -> (new_i, new_u)   (+ _backward)
+  bbgr::propagate_sym(x0, pair_key, num_layers) -> x_final   (+ _backward)
+  bbgr::bpr_loss(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair) -> loss
+  bbgr::bpr_loss_backward(dloss, uf, itf, ue, ie, users, pos, neg, reg, pop,
+                          lambda_fair) -> (g_uf, g_if, g_ue, g_ie)
+
+The sparse operators are not tensors: an OperatorPair is registered once
+(`pair_key`) and the ops look it up; shapes for the fake kernels come from
+the tensor arguments alone.
+"""
+from __future__ import annotations
+
+import ctypes
+import itertools
+from typing import Optional
+
+import torch
+from torch import Tensor
+from torch.library import custom_op
+
+from . import _lib
+from ._lib import call, stream_handle
+
+_PAIRS: dict = {}
+_keys = itertools.count(1)
+
+
+def pair_key(pair) -> int:
+    """The registry key of an OperatorPair (assigned on first use)."""
+    k = getattr(pair, "_op_key", None)
+    if k is None:
+        k = next(_keys)
+        pair._op_key = k
+        _PAIRS[k] = pair
+    return k
+
+
+def _pair(key: int):
+    try:
+        return _PAIRS[key]
+    except KeyError:
+        raise RuntimeError(f"bbgr ops: no operator pair registered under key {key}") from None
+
+
+# -- propagation -------------------------------------------------------------
+@custom_op("bbgr::propagate", mutates_args=())
+def propagate(u0: Tensor, i0: Tensor, pair_key: int, num_layers: int,
+              order: str) -> tuple[Tensor, Tensor]:
+    from .propagate import forward
+    _lib.require_gpu(u0)
+    return forward(_pair(pair_key), u0.contiguous(), i0.contiguous(), num_layers, order)
+
+
+@propagate.register_fake
+def _(u0, i0, pair_key, num_layers, order):
+    return u0.new_empty(u0.shape), i0.new_empty(i0.shape)
+
+
+@custom_op("bbgr::propagate_backward", mutates_args=())
+def propagate_backward(gU: Tensor, gI: Tensor, pair_key: int, num_layers: int,
+                       order: str) -> tuple[Tensor, Tensor]:
+    from .propagate import backward
+    _lib.require_gpu(gU)
+    return backward(_pair(pair_key), gU.contiguous(), gI.contiguous(), num_layers, order)
+
+
+@propagate_backward.register_fake
+def _(gU, gI, pair_key, num_layers, order):
+    return gU.new_empty(gU.shape), gI.new_empty(gI.shape)
+
+
+def _propagate_setup(ctx, inputs, output):
+    u0, i0, ctx.key, ctx.K, ctx.order = inputs
+    ctx.shapes = (u0.shape, i0.shape)
+
+
+def _propagate_bwd(ctx, gU, gI):
+    (su, si) = ctx.shapes
+    ref = gU if gU is not None else gI
+    if gU is None:
+        gU = ref.new_zeros(su)
+    if gI is None:
+        gI = ref.new_zeros(si)
+    gu0, gi0 = propagate_backward(gU, gI, ctx.key, ctx.K, ctx.order)
+    return gu0, gi0, None, None, None
+
+
+propagate.register_autograd(_propagate_bwd, setup_context=_propagate_setup)
+
+
+# -- one Jacobi layer (lightgcn_cu.py propagate_all_layers, :420-448) ------------
+@custom_op("bbgr::jacobi_layer", mutates_args=())
+def jacobi_layer(u: Tensor, i: Tensor, pair_key: int) -> tuple[Tensor, Tensor]:
+    from .propagate import spmm
+    _lib.require_gpu(u)
+    pair = _pair(pair_key)
+    u, i = u.contiguous(), i.contiguous()
+    FI, FU = pair.fwd_item, pair.fwd_user
+    new_i = torch.empty(pair.num_items, u.shape[1], device=u.device)
+    new_u = torch.empty(pair.num_users, u.shape[1], device=u.device)
+    spmm(FI, u, True, y=new_i, y_scale=FI.out_scale)
+    spmm(FU, i, True, y=new_u, y_scale=FU.out_scale)
+    return new_i, new_u
+
+
+@jacobi_layer.register_fake
+def _(u, i, pair_key):
+    return i.new_empty(i.shape), u.new_empty(u.shape)
+
+
+@custom_op("bbgr::jacobi_layer_backward", mutates_args=())
+def jacobi_layer_backward(g_i: Tensor, g_u: Tensor, pair_key: int) -> tuple[Tensor, Tensor]:
+    """(d/du, d/di): M_iu^T g_i on the user rows, M_ui^T g_u on the item rows."""
+    from .propagate import spmm
+    pair = _pair(pair_key)
+    BI, BU = pair.bwd_item, pair.bwd_user
+    gu = torch.empty(pair.num_users, g_i.shape[1], device=g_i.device)
+    gi = torch.empty(pair.num_items, g_u.shape[1], device=g_u.device)
+    spmm(BU, g_i.contiguous(), True, y=gu, y_scale=BU.out_scale)
+    spmm(BI, g_u.contiguous(), True, y=gi, y_scale=BI.out_scale)
+    return gu, gi
+
+
+@jacobi_layer_backward.register_fake
+def _(g_i, g_u, pair_key):
+    return g_u.new_empty(g_u.shape), g_i.new_empty(g_i.shape)
+
+
+def _layer_setup(ctx, inputs, output):
+    u, i, ctx.key = inputs
+    ctx.shapes = (u.shape, i.shape)
+
+
+def _layer_bwd(ctx, g_i, g_u):
+    su, si = ctx.shapes
+    ref = g_i if g_i is not None else g_u
+    g_i = ref.new_zeros(si) if g_i is None else g_i
+    g_u = ref.new_zeros(su) if g_u is None else g_u
+    gu, gi = jacobi_layer_backward(g_i, g_u, ctx.key)
+    return gu, gi, None
+
+
+jacobi_layer.register_autograd(_layer_bwd, setup_context=_layer_setup)
+
+
+# -- symmetric operator (lightgcn.py): one stacked [users; items] table ------------
+@custom_op("bbgr::propagate_sym", mutates_args=())
+def propagate_sym(x0: Tensor, pair_key: int, num_layers: int) -> Tensor:
+    from .propagate import ORDER_J, forward
+    _lib.require_gpu(x0)
+    pair = _pair(pair_key)
+    U = pair.num_users
+    x0 = x0.contiguous()
+    out = torch.empty_like(x0)
+    forward(pair, x0[:U], x0[U:], num_layers, ORDER_J, out_u=out[:U], out_i=out[U:])
+    return out
+
+
+@propagate_sym.register_fake
+def _(x0, pair_key, num_layers):
+    return x0.new_empty(x0.shape)
+
+
+@custom_op("bbgr::propagate_sym_backward", mutates_args=())
+def propagate_sym_backward(g: Tensor, pair_key: int, num_layers: int) -> Tensor:
+    from .propagate import ORDER_J, backward
+    pair = _pair(pair_key)
+    U = pair.num_users
+    g = g.contiguous()
+    gx = torch.empty_like(g)
+    backward(pair, g[:U], g[U:], num_layers, ORDER_J, out_u=gx[:U], out_i=gx[U:])
+    return gx
+
+
+@propagate_sym_backward.register_fake
+def _(g, pair_key, num_layers):
+    return g.new_empty(g.shape)
+
+
+def _sym_setup(ctx, inputs, output):
+    _, ctx.key, ctx.K = inputs
+
+
+def _sym_bwd(ctx, g):
+    return propagate_sym_backward(g, ctx.key, ctx.K), None, None
+
+
+propagate_sym.register_autograd(_sym_bwd, setup_context=_sym_setup)
+
+
+# -- BPR loss ------------------------------------------------------------------
+@custom_op("bbgr::bpr_loss", mutates_args=())
+def bpr_loss(uf: Tensor, itf: Tensor, ue: Tensor, ie: Tensor, users: Tensor, pos: Tensor,
+             neg: Tensor, reg: float, pop: Optional[Tensor], lambda_fair: float) -> Tensor:
+    from .bpr import bpr_loss_value
+    _lib.require_gpu(uf)
+    return bpr_loss_value(users, pos, neg, uf.contiguous(), itf.contiguous(), ue.contiguous(),
+                          ie.contiguous(), reg, pop, lambda_fair)
+
+
+@bpr_loss.register_fake
+def _(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair):
+    return uf.new_empty(())
+
+
+@custom_op("bbgr::bpr_loss_backward", mutates_args=())
+def bpr_loss_backward(dloss: Tensor, uf: Tensor, itf: Tensor, ue: Tensor, ie: Tensor,
+                      users: Tensor, pos: Tensor, neg: Tensor, reg: float,
+                      pop: Optional[Tensor], lambda_fair: float
+                      ) -> tuple[Tensor, Tensor, Tensor, Tensor]:
+    from .bpr import bpr_args
+    uf, itf, ue, ie = (t.contiguous() for t in (uf, itf, ue, ie))
+    g_uf, g_if, g_ue, g_ie = (torch.zeros_like(t) for t in (uf, itf, ue, ie))
+    d = dloss.to(torch.float32).contiguous().reshape(())
+    a = bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop, lambda_fair, dloss=d,
+                 g_uf=g_uf, g_if=g_if, g_ue=g_ue, g_ie=g_ie)
+    call("bbgr_bpr", ctypes.byref(a), stream_handle())
+    return g_uf, g_if, g_ue, g_ie
+
+
+@bpr_loss_backward.register_fake
+def _(dloss, uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair):
+    return (uf.new_empty(uf.shape), itf.new_empty(itf.shape), ue.new_empty(ue.shape),
+            ie.new_empty(ie.shape))
+
+
+def _bpr_setup(ctx, inputs, output):
+    uf, itf, ue, ie, users, pos, neg, reg, pop, lam = inputs
+    ctx.save_for_backward(uf, itf, ue, ie, users, pos, neg)
+    ctx.reg, ctx.lam = reg, lam
+    ctx.pop = pop
+
+
+def _bpr_bwd(ctx, gloss):
+    uf, itf, ue, ie, users, pos, neg = ctx.saved_tensors
+    g = bpr_loss_backward(gloss, uf, itf, ue, ie, users, pos, neg, ctx.reg, ctx.pop, ctx.lam)
+    return g[0], g[1], g[2], g[3], None, None, None, None, None, None
+
+
+bpr_loss.register_autograd(_bpr_bwd, setup_context=_bpr_setup)

@@ -522,36 +522,14 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
     return gu0, gi0
 
 
-class _PropagateFn(torch.autograd.Function):
-    """Differentiable (u0, i0) -> (u_final, i_final); replaces the autograd of
-    the reference's K x torch.sparse.mm + stack().mean() chain."""
-
-    @staticmethod
-    def forward(ctx, u0, i0, pair, num_layers, order):
-        _lib.require_gpu(u0)
-        u0c, i0c = u0.contiguous(), i0.contiguous()
-        uf, itf = forward(pair, u0c, i0c, num_layers, order)
-        ctx.pair, ctx.K, ctx.order = pair, num_layers, order
-        return uf, itf
-
-    @staticmethod
-    def backward(ctx, gU, gI):
-        pair = ctx.pair
-        if gU is None and gI is None:
-            return None, None, None, None, None
-        ref = gU if gU is not None else gI
-        d = ref.shape[1]
-        if gU is None:
-            gU = torch.zeros(pair.num_users, d, device=ref.device, dtype=torch.float32)
-        if gI is None:
-            gI = torch.zeros(pair.num_items, d, device=ref.device, dtype=torch.float32)
-        gu0, gi0 = backward(pair, gU.contiguous(), gI.contiguous(), ctx.K, ctx.order)
-        return gu0, gi0, None, None, None
-
-
 def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
               order: str = ORDER_GS):
-    return _PropagateFn.apply(u0, i0, pair, num_layers, order)
+    """Differentiable (u0, i0) -> (u_final, i_final): the registered operator
+    bbgr::propagate (ops.py), whose backward is bbgr::propagate_backward;
+    replaces the autograd of the reference's K x torch.sparse.mm +
+    stack().mean() chain."""
+    from . import ops
+    return ops.propagate(u0, i0, ops.pair_key(pair), int(num_layers), order)
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,135 @@
+"""GPU: the drop-in step through the registered torch operators (ops.py).
+
+The reference's step (Version-2/lighgcn_cu_pop.py:858-863):
+    u_final, i_final = model.propagate()
+    loss = model.bpr_loss(users, pos, neg, u_final, i_final, reg)
+    opt.zero_grad(); loss.backward(); opt.step()
+* under torch.compile (backend "aot_eager": dynamo + AOTAutograd trace the
+  bbgr ops through their fake kernels and registered backward; no code
+  generation) it gives the eager step's loss and gradients bit for bit;
+* captured whole into a CUDA graph (forward, backward and a capturable
+  torch.optim.Adam) and replayed, it gives the eager steps' weights bit for bit.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from bbgr import lightgcn as L  # noqa: E402
+from bbgr import lightgcn_cu as J  # noqa: E402
+from bbgr import lightgcn_cu_pop as V2  # noqa: E402
+from bbgr.synthetic import synthetic_credibility, synthetic_edges  # noqa: E402
+
+DEV = "cuda"
+U, I, E, D, K, B = 1500, 700, 20000, 64, 3, 512
+
+
+def _model(family, seed=0):
+    e = synthetic_edges(U, I, E, seed=4, items="zipf")
+    torch.manual_seed(seed)
+    if family == "v2":
+        cred = torch.as_tensor(synthetic_credibility(U, 4))
+        M_ui, M_iu = V2.build_message_passing_mats(e, U, I, cred, DEV)
+        m = V2.LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    elif family == "cu":
+        cred = torch.as_tensor(synthetic_credibility(U, 4))
+        M_ui, M_iu, deg_i = J.build_cred_weighted_mats(e, U, I, cred, DEV)
+        m = J.CredLightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+        m.pop = torch.as_tensor(deg_i / max(deg_i.max(), 1.0), device=DEV)
+    else:
+        A = L.build_norm_adj(e, U, I, DEV)
+        m = L.LightGCN(U, I, D, K, A).to(DEV)
+    return m
+
+
+def _batch(seed):
+    g = torch.Generator().manual_seed(seed)
+    users = torch.randint(0, U, (B,), generator=g).to(DEV)
+    pos = torch.randint(0, I, (B,), generator=g).to(DEV)
+    neg = torch.randint(0, I, (B,), generator=g).to(DEV)
+    return users, pos, neg
+
+
+def _loss(m, users, pos, neg):
+    if isinstance(m, J.CredLightGCN):   # lightgcn_cu.py:583-584, 635-648
+        uf, itf = m.final_embeddings()
+        return m.bpr_fair_loss(users, pos, neg, uf, itf, m.pop, 0.05, 1e-4)
+    uf, itf = m.get_user_item_emb()
+    return m.bpr_loss(users, pos, neg, uf, itf, 1e-4)
+
+
+def test_per_layer_op_matches_fused_propagation():
+    """propagate_all_layers (one bbgr::jacobi_layer per layer) -> layer mean
+    equals final_embeddings (bbgr::propagate) to fp32 rounding, forward and
+    gradient."""
+    m = _model("cu")
+    us, is_ = m.propagate_all_layers()
+    uf = torch.stack(us).mean(0)
+    itf = torch.stack(is_).mean(0)
+    ufr, itfr = m.final_embeddings()
+    for a, b in ((uf, ufr), (itf, itfr)):
+        assert float((a - b).norm() / b.norm()) < 1e-6
+    (uf.sum() + 2 * itf.sum()).backward()
+    g1 = [p.grad.clone() for p in m.parameters()]
+    m.zero_grad()
+    (ufr.sum() + 2 * itfr.sum()).backward()
+    for a, p in zip(g1, m.parameters()):
+        assert float((a - p.grad).norm() / p.grad.norm()) < 1e-6
+
+
+@pytest.mark.parametrize("family", ["v2", "cu", "sym"])
+def test_compiled_step_matches_eager(family):
+    a, b = _model(family), _model(family)
+    users, pos, neg = _batch(1)
+    la = _loss(a, users, pos, neg)
+    la.backward()
+    _loss(b, users, pos, neg)          # resolves the operator pair outside the trace
+    b.zero_grad()
+    step = torch.compile(_loss, backend="aot_eager", fullgraph=False)
+    lb = step(b, users, pos, neg)
+    lb.backward()
+    assert float(la) == float(lb)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa.grad, pb.grad)
+
+
+@pytest.mark.parametrize("family", ["v2", "sym"])
+def test_cuda_graph_captured_step_matches_eager(family):
+    """Whole drop-in step (forward, backward, Adam) captured once, replayed on
+    new batches copied into static buffers: weights equal the eager run."""
+    a, b = _model(family), _model(family)
+    oa = torch.optim.Adam(a.parameters(), lr=1e-3, capturable=True)
+    ob = torch.optim.Adam(b.parameters(), lr=1e-3, capturable=True)
+    batches = [_batch(s) for s in range(6)]
+
+    def eager_step(m, opt, bt):
+        loss = _loss(m, *bt)
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for bt in batches:
+        eager_step(a, oa, bt)
+    # b: two warm-up steps on a side stream, capture, replay the rest
+    static = [t.clone() for t in batches[0]]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for bt in batches[:2]:
+            for dst, src in zip(static, bt):
+                dst.copy_(src)
+            eager_step(b, ob, static)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_loss = eager_step(b, ob, static)
+    for bt in batches[2:]:
+        for dst, src in zip(static, bt):
+            dst.copy_(src)
+        graph.replay()
+    torch.cuda.synchronize()
+    assert np.isfinite(float(static_loss))
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)
