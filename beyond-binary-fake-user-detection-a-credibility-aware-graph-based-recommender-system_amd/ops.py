@@ -220,13 +220,22 @@ def bpr_loss_backward(dloss: Tensor, uf: Tensor, itf: Tensor, ue: Tensor, ie: Te
                       users: Tensor, pos: Tensor, neg: Tensor, reg: float,
                       pop: Optional[Tensor], lambda_fair: float
                       ) -> tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Deterministic: the kernel writes per-triple gradient rows of the final
+    tables (contrib) and bbgr_scatter_add_rows sums each destination's rows in
+    ascending triple order; the ego-L2 rows add one identical value per
+    occurrence, whose order cannot change the sum."""
     from .bpr import bpr_args
+    from .scatter import index_add_rows
     uf, itf, ue, ie = (t.contiguous() for t in (uf, itf, ue, ie))
     g_uf, g_if, g_ue, g_ie = (torch.zeros_like(t) for t in (uf, itf, ue, ie))
+    B = users.numel()
+    contrib = torch.empty(3 * B, uf.shape[1], dtype=torch.float32, device=uf.device)
     d = dloss.to(torch.float32).contiguous().reshape(())
     a = bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop, lambda_fair, dloss=d,
-                 g_uf=g_uf, g_if=g_if, g_ue=g_ue, g_ie=g_ie)
+                 g_ue=g_ue, g_ie=g_ie, contrib=contrib)
     call("bbgr_bpr", ctypes.byref(a), stream_handle())
+    index_add_rows(g_uf, users, contrib[:B])
+    index_add_rows(g_if, torch.cat([pos, neg]), contrib[B:])
     return g_uf, g_if, g_ue, g_ie
 
 

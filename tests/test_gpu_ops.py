@@ -44,6 +44,9 @@ def _model(family, seed=0):
 
 
 def _batch(seed):
+    """Random triples with repeated users and items: the BPR backward sums
+    each row's addends in a fixed order (bbgr::bpr_loss_backward), so runs
+    still compare bitwise."""
     g = torch.Generator().manual_seed(seed)
     users = torch.randint(0, U, (B,), generator=g).to(DEV)
     pos = torch.randint(0, I, (B,), generator=g).to(DEV)
