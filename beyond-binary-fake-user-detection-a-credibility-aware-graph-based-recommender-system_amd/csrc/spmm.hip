@@ -441,6 +441,7 @@ __device__ __forceinline__ void split_row_finish(const SpmmParams &P, int row, i
   float4 acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
   for (int sl = g; sl < c; sl += 16) {
     const float4 *src =
         reinterpret_cast<const float4 *>(P.partial) + (long)(base + sl) * (D / 4) + lane;
@@ -458,19 +459,31 @@ __device__ __forceinline__ void split_row_finish(const SpmmParams &P, int row, i
 
 // A chunk of a row cut into c > 1 chunks: publish this chunk's partial; the
 // last chunk of the row to arrive sums them all (split_row_finish) in this
-// launch. Hand-off per cdna_hip_programming.md (in-launch split reduction):
-// plain stores -> drain -> barrier -> one agent-scope release -> ticket
-// fetch_add (agent scope); the drawer of ticket c-1 takes one agent-scope
-// acquire before the workgroup reads the slots. The ticket counter lives at
-// arrivals[base] (base = the row's first chunk) and the reducer re-zeroes it.
+// launch. Hand-off per cdna_hip_programming.md Guideline 16 (R1 payload,
+// counter form): the partial is stored write-through (8-B relaxed agent
+// atomic stores = sc1, so no release fence: an agent release here would
+// write back the whole XCD L2 once per chunk workgroup) -> every wave drains
+// -> barrier -> one relaxed agent ticket fetch_add; the drawer of ticket c-1
+// takes one agent-scope acquire before its workgroup reads the slots with
+// plain loads. The ticket lives at arrivals[base] (base = the row's first
+// chunk) and the reducer re-zeroes it.
 template <int D>
 __device__ __forceinline__ void split_row_arrive(const SpmmParams &P, int4 ch, float4 *red,
                                                  int g, int lane) {
   constexpr int V = D / 64;
   if (g == 0) {
-    float4 *dst = reinterpret_cast<float4 *>(P.partial) + (long)ch.w * (D / 4) + lane;
+    unsigned long long *dst = reinterpret_cast<unsigned long long *>(
+        reinterpret_cast<float4 *>(P.partial) + (long)ch.w * (D / 4) + lane);
 #pragma unroll
-    for (int k = 0; k < V; ++k) dst[16 * k] = red[lane + 16 * k];
+    for (int k = 0; k < V; ++k) {
+      const float4 v = red[lane + 16 * k];
+      const unsigned long long lo =
+          (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32);
+      const unsigned long long hi =
+          (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32);
+      __hip_atomic_store(dst + 32 * k, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + 32 * k + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   // chunk j of c (plan_fill_kernel: chunk j starts at eb + floor(len*j/c)),
   // slot = base + j
@@ -483,8 +496,6 @@ __device__ __forceinline__ void split_row_arrive(const SpmmParams &P, int4 ch, f
   __syncthreads();   // every wave has read red[] and drained its stores
   int *flag = reinterpret_cast<int *>(red);
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int ticket =
         __hip_atomic_fetch_add(P.arrivals + base, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = ticket == c - 1;
