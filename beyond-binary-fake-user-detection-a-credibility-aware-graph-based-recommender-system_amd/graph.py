@@ -170,6 +170,8 @@ class Csr:
         vertex_order="degree"); then the hot prefix of the source table."""
         if not self.__dict__.get("cols_by_degree", False):
             return 0
+        if self.n_cols * 4 * d <= HOT_BYTES:   # the whole table stays cached (C1, C2)
+            return 0
         return max(1, min(self.n_cols // 8, HOT_BYTES // (4 * d)))
 
     def stream_out_from(self, d: int) -> int:
@@ -177,6 +179,8 @@ class Csr:
         rows are in descending-degree order; then the hot prefix of the output
         table (the next product gathers it)."""
         if not self.__dict__.get("rows_by_degree", False):
+            return 0
+        if self.n_rows * 4 * d <= HOT_BYTES:
             return 0
         return max(1, min(self.n_rows // 8, HOT_BYTES // (4 * d)))
 
