@@ -328,7 +328,8 @@ class ShardedTrainer(FusedTrainer):
                  device=None, group=None, u0=None, i0=None, user_offset: int = 0,
                  frontier="auto", exchange_parts: int = 4, fuse_adam: bool = True,
                  sparse_exchange: bool = True, vertex_order: str = "input",
-                 frontier_parts: int = 2, native_comm: bool = False):
+                 frontier_parts: int = 2, native_comm: bool = False,
+                 overlap_item_adam: bool | None = None):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
         this rank's users; i0: the full (replicated) item table; batch_size:
         users per step on THIS rank. vertex_order="degree": local users by
@@ -429,6 +430,17 @@ class ShardedTrainer(FusedTrainer):
         self.mask_i = torch.zeros(num_items, dtype=torch.uint8, device=dev)
         self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
         self.dev_state = None   # host step scalars (the sharded step is not graph-captured)
+        # GS item Adam on a side stream beside the backward chain: its gradient
+        # (gI/(K+1) + ego rows) is final once the all-gathered BPR rows are
+        # summed, and with N > 1 the chain waits on its dense exchanges, so the
+        # Adam pass (28 B/param over the replicated item table) fills link-bound
+        # time instead of following the chain. At N = 1 it only contends with the
+        # SpMMs for HBM (measured slower), hence the default.
+        if overlap_item_adam is None:
+            overlap_item_adam = self.world > 1
+        self.overlap_item_adam = bool(overlap_item_adam) and self.fuse_adam
+        self.g_adam = z(num_items) if self.overlap_item_adam else None
+        self._adam_stream = torch.cuda.Stream(device=dev) if self.overlap_item_adam else None
         # sparse frontier exchange: the step's global item frontier as a row list
         self.sparse_exchange = bool(sparse_exchange) and self.frontier
         self.item_list = torch.empty(max(num_items, 1), dtype=torch.int64, device=dev)
@@ -518,6 +530,31 @@ class ShardedTrainer(FusedTrainer):
         self.exchange.set_rows(self.graph.item_csr, self.mask_i, self.item_list,
                                self.item_offs_host)
 
+    def _item_adam_beside(self) -> torch.cuda.Event:
+        """The item Adam of this step on the side stream: its gradient rows are
+        copied out of g_if (which the backward chain still reads as its addend)
+        into g_adam, the ego rows are added there, Adam runs, and g_adam's rows
+        are zeroed again. Values are those of the in-chain Adam bit for bit.
+        The step count it uses is the one _backward_fused is about to take."""
+        main = torch.cuda.current_stream()
+        side = self._adam_stream
+        side.wait_stream(main)
+        rows = self.all_items
+        gl = 1.0 / (self.K + 1)
+        a_gl = (2.0 * self.reg / self.B_global) / gl
+        step_count, self.step_count = self.step_count, self.step_count + 1
+        with torch.cuda.stream(side):
+            self.g_adam.index_copy_(0, rows, self.g_if.index_select(0, rows))
+            self._item_adam(rows, self.g_adam, a_gl, gl)
+            call("bbgr_rows_zero", rows.numel(), ptr(rows), ptr(self.g_adam),
+                 ld(self.g_adam), self.d, stream_handle())
+        self.step_count = step_count
+        for t in (rows, self.g_if, self.g_adam, self.item_w, self.m_i, self.v_i):
+            t.record_stream(side)
+        done = torch.cuda.Event()
+        done.record(side)
+        return done
+
     def step(self) -> torch.Tensor:
         users = self.next_users()
         self._last_users = users
@@ -541,7 +578,12 @@ class ShardedTrainer(FusedTrainer):
         _all_gather(self.all_contrib, self.contrib[B: 3 * B], self.group)
         self.scatter(self.g_if, self.all_items, self.all_contrib)
         alpha = 2.0 * self.reg / self.B_global            # ego L2 (Version-2:503-507)
-        if self.fuse_adam:
+        if self.fuse_adam and self.overlap_item_adam:
+            done = self._item_adam_beside()
+            self._backward_fused(users, self.all_items, masks, alpha, reduce=self.exchange,
+                                 item_adam=False)
+            torch.cuda.current_stream().wait_event(done)
+        elif self.fuse_adam:
             self._backward_fused(users, self.all_items, masks, alpha, reduce=self.exchange)
         else:
             backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,

@@ -32,8 +32,19 @@ import torch
 from . import _lib
 from ._lib import call, ptr, stream_handle
 
-DEFAULT_LONG_THRESHOLD = 256
+DEFAULT_LONG_THRESHOLD = None   # None: long_threshold_for(nnz)
 DEFAULT_CHUNK_EDGES = 2048
+# Rows longer than the threshold are cut into chunk workgroups (16 lane groups
+# on one row) instead of one lane group walking the row in 16-edge batches.
+# On a small graph the longest short row is the launch's critical path: at C2
+# (1M edges) the step ran 0.887 ms with 256, 0.710 with 128, 0.579 with 64,
+# 0.579 with 32, 0.812 with 16; at C4 (50M) 16.77 / 16.76 / 16.97 ms for
+# 256 / 128 / 64 (tools/chunk_probe.py, profiles/r15_chunk_probe.jsonl).
+SMALL_CSR_EDGES = 8_000_000
+
+
+def long_threshold_for(nnz: int) -> int:
+    return 64 if nnz < SMALL_CSR_EDGES else 256
 # Hot-row budget of a gathered table in descending-degree order: rows past it
 # are loaded non-temporal (bbgr_spmm_args.stream_from). Sized to leave room in
 # the 256 MB Infinity Cache for the streams of the launch; at most 1/8 of the
@@ -58,7 +69,7 @@ class Csr:
 
     def __init__(self, rows, cols, n_rows: int, n_cols: int, device,
                  edge_values: torch.Tensor | None = None,
-                 long_threshold: int = DEFAULT_LONG_THRESHOLD,
+                 long_threshold: int | None = DEFAULT_LONG_THRESHOLD,
                  chunk_edges: int = DEFAULT_CHUNK_EDGES, keep_perm: bool = False):
         _lib.require_gpu()
         device = torch.device(device)
@@ -73,6 +84,8 @@ class Csr:
                     or int(cols.min()) < 0 or int(cols.max()) >= n_cols):
             raise ValueError("edge index out of range")
         self.n_rows, self.n_cols, self.nnz = int(n_rows), int(n_cols), int(nnz)
+        if long_threshold is None:
+            long_threshold = long_threshold_for(self.nnz)
         self.device = device
         self.indptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=device)
         self.indices = torch.empty(max(nnz, 1), dtype=torch.int32, device=device)
@@ -275,7 +288,7 @@ class BipartiteGraph:
     sharded trainer passes an all-reduce so every rank orders items alike."""
 
     def __init__(self, train_edges_2xE, num_users: int, num_items: int, device,
-                 long_threshold: int = DEFAULT_LONG_THRESHOLD,
+                 long_threshold: int | None = DEFAULT_LONG_THRESHOLD,
                  chunk_edges: int = DEFAULT_CHUNK_EDGES, vertex_order: str = "input",
                  item_degree_hook=None):
         device = torch.device(device)

@@ -234,7 +234,8 @@ class FusedTrainer:
             self._set_masks(users, pos, neg, 0)
         return self.loss
 
-    def _backward_fused(self, users, item_rows, masks, alpha: float, reduce=None) -> None:
+    def _backward_fused(self, users, item_rows, masks, alpha: float, reduce=None,
+                        item_adam: bool = True) -> None:
         """GS backward with Adam fused (see __init__). The ego-L2 rows enter
         through the sparse tables: grad_u0 = out*T + gl*(gU + alpha/gl*u0[b])
         and grad_i0 = gl*(gI + alpha/gl*i0[pos,neg]) (Version-2:503-507).
@@ -256,10 +257,17 @@ class FusedTrainer:
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
                  before_last=before_last, reduce=reduce)
+        if item_adam:
+            self._item_adam(item_rows, self.g_if, a_gl, gl)
+
+    def _item_adam(self, item_rows, g, a_gl: float, gl: float) -> None:
+        """GS item Adam: grad_i0 = gl * (gI + a_gl * i0[pos, neg]) (Version-2:
+        503-507), the ego rows added into the sparse table g first."""
+        st = stream_handle()
         # duplicates add the same value, so the atomic order cannot matter
         call("bbgr_rows_axpy", item_rows.numel(), ptr(item_rows), a_gl, ptr(self.item_w),
-             ld(self.item_w), ptr(self.g_if), ld(self.g_if), self.d, st)
-        adam_step(self.item_w, self.g_if, self.m_i, self.v_i, self.step_count, self.lr,
+             ld(self.item_w), ptr(g), ld(g), self.d, st)
+        adam_step(self.item_w, g, self.m_i, self.v_i, self.step_count, self.lr,
                   grad_scale=gl, dev=self.dev_state)
 
     def _backward_fused_j(self, users, item_rows, masks, alpha: float) -> None:

@@ -90,6 +90,16 @@ def fused_vs_separate(out_dir, variant):
             out[f"{tag}_m_i"] = tr.m_i.cpu().numpy()
             out[f"{tag}_loss"] = np.array(losses)
             out[f"{tag}_fused"] = np.array(tr.fuse_adam)
+    # the item Adam in the chain instead of on the side stream (world 2
+    # overlaps it by default): bitwise the same step
+    tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3, batch_size=32,
+                        device="cuda:0", u0=u0, i0=i0, user_offset=rank * WEAK_U,
+                        exchange_parts=2, fuse_adam=True, frontier=True, overlap_item_adam=False)
+    losses = [float(tr.step()) for _ in range(3)]
+    out["inchain_user_w"] = tr.user_w.cpu().numpy()
+    out["inchain_item_w"] = tr.item_w.cpu().numpy()
+    out["inchain_m_i"] = tr.m_i.cpu().numpy()
+    out["inchain_loss"] = np.array(losses)
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"fused{rank}.npz"), **out)
     dist.destroy_process_group()

@@ -124,6 +124,9 @@ def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
         np.testing.assert_allclose(rk["fused_sparse_loss"], rk["sep_sparse_loss"], rtol=1e-6)
     for key in ("sep_sparse_item_w", "fused_sparse_item_w", "fused_sparse_m_i"):
         np.testing.assert_array_equal(ranks[0][key], ranks[1][key])   # replicas identical
+    for rk in ranks:   # item Adam beside the chain (default at N > 1) == in the chain
+        for key in ("user_w", "item_w", "m_i", "loss"):
+            np.testing.assert_array_equal(rk[f"fused_sparse_{key}"], rk[f"inchain_{key}"])
 
 
 @pytest.mark.parametrize("variant,order", [("v2_pop", "input"), ("cu_fair", "input"),

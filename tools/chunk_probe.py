@@ -29,14 +29,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2")
     ap.add_argument("--chunks", default="2048,1024,512,256")
+    ap.add_argument("--thresholds", default="256",
+                    help="long-row thresholds (rows above are cut into chunk workgroups)")
     ap.add_argument("--steps", type=int, default=50)
     a = ap.parse_args()
     c = CONFIGS[a.config]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
     e = config_edges(a.config)
     cred = synthetic_credibility(U, CONFIG_SEED[a.config])
-    for ch in (int(x) for x in a.chunks.split(",")):
-        g = BipartiteGraph(e, U, I, "cuda", vertex_order="degree", chunk_edges=ch)
+    for ch, thr in ((int(x), int(t)) for x in a.chunks.split(",")
+                    for t in a.thresholds.split(",")):
+        g = BipartiteGraph(e, U, I, "cuda", vertex_order="degree", chunk_edges=ch,
+                           long_threshold=thr)
         tr = FusedTrainer(g, "v2_pop", cred=cred, emb_dim=d, num_layers=K, batch_size=B)
         for _ in range(5):
             tr.step()
@@ -45,7 +49,8 @@ def main():
         for _ in range(a.steps):
             tr.step()
         torch.cuda.synchronize()
-        print(json.dumps({"config": a.config, "chunk_edges": ch, "item_chunks": g.item_csr.n_chunks,
+        print(json.dumps({"config": a.config, "chunk_edges": ch, "long_threshold": thr,
+                          "item_chunks": g.item_csr.n_chunks, "user_chunks": g.user_csr.n_chunks,
                           "ms_per_step": round(1000 * (time.perf_counter() - t0) / a.steps, 4)}),
               flush=True)
         del tr, g
