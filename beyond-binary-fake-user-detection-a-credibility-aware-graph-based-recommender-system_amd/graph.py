@@ -45,7 +45,8 @@ SMALL_CSR_EDGES = 8_000_000
 
 def long_threshold_for(nnz: int) -> int:
     return 64 if nnz < SMALL_CSR_EDGES else 256
-# Hot-row budget of a gathered table in descending-degree order: rows past it
+# Hot-row budget of a gathered table in descending-degree order (per CSR:
+# Csr.hot_bytes overrides it; a table within the budget streams nothing): rows past it
 # are loaded non-temporal (bbgr_spmm_args.stream_from). Sized to leave room in
 # the 256 MB Infinity Cache for the streams of the launch; at most 1/8 of the
 # rows (C4: the 625k highest-degree users and 125k items stay cached).
@@ -183,9 +184,10 @@ class Csr:
         vertex_order="degree"); then the hot prefix of the source table."""
         if not self.__dict__.get("cols_by_degree", False):
             return 0
-        if self.n_cols * 4 * d <= HOT_BYTES:   # the whole table stays cached (C1, C2)
+        hot = self.__dict__.get("hot_bytes", HOT_BYTES)
+        if self.n_cols * 4 * d <= hot:   # the whole table stays cached (C1, C2)
             return 0
-        return max(1, min(self.n_cols // 8, HOT_BYTES // (4 * d)))
+        return max(1, min(self.n_cols // 8, hot // (4 * d)))
 
     def stream_out_from(self, d: int) -> int:
         """bbgr_spmm_args.stream_out_from for d-wide output rows: 0 unless the
@@ -193,9 +195,10 @@ class Csr:
         table (the next product gathers it)."""
         if not self.__dict__.get("rows_by_degree", False):
             return 0
-        if self.n_rows * 4 * d <= HOT_BYTES:
+        hot = self.__dict__.get("hot_bytes", HOT_BYTES)
+        if self.n_rows * 4 * d <= hot:
             return 0
-        return max(1, min(self.n_rows // 8, HOT_BYTES // (4 * d)))
+        return max(1, min(self.n_rows // 8, hot // (4 * d)))
 
     def partial_workspace(self, d: int) -> torch.Tensor | None:
         """bbgr_spmm_args.partial: n_chunks*d floats of chunk partials, then

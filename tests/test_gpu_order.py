@@ -64,6 +64,10 @@ def test_ordered_graph_csrs_are_the_relabelled_graph():
     # internal degrees are non-increasing
     assert (np.diff(np.diff(g.user_csr.indptr.cpu().numpy())) <= 0).all()
     assert (np.diff(np.diff(g.item_csr.indptr.cpu().numpy())) <= 0).all()
+    # small tables fit the cache budget and stream nothing; with a smaller
+    # budget the hot prefix rule applies
+    assert g.user_csr.stream_from(64) == 0 and g.item_csr.stream_out_from(64) == 0
+    g.user_csr.hot_bytes = g.item_csr.hot_bytes = 1 << 12
     assert g.user_csr.stream_from(64) > 0 and g.item_csr.stream_from(256) > 0
     assert BipartiteGraph(e, U, I, DEV).user_csr.stream_from(64) == 0
     with pytest.raises(ValueError):
@@ -83,6 +87,7 @@ def test_stream_from_loads_leave_results_bitwise_equal(d, side):
     e = synthetic_edges(U, I, 30000, 11, items="zipf")
     rows, cols, nr, nc = (e[1], e[0], I, U) if side == "item_rows" else (e[0], e[1], U, I)
     c = Csr(rows, cols, nr, nc, DEV, long_threshold=64, chunk_edges=128)
+    c.hot_bytes = 1 << 12   # a small budget: these tables would otherwise stay cached
     prod = Product(c, None, None, None, {})
     x = torch.randn(nc, d, device=DEV)
     mask = (torch.rand(nc, device=DEV) < 0.3).to(torch.uint8)
