@@ -366,6 +366,37 @@ def test_sampler_full_row_user_flags_failure():
     assert neg[1].item() in (1, 2)
 
 
+def test_step_with_a_user_holding_every_item():
+    """The reference's negative loop never ends for a user who holds every item
+    (Version-2:364-376). Here the sampler gives up (neg = -1, fail_count += 1),
+    the BPR kernel drops that triple (no loss, no gradient) and the batch mean
+    still divides by B: loss = (B-1)/B x the oracle mean over the kept triples."""
+    from bbgr.trainer import FusedTrainer
+    rng = np.random.default_rng(4)
+    U, I, d, K = 60, 20, 64, 2
+    rows = [np.zeros(I, np.int32)]                     # user 0: every item
+    cols = [np.arange(I, dtype=np.int32)]
+    for u in range(1, U):
+        it = rng.choice(I, 3, replace=False).astype(np.int32)
+        rows.append(np.full(3, u, np.int32))
+        cols.append(it)
+    e = np.vstack([np.concatenate(rows), np.concatenate(cols)])
+    u0 = rng.uniform(-0.5, 0.5, (U, d)).astype(np.float32)
+    i0 = rng.uniform(-0.5, 0.5, (I, d)).astype(np.float32)
+    g = BipartiteGraph(e, U, I, DEV)
+    tr = FusedTrainer(g, "cu_message", emb_dim=d, num_layers=K, batch_size=U, u0=u0, i0=i0,
+                      neg_max_tries=5, frontier=False)
+    loss = float(tr.step())
+    users, pos, neg = (x.cpu().numpy() for x in tr.batch())
+    assert (neg == -1).sum() == 1 and users[neg == -1][0] == 0
+    assert int(tr.sampler.fail_count.item()) == 1
+    keep = neg >= 0
+    M_ui, M_iu = R.gs_mats(e, U, I)
+    uf, itf, _, _ = R.propagate_gs(M_ui, M_iu, u0, i0, K)
+    want, _ = R.bpr_loss(uf, itf, u0, i0, users[keep], pos[keep], neg[keep], 1e-4)
+    assert abs(loss - want * keep.sum() / U) <= 1e-5 * want
+
+
 def test_shuffle_and_nonempty_rows():
     from bbgr.sampler import nonempty_rows, shuffle
     e = np.array([[0, 2, 2, 5], [0, 1, 2, 0]], np.int32)
