@@ -1,0 +1,105 @@
+/* Host-side ABI check under AddressSanitizer + UndefinedBehaviorSanitizer.
+ *
+ * Built by `make -C <pkg>/csrc sanitize` from the library's host code only
+ * (--cuda-host-only: kernels are stubs, so nothing here may reach a launch)
+ * and run by tests/test_sanitize.py on the CPU. It drives every entry
+ * point's argument validation and error reporting: each call must return a
+ * negative bbgr_status with a message, without touching the device, and
+ * without any sanitizer report (invalid reads, overflows, UB in the checks).
+ */
+#include <stdio.h>
+#include <string.h>
+
+#include "bbgr.h"
+
+static int failures = 0;
+
+static void expect_error(const char *what, int rc) {
+  const char *msg = bbgr_last_error();
+  if (rc >= 0 || !msg || !*msg) {
+    fprintf(stderr, "FAIL %s: rc=%d msg=%s\n", what, rc, msg ? msg : "(null)");
+    ++failures;
+  }
+}
+
+static void expect_ok(const char *what, int rc) {
+  if (rc != 0) {
+    fprintf(stderr, "FAIL %s: rc=%d (%s)\n", what, rc, bbgr_last_error());
+    ++failures;
+  }
+}
+
+int main(void) {
+  if (bbgr_abi_version() != BBGR_ABI_VERSION) {
+    fprintf(stderr, "FAIL abi version %d\n", bbgr_abi_version());
+    return 1;
+  }
+  bbgr_csr csr;
+  memset(&csr, 0, sizeof csr);
+  bbgr_spmm_args a;
+  memset(&a, 0, sizeof a);
+  float f4[16] __attribute__((aligned(16)));
+  memset(f4, 0, sizeof f4);
+
+  expect_error("spmm null csr", bbgr_spmm(NULL, &a, NULL));
+  expect_error("spmm null args", bbgr_spmm(&csr, NULL, NULL));
+  csr.n_rows = -1;
+  expect_error("spmm negative rows", bbgr_spmm(&csr, &a, NULL));
+  csr.n_rows = 4;
+  csr.n_cols = 4;
+  csr.nnz = 0;
+  csr.indptr = (const int32_t *)f4;
+  a.d = 48;
+  expect_error("spmm unsupported d", bbgr_spmm(&csr, &a, NULL));
+  a.d = 64;
+  a.x = f4;
+  a.ldx = 63;   /* ld not a multiple of 4 and < d */
+  expect_error("spmm bad ld", bbgr_spmm(&csr, &a, NULL));
+  a.ldx = 64;
+  a.weight_mode = 1;   /* needs edge values */
+  expect_error("spmm weight_mode 1 without values", bbgr_spmm(&csr, &a, NULL));
+  a.weight_mode = 0;
+  a.adam_param = f4;   /* fused Adam without moments */
+  expect_error("spmm adam without moments", bbgr_spmm(&csr, &a, NULL));
+  a.adam_param = NULL;
+  a.use_range = 1;
+  a.range[0] = 3;
+  a.range[1] = 2;      /* row0 > row1 */
+  expect_error("spmm bad range", bbgr_spmm(&csr, &a, NULL));
+  a.use_range = 0;
+  a.row_list = (const int64_t *)f4;
+  a.n_row_list = -5;
+  expect_error("spmm negative row list", bbgr_spmm(&csr, &a, NULL));
+
+  expect_error("epilogue null args", bbgr_epilogue(4, f4, 64, NULL, NULL));
+  expect_error("epilogue negative rows", bbgr_epilogue(-1, f4, 64, &a, NULL));
+  expect_error("bpr null", bbgr_bpr(NULL, NULL));
+  expect_error("adam negative n", bbgr_adam(-1, f4, f4, f4, f4, 1e-3f, 0.9f, 0.999f, 1e-8f,
+                                            0.f, 1.f, 0.1f, 0.03f, NULL));
+  expect_error("adam null tensor", bbgr_adam(4, NULL, f4, f4, f4, 1e-3f, 0.9f, 0.999f, 1e-8f,
+                                             0.f, 1.f, 0.1f, 0.03f, NULL));
+  expect_ok("adam empty", bbgr_adam(0, NULL, NULL, NULL, NULL, 1e-3f, 0.9f, 0.999f, 1e-8f,
+                                    0.f, 1.f, 0.1f, 0.03f, NULL));
+  expect_error("adam_dev null state", bbgr_adam_dev(4, f4, f4, f4, f4, 1e-3f, 0.9f, 0.999f,
+                                                    1e-8f, 0.f, 1.f, f4, NULL, NULL));
+  expect_error("step_begin null", bbgr_step_begin(NULL, NULL));
+  expect_error("sample bad sizes", bbgr_sample(1, NULL, NULL, NULL, 0, NULL, 0.f, 5, 1, 0,
+                                               NULL, NULL, NULL, NULL));
+  expect_error("sample_dev null state", bbgr_sample_dev(1, NULL, NULL, NULL, 5, NULL, 0.f, 5,
+                                                        1, NULL, NULL, NULL, NULL, NULL));
+  expect_error("plan count null", bbgr_csr_plan_count(NULL, NULL, NULL, NULL, NULL, NULL));
+  expect_error("plan build null", bbgr_csr_plan_build(NULL, NULL, NULL, NULL, NULL, NULL));
+  expect_error("shuffle null size", bbgr_shuffle(4, NULL, NULL, 1, 1, NULL, NULL, NULL));
+  expect_error("mark_rows bad", bbgr_mark_rows(-1, NULL, 1, NULL, 4, NULL));
+  expect_error("rows_zero bad", bbgr_rows_zero(-1, NULL, NULL, 64, 64, NULL));
+  expect_error("allreduce null comm", bbgr_allreduce_items(NULL, f4, 4, NULL));
+  expect_error("eval sampled null", bbgr_eval_sampled(NULL, NULL, NULL, NULL));
+  expect_error("eval full null", bbgr_eval_full(NULL, NULL, NULL, NULL));
+
+  if (failures) {
+    fprintf(stderr, "%d failures\n", failures);
+    return 1;
+  }
+  printf("abi host check ok\n");
+  return 0;
+}
