@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import itertools
+import weakref
 from typing import Optional
 
 import torch
@@ -33,7 +34,9 @@ from torch.library import custom_op
 from . import _lib
 from ._lib import call, stream_handle
 
-_PAIRS: dict = {}
+# key -> OperatorPair, held weakly: the model that owns a pair keeps it (and
+# its device CSRs) alive, the registry does not
+_PAIRS: "weakref.WeakValueDictionary[int, object]" = weakref.WeakValueDictionary()
 _keys = itertools.count(1)
 
 
