@@ -272,6 +272,47 @@ def pmc_traffic():
     return json.load(open(p))
 
 
+def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> dict:
+    """`--weak-beside` steps of the weak-scaled sharded step (N x the config's
+    edges, N x its batch): timed like the main loop (barrier + sync on both
+    sides, max over ranks), gathered edges counted over one extra step."""
+    from bbgr.distributed import ShardedTrainer
+    U, I, d, K, B = (cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"],
+                     cfg["batch"])
+    seed = CONFIG_SEED[args.config]
+    edges = shard_edges_weak(args.config, rank)
+    cred = synthetic_credibility(U, seed + 7919 * rank, args.cred)
+    tr = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d, num_layers=K,
+                        batch_size=B, device=dev, user_offset=rank * U, frontier=frontier, **xp)
+    E = int(_allreduce(tr.graph.item_csr.nnz, dev, torch.distributed.ReduceOp.SUM))
+    del edges
+    for _ in range(max(1, args.warmup)):
+        tr.step()
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.weak_beside):
+        tr.step()
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    el = _allreduce(time.perf_counter() - t0, dev, torch.distributed.ReduceOp.MAX)
+    counter = P.SpmmTimer(count=True)
+    P.set_spmm_timer(counter)
+    tr.step()
+    torch.cuda.synchronize()
+    P.set_spmm_timer(None)
+    gathered = _allreduce(sum(c[3] for c in counter.edge_counts().values()), dev,
+                          torch.distributed.ReduceOp.SUM)
+    tr.close()
+    steps_per_s = args.weak_beside / el
+    return {"value": gathered * steps_per_s, "unit": "edges/s", "scaling": "weak",
+            "ms_per_step": 1000.0 * el / args.weak_beside, "steps": args.weak_beside,
+            "bpr_steps_per_s": steps_per_s, "num_edges": E, "num_users": U * world,
+            "global_batch": tr.B_global,
+            "note": f"{world} x {args.config} user shards over the shared items, measured "
+                    "after the strong line in the same run"}
+
+
 def main():
     global cfg_name_global
     out_stream = _quiet_stdout()
@@ -314,6 +355,10 @@ def main():
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="sharded runs: steps after the timed region whose SpMM launches "
                          "are bracketed by HIP events for the roofline")
+    ap.add_argument("--weak-beside", type=int, default=10,
+                    help="N>1 strong runs: afterwards time this many weak-scaled steps "
+                         "(each rank a full config-sized shard) and report them beside "
+                         "the strong line (0 = skip)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="N>1: strong (default) = the config's one graph cut into N user "
                          "ranges (the metric's |E|); weak = every rank owns a full "
@@ -483,9 +528,17 @@ def main():
             dense_s = _allreduce(dense_s, dev, torch.distributed.ReduceOp.MAX)
         dense_ms = 1000.0 * dense_s / args.dense_check
         trainer.frontier = True
+    frontier_on = bool(trainer.frontier)
     if dist_mode:
         trainer.close()                    # the native exchange's communicator, if any
     groups = roofline_groups(timer, counts, timer_steps, count_steps, I)
+    weak_beside = None
+    if world > 1 and not weak and args.weak_beside > 0 and not sharded_gen:
+        # the same machinery at fixed per-GPU work, beside the strong line:
+        # every rank a full config-sized user shard over the shared items
+        del trainer
+        torch.cuda.empty_cache()
+        weak_beside = measure_weak(args, cfg, rank, world, dev, xp, frontier)
     # the dominant kernel: full-CSR item<-user products (spmm_kernel)
     dom = [g for g in groups if g["kind"] == "full" and g["side"] == "item<-user"]
     dom_n = sum(g["launches_per_step"] for g in dom)
@@ -531,6 +584,7 @@ def main():
                    "parallelism": f"user-rows x{world}"
                                   + (" (sharded trainer)" if dist_mode and world == 1 else "")},
         "bpr_steps_per_s": steps_per_s,
+        "weak_beside": weak_beside,
         "graph_replay": use_graph,
         "value_note": "value = SpMM edges actually gathered (source row read and "
                       "multiply-added) per second, whole job: every launch's edges counted "
@@ -548,7 +602,7 @@ def main():
         "dense_note": "same trainer, frontier sparsity off (every SpMM over the full CSR; "
                       "loss, gradients and updates equal): timed after the main loop; "
                       "dense_edges_per_s = 4*K*E traversed per dense step",
-        "frontier": {"enabled": bool(trainer.frontier),
+        "frontier": {"enabled": frontier_on,
                      "full_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
                          for r, z, ms in timer.sequence("full", timer_steps)],

@@ -5,6 +5,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 T=${1:-rehearsal}
-BBGR_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --dense-check 0 > gpurun_out/${T}_gloo2.json 2> gpurun_out/${T}_gloo2.log || { echo GLOO2_FAILED; tail -30 gpurun_out/${T}_gloo2.log; exit 1; }
+BBGR_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --dense-check 0 --weak-beside 2 > gpurun_out/${T}_gloo2.json 2> gpurun_out/${T}_gloo2.log || { echo GLOO2_FAILED; tail -30 gpurun_out/${T}_gloo2.log; exit 1; }
 timeout -k 10 400 python bench.py --sharded --steps 20 --warmup 3 --no-cpu-baseline --dense-check 0 > gpurun_out/${T}_sharded1.json 2> gpurun_out/${T}_sharded1.log || { echo SHARDED1_FAILED; tail -30 gpurun_out/${T}_sharded1.log; exit 1; }
 echo ALL_OK
