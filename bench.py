@@ -355,6 +355,14 @@ def main():
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="sharded runs: steps after the timed region whose SpMM launches "
                          "are bracketed by HIP events for the roofline")
+    ap.add_argument("--partition", default="auto", choices=["auto", "columns", "users"],
+                    help="N>1 strong scaling: columns = every rank the whole graph and d/N "
+                         "embedding columns (no item exchange; 12 B per triple all-reduced); "
+                         "users = user-row shards with item all-reduces (DESIGN §6); auto = "
+                         "columns when d/N is a supported width and the graph is drawn whole")
+    ap.add_argument("--emulate-columns", type=int, default=0,
+                    help="single GPU: run ONE column shard of N (d/N columns, the whole graph) "
+                         "alone, the per-rank work of a column-sharded N-GPU step")
     ap.add_argument("--weak-beside", type=int, default=10,
                     help="N>1 strong runs: afterwards time this many weak-scaled steps "
                          "(each rank a full config-sized shard) and report them beside "
@@ -398,6 +406,15 @@ def main():
     weak = world > 1 and scaling == "weak"
     # configs too large to draw whole on every rank (C5) are drawn per user shard
     sharded_gen = not weak and cfg["num_edges"] > 100_000_000
+    from bbgr.columns import can_shard_columns
+    partition = args.partition
+    if partition == "auto":
+        partition = ("columns" if world > 1 and not weak and not sharded_gen
+                     and can_shard_columns(d, world) else "users")
+    columns = dist_mode and partition == "columns" and not weak
+    if columns:
+        sharded_gen = False
+    emulate = args.emulate_columns if not dist_mode else 0
     t0 = time.perf_counter()
     seed = CONFIG_SEED[args.config]
     lo = hi = 0
@@ -420,12 +437,23 @@ def main():
     frontier = {"auto": "auto", "on": True, "off": False}[args.frontier]
     if args.dense:
         frontier = False
-    if not dist_mode:
+    if emulate:
+        from bbgr.columns import ColumnShardedTrainer
+        trainer = ColumnShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
+                                       num_layers=K, batch_size=B, device=dev,
+                                       vertex_order=args.vertex_order, frontier=frontier,
+                                       column_parts=emulate, column_index=0)
+    elif not dist_mode:
         from bbgr.graph import BipartiteGraph
         from bbgr.trainer import FusedTrainer
         graph = BipartiteGraph(edges, U, I, dev, vertex_order=args.vertex_order)
         trainer = FusedTrainer(graph, args.variant, cred=cred, emb_dim=d, num_layers=K,
                                batch_size=B, frontier=frontier)
+    elif columns:
+        from bbgr.columns import ColumnShardedTrainer
+        trainer = ColumnShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
+                                       num_layers=K, batch_size=B, device=dev,
+                                       vertex_order=args.vertex_order, frontier=frontier)
     elif weak:
         from bbgr.distributed import ShardedTrainer
         trainer = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
@@ -441,9 +469,11 @@ def main():
         trainer = ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
                                                    emb_dim=d, num_layers=K, batch_size=B,
                                                    device=dev, frontier=frontier, **xp)
-    # edges of the whole job's graph: the sum of the ranks' shards
+    # edges of the whole job's graph: the sum of the ranks' shards (column
+    # shards all hold the whole graph)
     E_local = trainer.graph.item_csr.nnz
-    E = int(_allreduce(E_local, dev, torch.distributed.ReduceOp.SUM)) if dist_mode else E_local
+    E = int(_allreduce(E_local, dev, torch.distributed.ReduceOp.SUM)) if dist_mode and \
+        not columns else E_local
     U_job = U * (world if weak else 1)
     if dist_mode:
         del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
@@ -508,6 +538,9 @@ def main():
     if dist_mode:
         gathered_step = _allreduce(gathered_step, dev, torch.distributed.ReduceOp.SUM)
         visited_step = _allreduce(visited_step, dev, torch.distributed.ReduceOp.SUM)
+        if columns:   # every rank gathers every edge on 1/N of the columns
+            gathered_step /= world
+            visited_step /= world
     dense_ms = None
     if trainer.frontier and args.dense_check > 0:
         # the same trainer with frontier sparsity off (every product over the
@@ -533,7 +566,7 @@ def main():
         trainer.close()                    # the native exchange's communicator, if any
     groups = roofline_groups(timer, counts, timer_steps, count_steps, I)
     weak_beside = None
-    if world > 1 and not weak and args.weak_beside > 0 and not sharded_gen:
+    if world > 1 and not weak and not columns and args.weak_beside > 0 and not sharded_gen:
         # the same machinery at fixed per-GPU work, beside the strong line:
         # every rank a full config-sized user shard over the shared items
         del trainer
@@ -581,8 +614,12 @@ def main():
                    "vertex_order": args.vertex_order,
                    "emb_dim": d, "num_layers": K,
                    "global_batch": B * (world if weak else 1),
-                   "parallelism": f"user-rows x{world}"
-                                  + (" (sharded trainer)" if dist_mode and world == 1 else "")},
+                   "parallelism": (f"embedding-columns x{world} ({d // world} columns per "
+                                   "rank, whole graph on every rank)" if columns else
+                                   f"one column shard of {emulate} ({d // emulate} columns): "
+                                   "single-GPU stand-in for one rank" if emulate else
+                                   f"user-rows x{world}"
+                                   + (" (sharded trainer)" if dist_mode and world == 1 else ""))},
         "bpr_steps_per_s": steps_per_s,
         "weak_beside": weak_beside,
         "graph_replay": use_graph,

@@ -105,6 +105,7 @@ class BprArgs(ctypes.Structure):
         ("g_ue", c_void_p), ("ldgue", c_int64),
         ("g_ie", c_void_p), ("ldgie", c_int64),
         ("contrib", c_void_p), ("ldcontrib", c_int64),
+        ("scores_out", c_void_p), ("scores", c_void_p),
     ]
 
 

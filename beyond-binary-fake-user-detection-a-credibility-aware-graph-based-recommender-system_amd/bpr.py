@@ -22,7 +22,7 @@ def _idx(t: torch.Tensor, device) -> torch.Tensor:
 
 def bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop=None, lambda_fair=0.0,
              parts=None, dloss=None, g_uf=None, g_if=None, g_ue=None, g_ie=None,
-             contrib=None):
+             contrib=None, scores_out=None, scores=None):
     a = _lib.BprArgs()
     a.batch, a.d = users.numel(), uf.shape[1]
     a.n_users, a.n_items = uf.shape[0], itf.shape[0]
@@ -41,6 +41,7 @@ def bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop=None, lambda_fair=0.0,
     a.g_ue, a.ldgue = ptr(g_ue), ld(g_ue)
     a.g_ie, a.ldgie = ptr(g_ie), ld(g_ie)
     a.contrib, a.ldcontrib = ptr(contrib), ld(contrib)
+    a.scores_out, a.scores = ptr(scores_out), ptr(scores)
     return a
 
 

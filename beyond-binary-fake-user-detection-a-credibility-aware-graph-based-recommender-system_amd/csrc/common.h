@@ -78,6 +78,23 @@ __device__ __forceinline__ double u01_53(uint32_t a, uint32_t b) {
 }
 
 // ---------------------------------------------------------------------------
+// Row shape of a d-wide fp32 table row held by one 16-lane group: d >= 64 ->
+// all 16 lanes, V = d/64 float4 each (lane l holds float4 columns l, l+16, ..);
+// narrow rows (d = 8, 16, 32: the column slices of a column-sharded table)
+// -> the first d/4 lanes, one float4 each; the other lanes idle.
+// ---------------------------------------------------------------------------
+template <int D> struct RowShape {
+  static_assert(D == 8 || D == 16 || D == 32 || D == 64 || D == 128 || D == 256,
+                "row width");
+  static constexpr int LANES = D >= 64 ? 16 : D / 4;
+  static constexpr int V = D >= 64 ? D / 64 : 1;
+};
+
+inline bool supported_width(int d) {
+  return d == 8 || d == 16 || d == 32 || d == 64 || d == 128 || d == 256;
+}
+
+// ---------------------------------------------------------------------------
 // torch.optim.Adam on one element (amsgrad=False, maximize=False). Shared by
 // adam_kernel and the SpMM epilogue's fused step with every rounding spelled
 // out (explicit fmaf, no contraction) so the two paths agree bit for bit.

@@ -151,7 +151,10 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 #define BBGR_PAIR_WAVES256 0
 #endif
 
-template <int D> struct Tune;
+template <int D> struct Tune {   // narrow rows (8, 16, 32): one-row kernels only
+  static constexpr int row_u = 0, row_waves = 0, pair_u = 0, pair_u_masked = 0;
+  static constexpr int pair_waves = 0, pair_waves_masked = 0;
+};
 template <> struct Tune<64> {
   static constexpr int row_u = BBGR_ROW_U, row_waves = BBGR_ROW_WAVES;
   static constexpr int pair_u = BBGR_PAIR_U, pair_u_masked = BBGR_PAIR_U_MASKED;
@@ -223,6 +226,73 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
         }
       }
     }
+  }
+}
+
+// Narrow rows (D = 8, 16, 32; column-sharded tables): the 16-lane group
+// still owns one output row and loads 16 column indices at a time, but L =
+// D/4 lanes cover one gathered row, so S = 16/L edges are gathered per load
+// round and each lane keeps R = L loads in flight per 16-edge batch. Lane
+// (slot, sub) accumulates edges slot, slot+S, ... of every batch; the S slot
+// sums are added by a fixed xor tree at the end (deterministic; every lane
+// then holds its sub-column block of the row sum).
+template <int D, int WMODE, bool MASKED>
+__device__ __forceinline__ void gather_range_narrow(const SpmmParams &P, int eb, int ee,
+                                                    int lane, float4 &acc) {
+  constexpr int L = D / 4;
+  constexpr int S = 16 / L;
+  constexpr int R = L;
+  const int slot = lane / L, sub = lane - slot * L;
+  for (int e0 = eb; e0 < ee; e0 += 16) {
+    const int n = min(16, ee - e0);
+    int my = -1;
+    float mw = 0.f;
+    if (lane < n) {
+      my = P.indices[e0 + lane];
+      if (MASKED && P.src_mask && !P.src_mask[my]) my = -1;
+      if (my >= 0) {
+        if (WMODE == 1) mw = P.edge_val[e0 + lane];
+        if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
+      }
+    }
+    if (MASKED && P.src_mask) {
+      const unsigned long long live = __ballot(my >= 0);
+      if (((live >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
+    }
+    float4 v[R];
+    float w[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = r * S + slot;
+      const int c = __shfl(my, e, 16);
+      w[r] = WMODE == 0 ? 1.f : __shfl(mw, e, 16);
+      if (e < n && (!MASKED || c >= 0)) {
+        const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + sub;
+        v[r] = c >= P.nt_from ? ld_nt(src) : *src;
+      } else {
+        v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc = WMODE == 0 ? f4_add(acc, v[r]) : f4_fma(w[r], v[r], acc);
+  }
+#pragma unroll
+  for (int off = L; off < 16; off <<= 1) {
+    acc.x += __shfl_xor(acc.x, off, 16);
+    acc.y += __shfl_xor(acc.y, off, 16);
+    acc.z += __shfl_xor(acc.z, off, 16);
+    acc.w += __shfl_xor(acc.w, off, 16);
+  }
+}
+
+// A row's gather for any width: the narrow form below 64 columns.
+template <int D, int WMODE, bool MASKED>
+__device__ __forceinline__ void gather_row(const SpmmParams &P, int eb, int ee, int lane,
+                                           float4 (&acc)[RowShape<D>::V]) {
+  if constexpr (D < 64) {
+    gather_range_narrow<D, WMODE, MASKED>(P, eb, ee, lane, acc[0]);
+  } else {
+    gather_range<D, WMODE, MASKED>(P, eb, ee, lane, acc);
   }
 }
 
@@ -337,8 +407,8 @@ __device__ __forceinline__ AdamConsts launch_adam_consts(const SpmmParams &P) {
 
 template <int D>
 __device__ __forceinline__ void adam_row(const SpmmParams &P, int row, int lane,
-                                         const float4 (&G)[D / 64]) {
-  constexpr int V = D / 64;
+                                         const float4 (&G)[RowShape<D>::V]) {
+  constexpr int V = RowShape<D>::V;
   const AdamConsts ac = launch_adam_consts(P);
   float4 *pp = reinterpret_cast<float4 *>(P.adam_p + (long)row * P.adam_ld) + lane;
   float4 *pm = reinterpret_cast<float4 *>(P.adam_m + (long)row * P.adam_ld) + lane;
@@ -367,8 +437,9 @@ __device__ __forceinline__ void adam_row(const SpmmParams &P, int row, int lane,
 
 template <int D>
 __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
-                                         const float4 (&T)[D / 64]) {
-  constexpr int V = D / 64;
+                                         const float4 (&T)[RowShape<D>::V]) {
+  constexpr int V = RowShape<D>::V;
+  if (lane >= RowShape<D>::LANES) return;   // narrow rows: idle lanes
   if (P.y || P.adam_p) {
     const float ys = (P.y_scale ? P.y_scale[row] : 1.f) * P.y_scale_s;
     float4 G[V];
@@ -416,11 +487,13 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
 // red[0][*]. Called by all 256 threads.
 template <int D>
 __device__ __forceinline__ void block_reduce16(float4 *red, int g, int lane,
-                                               const float4 (&acc)[D / 64]) {
-  constexpr int V = D / 64;
+                                               const float4 (&acc)[RowShape<D>::V]) {
+  constexpr int V = RowShape<D>::V;
   constexpr int W = D / 4;  // float4 per row
+  if (lane < RowShape<D>::LANES) {
 #pragma unroll
-  for (int k = 0; k < V; ++k) red[g * W + lane + 16 * k] = acc[k];
+    for (int k = 0; k < V; ++k) red[g * W + lane + 16 * k] = acc[k];
+  }
   __syncthreads();
   if (threadIdx.x < W) {
     float4 s = red[threadIdx.x];
@@ -437,12 +510,13 @@ __device__ __forceinline__ void block_reduce16(float4 *red, int g, int lane,
 template <int D>
 __device__ __forceinline__ void split_row_finish(const SpmmParams &P, int row, int base, int c,
                                                  float4 *red, int g, int lane) {
-  constexpr int V = D / 64;
+  constexpr int V = RowShape<D>::V;
   float4 acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int c_lane = lane < RowShape<D>::LANES ? c : 0;   // idle lanes read nothing
 #pragma unroll 4
-  for (int sl = g; sl < c; sl += 16) {
+  for (int sl = g; sl < c_lane; sl += 16) {
     const float4 *src =
         reinterpret_cast<const float4 *>(P.partial) + (long)(base + sl) * (D / 4) + lane;
 #pragma unroll
@@ -470,8 +544,8 @@ __device__ __forceinline__ void split_row_finish(const SpmmParams &P, int row, i
 template <int D>
 __device__ __forceinline__ void split_row_arrive(const SpmmParams &P, int4 ch, float4 *red,
                                                  int g, int lane) {
-  constexpr int V = D / 64;
-  if (g == 0) {
+  constexpr int V = RowShape<D>::V;
+  if (g == 0 && lane < RowShape<D>::LANES) {
     unsigned long long *dst = reinterpret_cast<unsigned long long *>(
         reinterpret_cast<float4 *>(P.partial) + (long)ch.w * (D / 4) + lane);
 #pragma unroll
@@ -514,7 +588,7 @@ __device__ __forceinline__ void split_row_arrive(const SpmmParams &P, int4 ch, f
 
 template <int D, int WMODE, bool MASKED, bool PAIR>
 __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
-  constexpr int V = D / 64;
+  constexpr int V = RowShape<D>::V;
   __shared__ float4 red[16 * (D / 4)];
   const int g = threadIdx.x >> 4;
   const int lane = threadIdx.x & 15;
@@ -531,10 +605,10 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     const int per = (((len + 15) >> 4) + 15) & ~15;  // multiple of 16
     const int gb = ch.y + g * per;
     const int ge = min(ch.z, gb + per);
-    if (gb < ge) gather_range<D, WMODE, MASKED>(P, gb, ge, lane, acc);
+    if (gb < ge) gather_row<D, WMODE, MASKED>(P, gb, ge, lane, acc);
     block_reduce16<D>(red, g, lane, acc);
     if (ch.w < 0) {   // the row's only chunk
-      if (g == 0) {
+      if (g == 0 && lane < RowShape<D>::LANES) {
         float4 T[V];
 #pragma unroll
         for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
@@ -546,7 +620,7 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     return;
   }
 
-  if (PAIR) {   // ---- short rows, two per 16-lane group (rows j and j + 16)
+  if constexpr (PAIR && D >= 64) {   // ---- short rows, two per 16-lane group (rows j, j + 16)
     long rr[2];
     int eb[2], ee[2];
 #pragma unroll
@@ -591,7 +665,7 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   const int ee = P.indptr[row + 1];
   if (ee - eb > P.long_threshold) return;  // owned by chunk blocks
   if (MASKED && !P.row_list && P.row_mask && !P.row_mask[row]) return;
-  gather_range<D, WMODE, MASKED>(P, eb, ee, lane, acc);
+  gather_row<D, WMODE, MASKED>(P, eb, ee, lane, acc);
   epilogue<D>(P, (int)row, lane, acc);
 }
 
@@ -637,7 +711,7 @@ __global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves) void spmm_adam
 template <int D>
 __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float *t,
                                                        long ldt) {
-  constexpr int V = D / 64;
+  constexpr int V = RowShape<D>::V;
   const long j = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
   long row = j;
@@ -648,6 +722,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float
   }
   if (row >= P.n_rows) return;
   if (P.row_mask && !P.row_mask[row]) return;
+  if (lane >= RowShape<D>::LANES) return;
   const float4 *src = reinterpret_cast<const float4 *>(t + j * ldt) + lane;
   float4 T[V];
 #pragma unroll
@@ -659,22 +734,24 @@ template <int D, int WMODE>
 static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
   const bool masked = P.src_mask || P.row_mask || P.row_list;
   const long short_rows = P.row_list ? P.n_row_list : (long)(P.row_end - P.row_begin);
-  const bool pair = P.pair_rows;
+  const bool pair = D >= 64 && P.pair_rows;
   const long per_block = pair ? 32 : 16;
   const long short_blocks = (short_rows + per_block - 1) / per_block;
   const long grid = (long)P.n_chunks + short_blocks;
   if (grid > 0) {
     const dim3 gd((unsigned)grid), bd(256);
-    if (masked) {
-      if (pair) hipLaunchKernelGGL((spmm_masked_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
-      else hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE>), gd, bd, 0, st, P);
-    } else if (P.adam_p) {
-      if (pair) hipLaunchKernelGGL((spmm_adam_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
-      else hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE>), gd, bd, 0, st, P);
-    } else {
-      if (pair) hipLaunchKernelGGL((spmm_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
-      else hipLaunchKernelGGL((spmm_kernel<D, WMODE>), gd, bd, 0, st, P);
+    if constexpr (D >= 64) {
+      if (pair) {
+        if (masked) hipLaunchKernelGGL((spmm_masked_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+        else if (P.adam_p) hipLaunchKernelGGL((spmm_adam_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+        else hipLaunchKernelGGL((spmm_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+        BBGR_LAUNCHED("spmm_kernel");
+        return BBGR_OK;
+      }
     }
+    if (masked) hipLaunchKernelGGL((spmm_masked_kernel<D, WMODE>), gd, bd, 0, st, P);
+    else if (P.adam_p) hipLaunchKernelGGL((spmm_adam_kernel<D, WMODE>), gd, bd, 0, st, P);
+    else hipLaunchKernelGGL((spmm_kernel<D, WMODE>), gd, bd, 0, st, P);
     BBGR_LAUNCHED("spmm_kernel");
   }
   (void)n_split;   // split rows are finished in-launch (split_row_arrive)
@@ -756,8 +833,8 @@ extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
                              const bbgr_spmm_args *a, bbgr_stream_t stream) {
   BBGR_REQUIRE(a && n_rows >= 0, "bbgr_epilogue: bad args");
   const int d = a->d;
-  if (d != 64 && d != 128 && d != 256) {
-    set_error("bbgr_epilogue: embedding dim %d unsupported (64, 128, 256)", d);
+  if (!supported_width(d)) {
+    set_error("bbgr_epilogue: embedding dim %d unsupported (8, 16, 32, 64, 128, 256)", d);
     return BBGR_ERR_UNSUPPORTED;
   }
   if (n_rows == 0) return BBGR_OK;
@@ -778,6 +855,9 @@ extern "C" int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
   const unsigned grid = (unsigned)((n_in + 15) / 16);
   hipStream_t st = as_stream(stream);
   switch (d) {
+    case 8: hipLaunchKernelGGL(epilogue_kernel<8>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
+    case 16: hipLaunchKernelGGL(epilogue_kernel<16>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
+    case 32: hipLaunchKernelGGL(epilogue_kernel<32>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
     case 64: hipLaunchKernelGGL(epilogue_kernel<64>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
     case 128: hipLaunchKernelGGL(epilogue_kernel<128>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
     default: hipLaunchKernelGGL(epilogue_kernel<256>, dim3(grid), dim3(256), 0, st, P, t, (long)ldt); break;
@@ -794,8 +874,8 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   BBGR_REQUIRE(csr->indptr && (csr->nnz == 0 || csr->indices),
                "bbgr_spmm: null csr arrays");
   const int d = a->d;
-  if (d != 64 && d != 128 && d != 256) {
-    set_error("bbgr_spmm: embedding dim %d unsupported (64, 128, 256)", d);
+  if (!supported_width(d)) {
+    set_error("bbgr_spmm: embedding dim %d unsupported (8, 16, 32, 64, 128, 256)", d);
     return BBGR_ERR_UNSUPPORTED;
   }
   BBGR_REQUIRE(a->x || csr->nnz == 0, "bbgr_spmm: null x");
@@ -864,11 +944,14 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   // would be skipped and the fix-up would sum stale partials
   BBGR_REQUIRE(!a->row_list || a->row_mask || csr->n_chunks == 0,
                "bbgr_spmm: row_list needs row_mask when the plan has long-row chunks");
-  P.pair_rows = pair_rows(csr);
+  P.pair_rows = d >= 64 && pair_rows(csr);
   P.nt_from = a->stream_from > 0 ? a->stream_from : 0x7fffffff;
   P.nt_out_from = a->stream_out_from > 0 ? a->stream_out_from : 0x7fffffff;
   hipStream_t st = as_stream(stream);
   switch (d) {
+    case 8: return dispatch_wmode<8>(P, a->weight_mode, n_split, st);
+    case 16: return dispatch_wmode<16>(P, a->weight_mode, n_split, st);
+    case 32: return dispatch_wmode<32>(P, a->weight_mode, n_split, st);
     case 64: return dispatch_wmode<64>(P, a->weight_mode, n_split, st);
     case 128: return dispatch_wmode<128>(P, a->weight_mode, n_split, st);
     default: return dispatch_wmode<256>(P, a->weight_mode, n_split, st);

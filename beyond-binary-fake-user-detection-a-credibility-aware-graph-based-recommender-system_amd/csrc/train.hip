@@ -23,6 +23,8 @@ struct BprParams {
   long ldguf, ldgif, ldgue, ldgie;
   float *contrib;
   long ldc;
+  float *scores_out;      // partial (s+, s-, r) over this table's columns
+  const float *scores;    // complete (s+, s-, r) (all-reduced over column shards)
 };
 
 __device__ __forceinline__ float group16_sum(float v) {
@@ -55,18 +57,25 @@ __device__ __forceinline__ void atomic_axpby4(float *dst, float a, float4 x,
 // One 16-lane group per (user, pos, neg) triple.
 template <int D>
 __global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
-  constexpr int V = D / 64;
+  constexpr int V = RowShape<D>::V;
+  constexpr int LANES = RowShape<D>::LANES;
   const long b = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
   if (b >= P.batch) return;
   const long u = P.users[b], ip = P.pos[b], in = P.neg[b];
   if (u < 0 || u >= P.n_users || ip < 0 || ip >= P.n_items || in < 0 || in >= P.n_items) {
+    if (P.scores_out && lane == 0) {
+      P.scores_out[3 * b + 0] = 0.f;
+      P.scores_out[3 * b + 1] = 0.f;
+      P.scores_out[3 * b + 2] = 0.f;
+    }
+    if (P.scores_out) return;
     if (P.parts && lane == 0) {
       P.parts[3 * b + 0] = 0.f;
       P.parts[3 * b + 1] = 0.f;
       P.parts[3 * b + 2] = 0.f;
     }
-    if (P.contrib) {
+    if (P.contrib && lane < LANES) {
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int r = 0; r < 3; ++r)
@@ -76,15 +85,17 @@ __global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
     }
     return;  // whole group leaves together
   }
+  const bool act = lane < LANES;   // narrow rows: the first d/4 lanes hold the row
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 fu[V], fp[V], fn[V];
   const float4 *pu = reinterpret_cast<const float4 *>(P.uf + u * P.lduf) + lane;
   const float4 *pp = reinterpret_cast<const float4 *>(P.itf + ip * P.ldif) + lane;
   const float4 *pn = reinterpret_cast<const float4 *>(P.itf + in * P.ldif) + lane;
 #pragma unroll
   for (int k = 0; k < V; ++k) {
-    fu[k] = pu[16 * k];
-    fp[k] = pp[16 * k];
-    fn[k] = pn[16 * k];
+    fu[k] = act ? pu[16 * k] : z4;
+    fp[k] = act ? pp[16 * k] : z4;
+    fn[k] = act ? pn[16 * k] : z4;
   }
   float sp = 0.f, sn = 0.f;
 #pragma unroll
@@ -94,9 +105,7 @@ __global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
   }
   sp = group16_sum(sp);
   sn = group16_sum(sn);
-  const float x = sp - sn;
-  const float sig = 1.0f / (1.0f + expf(-x));
-  const bool need_reg = P.parts || P.g_ue || P.g_ie;
+  const bool need_reg = P.parts || P.g_ue || P.g_ie || P.scores_out;
   float4 eu[V], ep[V], en[V];
   if (need_reg) {
     const float4 *qu = reinterpret_cast<const float4 *>(P.ue + u * P.ldue) + lane;
@@ -104,16 +113,35 @@ __global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
     const float4 *qn = reinterpret_cast<const float4 *>(P.ie + in * P.ldie) + lane;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      eu[k] = qu[16 * k];
-      ep[k] = qp[16 * k];
-      en[k] = qn[16 * k];
+      eu[k] = act ? qu[16 * k] : z4;
+      ep[k] = act ? qp[16 * k] : z4;
+      en[k] = act ? qn[16 * k] : z4;
     }
   }
-  if (P.parts) {
+  float r_full = 0.f;
+  if (P.parts || P.scores_out) {
     float r = 0.f;
 #pragma unroll
     for (int k = 0; k < V; ++k) r += dot4(eu[k], eu[k]) + dot4(ep[k], ep[k]) + dot4(en[k], en[k]);
-    r = group16_sum(r);
+    r_full = group16_sum(r);
+  }
+  if (P.scores_out) {   // column shard: this table's share of (s+, s-, r) only
+    if (lane == 0) {
+      P.scores_out[3 * b + 0] = sp;
+      P.scores_out[3 * b + 1] = sn;
+      P.scores_out[3 * b + 2] = r_full;
+    }
+    return;
+  }
+  if (P.scores) {       // column shard: the complete sums over every shard
+    sp = P.scores[3 * b + 0];
+    sn = P.scores[3 * b + 1];
+    r_full = P.scores[3 * b + 2];
+  }
+  const float x = sp - sn;
+  const float sig = 1.0f / (1.0f + expf(-x));
+  if (P.parts) {
+    const float r = r_full;
     if (lane == 0) {
       P.parts[3 * b + 0] = -logf(sig + 1e-12f);
       P.parts[3 * b + 1] = r;
@@ -126,6 +154,7 @@ __global__ __launch_bounds__(256) void bpr_kernel(BprParams P) {
   const float gx = -(sig * (1.0f - sig)) / (sig + 1e-12f) * G;
   const float gpos = gx + (P.pop ? P.lambda_fair * P.pop[ip] * G : 0.f);
   const float gneg = -gx;
+  if (!act) return;   // narrow rows: lanes past the row write nothing
   if (P.contrib) {   // deterministic mode: per-triple rows, summed by scatter_add_rows
     float4 *cu = reinterpret_cast<float4 *>(P.contrib + b * P.ldc) + lane;
     float4 *cp = reinterpret_cast<float4 *>(P.contrib + (P.batch + b) * P.ldc) + lane;
@@ -322,10 +351,10 @@ __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const uns
                                                                const float *src, long lds,
                                                                float *dst, long ldd,
                                                                unsigned skip) {
-  constexpr int V = D / 64;
+  constexpr int V = RowShape<D>::V;
   const long s = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
-  if (s >= n) return;
+  if (s >= n || lane >= RowShape<D>::LANES) return;
   const unsigned key = keys[s];
   if (key == skip || (s > 0 && keys[s - 1] == key)) return;
   float4 acc[V];
@@ -357,8 +386,8 @@ extern "C" int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float 
                                      bbgr_stream_t stream) {
   BBGR_REQUIRE(n >= 0 && n < (1ll << 31) && n_dst >= 0 && n_dst < 0xFFFFFFFFll && workspace_bytes,
                "bbgr_scatter_add_rows: bad sizes");
-  if (d != 64 && d != 128 && d != 256) {
-    set_error("bbgr_scatter_add_rows: d = %d unsupported (64, 128, 256)", d);
+  if (!supported_width(d)) {
+    set_error("bbgr_scatter_add_rows: d = %d unsupported (8, 16, 32, 64, 128, 256)", d);
     return BBGR_ERR_UNSUPPORTED;
   }
   int end_bit = 1;   // keys are in [0, n_dst] (n_dst marks skipped rows)
@@ -394,6 +423,9 @@ extern "C" int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float 
                                               end_bit, st));
   const unsigned grid = (unsigned)((n + 15) / 16);
   switch (d) {
+    case 8: hipLaunchKernelGGL(scatter_segments_kernel<8>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
+    case 16: hipLaunchKernelGGL(scatter_segments_kernel<16>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
+    case 32: hipLaunchKernelGGL(scatter_segments_kernel<32>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
     case 64: hipLaunchKernelGGL(scatter_segments_kernel<64>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
     case 128: hipLaunchKernelGGL(scatter_segments_kernel<128>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
     default: hipLaunchKernelGGL(scatter_segments_kernel<256>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
@@ -407,15 +439,16 @@ extern "C" int bbgr_bpr(const bbgr_bpr_args *a, bbgr_stream_t stream) {
   BBGR_REQUIRE(a->batch >= 0, "bbgr_bpr: negative batch");
   if (a->batch == 0) return BBGR_OK;
   const int d = a->d;
-  if (d != 64 && d != 128 && d != 256) {
-    set_error("bbgr_bpr: embedding dim %d unsupported (64, 128, 256)", d);
+  if (!supported_width(d)) {
+    set_error("bbgr_bpr: embedding dim %d unsupported (8, 16, 32, 64, 128, 256)", d);
     return BBGR_ERR_UNSUPPORTED;
   }
   BBGR_REQUIRE(a->users && a->pos && a->neg && a->uf && a->itf,
                "bbgr_bpr: null index/table");
   BBGR_REQUIRE(a->n_users > 0 && a->n_items > 0, "bbgr_bpr: n_users/n_items must be set");
-  const bool need_reg = a->parts || a->g_ue || a->g_ie;
+  const bool need_reg = a->parts || a->g_ue || a->g_ie || a->scores_out;
   BBGR_REQUIRE(!need_reg || (a->ue && a->ie), "bbgr_bpr: ego tables required");
+  BBGR_REQUIRE(!(a->scores_out && a->scores), "bbgr_bpr: scores_out and scores exclude each other");
   BprParams P;
   P.batch = a->batch;
   P.n_users = a->n_users;
@@ -438,6 +471,8 @@ extern "C" int bbgr_bpr(const bbgr_bpr_args *a, bbgr_stream_t stream) {
   P.g_ue = a->g_ue; P.ldgue = a->ldgue;
   P.g_ie = a->g_ie; P.ldgie = a->ldgie;
   P.contrib = a->contrib; P.ldc = a->ldcontrib;
+  P.scores_out = a->scores_out;
+  P.scores = a->scores;
   const long lds[] = {P.lduf, P.ldif, P.ldue, P.ldie, P.ldguf, P.ldgif, P.ldgue, P.ldgie, P.ldc};
   const void *ptrs[] = {P.uf, P.itf, P.ue, P.ie, P.g_uf, P.g_if, P.g_ue, P.g_ie, P.contrib};
   for (int k = 0; k < 9; ++k) {
@@ -448,6 +483,9 @@ extern "C" int bbgr_bpr(const bbgr_bpr_args *a, bbgr_stream_t stream) {
   const unsigned grid = (unsigned)((a->batch + 15) / 16);
   hipStream_t st = as_stream(stream);
   switch (d) {
+    case 8: hipLaunchKernelGGL(bpr_kernel<8>, dim3(grid), dim3(256), 0, st, P); break;
+    case 16: hipLaunchKernelGGL(bpr_kernel<16>, dim3(grid), dim3(256), 0, st, P); break;
+    case 32: hipLaunchKernelGGL(bpr_kernel<32>, dim3(grid), dim3(256), 0, st, P); break;
     case 64: hipLaunchKernelGGL(bpr_kernel<64>, dim3(grid), dim3(256), 0, st, P); break;
     case 128: hipLaunchKernelGGL(bpr_kernel<128>, dim3(grid), dim3(256), 0, st, P); break;
     default: hipLaunchKernelGGL(bpr_kernel<256>, dim3(grid), dim3(256), 0, st, P); break;

@@ -197,10 +197,7 @@ class FusedTrainer:
         # (a caller's batch may repeat a user: its last user layer then runs on
         # the de-duplicated mask instead of a row list, whose repeated rows
         # would update the in-place accumulator twice)
-        a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
-                     self.pop, self.lambda_fair, parts=self.parts[: 3 * B],
-                     contrib=self.contrib)
-        call("bbgr_bpr", ctypes.byref(a), st)
+        self._bpr(users, pos, neg, B)
         self.scatter(self.g_uf, users, self.contrib[:B])
         self.scatter(self.g_if, self.posneg[: 2 * B], self.contrib[B: 3 * B])
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
@@ -233,6 +230,13 @@ class FusedTrainer:
         if masks is not None:
             self._set_masks(users, pos, neg, 0)
         return self.loss
+
+    def _bpr(self, users, pos, neg, B: int) -> None:
+        """Fused BPR forward + per-triple gradient rows (bbgr_bpr, contrib mode)."""
+        a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
+                     self.pop, self.lambda_fair, parts=self.parts[: 3 * B],
+                     contrib=self.contrib)
+        call("bbgr_bpr", ctypes.byref(a), stream_handle())
 
     def _backward_fused(self, users, item_rows, masks, alpha: float, reduce=None,
                         item_adam: bool = True) -> None:

@@ -176,7 +176,9 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*                cs_r = (acc_scale ? acc_scale[r] : 1) * acc_scale_s;        */
 /*                acc_in NULL => 0                                            */
 /* Tables are fp32 row-major with leading dimension ld* (floats, multiple of  */
-/* 4, 16-byte aligned base). d in {64, 128, 256}.                             */
+/* 4, 16-byte aligned base). d in {64, 128, 256}, or 8, 16, 32 for the      */
+/* column slices of a column-sharded model (narrow rows: d/4 lanes gather one */
+/* row, 16/(d/4) edges per load round, slot sums added by a fixed xor tree).  */
 /* partial: workspace of (csr->n_chunks * d) floats when csr->n_split > 0.    */
 /* src_mask (nullable, [n_cols] bytes): edges whose column is 0 in the mask    */
 /*   are skipped — exact when x is zero on those rows (sparse gradients).     */
@@ -309,6 +311,13 @@ int bbgr_epilogue(int32_t n_rows, const float *t, int64_t ldt,
 /*   reproducible training step).                                            */
 /* A triple with an index outside [0,n_users) / [0,n_items) (e.g. the        */
 /* sampler's -1 for a user without positives) contributes zero everywhere.   */
+/* Column-sharded tables (each rank holds d of the model's columns): a first  */
+/*   call with scores_out writes this shard's (s+, s-, |ue|^2+|ie+|^2+|ie-|^2) */
+/*   per triple and nothing else; the caller sums them over the shards        */
+/*   (all-reduce, 12 B per triple) and a second call with scores uses the     */
+/*   complete sums for the loss parts and the gradient coefficients, writing  */
+/*   this shard's columns of the gradient rows.                               */
+/* d: 8, 16, 32, 64, 128 or 256 (narrow widths: column shards).               */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int64_t batch;
@@ -332,6 +341,8 @@ typedef struct {
   float *g_ue; int64_t ldgue;
   float *g_ie; int64_t ldgie;
   float *contrib; int64_t ldcontrib;
+  float *scores_out;               /* nullable, [3*batch]: see below */
+  const float *scores;             /* nullable, [3*batch]: see below */
 } bbgr_bpr_args;
 
 int bbgr_bpr(const bbgr_bpr_args *args, bbgr_stream_t stream);

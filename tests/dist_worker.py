@@ -28,6 +28,8 @@ def main():
         return fused_vs_separate(out_dir, variant)
     if mode == "rccl1":
         return rccl_single_rank(out_dir, variant, order)
+    if mode == "columns":
+        return column_sharded(out_dir, variant, frontier, order)
     dist.init_process_group("gloo")
     rank = dist.get_rank()
     torch.cuda.set_device(0)
@@ -133,6 +135,44 @@ def rccl_single_rank(out_dir, variant, order="input"):
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, "rccl1.npz"), **out)
     nat.close()   # bbgr_comm_destroy
+    dist.destroy_process_group()
+
+
+def column_sharded(out_dir, variant, frontier, order):
+    """Column (embedding-dimension) sharding: each rank holds the whole graph
+    and d/world columns; three steps, then the full-width tables (all-gathered)
+    and the losses, with rank 0's single-GPU FusedTrainer on the same inputs."""
+    from bbgr.columns import ColumnShardedTrainer
+    from bbgr.graph import BipartiteGraph
+    from bbgr.synthetic import synthetic_credibility
+    from bbgr.trainer import FusedTrainer
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    U, I, E = 3000, 900, 40000
+    e = synthetic_edges(U, I, E, 21, items="zipf")
+    rng = np.random.default_rng(21)
+    u0 = rng.uniform(-0.3, 0.3, (U, 64)).astype(np.float32)
+    i0 = rng.uniform(-0.3, 0.3, (I, 64)).astype(np.float32)
+    kw = dict(cred=synthetic_credibility(U, 21), emb_dim=64, num_layers=3, batch_size=512,
+              u0=u0, i0=i0, frontier=frontier,
+              lambda_fair=0.05 if variant == "cu_fair" else 0.0)
+    tr = ColumnShardedTrainer(e, U, I, variant, device="cuda:0", vertex_order=order, **kw)
+    losses = [float(tr.step()) for _ in range(3)]
+    sd = tr.full_state_dict()
+    out = {"loss": np.array(losses), "c0": np.array(tr.c0), "c1": np.array(tr.c1),
+           "user_w": sd["user_emb.weight"].cpu().numpy(),
+           "item_w": sd["item_emb.weight"].cpu().numpy(),
+           "users": tr.batch()[0].cpu().numpy()}
+    if rank == 0:
+        one = FusedTrainer(BipartiteGraph(e, U, I, "cuda:0", vertex_order=order), variant, **kw)
+        out["ref_loss"] = np.array([float(one.step()) for _ in range(3)])
+        rsd = one.state_dict()
+        out["ref_user_w"] = rsd["user_emb.weight"].cpu().numpy()
+        out["ref_item_w"] = rsd["item_emb.weight"].cpu().numpy()
+        out["ref_users"] = one.batch()[0].cpu().numpy()
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"columns{rank}.npz"), **out)
     dist.destroy_process_group()
 
 

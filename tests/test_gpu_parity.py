@@ -81,7 +81,7 @@ def test_plan_chunks_cover_long_rows():
 # ---------------------------------------------------------------------------
 # Single fused SpMM vs scipy float64, all weight modes and dims
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("d", [8, 16, 32, 64, 128, 256])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("thr", [256, 8])
 def test_spmm_modes(d, mode, thr):
@@ -112,6 +112,74 @@ def test_spmm_modes(d, mode, thr):
     want_acc = 0.25 * (acc_in + 1.25 * accs[:, None] * Tm)
     assert_parity(y, want_y, "y")
     assert_parity(acc, want_acc, "acc")
+
+
+@pytest.mark.parametrize("d", [8, 16, 32])
+def test_narrow_spmm_masks_lists_and_fused_adam(d):
+    """Column-shard widths (d/4 lanes per row): src mask, row mask, row list
+    (with chunked rows flagged in the mask) and the fused Adam epilogue against
+    float64 / the separate Adam on the materialised product."""
+    from bbgr.optim import AdamRows
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(d)
+    R_, C_ = 600, 2500
+    e = synthetic_edges(C_, R_, 40000, 5, items="zipf")
+    rows, cols = e[1], e[0]
+    c = Csr(rows, cols, R_, C_, DEV, long_threshold=32, chunk_edges=128)
+    assert c.n_split > 0
+    prod = Product(c, None, None, None, {})
+    x = rng.uniform(-1, 1, (C_, d)).astype(np.float32)
+    src = (rng.random(C_) < 0.2).astype(np.uint8)
+    rmask = (rng.random(R_) < 0.3).astype(np.uint8)
+    M = R.csr64(rows, cols, np.ones(rows.size, np.float32), (R_, C_))
+    full = M @ x.astype(np.float64)
+    y = torch.empty(R_, d, device=DEV)
+    spmm(prod, t(x), False, y=y)
+    assert_parity(y, full, "plain")
+    y = torch.zeros(R_, d, device=DEV)
+    spmm(prod, t(x), False, y=y, src_mask=t(src, torch.uint8))
+    assert_parity(y, M @ (x.astype(np.float64) * src[:, None]), "src mask")
+    y = torch.zeros(R_, d, device=DEV)
+    spmm(prod, t(x), False, y=y, row_mask=t(rmask, torch.uint8))
+    assert_parity(y, full * rmask[:, None], "row mask")
+    lst = torch.as_tensor(np.flatnonzero(rmask), dtype=torch.int64, device=DEV)
+    y = torch.zeros(R_, d, device=DEV)
+    spmm(prod, t(x), False, y=y, row_mask=t(rmask, torch.uint8), row_list=lst)
+    assert_parity(y, full * rmask[:, None], "row list")
+    p0 = rng.normal(size=(R_, d)).astype(np.float32)
+    p1, m1, v1 = t(p0), torch.full((R_, d), 0.01, device=DEV), torch.full((R_, d), 0.02, device=DEV)
+    spmm(prod, t(x), False, adam=AdamRows(p1, m1, v1, 3, 1e-3))
+    p2, m2, v2 = t(p0), torch.full((R_, d), 0.01, device=DEV), torch.full((R_, d), 0.02, device=DEV)
+    g = torch.empty(R_, d, device=DEV)
+    spmm(prod, t(x), False, y=g)
+    AdamRows(p2, m2, v2, 3, 1e-3).apply(g)
+    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+
+
+def test_column_shard_forward_equals_full_width_columns():
+    """One column shard alone (ColumnShardedTrainer without a process group):
+    its forward tables are the full-width trainer's columns [c0, c1)."""
+    from bbgr.columns import ColumnShardedTrainer
+    from bbgr.trainer import FusedTrainer
+    U, I = 2000, 700
+    e = synthetic_edges(U, I, 30000, 13, items="zipf")
+    rng = np.random.default_rng(13)
+    u0 = rng.uniform(-0.5, 0.5, (U, 64)).astype(np.float32)
+    i0 = rng.uniform(-0.5, 0.5, (I, 64)).astype(np.float32)
+    cred = synthetic_credibility(U, 13)
+    full = FusedTrainer(BipartiteGraph(e, U, I, DEV, vertex_order="degree"), "v2_pop", cred=cred,
+                        emb_dim=64, num_layers=3, batch_size=256, u0=u0, i0=i0)
+    uf, itf = (x.double().cpu().numpy() for x in full.forward())
+    for parts in (2, 4, 8):
+        for idx in (0, parts - 1):
+            sh = ColumnShardedTrainer(e, U, I, "v2_pop", cred=cred, emb_dim=64, num_layers=3,
+                                      batch_size=256, u0=u0, i0=i0, column_parts=parts,
+                                      column_index=idx, device=DEV)
+            su, si = sh.forward()
+            c0, c1 = sh.c0, sh.c1
+            assert c1 - c0 == 64 // parts
+            assert_parity(su, uf[:, c0:c1], f"users {parts}/{idx}")
+            assert_parity(si, itf[:, c0:c1], f"items {parts}/{idx}")
 
 
 def test_spmm_deterministic():
