@@ -108,6 +108,9 @@ class ColumnShardedTrainer(FusedTrainer):
                      contrib=self.contrib, scores=sc)
         call("bbgr_bpr", ctypes.byref(a), st)
 
+    def close(self) -> None:
+        """Nothing to release (the sharded trainers' close() interface)."""
+
     def gather_columns(self, t: torch.Tensor) -> torch.Tensor:
         """The full-width table from every rank's column slice (collective)."""
         if not (self.distributed and self.world > 1):

@@ -285,6 +285,57 @@ __device__ __forceinline__ void gather_range_narrow(const SpmmParams &P, int eb,
   }
 }
 
+// Narrow short rows (D = 8, 16, 32): S = 16/L rows per 16-lane group, one
+// per L-lane slot, walked independently (a slot leaves its loop when its row
+// ends), so a wave keeps 64/L rows in flight: one row per group left these
+// launches bound by the per-row latency chain (indptr -> indices -> gathers
+// -> store) at 5M rows. Each lane adds its row's edges in CSR order, as the
+// full-width one-row kernel does per column block: a column slice of the
+// result is bitwise the full-width kernel's columns.
+template <int D, int WMODE, bool MASKED>
+__device__ __forceinline__ void gather_slot(const SpmmParams &P, int eb, int ee, int slot,
+                                            int sub, float4 &acc) {
+  constexpr int L = D / 4;
+  for (int e0 = eb; e0 < ee; e0 += 2 * L) {
+    int my0 = -1, my1 = -1;
+    float mw0 = 0.f, mw1 = 0.f;
+    const int ea = e0 + sub, eb2 = e0 + L + sub;
+    if (ea < ee) {
+      my0 = P.indices[ea];
+      if (MASKED && P.src_mask && !P.src_mask[my0]) my0 = -1;
+      if (my0 >= 0) {
+        if (WMODE == 1) mw0 = P.edge_val[ea];
+        if (WMODE == 2) mw0 = P.col_scale[my0] * P.col_scale_s;
+      }
+    }
+    if (eb2 < ee) {
+      my1 = P.indices[eb2];
+      if (MASKED && P.src_mask && !P.src_mask[my1]) my1 = -1;
+      if (my1 >= 0) {
+        if (WMODE == 1) mw1 = P.edge_val[eb2];
+        if (WMODE == 2) mw1 = P.col_scale[my1] * P.col_scale_s;
+      }
+    }
+    float4 v[2 * L];
+    float w[2 * L];
+#pragma unroll
+    for (int j = 0; j < 2 * L; ++j) {
+      const int src_lane = slot * L + (j % L);
+      const int c = __shfl(j < L ? my0 : my1, src_lane, 16);
+      w[j] = WMODE == 0 ? 1.f : __shfl(j < L ? mw0 : mw1, src_lane, 16);
+      if (e0 + j < ee && (!MASKED || c >= 0)) {
+        const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + sub;
+        v[j] = c >= P.nt_from ? ld_nt(src) : *src;
+      } else {
+        v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * L; ++j)
+      acc = WMODE == 0 ? f4_add(acc, v[j]) : f4_fma(w[j], v[j], acc);
+  }
+}
+
 // A row's gather for any width: the narrow form below 64 columns.
 template <int D, int WMODE, bool MASKED>
 __device__ __forceinline__ void gather_row(const SpmmParams &P, int eb, int ee, int lane,
@@ -651,6 +702,29 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     if (rr[1] >= 0) epilogue<D>(P, (int)rr[1], lane, accB);
     return;
   }
+  if constexpr (D < 64) {   // ---- narrow short rows: 16/L per group, one per slot
+    constexpr int L = D / 4, S = 16 / L;
+    const int slot = lane / L, sub = lane - slot * L;
+    long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * (16 * S) + g * S + slot;
+    if (MASKED && P.row_list) {
+      row = row < P.n_row_list ? P.row_list[row] : -1;
+    } else if (row >= P.row_end) {
+      row = -1;
+    }
+    if (row >= P.n_rows) row = -1;
+    int eb = 0, ee = 0;
+    if (row >= 0) {
+      eb = P.indptr[row];
+      ee = P.indptr[row + 1];
+      if (ee - eb > P.long_threshold || (MASKED && !P.row_list && P.row_mask && !P.row_mask[row]))
+        row = -1;
+    }
+    if (row < 0) eb = ee = 0;
+    float4 T[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
+    gather_slot<D, WMODE, MASKED>(P, eb, ee, slot, sub, T[0]);
+    if (row >= 0) epilogue<D>(P, (int)row, sub, T);
+    return;
+  }
   // ---- short rows: one 16-lane group per row ------------------------------
   long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * 16 + g;
   if (MASKED && P.row_list) {
@@ -735,7 +809,7 @@ static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
   const bool masked = P.src_mask || P.row_mask || P.row_list;
   const long short_rows = P.row_list ? P.n_row_list : (long)(P.row_end - P.row_begin);
   const bool pair = D >= 64 && P.pair_rows;
-  const long per_block = pair ? 32 : 16;
+  const long per_block = D < 64 ? 16 * (16 / (D / 4)) : (pair ? 32 : 16);
   const long short_blocks = (short_rows + per_block - 1) / per_block;
   const long grid = (long)P.n_chunks + short_blocks;
   if (grid > 0) {
