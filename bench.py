@@ -406,11 +406,13 @@ def main():
     weak = world > 1 and scaling == "weak"
     # configs too large to draw whole on every rank (C5) are drawn per user shard
     sharded_gen = not weak and cfg["num_edges"] > 100_000_000
-    from bbgr.columns import can_shard_columns
+    from bbgr.columns import MIN_AUTO_WIDTH, can_shard_columns
     partition = args.partition
     if partition == "auto":
+        # columns while the shards stay >= 16 columns wide (C4: N = 2, 4),
+        # user rows beyond
         partition = ("columns" if world > 1 and not weak and not sharded_gen
-                     and can_shard_columns(d, world) else "users")
+                     and can_shard_columns(d, world, MIN_AUTO_WIDTH) else "users")
     columns = dist_mode and partition == "columns" and not weak
     if columns:
         sharded_gen = False
@@ -622,6 +624,8 @@ def main():
                                    + (" (sharded trainer)" if dist_mode and world == 1 else ""))},
         "bpr_steps_per_s": steps_per_s,
         "weak_beside": weak_beside,
+        "partition": ("columns" if columns else "users") if dist_mode else
+                     (f"one column shard of {emulate}" if emulate else "single GPU"),
         "graph_replay": use_graph,
         "value_note": "value = SpMM edges actually gathered (source row read and "
                       "multiply-added) per second, whole job: every launch's edges counted "

@@ -48,8 +48,17 @@ def column_range(emb_dim: int, parts: int, index: int) -> tuple[int, int]:
     return index * w, (index + 1) * w
 
 
-def can_shard_columns(emb_dim: int, parts: int) -> bool:
-    return parts >= 1 and emb_dim % parts == 0 and emb_dim // parts in WIDTHS
+# Narrowest column shard the bench's auto partition picks: random gathers of
+# rows under 64 B (16 fp32 columns) fetch whole cache lines for a fraction of
+# them. Measured per-rank C4 steps (one shard alone, tools/column_probe.py,
+# profiles/r23_*): 32 columns 9.30 ms, 16 columns 7.85 ms, 8 columns 7.76 ms
+# (the 8-column item product fetches ~3.7x its bytes); single GPU 16.7 ms.
+MIN_AUTO_WIDTH = 16
+
+
+def can_shard_columns(emb_dim: int, parts: int, min_width: int = 8) -> bool:
+    return (parts >= 1 and emb_dim % parts == 0 and emb_dim // parts in WIDTHS
+            and emb_dim // parts >= min_width)
 
 
 class ColumnShardedTrainer(FusedTrainer):
