@@ -151,11 +151,14 @@ def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
         y.backward(gy)
         return time.perf_counter() - t0
 
-    t_f_iu, _ = _median_s(lambda: torch.sparse.mm(A_f_iu, x_u), reps)
-    t_f_ui, _ = _median_s(lambda: torch.sparse.mm(A_f_ui, x_i), reps)
+    # the sampled products are short (~0.3 s): 2 more runs each steady their
+    # medians (r26: two bench runs 6 % apart with 5)
+    pr = reps + 2
+    t_f_iu, _ = _median_s(lambda: torch.sparse.mm(A_f_iu, x_u), pr)
+    t_f_ui, _ = _median_s(lambda: torch.sparse.mm(A_f_ui, x_i), pr)
     gi, gu = torch.rand(I, d, generator=g), torch.rand(U, d, generator=g)
-    t_b_u, _ = _median_s(lambda: bwd(A_b_u, x_u[::every].contiguous(), gi), reps)
-    t_b_i, _ = _median_s(lambda: bwd(A_b_i, x_i[::every].contiguous(), gu), reps)
+    t_b_u, _ = _median_s(lambda: bwd(A_b_u, x_u[::every].contiguous(), gi), pr)
+    t_b_i, _ = _median_s(lambda: bwd(A_b_i, x_i[::every].contiguous(), gu), pr)
     del A_f_iu, A_f_ui, A_b_u, A_b_i, gi, gu
     s_iu, s_ui = E / max(e_iu, 1), E / max(e_ui, 1)
     t_prop = K * (t_f_iu * s_iu + t_f_ui * s_ui + t_b_u * s_ui + t_b_i * s_iu)
@@ -179,7 +182,7 @@ def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
     return {
         "value": 4 * K * E / t_step, "unit": "edges/s", "cores": cores, "kind": "port",
         "bpr_steps_per_s": 1.0 / t_step,
-        "sample": (f"{cfg_name_global} step from sampled products (median of {reps} after 1 "
+        "sample": (f"{cfg_name_global} step from sampled products (median of {pr} after 1 "
                    f"warm-up, rows of every {every}th output vertex, scaled by edges): "
                    f"fwd item<-user {t_f_iu * s_iu:.2f}s, fwd user<-item {t_f_ui * s_ui:.2f}s, "
                    f"bwd grad-u {t_b_u * s_ui:.2f}s, bwd grad-i {t_b_i * s_iu:.2f}s per layer "
