@@ -355,6 +355,8 @@ class GraphedStep:
         # at capture time is irrelevant
         self.users = torch.zeros(trainer.B, dtype=torch.int64, device=trainer.device)
         host = (trainer.step_count, trainer.sampler.counter)
+        # the graph records the launches of THIS configuration
+        self._captured = (trainer.frontier, trainer.fuse_adam, trainer.B)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
@@ -366,6 +368,9 @@ class GraphedStep:
 
     def step(self) -> torch.Tensor:
         tr = self.tr
+        if (tr.frontier, tr.fuse_adam, tr.B) != self._captured:
+            raise RuntimeError("GraphedStep: the trainer's frontier / fuse_adam / batch size "
+                               "changed since capture; build a new GraphedStep")
         users = tr.next_users()
         if users.numel() != tr.B:       # short tail of an epoch: eager (same device state)
             return tr._step(users, True)
