@@ -92,3 +92,18 @@ def test_median_uses_returned_interval(bench):
     t, ts = bench._median_s(lambda: 2.0, reps=3, warmup=1)
     assert t == 2.0 and ts == [2.0, 2.0, 2.0]
     assert np.isfinite(bench._median_s(lambda: None, reps=1)[0])
+
+
+def test_column_shard_widths_and_partition_rule():
+    """Column shards are equal widths from the supported set; the bench's auto
+    partition takes columns while shards stay >= MIN_AUTO_WIDTH wide."""
+    from bbgr.columns import MIN_AUTO_WIDTH, can_shard_columns, column_range
+    assert column_range(64, 2, 1) == (32, 64)
+    assert column_range(64, 8, 0) == (0, 8)
+    assert column_range(256, 8, 7) == (224, 256)
+    for bad in ((64, 3, 0), (64, 2, 2), (64, 16, 0), (48, 2, 0)):
+        with pytest.raises(ValueError):
+            column_range(*bad)
+    assert can_shard_columns(64, 4, MIN_AUTO_WIDTH) and not can_shard_columns(64, 8, MIN_AUTO_WIDTH)
+    assert can_shard_columns(64, 8) and not can_shard_columns(64, 16)
+    assert can_shard_columns(256, 8, MIN_AUTO_WIDTH)
