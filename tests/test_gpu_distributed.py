@@ -3,6 +3,7 @@ sizes 2 and 3. RCCL cannot run two ranks on one device, so the ranks share
 cuda:0 over the gloo backend; the collective schedule is the one RCCL runs
 at round end on 8 GPUs. Checked against the float64 oracle on the union of
 the ranks' batches."""
+import json
 import os
 import socket
 import subprocess
@@ -12,6 +13,7 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -179,3 +181,28 @@ def test_column_sharded_step_matches_single_gpu(tmp_path, variant, frontier, ord
             err = np.linalg.norm(a - b) / np.linalg.norm(b)
             assert err < 1e-6, (key, err)
         np.testing.assert_array_equal(rk["user_w"], ranks[0]["user_w"])   # same gather
+
+
+@pytest.mark.parametrize("partition", ["columns", "users"])
+def test_bench_two_ranks_on_c2(tmp_path, partition):
+    """bench.py's N > 1 path end to end (the driver's multi-GPU run) with both
+    partitions, 2 gloo ranks sharing the device, on C2: one JSON line from
+    rank 0 with the whole job's graph and the partition named."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "3",
+           "--warmup", "1", "--dense-check", "1", "--frontier", "on", "--partition", partition,
+           "--weak-beside", "2"]
+    env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["scaling"] == "strong" and j["partition"] == partition
+    assert j["config"]["num_edges"] == 1_000_000 and j["value"] > 0
+    assert j["roofline"]["bound"] == "hbm" and j["dense_ms_per_step"] > 0
+    if partition == "users":
+        assert j["weak_beside"]["num_edges"] == 2_000_000
+    else:
+        assert j["weak_beside"] is None
