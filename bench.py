@@ -304,8 +304,8 @@ def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> d
     tr.step()
     torch.cuda.synchronize()
     P.set_spmm_timer(None)
-    gathered = _allreduce(sum(c[3] for c in counter.edge_counts().values()), dev,
-                          torch.distributed.ReduceOp.SUM)
+    gathered = _allreduce(sum(c[3] * k[4] / d for k, c in counter.edge_counts().items()),
+                          dev, torch.distributed.ReduceOp.SUM)
     tr.close()
     steps_per_s = args.weak_beside / el
     return {"value": gathered * steps_per_s, "unit": "edges/s", "scaling": "weak",
@@ -347,6 +347,10 @@ def main():
     ap.add_argument("--native-comm", action="store_true",
                     help="N>1: item all-reduces through the C ABI's own RCCL communicator "
                          "(bbgr_allreduce_items) instead of torch.distributed")
+    ap.add_argument("--column-chains", type=int, default=1,
+                    help="users partition: run the propagation as this many column chains "
+                         "(d/C columns each, own stream and exchange group) so one chain's "
+                         "SpMMs overlap another's item all-reduces")
     ap.add_argument("--frontier-parts", type=int, default=2,
                     help="N>1: item-row ranges per frontier (row-list) exchange")
     ap.add_argument("--dense-check", type=int, default=5,
@@ -439,6 +443,8 @@ def main():
               vertex_order=args.vertex_order)
     if args.native_comm:
         xp["native_comm"] = True
+    if args.column_chains > 1:
+        xp["column_chains"] = args.column_chains
     frontier = {"auto": "auto", "on": True, "off": False}[args.frontier]
     if args.dense:
         frontier = False
@@ -538,14 +544,13 @@ def main():
     torch.cuda.synchronize()
     P.set_spmm_timer(None)
     counts = counter.edge_counts()
-    gathered_step = sum(c[3] for c in counts.values()) / count_steps
-    visited_step = sum(c[2] for c in counts.values()) / count_steps
+    # a launch over a column slice (column shards, column chains) gathers
+    # d_launch / d of each edge's row: counted as that fraction of an edge
+    gathered_step = sum(c[3] * k[4] / d for k, c in counts.items()) / count_steps
+    visited_step = sum(c[2] * k[4] / d for k, c in counts.items()) / count_steps
     if dist_mode:
         gathered_step = _allreduce(gathered_step, dev, torch.distributed.ReduceOp.SUM)
         visited_step = _allreduce(visited_step, dev, torch.distributed.ReduceOp.SUM)
-        if columns:   # every rank gathers every edge on 1/N of the columns
-            gathered_step /= world
-            visited_step /= world
     dense_ms = None
     if trainer.frontier and args.dense_check > 0:
         # the same trainer with frontier sparsity off (every product over the
@@ -624,7 +629,10 @@ def main():
                                    f"one column shard of {emulate} ({d // emulate} columns): "
                                    "single-GPU stand-in for one rank" if emulate else
                                    f"user-rows x{world}"
-                                   + (" (sharded trainer)" if dist_mode and world == 1 else ""))},
+                                   + (" (sharded trainer)" if dist_mode and world == 1 else "")
+                                   + (f", {args.column_chains} column chains"
+                                      if dist_mode and not columns and args.column_chains > 1
+                                      else ""))},
         "bpr_steps_per_s": steps_per_s,
         "weak_beside": weak_beside,
         "partition": ("columns" if columns else "users") if dist_mode else

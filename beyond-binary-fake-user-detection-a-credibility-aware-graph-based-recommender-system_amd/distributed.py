@@ -44,7 +44,7 @@ from . import _lib
 from ._lib import OP_SYM, call, ld, ptr, stream_handle
 from .bpr import bpr_args
 from .graph import BipartiteGraph, Scales
-from .optim import adam_step
+from .optim import AdamRows, adam_step
 from .propagate import ORDER_GS, OperatorPair, backward, epilogue, forward, spmm
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .scatter import RowScatter
@@ -162,6 +162,10 @@ class ItemExchange:
         self.native: RcclItemComm | None = None   # set: bbgr_allreduce_items instead
 
     def _allreduce_async(self, t: torch.Tensor, works: list) -> None:
+        # a collective reduces numel() elements from the data pointer on: a
+        # column view would have the wrong elements summed (gloo does not check)
+        if not t.is_contiguous():
+            raise ValueError("item exchange: all-reduce of a non-contiguous table")
         if self.native is not None:
             self.native.allreduce_async(t)
         else:
@@ -247,7 +251,9 @@ class ItemExchange:
             epilogue(c, row_list=lst[:n], n_rows=prod.csr.n_rows, **kw)
             return
         y = kw.get("y")
-        if (row_mask is None and y is not None
+        # linear form: y itself is all-reduced, so it must be one contiguous
+        # block (a column chain's output slice is not: partial sums instead)
+        if (row_mask is None and y is not None and y.is_contiguous()
                 and not (kw.get("add") is not None and kw.get("acc_out") is not None)):
             self._linear_product(prod, x, first, src_mask, y, kw)
             return
@@ -329,11 +335,15 @@ class ShardedTrainer(FusedTrainer):
                  frontier="auto", exchange_parts: int = 4, fuse_adam: bool = True,
                  sparse_exchange: bool = True, vertex_order: str = "input",
                  frontier_parts: int = 2, native_comm: bool = False,
-                 overlap_item_adam: bool | None = None):
+                 overlap_item_adam: bool | None = None, column_chains: int = 1):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
         this rank's users; i0: the full (replicated) item table; batch_size:
         users per step on THIS rank. vertex_order="degree": local users by
-        local degree, items by GLOBAL degree (identical on every rank)."""
+        local degree, items by GLOBAL degree (identical on every rank).
+        column_chains=C > 1: the propagation runs as C independent chains over
+        d/C-column slices of the tables, each on its own stream with its own
+        exchange group, so one chain's SpMMs overlap the other's item
+        all-reduces (see _Chain)."""
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}")
@@ -368,6 +378,8 @@ class ShardedTrainer(FusedTrainer):
             cred_t = _internal_rows(self.graph.user_order, cred_t)
         self.scales = _scales(kind, self.graph, indptr_i, cred_t)
         self.pair = OperatorPair.factored(self.graph, self.scales)
+        self.chains = self._build_chains(int(column_chains), emb_dim, group, exchange_parts,
+                                         frontier_parts, native_comm, indptr_i, dev)
 
         f32 = dict(dtype=torch.float32, device=dev)
         if u0 is None:   # rank-local stream for users, shared stream for items
@@ -474,13 +486,48 @@ class ShardedTrainer(FusedTrainer):
         tr.bounds = bounds
         return tr
 
+    def _build_chains(self, n: int, emb_dim: int, group, parts: int, frontier_parts: int,
+                      native_comm: bool, indptr_i, dev) -> list:
+        if n == 1:
+            return []
+        from .columns import WIDTHS
+        if n < 1 or emb_dim % n or emb_dim // n not in WIDTHS:
+            raise ValueError(f"cannot run {n} column chains over {emb_dim} columns "
+                             f"(slice widths must be one of {WIDTHS})")
+        ranks = dist.get_process_group_ranks(group if group is not None else dist.group.WORLD)
+        backend = dist.get_backend(group)
+        w = emb_dim // n
+        chains = []
+        for c in range(n):
+            # each chain its own group: its collectives run on their own comm
+            # stream instead of queueing behind the other chain's (every rank
+            # creates the groups in the same order)
+            g = group if c == 0 else dist.new_group(ranks=ranks, backend=backend)
+            ex = self.exchange if c == 0 else ItemExchange(g, parts, frontier_parts)
+            if c > 0:
+                ex.balance_indptr = indptr_i
+                if native_comm:
+                    ex.native = RcclItemComm(g, dev)
+            chains.append(_Chain(c * w, (c + 1) * w, ex, torch.cuda.Stream(device=dev), {}))
+        # the first-product slot values are built lazily on first use; build
+        # them now, on this stream, before two chain streams could race for them
+        for prod in (self.pair.fwd_item, self.pair.fwd_user, self.pair.bwd_item,
+                     self.pair.bwd_user):
+            if prod.vals is None and prod.in_scale is not None:
+                prod.first_layer_values()
+        return chains
+
+    def _exchanges(self) -> list:
+        return [ch.exchange for ch in self.chains] if self.chains else [self.exchange]
+
     def close(self) -> None:
-        """Destroy the exchange's own RCCL communicator (native_comm), if any;
+        """Destroy the exchanges' own RCCL communicators (native_comm), if any;
         collective: every rank calls it before the process group goes."""
-        if self.exchange.native is not None:
-            torch.cuda.synchronize(self.device)
-            self.exchange.native.close()
-            self.exchange.native = None
+        for ex in self._exchanges():
+            if ex.native is not None:
+                torch.cuda.synchronize(self.device)
+                ex.native.close()
+                ex.native = None
 
     # -- batching ------------------------------------------------------------
     def next_users(self) -> torch.Tensor:
@@ -527,8 +574,8 @@ class ShardedTrainer(FusedTrainer):
         have = ctypes.c_size_t(self._list_ws.numel())
         call("bbgr_mask_to_list", I, ptr(self.mask_i), ptr(self.item_list),
              ptr(self.item_count), ptr(self._list_ws), ctypes.byref(have), st)
-        self.exchange.set_rows(self.graph.item_csr, self.mask_i, self.item_list,
-                               self.item_offs_host)
+        for ex in self._exchanges():
+            ex.set_rows(self.graph.item_csr, self.mask_i, self.item_list, self.item_offs_host)
 
     def _item_adam_beside(self) -> torch.cuda.Event:
         """The item Adam of this step on the side stream: its gradient rows are
@@ -562,9 +609,12 @@ class ShardedTrainer(FusedTrainer):
         pos, neg = self.sampler.sample(users, self.pos, self.neg)
         st = stream_handle()
         masks = self._masks(users, pos, neg) if self.frontier else None
-        forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
-                out_i=self.itf, ws=self.ws, reduce=self.exchange,
-                final_rows=None if masks is None else (masks[0], masks[1], users))
+        final_rows = None if masks is None else (masks[0], masks[1], users)
+        if self.chains:
+            self._forward_chains(final_rows)
+        else:
+            forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
+                    out_i=self.itf, ws=self.ws, reduce=self.exchange, final_rows=final_rows)
         a = bpr_args(users, pos, neg, self.uf, self.itf, self.user_w, self.item_w, self.reg,
                      self.pop, self.lambda_fair, parts=self.parts[: 3 * B], dloss=self.dloss,
                      contrib=self.contrib)
@@ -578,7 +628,9 @@ class ShardedTrainer(FusedTrainer):
         _all_gather(self.all_contrib, self.contrib[B: 3 * B], self.group)
         self.scatter(self.g_if, self.all_items, self.all_contrib)
         alpha = 2.0 * self.reg / self.B_global            # ego L2 (Version-2:503-507)
-        if self.fuse_adam and self.overlap_item_adam:
+        if self.chains:
+            self._backward_chains(users, masks, alpha)
+        elif self.fuse_adam and self.overlap_item_adam:
             done = self._item_adam_beside()
             self._backward_fused(users, self.all_items, masks, alpha, reduce=self.exchange,
                                  item_adam=False)
@@ -601,10 +653,85 @@ class ShardedTrainer(FusedTrainer):
         if masks is not None:
             call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), self.U, st)
             self.mask_i.zero_()
-        self.exchange.clear_rows()
+        for ex in self._exchanges():
+            ex.clear_rows()
         dist.all_reduce(self.loss, op=dist.ReduceOp.SUM, group=self.group)
         self.loss.mul_(1.0 / self.world)
         return self.loss
+
+
+    # -- column chains -------------------------------------------------------
+    def _run_chains(self, body) -> None:
+        """body(chain, cols) on every chain's stream, after this stream's work
+        so far; this stream then waits for all of them. Host issue order is the
+        same on every rank, so each chain group sees its collectives in the
+        same order everywhere."""
+        main = torch.cuda.current_stream()
+        for ch in self.chains:
+            ch.stream.wait_stream(main)
+            with torch.cuda.stream(ch.stream):
+                body(ch, slice(ch.c0, ch.c1))
+        for ch in self.chains:
+            main.wait_stream(ch.stream)
+
+    def _forward_chains(self, final_rows) -> None:
+        def body(ch, cs):
+            forward(self.pair, self.user_w[:, cs], self.item_w[:, cs], self.K, self.order,
+                    out_u=self.uf[:, cs], out_i=self.itf[:, cs], ws=ch.ws,
+                    reduce=ch.exchange, final_rows=final_rows)
+        self._run_chains(body)
+
+    def _backward_chains(self, users, masks, alpha: float) -> None:
+        """The backward of every chain on its column slice, then (on this
+        stream) what needs whole rows: the item Adam — or, unfused, the ego-L2
+        rows and both Adam steps. Per column the arithmetic is the one-chain
+        step's, so results match it bit for bit."""
+        B = users.numel()
+        gl = 1.0 / (self.K + 1)
+        a_gl = alpha / gl
+        if not self.fuse_adam:
+            def body(ch, cs):
+                backward(self.pair, self.g_uf[:, cs], self.g_if[:, cs], self.K, self.order,
+                         out_u=self.g_u0[:, cs], out_i=self.g_i0[:, cs], ws=ch.ws,
+                         reduce=ch.exchange, grad_support=masks)
+            self._run_chains(body)
+            st = stream_handle()
+            call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
+                 ptr(self.g_u0), ld(self.g_u0), self.d, st)
+            call("bbgr_rows_axpy", self.all_items.numel(), ptr(self.all_items), alpha,
+                 ptr(self.item_w), ld(self.item_w), ptr(self.g_i0), ld(self.g_i0), self.d, st)
+            self.step_count += 1
+            adam_step(self.user_w, self.g_u0, self.m_u, self.v_u, self.step_count, self.lr)
+            adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr)
+            return
+        done = self._item_adam_beside() if self.overlap_item_adam else None
+        self.step_count += 1
+
+        def body(ch, cs):
+            w = ch.c1 - ch.c0
+            adam_u = AdamRows(self.user_w[:, cs], self.m_u[:, cs], self.v_u[:, cs],
+                              self.step_count, self.lr)
+
+            def before_last():
+                call("bbgr_rows_axpy", B, ptr(users), a_gl, ptr(self.user_w[:, cs]),
+                     ld(self.user_w), ptr(self.g_uf[:, cs]), ld(self.g_uf), w, stream_handle())
+            backward(self.pair, self.g_uf[:, cs], self.g_if[:, cs], self.K, self.order,
+                     out_u=self.g_u0[:, cs], ws=ch.ws, grad_support=masks,
+                     grad_i0_dense=False, adam_u=adam_u, before_last=before_last,
+                     reduce=ch.exchange)
+        self._run_chains(body)
+        if done is not None:
+            torch.cuda.current_stream().wait_event(done)
+        else:
+            self._item_adam(self.all_items, self.g_if, a_gl, gl)
+
+
+class _Chain:
+    """One column chain of a ShardedTrainer: columns [c0, c1) of every table,
+    its stream, its item exchange (own process group) and its workspaces."""
+
+    def __init__(self, c0: int, c1: int, exchange: ItemExchange, stream, ws: dict):
+        self.c0, self.c1, self.exchange, self.stream, self.ws = c0, c1, exchange, stream, ws
 
 
 class _GlobalItemCsr:

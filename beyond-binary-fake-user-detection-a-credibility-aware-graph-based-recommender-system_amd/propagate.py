@@ -65,12 +65,15 @@ class Product:
         return self.first_vals
 
     def workspace(self, d: int):
+        """Split-row partials and arrival counters, one set per (width, stream):
+        launches on two streams (column chains) must not share counters."""
         if self.csr.n_split == 0:
             return None
-        w = self.partial.get(d)
+        key = (d, torch.cuda.current_stream(self.csr.device).cuda_stream)
+        w = self.partial.get(key)
         if w is None:
             w = self.csr.partial_workspace(d)
-            self.partial[d] = w
+            self.partial[key] = w
         return w
 
 

@@ -102,6 +102,17 @@ def fused_vs_separate(out_dir, variant):
     out["inchain_item_w"] = tr.item_w.cpu().numpy()
     out["inchain_m_i"] = tr.m_i.cpu().numpy()
     out["inchain_loss"] = np.array(losses)
+    # two column chains (32 columns each, own streams and exchange groups)
+    for fuse in (False, True):
+        tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3,
+                            batch_size=32, device="cuda:0", u0=u0, i0=i0,
+                            user_offset=rank * WEAK_U, exchange_parts=2, fuse_adam=fuse,
+                            frontier=True, column_chains=2)
+        losses = [float(tr.step()) for _ in range(3)]
+        tag = f"chains_{'fused' if fuse else 'sep'}"
+        out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
+        out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
+        out[f"{tag}_loss"] = np.array(losses)
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"fused{rank}.npz"), **out)
     dist.destroy_process_group()
@@ -126,8 +137,10 @@ def rccl_single_rank(out_dir, variant, order="input"):
     one = FusedTrainer(BipartiteGraph(e, U, I, "cuda:0", vertex_order=order), variant, **kw)
     nat = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
                          vertex_order=order, native_comm=True, **kw)   # bbgr_allreduce_items
+    chains = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
+                            vertex_order=order, column_chains=2, **kw)   # two RCCL groups
     out = {}
-    for tag, tr in (("sharded", sh), ("single", one), ("native", nat)):
+    for tag, tr in (("sharded", sh), ("single", one), ("native", nat), ("chains", chains)):
         out[f"{tag}_loss"] = np.array([float(tr.step()) for _ in range(3)])
         out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
         out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()

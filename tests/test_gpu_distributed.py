@@ -129,6 +129,20 @@ def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
     for rk in ranks:   # item Adam beside the chain (default at N > 1) == in the chain
         for key in ("user_w", "item_w", "m_i", "loss"):
             np.testing.assert_array_equal(rk[f"fused_sparse_{key}"], rk[f"inchain_{key}"])
+    # two column chains (column_chains=2): the same step over two 32-column
+    # slices on their own streams and groups; narrow rows sum in slot order,
+    # so equal to rounding, and replicas still bitwise identical
+    for rk in ranks:
+        for fuse in ("sep", "fused"):
+            for key in ("user_w", "item_w"):
+                a, b = rk[f"chains_{fuse}_{key}"], rk[f"{fuse}_sparse_{key}"]
+                err = np.linalg.norm(a - b) / np.linalg.norm(b)
+                assert err < 1e-6, (fuse, key, err)
+            np.testing.assert_allclose(rk[f"chains_{fuse}_loss"], rk[f"{fuse}_sparse_loss"],
+                                       rtol=1e-6)
+    for fuse in ("sep", "fused"):
+        np.testing.assert_array_equal(ranks[0][f"chains_{fuse}_item_w"],
+                                      ranks[1][f"chains_{fuse}_item_w"])
 
 
 @pytest.mark.parametrize("variant,order", [("v2_pop", "input"), ("cu_fair", "input"),
@@ -151,6 +165,10 @@ def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, 
         assert err < 1e-6, (key, err)
         # the C ABI's own RCCL communicator (bbgr_allreduce_items) == torch's
         np.testing.assert_array_equal(z[f"native_{key}"], z[f"sharded_{key}"])
+        # two column chains on two RCCL groups and streams
+        err = np.linalg.norm(z[f"chains_{key}"] - b) / np.linalg.norm(b)
+        assert err < 1e-6, ("chains", key, err)
+    np.testing.assert_allclose(z["chains_loss"], z["single_loss"], rtol=1e-6)
     np.testing.assert_array_equal(z["native_loss"], z["sharded_loss"])
 
 
