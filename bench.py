@@ -327,6 +327,8 @@ def main():
     ap.add_argument("--variant", default="v2_pop")
     ap.add_argument("--cred", default="beta", choices=["beta", "ones"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-torch-reference", action="store_true",
+                    help="skip timing the reference step in stock PyTorch on the GPU")
     ap.add_argument("--dense", action="store_true",
                     help="disable exact frontier sparsity (every SpMM over the full CSR)")
     ap.add_argument("--frontier", default="auto", choices=["auto", "on", "off"],
@@ -604,6 +606,34 @@ def main():
         t_cpu = time.perf_counter()
         cpu = cpu_baseline(edges, cfg, args.config, cred)
         log(f"[bench] cpu baseline took {time.perf_counter() - t_cpu:.1f}s")
+    torch_ref = None
+    if not args.no_torch_reference and not dist_mode and not sharded_gen and not emulate:
+        # the reference's step in stock PyTorch-ROCm on this GPU (torch.sparse.mm
+        # COO products, autograd, torch Adam): the like-for-like GPU baseline
+        log("[bench] timing the stock-torch reference step on the GPU ...")
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from torch_sparse_step import run as torch_reference_run
+        torch_ref = torch_reference_run(args.config, edges, cred, device=dev)
+        torch_ref["speedup_vs_torch"] = torch_ref["step_ms"] / (1000.0 * elapsed / args.steps)
+        torch_ref["note"] = ("the reference's V2 step written with its own torch calls "
+                             "(sparse_coo_tensor.coalesce, torch.sparse.mm, stack.mean, "
+                             "autograd, torch.optim.Adam) on this GPU, uniform batches "
+                             "(tools/torch_sparse_step.py); not the oracle, not the product")
+    dropin = None
+    if (not args.no_torch_reference and not dist_mode and not sharded_gen and not emulate
+            and args.variant == "v2_pop"):
+        # the same step through the drop-in module API (lightgcn_cu_pop.LightGCN on
+        # the registered bbgr ops, autograd, the reference's default torch Adam)
+        log("[bench] timing the drop-in module step ...")
+        if os.path.join(ROOT, "tools") not in sys.path:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from dropin_probe import run as dropin_run
+        dropin = dropin_run(args.config, edges, cred, device=dev)
+        dropin["note"] = ("Version-2 LightGCN drop-in (bbgr ops: propagate, bpr_loss and "
+                          "their registered backward) + torch.optim.Adam(foreach), input "
+                          "vertex order, uniform batches (tools/dropin_probe.py)")
+        if torch_ref is not None:
+            dropin["speedup_vs_torch"] = torch_ref["step_ms"] / dropin["step_ms"]
     dense_equiv = 4 * K * E
     out = {
         "metric": "SpMM edges/sec + BPR steps/sec, |E|=50M d=64, 1/2/4/8 MI355X; %HBM roofline",
@@ -634,6 +664,8 @@ def main():
                                       if dist_mode and not columns and args.column_chains > 1
                                       else ""))},
         "bpr_steps_per_s": steps_per_s,
+        "torch_gpu_reference": torch_ref,
+        "dropin_module_step": dropin,
         "weak_beside": weak_beside,
         "partition": ("columns" if columns else "users") if dist_mode else
                      (f"one column shard of {emulate}" if emulate else "single GPU"),

@@ -163,6 +163,7 @@ _SIGNATURES = {
     "bbgr_scatter_add_rows": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P,
                                ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
+    "bbgr_row_support": ([c_int64, c_int32, _P, c_int64, _P, _P, _P, _P, _P], c_int32),
     "bbgr_rows_zero": ([c_int64, _P, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_rows_axpy": ([c_int64, _P, c_float, _P, c_int64, _P, c_int64, c_int32, _P],
                        c_int32),

@@ -304,6 +304,37 @@ __global__ void mark_neighbors_kernel(long n, const long *rows, const int *indpt
     mask[indices[e]] = v;
 }
 
+// mask[r] = 1 if row r of x holds a nonzero (a -0.0 counts as zero: skipping
+// a signed-zero source row leaves every sum unchanged), else 0; with a CSR,
+// every neighbour of a flagged row is also set in nbr. One 16-lane group per
+// row; VEC: float4 loads (d, ldx multiples of 4, x 16-byte aligned).
+template <bool VEC>
+__global__ __launch_bounds__(256) void row_support_kernel(long n_rows, int d, const float *x,
+                                                          long ldx, unsigned char *mask,
+                                                          const int *indptr, const int *indices,
+                                                          unsigned char *nbr) {
+  const long r = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  bool nz = false;
+  if (r < n_rows) {
+    const float *row = x + r * ldx;
+    if (VEC) {
+      for (int c = lane * 4; c < d; c += 64) {
+        const float4 v = *reinterpret_cast<const float4 *>(row + c);
+        nz |= (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f);
+      }
+    } else {
+      for (int c = lane; c < d; c += 16) nz |= row[c] != 0.f;
+    }
+  }
+  const unsigned long long b = __ballot(nz);
+  const bool any = ((b >> (threadIdx.x & 48)) & 0xFFFFull) != 0;
+  if (r >= n_rows) return;
+  if (lane == 0) mask[r] = any ? 1 : 0;
+  if (any && indptr)
+    for (int e = indptr[r] + lane; e < indptr[r + 1]; e += 16) nbr[indices[e]] = 1;
+}
+
 __global__ void rows_axpy_kernel(long n, const long *idx, float alpha,
                                  const float *src, long lds, float *dst, long ldd,
                                  int d) {
@@ -597,6 +628,25 @@ extern "C" int bbgr_mark_neighbors(int64_t n, const int64_t *rows,
                      as_stream(stream), (long)n, (const long *)rows, indptr, indices, value,
                      mask);
   BBGR_LAUNCHED("mark_neighbors_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_row_support(int64_t n_rows, int32_t d, const float *x, int64_t ldx,
+                                uint8_t *mask, const int32_t *indptr, const int32_t *indices,
+                                uint8_t *nbr_mask, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n_rows >= 0 && d > 0 && ldx >= d, "bbgr_row_support: bad sizes");
+  if (n_rows == 0) return BBGR_OK;
+  BBGR_REQUIRE(x && mask, "bbgr_row_support: null arrays");
+  BBGR_REQUIRE(!indptr || (indices && nbr_mask), "bbgr_row_support: CSR without indices / nbr_mask");
+  const bool vec = d % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
+  const dim3 grid((unsigned)((n_rows + 15) / 16));
+  if (vec)
+    hipLaunchKernelGGL(row_support_kernel<true>, grid, dim3(256), 0, as_stream(stream),
+                       (long)n_rows, (int)d, x, (long)ldx, mask, indptr, indices, nbr_mask);
+  else
+    hipLaunchKernelGGL(row_support_kernel<false>, grid, dim3(256), 0, as_stream(stream),
+                       (long)n_rows, (int)d, x, (long)ldx, mask, indptr, indices, nbr_mask);
+  BBGR_LAUNCHED("row_support_kernel");
   return BBGR_OK;
 }
 

@@ -71,12 +71,38 @@ def _(u0, i0, pair_key, num_layers, order):
     return u0.new_empty(u0.shape), i0.new_empty(i0.shape)
 
 
+def grad_support(pair, gU: Tensor, gI: Tensor, order: str):
+    """(user mask, item mask) for propagate.backward's grad_support, read off
+    the gradients themselves (bbgr_row_support, one pass over each table): the
+    users with a nonzero gU row; the items with a nonzero gI row, plus for GS
+    every neighbour of a flagged user (the first item product's output
+    support). A BPR loss touches only the batch rows, so the first backward
+    products then skip all but those rows — bitwise the dense chain's result
+    (a skipped row is exactly zero)."""
+    from .propagate import ORDER_GS
+    st = stream_handle()
+    U, I = pair.num_users, pair.num_items
+    mu = torch.empty(max(U, 1), dtype=torch.uint8, device=gU.device)
+    mi = torch.empty(max(I, 1), dtype=torch.uint8, device=gU.device)
+    d = gU.shape[1]
+    call("bbgr_row_support", I, d, _lib.ptr(gI), _lib.ld(gI), _lib.ptr(mi), None, None, None, st)
+    uc = pair.fwd_user.csr if order == ORDER_GS else None   # user rows -> item neighbours
+    call("bbgr_row_support", U, d, _lib.ptr(gU), _lib.ld(gU), _lib.ptr(mu),
+         None if uc is None else _lib.ptr(uc.indptr),
+         None if uc is None else _lib.ptr(uc.indices),
+         None if uc is None else _lib.ptr(mi), st)
+    return mu[:U], mi[:I]
+
+
 @custom_op("bbgr::propagate_backward", mutates_args=())
 def propagate_backward(gU: Tensor, gI: Tensor, pair_key: int, num_layers: int,
                        order: str) -> tuple[Tensor, Tensor]:
     from .propagate import backward
     _lib.require_gpu(gU)
-    return backward(_pair(pair_key), gU.contiguous(), gI.contiguous(), num_layers, order)
+    pair = _pair(pair_key)
+    gU, gI = gU.contiguous(), gI.contiguous()
+    return backward(pair, gU, gI, num_layers, order,
+                    grad_support=grad_support(pair, gU, gI, order))
 
 
 @propagate_backward.register_fake
@@ -183,7 +209,8 @@ def propagate_sym_backward(g: Tensor, pair_key: int, num_layers: int) -> Tensor:
     U = pair.num_users
     g = g.contiguous()
     gx = torch.empty_like(g)
-    backward(pair, g[:U], g[U:], num_layers, ORDER_J, out_u=gx[:U], out_i=gx[U:])
+    backward(pair, g[:U], g[U:], num_layers, ORDER_J, out_u=gx[:U], out_i=gx[U:],
+             grad_support=grad_support(pair, g[:U], g[U:], ORDER_J))
     return gx
 
 

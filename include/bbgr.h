@@ -449,6 +449,16 @@ int bbgr_mark_neighbors(int64_t n, const int64_t *rows, const int32_t *indptr,
                         const int32_t *indices, uint8_t value, uint8_t *mask,
                         bbgr_stream_t stream);
 
+/* mask[r] = 1 if row r of x [n_rows, d] (leading dimension ldx) holds a
+ * nonzero, else 0 (every row written; -0.0 counts as zero). With a CSR
+ * (indptr, indices over the rows of x): nbr_mask[indices[e]] = 1 for every edge
+ * of a flagged row (other entries untouched). The gradient support of a
+ * backward pass whose caller did not say which rows are live (the registered
+ * propagate_backward op: BPR gradients touch only the batch rows). */
+int bbgr_row_support(int64_t n_rows, int32_t d, const float *x, int64_t ldx, uint8_t *mask,
+                     const int32_t *indptr, const int32_t *indices, uint8_t *nbr_mask,
+                     bbgr_stream_t stream);
+
 /* ------------------------------------------------------------------------- */
 /* Item exchange over RCCL (the sharded step's per-layer all-reduce of item   */
 /* partial sums) for callers without torch.distributed.        */

@@ -92,6 +92,12 @@ int main(void) {
   expect_error("shuffle null size", bbgr_shuffle(4, NULL, NULL, 1, 1, NULL, NULL, NULL));
   expect_error("mark_rows bad", bbgr_mark_rows(-1, NULL, 1, NULL, 4, NULL));
   expect_error("rows_zero bad", bbgr_rows_zero(-1, NULL, NULL, 64, 64, NULL));
+  expect_error("row_support bad ld", bbgr_row_support(4, 64, f4, 32, NULL, NULL, NULL, NULL,
+                                                      NULL));
+  expect_error("row_support csr without nbr", bbgr_row_support(4, 64, f4, 64, (uint8_t *)f4,
+                                                               (const int32_t *)f4, NULL, NULL,
+                                                               NULL));
+  expect_ok("row_support empty", bbgr_row_support(0, 64, NULL, 64, NULL, NULL, NULL, NULL, NULL));
   expect_error("allreduce null comm", bbgr_allreduce_items(NULL, f4, 4, NULL));
   expect_error("eval sampled null", bbgr_eval_sampled(NULL, NULL, NULL, NULL));
   expect_error("eval full null", bbgr_eval_full(NULL, NULL, NULL, NULL));

@@ -136,3 +136,58 @@ def test_cuda_graph_captured_step_matches_eager(family):
     assert np.isfinite(float(static_loss))
     for pa, pb in zip(a.parameters(), b.parameters()):
         assert torch.equal(pa, pb)
+
+
+@pytest.mark.parametrize("d,ld", [(64, 64), (8, 8), (32, 64), (256, 256), (12, 13)])
+def test_row_support_kernel(d, ld):
+    """bbgr_row_support: nonzero rows flagged (-0.0 is zero), every other row
+    cleared, and with a CSR every neighbour of a flagged row set."""
+    import ctypes  # noqa: F401
+    from bbgr._lib import call, ld as ld_, ptr, stream_handle
+    n, m = 3000, 500
+    g = torch.Generator().manual_seed(d)
+    x = torch.zeros(n, ld)
+    live = torch.randperm(n, generator=g)[:200]
+    x[live, torch.randint(0, d, (200,), generator=g)] = torch.randn(200, generator=g)
+    x[torch.randperm(n, generator=g)[:50], 0] = -0.0
+    if ld > d:   # junk beyond the row's d columns must not count
+        x[:, d:] = 7.0
+    x = x.to(DEV)
+    xs = x[:, :d] if ld > d else x
+    e = torch.stack([torch.randint(0, n, (20000,), generator=g),
+                     torch.randint(0, m, (20000,), generator=g)])
+    order = torch.argsort(e[0] * m + e[1])
+    rows, cols = e[0][order], e[1][order]
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    indptr_d = indptr.to(torch.int32).to(DEV)
+    cols_d = cols.to(torch.int32).to(DEV)
+    mask = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
+    nbr = torch.zeros(m, dtype=torch.uint8, device=DEV)
+    call("bbgr_row_support", n, d, ptr(xs), ld_(xs), ptr(mask), ptr(indptr_d), ptr(cols_d),
+         ptr(nbr), stream_handle())
+    want = (x[:, :d].cpu() != 0).any(1)
+    assert torch.equal(mask.cpu().bool(), want) and int(mask.max()) <= 1
+    want_nbr = torch.zeros(m, dtype=torch.bool)
+    sel = want[rows]
+    want_nbr[cols[sel]] = True
+    assert torch.equal(nbr.cpu().bool(), want_nbr)
+
+
+@pytest.mark.parametrize("order", ["gs", "jacobi"])
+def test_backward_op_support_masks_are_bitwise_dense(order):
+    """bbgr::propagate_backward reads the gradients' row support and masks the
+    first backward products: bitwise the unmasked (dense) chain on a BPR-shaped
+    gradient (batch rows only)."""
+    from bbgr import ops
+    from bbgr.propagate import backward
+    m = _model("v2")
+    pair = m._operator_pair()
+    users, pos, neg = _batch(3)
+    gU = torch.zeros(U, D, device=DEV)
+    gI = torch.zeros(I, D, device=DEV)
+    gU[users] = torch.randn(B, D, device=DEV)
+    gI[torch.cat([pos, neg])] = torch.randn(2 * B, D, device=DEV)
+    a_u, a_i = ops.propagate_backward(gU, gI, ops.pair_key(pair), K, order)
+    b_u, b_i = backward(pair, gU, gI, K, order)
+    assert torch.equal(a_u, b_u) and torch.equal(a_i, b_i)

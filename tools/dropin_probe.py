@@ -1,0 +1,99 @@
+"""Probe: the reference's own training step through the drop-in module API
+(Version-2/lighgcn_cu_pop.py:858-863 — propagate, bpr_loss, zero_grad,
+backward, torch.optim.Adam.step) on a BASELINE config, beside the fused
+trainer's step on the same graph. Batches are drawn on the device up front
+(uniform users / items: the sampler is not what this times).
+
+    python tools/dropin_probe.py [--config C4] [--steps 10] [--adam foreach|fused]
+
+Prints one JSON line per variant: ms per step and a breakdown
+(forward, forward+backward, Adam) from separately synchronised runs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bbgr  # noqa: E402,F401
+from bbgr import lightgcn_cu_pop as V2  # noqa: E402
+from bbgr.synthetic import CONFIGS, CONFIG_SEED, config_edges, synthetic_credibility  # noqa: E402
+
+
+def timed(fn, steps: int) -> float:
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return 1000.0 * (time.perf_counter() - t0) / steps
+
+
+def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
+        adam: str = "foreach", device=None) -> dict:
+    c = CONFIGS[cfg_name]
+    U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
+    e = config_edges(cfg_name) if edges is None else edges
+    if cred_np is None:
+        cred_np = synthetic_credibility(U, CONFIG_SEED[cfg_name])
+    cred = torch.as_tensor(cred_np)
+    dev = torch.device(device) if device is not None else torch.device("cuda")
+    t0 = time.perf_counter()
+    M_ui, M_iu = V2.build_message_passing_mats(e, U, I, cred, dev)
+    model = V2.LightGCN(U, I, d, K, M_ui, M_iu).to(dev)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3,
+                           **({"fused": True} if adam == "fused" else {"foreach": True}))
+    g = torch.Generator(device=dev).manual_seed(1)
+    n_b = warmup + steps
+    users = torch.randint(0, U, (n_b, B), device=dev, generator=g)
+    pos = torch.randint(0, I, (n_b, B), device=dev, generator=g)
+    neg = torch.randint(0, I, (n_b, B), device=dev, generator=g)
+    it = iter(range(10**9))
+
+    def fwd_bwd():
+        k = next(it) % n_b
+        uf, itf = model.propagate()
+        loss = model.bpr_loss(users[k], pos[k], neg[k], uf, itf, 1e-4)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+
+    def step():
+        fwd_bwd()
+        opt.step()
+
+    def fwd():
+        with torch.no_grad():
+            model.propagate()
+
+    for _ in range(warmup):
+        step()
+    out = {"config": cfg_name, "adam": adam, "setup_s": setup_s, "steps": steps,
+           "step_ms": timed(step, steps), "forward_ms": timed(fwd, steps),
+           "forward_backward_ms": timed(fwd_bwd, steps)}
+    fwd_bwd()
+    out["adam_ms"] = timed(opt.step, steps)
+    del model, opt, M_ui, M_iu, users, pos, neg
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--adam", default="foreach", choices=["foreach", "fused"])
+    a = ap.parse_args()
+    print(json.dumps(run(a.config, steps=a.steps, warmup=a.warmup, adam=a.adam)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
