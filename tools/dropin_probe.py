@@ -4,7 +4,7 @@ backward, torch.optim.Adam.step) on a BASELINE config, beside the fused
 trainer's step on the same graph. Batches are drawn on the device up front
 (uniform users / items: the sampler is not what this times).
 
-    python tools/dropin_probe.py [--config C4] [--steps 10] [--adam foreach|fused]
+    python tools/dropin_probe.py [--config C4] [--steps 10] [--adam foreach|fused|bbgr]
 
 Prints one JSON line per variant: ms per step and a breakdown
 (forward, forward+backward, Adam) from separately synchronised runs.
@@ -49,8 +49,12 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
     model = V2.LightGCN(U, I, d, K, M_ui, M_iu).to(dev)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3,
-                           **({"fused": True} if adam == "fused" else {"foreach": True}))
+    if adam == "bbgr":   # bbgr.optim.FusedAdam (bbgr_adam per parameter)
+        from bbgr.optim import FusedAdam
+        opt = FusedAdam(model.parameters(), lr=1e-3)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3,
+                               **({"fused": True} if adam == "fused" else {"foreach": True}))
     g = torch.Generator(device=dev).manual_seed(1)
     n_b = warmup + steps
     users = torch.randint(0, U, (n_b, B), device=dev, generator=g)
@@ -90,7 +94,7 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--adam", default="foreach", choices=["foreach", "fused"])
+    ap.add_argument("--adam", default="foreach", choices=["foreach", "fused", "bbgr"])
     a = ap.parse_args()
     print(json.dumps(run(a.config, steps=a.steps, warmup=a.warmup, adam=a.adam)), flush=True)
 
