@@ -5,7 +5,7 @@
 # Usage: tools/profile_box.sh <tag> [bench args...]
 set -euo pipefail
 TAG=${1:-r01}; shift || true
-ARGS=${@:---steps 5 --warmup 2 --no-cpu-baseline --dense-check 0}
+ARGS=${@:---steps 5 --warmup 2 --no-cpu-baseline --no-torch-reference --dense-check 0}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
