@@ -103,6 +103,45 @@ def _reference_step_s(cfg_name: str, reps: int = 5):
     return med, ts, 4 * K * e.shape[1]
 
 
+def _cpu_list_text(cpus) -> str:
+    """[0,1,2,3,8] -> "0-3,8"."""
+    cpus = sorted(cpus)
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def numa_local_cpus(n: int) -> list[int]:
+    """Up to n CPUs of this process's affinity set that share one NUMA node
+    (the node holding most of them), so a pinned CPU baseline's threads and
+    first-touch memory stay on one socket."""
+    allowed = os.sched_getaffinity(0)
+    best: list[int] = []
+    base = "/sys/devices/system/node"
+    try:
+        nodes = sorted(x for x in os.listdir(base) if x.startswith("node") and x[4:].isdigit())
+    except OSError:
+        nodes = []
+    for nd in nodes:
+        cpus = []
+        try:
+            text = open(os.path.join(base, nd, "cpulist")).read().strip()
+        except OSError:
+            continue
+        for part in filter(None, text.split(",")):
+            lo, _, hi = part.partition("-")
+            cpus.extend(range(int(lo), int(hi or lo) + 1))
+        mine = [c for c in cpus if c in allowed]
+        if len(mine) > len(best):
+            best = mine
+    return (best or sorted(allowed))[:n]
+
+
 def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
                  whole_steps=("C2", "C1")):
     """The reference's CPU path (oracle/ref_torch.py: the same torch calls as
@@ -124,7 +163,7 @@ def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
     from oracle import ref_numpy as R
     from oracle import ref_torch as T
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    cores = max(1, min(cores, os.cpu_count() or 1))
+    cores = max(1, min(cores, len(os.sched_getaffinity(0))))
     torch.set_num_threads(cores)
     U, I, d, K, B = (cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"],
                      cfg["batch"])
@@ -385,6 +424,14 @@ def main():
     cfg = CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    pinned = None
+    if world == 1 and not args.no_cpu_baseline and not args.sharded:
+        # the CPU baseline's threads on one NUMA node (before any thread pool
+        # exists): on the box's 2-socket host, free-floating threads measured
+        # 83-92 s/step across runs, pinned 78-85 (tools/cpu_baseline_probe.py)
+        want = int(os.environ.get("OMP_NUM_THREADS", "16"))
+        pinned = numa_local_cpus(max(1, want))
+        os.sched_setaffinity(0, pinned)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -605,6 +652,8 @@ def main():
         log("[bench] timing the reference CPU path (bounded sample) ...")
         t_cpu = time.perf_counter()
         cpu = cpu_baseline(edges, cfg, args.config, cred)
+        if pinned is not None:
+            cpu["cpus"] = _cpu_list_text(pinned)
         log(f"[bench] cpu baseline took {time.perf_counter() - t_cpu:.1f}s")
     torch_ref = None
     if not args.no_torch_reference and not dist_mode and not sharded_gen and not emulate:

@@ -107,3 +107,13 @@ def test_column_shard_widths_and_partition_rule():
     assert can_shard_columns(64, 4, MIN_AUTO_WIDTH) and not can_shard_columns(64, 8, MIN_AUTO_WIDTH)
     assert can_shard_columns(64, 8) and not can_shard_columns(64, 16)
     assert can_shard_columns(256, 8, MIN_AUTO_WIDTH)
+
+
+def test_numa_local_cpu_pinning_helpers(bench):
+    """The CPU baseline's pinning: CPUs come from this process's affinity set,
+    at most n of them, and print as ranges."""
+    import os
+    cpus = bench.numa_local_cpus(4)
+    assert 1 <= len(cpus) <= 4 and set(cpus) <= os.sched_getaffinity(0)
+    assert bench._cpu_list_text([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
+    assert bench._cpu_list_text([5]) == "5"

@@ -11,5 +11,6 @@ for k in 1 2; do
   timeout -k 10 400 python bench.py > gpurun_out/${T}_bench$k.json 2> gpurun_out/${T}_bench$k.log || { echo BENCH${k}_FAILED; tail -20 gpurun_out/${T}_bench$k.log; exit 1; }
 done
 timeout -k 10 200 python bench.py --config C2 --steps 300 --warmup 20 > gpurun_out/${T}_c2.json 2> gpurun_out/${T}_c2.log || { echo C2_FAILED; tail -20 gpurun_out/${T}_c2.log; exit 1; }
+timeout -k 10 300 python tools/dropin_probe.py --adam bbgr > gpurun_out/${T}_dropin_bbgr.json 2> gpurun_out/${T}_dropin_bbgr.log || { echo DROPIN_FAILED; tail -20 gpurun_out/${T}_dropin_bbgr.log; exit 1; }
 bash tools/profile_box.sh $T || { echo PROFILE_FAILED; exit 1; }
 echo ALL_OK
