@@ -179,7 +179,6 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /* 4, 16-byte aligned base). d in {64, 128, 256}, or 8, 16, 32 for the      */
 /* column slices of a column-sharded model (narrow rows: d/4 lanes gather one */
 /* row, 16/(d/4) edges per load round, slot sums added by a fixed xor tree).  */
-/* partial: workspace of (csr->n_chunks * d) floats when csr->n_split > 0.    */
 /* src_mask (nullable, [n_cols] bytes): edges whose column is 0 in the mask    */
 /*   are skipped — exact when x is zero on those rows (sparse gradients).     */
 /* row_mask (nullable, [n_rows] bytes): rows that are 0 are not computed and  */
@@ -223,7 +222,8 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
-/*   launch (no separate fix-up kernel).                                      */
+/*   launch (no separate fix-up kernel). Needed when csr->n_split > 0. Two    */
+/*   launches that may run at once (different streams) need two buffers.     */
 /* ------------------------------------------------------------------------- */
 typedef struct {
   int32_t d;
