@@ -147,26 +147,43 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 #ifndef BBGR_PAIR_U256
 #define BBGR_PAIR_U256 2
 #endif
+#ifndef BBGR_SLOT_ROUNDS32   // narrow short rows: 8-edge index rounds per load round
+#define BBGR_SLOT_ROUNDS32 1
+#endif
+#ifndef BBGR_NARROW_WAVES32   // occupancy target of the 32-column kernels (0: none)
+#define BBGR_NARROW_WAVES32 0
+#endif
+#ifndef BBGR_NARROW_MASKED_WAVES32   // ... of the 32-column masked kernel (no edge values)
+#define BBGR_NARROW_MASKED_WAVES32 8
+#endif
+#ifndef BBGR_SLOT_ROUNDS16
+#define BBGR_SLOT_ROUNDS16 2
+#endif
 #ifndef BBGR_PAIR_WAVES256
 #define BBGR_PAIR_WAVES256 0
 #endif
 
 template <int D> struct Tune {   // narrow rows (8, 16, 32): one-row kernels only
-  static constexpr int row_u = 0, row_waves = 0, pair_u = 0, pair_u_masked = 0;
+  static constexpr int row_u = 0, row_waves = D == 32 ? BBGR_NARROW_WAVES32 : 0;
+  static constexpr int masked_waves = D == 32 ? BBGR_NARROW_MASKED_WAVES32 : 0;
+  static constexpr int pair_u = 0, pair_u_masked = 0;
   static constexpr int pair_waves = 0, pair_waves_masked = 0;
 };
 template <> struct Tune<64> {
   static constexpr int row_u = BBGR_ROW_U, row_waves = BBGR_ROW_WAVES;
+  static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U, pair_u_masked = BBGR_PAIR_U_MASKED;
   static constexpr int pair_waves = BBGR_PAIR_WAVES, pair_waves_masked = BBGR_PAIR_WAVES_MASKED;
 };
 template <> struct Tune<128> {
   static constexpr int row_u = BBGR_ROW_U128, row_waves = BBGR_ROW_WAVES128;
+  static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U128, pair_u_masked = BBGR_PAIR_U128;
   static constexpr int pair_waves = BBGR_PAIR_WAVES128, pair_waves_masked = BBGR_PAIR_WAVES128;
 };
 template <> struct Tune<256> {
   static constexpr int row_u = BBGR_ROW_U256, row_waves = BBGR_ROW_WAVES256;
+  static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U256, pair_u_masked = BBGR_PAIR_U256;
   static constexpr int pair_waves = BBGR_PAIR_WAVES256, pair_waves_masked = BBGR_PAIR_WAVES256;
 };
@@ -292,37 +309,39 @@ __device__ __forceinline__ void gather_range_narrow(const SpmmParams &P, int eb,
 // -> store) at 5M rows. Each lane adds its row's edges in CSR order, as the
 // full-width one-row kernel does per column block: a column slice of the
 // result is bitwise the full-width kernel's columns.
+template <int D> struct SlotRounds {   // index rounds (L edges each) per load round
+  static constexpr int value = D == 32 ? BBGR_SLOT_ROUNDS32 : D == 16 ? BBGR_SLOT_ROUNDS16 : 2;
+};
+
 template <int D, int WMODE, bool MASKED>
 __device__ __forceinline__ void gather_slot(const SpmmParams &P, int eb, int ee, int slot,
                                             int sub, float4 &acc) {
   constexpr int L = D / 4;
-  for (int e0 = eb; e0 < ee; e0 += 2 * L) {
-    int my0 = -1, my1 = -1;
-    float mw0 = 0.f, mw1 = 0.f;
-    const int ea = e0 + sub, eb2 = e0 + L + sub;
-    if (ea < ee) {
-      my0 = P.indices[ea];
-      if (MASKED && P.src_mask && !P.src_mask[my0]) my0 = -1;
-      if (my0 >= 0) {
-        if (WMODE == 1) mw0 = P.edge_val[ea];
-        if (WMODE == 2) mw0 = P.col_scale[my0] * P.col_scale_s;
-      }
-    }
-    if (eb2 < ee) {
-      my1 = P.indices[eb2];
-      if (MASKED && P.src_mask && !P.src_mask[my1]) my1 = -1;
-      if (my1 >= 0) {
-        if (WMODE == 1) mw1 = P.edge_val[eb2];
-        if (WMODE == 2) mw1 = P.col_scale[my1] * P.col_scale_s;
-      }
-    }
-    float4 v[2 * L];
-    float w[2 * L];
+  constexpr int RR = SlotRounds<D>::value;
+  for (int e0 = eb; e0 < ee; e0 += RR * L) {
+    int my[RR];
+    float mw[RR];
 #pragma unroll
-    for (int j = 0; j < 2 * L; ++j) {
+    for (int r = 0; r < RR; ++r) {
+      const int e = e0 + r * L + sub;
+      my[r] = -1;
+      mw[r] = 0.f;
+      if (e < ee) {
+        my[r] = P.indices[e];
+        if (MASKED && P.src_mask && !P.src_mask[my[r]]) my[r] = -1;
+        if (my[r] >= 0) {
+          if (WMODE == 1) mw[r] = P.edge_val[e];
+          if (WMODE == 2) mw[r] = P.col_scale[my[r]] * P.col_scale_s;
+        }
+      }
+    }
+    float4 v[RR * L];
+    float w[RR * L];
+#pragma unroll
+    for (int j = 0; j < RR * L; ++j) {
       const int src_lane = slot * L + (j % L);
-      const int c = __shfl(j < L ? my0 : my1, src_lane, 16);
-      w[j] = WMODE == 0 ? 1.f : __shfl(j < L ? mw0 : mw1, src_lane, 16);
+      const int c = __shfl(my[j / L], src_lane, 16);
+      w[j] = WMODE == 0 ? 1.f : __shfl(mw[j / L], src_lane, 16);
       if (e0 + j < ee && (!MASKED || c >= 0)) {
         const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + sub;
         v[j] = c >= P.nt_from ? ld_nt(src) : *src;
@@ -331,7 +350,7 @@ __device__ __forceinline__ void gather_slot(const SpmmParams &P, int eb, int ee,
       }
     }
 #pragma unroll
-    for (int j = 0; j < 2 * L; ++j)
+    for (int j = 0; j < RR * L; ++j)
       acc = WMODE == 0 ? f4_add(acc, v[j]) : f4_fma(w[j], v[j], acc);
   }
 }
@@ -759,7 +778,8 @@ __global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves) void spmm_pair
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::row_waves) void spmm_masked_kernel(SpmmParams P) {
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::masked_waves : Tune<D>::row_waves) void
+spmm_masked_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true, false>(P);
 }
 
