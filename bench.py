@@ -379,9 +379,13 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU trainer (torch.distributed) even at N=1: "
                          "measures the sharded step's own overhead, collectives included")
-    ap.add_argument("--exchange-parts", type=int, default=8,
+    ap.add_argument("--exchange-parts", type=int, default=4,
                     help="N>1: item-row ranges per dense exchange (all-reduce of range c "
-                         "overlaps the SpMM of range c+1)")
+                         "overlaps the SpMM of range c+1). Each range costs a launch tail "
+                         "and a collective call: one C4 rank of 8 measured 3.10 / 3.18 / "
+                         "3.43 / 4.00 ms of compute with 1 / 2 / 4 / 8 ranges "
+                         "(tools/shard_probe.py), against ≤ t_item*(1-1/P) of hidden wire "
+                         "time per exchange")
     ap.add_argument("--vertex-order", default="degree", choices=["degree", "input"],
                     help="number users / items by descending degree inside the graph "
                          "(hot rows cached, cold rows streamed) or keep the input ids")

@@ -1,0 +1,73 @@
+"""Probe: one rank's share of the user-row-sharded C4 step, alone on one GPU.
+
+Rank 0 of an N-way strong split of the config's graph (edge-balanced user
+range, global batch / N users per step) runs as a world-size-1 RCCL
+ShardedTrainer: its collectives are local copies, so the time is the rank's
+compute plus the exchange machinery's launch / range overheads without the
+wire time (DESIGN §6 model: compute(N)). Swept over exchange_parts.
+
+    python tools/shard_probe.py [--config C4] [--parts-of 8] [--exchange-parts 1,2,4,8]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bbgr  # noqa: E402,F401
+from bbgr.distributed import ShardedTrainer, partition_users, shard_edges  # noqa: E402
+from bbgr.synthetic import CONFIGS, CONFIG_SEED, config_edges, synthetic_credibility  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--parts-of", type=int, default=8)
+    ap.add_argument("--exchange-parts", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29581")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    c = CONFIGS[a.config]
+    U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
+    e = config_edges(a.config)
+    deg_u = np.bincount(e[0].astype(np.int64), minlength=U)
+    bounds = partition_users(deg_u, a.parts_of)
+    lo, hi = int(bounds[0]), int(bounds[1])
+    local = shard_edges(e, lo, hi)
+    cred = synthetic_credibility(U, CONFIG_SEED[a.config])[lo:hi]
+    del e
+    for xp in (int(x) for x in a.exchange_parts.split(",")):
+        tr = ShardedTrainer(local, hi - lo, I, "v2_pop", cred=cred, emb_dim=d, num_layers=K,
+                            batch_size=max(1, B // a.parts_of), device="cuda",
+                            vertex_order="degree", exchange_parts=xp,
+                            overlap_item_adam=True)
+        for _ in range(3):
+            tr.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            tr.step()
+        torch.cuda.synchronize()
+        ms = 1000.0 * (time.perf_counter() - t0) / a.steps
+        print(json.dumps({"config": a.config, "rank_of": a.parts_of, "users": hi - lo,
+                          "edges": int(local.shape[1]), "exchange_parts": xp,
+                          "ms_per_step": ms}), flush=True)
+        tr.close()
+        del tr
+        torch.cuda.empty_cache()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
