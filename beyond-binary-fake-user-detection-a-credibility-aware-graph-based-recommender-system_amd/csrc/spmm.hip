@@ -156,6 +156,12 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 #ifndef BBGR_NARROW_MASKED_WAVES32   // ... of the 32-column masked kernel (no edge values)
 #define BBGR_NARROW_MASKED_WAVES32 8
 #endif
+#ifndef BBGR_NARROW_WAVES16
+#define BBGR_NARROW_WAVES16 0
+#endif
+#ifndef BBGR_NARROW_MASKED_WAVES16
+#define BBGR_NARROW_MASKED_WAVES16 0
+#endif
 #ifndef BBGR_SLOT_ROUNDS16
 #define BBGR_SLOT_ROUNDS16 2
 #endif
@@ -164,8 +170,10 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 #endif
 
 template <int D> struct Tune {   // narrow rows (8, 16, 32): one-row kernels only
-  static constexpr int row_u = 0, row_waves = D == 32 ? BBGR_NARROW_WAVES32 : 0;
-  static constexpr int masked_waves = D == 32 ? BBGR_NARROW_MASKED_WAVES32 : 0;
+  static constexpr int row_u = 0;
+  static constexpr int row_waves = D == 32 ? BBGR_NARROW_WAVES32 : D == 16 ? BBGR_NARROW_WAVES16 : 0;
+  static constexpr int masked_waves =
+      D == 32 ? BBGR_NARROW_MASKED_WAVES32 : D == 16 ? BBGR_NARROW_MASKED_WAVES16 : 0;
   static constexpr int pair_u = 0, pair_u_masked = 0;
   static constexpr int pair_waves = 0, pair_waves_masked = 0;
 };

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of the narrow (column-shard) kernels: one column shard of 2 (32 columns)
-# and of 4 (16 columns) with the in-tree build and lib/ab variants.
+# and of 4 (16 columns) with the in-tree build and lib/ab variants
+# (VARIANTS="tag:parts:libdir ..."; r32 runs: c2base/c2r1/c2w8/c2r1w8, c4base/c4r1).
 set -o pipefail
 mkdir -p gpurun_out/abn
 L=beyond-binary-fake-user-detection-a-credibility-aware-graph-based-recommender-system_amd/lib/ab
@@ -11,5 +12,9 @@ run() {  # tag, parts, lib
 import json;j=json.load(open('gpurun_out/abn/$tag.json'))
 print('$tag', round(j['ms_per_step'],3), [(k['kind'],k['side'][:4],k.get('masks',''),round(k['avg_ms'],3)) for k in j['roofline']['per_kernel']])"
 }
-run c2base 2 "" && run c2r1 2 r1 && run c2w8 2 w8 && run c2r1w8 2 r1w8 && run c2base_b 2 "" && \
-run c4base 4 "" && run c4r1 4 r1s16 && echo ALL_OK
+VARIANTS=${VARIANTS:-"c4base:4: c4w16:4:w16 c4mw16:4:mw16 c4r3:4:r3s16 c4base_b:4:"}
+for v in $VARIANTS; do
+  IFS=: read tag parts lib <<< "$v"
+  run $tag $parts "$lib" || exit 1
+done
+echo ALL_OK
