@@ -179,6 +179,8 @@ class ItemExchange:
             self.native.wait()
 
     def __call__(self, t: torch.Tensor) -> None:
+        if not t.is_contiguous():
+            raise ValueError("item exchange: all-reduce of a non-contiguous table")
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def ranges(self, csr):
