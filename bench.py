@@ -258,6 +258,15 @@ def _allreduce(x: float, dev, op) -> float:
     return float(t.item())
 
 
+def edges_per_step(counts: dict, d: int, steps: int) -> tuple[float, float]:
+    """(gathered, visited) edges per step from SpmmTimer.edge_counts(). A
+    launch over a column slice (column shards, column chains) gathers
+    d_launch / d of each edge's row and counts as that fraction of an edge."""
+    gathered = sum(c[3] * k[4] / d for k, c in counts.items()) / steps
+    visited = sum(c[2] * k[4] / d for k, c in counts.items()) / steps
+    return gathered, visited
+
+
 def _compulsory_bytes(nnz: int, rows: int, n_cols: int, d: int) -> int:
     """every edge's index + weight once, every source row
     once, every output row (+ indptr) once: E*8 + C*4d + R*(4 + 4d)."""
@@ -343,7 +352,7 @@ def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> d
     tr.step()
     torch.cuda.synchronize()
     P.set_spmm_timer(None)
-    gathered = _allreduce(sum(c[3] * k[4] / d for k, c in counter.edge_counts().items()),
+    gathered = _allreduce(edges_per_step(counter.edge_counts(), d, 1)[0],
                           dev, torch.distributed.ReduceOp.SUM)
     tr.close()
     steps_per_s = args.weak_beside / el
@@ -597,10 +606,7 @@ def main():
     torch.cuda.synchronize()
     P.set_spmm_timer(None)
     counts = counter.edge_counts()
-    # a launch over a column slice (column shards, column chains) gathers
-    # d_launch / d of each edge's row: counted as that fraction of an edge
-    gathered_step = sum(c[3] * k[4] / d for k, c in counts.items()) / count_steps
-    visited_step = sum(c[2] * k[4] / d for k, c in counts.items()) / count_steps
+    gathered_step, visited_step = edges_per_step(counts, d, count_steps)
     if dist_mode:
         gathered_step = _allreduce(gathered_step, dev, torch.distributed.ReduceOp.SUM)
         visited_step = _allreduce(visited_step, dev, torch.distributed.ReduceOp.SUM)

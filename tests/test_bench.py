@@ -117,3 +117,14 @@ def test_numa_local_cpu_pinning_helpers(bench):
     assert 1 <= len(cpus) <= 4 and set(cpus) <= os.sched_getaffinity(0)
     assert bench._cpu_list_text([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
     assert bench._cpu_list_text([5]) == "5"
+
+
+def test_edges_per_step_weights_column_slices(bench):
+    """A launch over d/N columns counts d_launch/d of its edges: two 32-column
+    chains (or one 32-column shard per rank of 2) add up to one 64-column pass."""
+    full = {("full", "", 1000, 500, 64): [2, 2000, 800, 800]}
+    halves = {("full", "", 1000, 500, 32): [4, 4000, 1600, 1600]}
+    assert bench.edges_per_step(full, 64, 2) == (400.0, 400.0)
+    assert bench.edges_per_step(halves, 64, 2) == (400.0, 400.0)
+    masked = {("masked", "src", 1000, 500, 64): [1, 10, 90, 30]}
+    assert bench.edges_per_step(masked, 64, 1) == (30.0, 90.0)
