@@ -333,8 +333,12 @@ def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> d
     seed = CONFIG_SEED[args.config]
     edges = shard_edges_weak(args.config, rank)
     cred = synthetic_credibility(U, seed + 7919 * rank, args.cred)
+    # full config-sized shards: the item products hide the exchange themselves
+    # (range pipeline); column chains would only add compute
+    xpw = dict(xp, column_chains=1, exchange_parts=4)
     tr = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d, num_layers=K,
-                        batch_size=B, device=dev, user_offset=rank * U, frontier=frontier, **xp)
+                        batch_size=B, device=dev, user_offset=rank * U, frontier=frontier,
+                        **xpw)
     E = int(_allreduce(tr.graph.item_csr.nnz, dev, torch.distributed.ReduceOp.SUM))
     del edges
     for _ in range(max(1, args.warmup)):
@@ -388,23 +392,27 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU trainer (torch.distributed) even at N=1: "
                          "measures the sharded step's own overhead, collectives included")
-    ap.add_argument("--exchange-parts", type=int, default=4,
+    ap.add_argument("--exchange-parts", type=int, default=None,
                     help="N>1: item-row ranges per dense exchange (all-reduce of range c "
                          "overlaps the SpMM of range c+1). Each range costs a launch tail "
                          "and a collective call: one C4 rank of 8 measured 3.10 / 3.18 / "
                          "3.43 / 4.00 ms of compute with 1 / 2 / 4 / 8 ranges "
                          "(tools/shard_probe.py), against ≤ t_item*(1-1/P) of hidden wire "
-                         "time per exchange")
+                         "time per exchange. Default 1 with column chains (the other chain "
+                         "hides the wire time), else 4")
     ap.add_argument("--vertex-order", default="degree", choices=["degree", "input"],
                     help="number users / items by descending degree inside the graph "
                          "(hot rows cached, cold rows streamed) or keep the input ids")
     ap.add_argument("--native-comm", action="store_true",
                     help="N>1: item all-reduces through the C ABI's own RCCL communicator "
                          "(bbgr_allreduce_items) instead of torch.distributed")
-    ap.add_argument("--column-chains", type=int, default=1,
+    ap.add_argument("--column-chains", type=int, default=None,
                     help="users partition: run the propagation as this many column chains "
-                         "(d/C columns each, own stream and exchange group) so one chain's "
-                         "SpMMs overlap another's item all-reduces")
+                         "(d/C columns each, own stream, issue interleaved per exchange) so "
+                         "one chain's SpMMs overlap another's item all-reduces. Default: 2 "
+                         "for strong scaling at N >= 8 (small per-rank shards: one C4 rank "
+                         "of 8 computes in 3.38 ms with 2 chains and no ranges, as with 1 "
+                         "chain and 4 ranges), else 1")
     ap.add_argument("--frontier-parts", type=int, default=2,
                     help="N>1: item-row ranges per frontier (row-list) exchange")
     ap.add_argument("--dense-check", type=int, default=5,
@@ -501,6 +509,11 @@ def main():
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} d={d} K={K} B={B} "
         f"scaling={scaling} generated in {time.perf_counter() - t0:.1f}s")
 
+    if args.column_chains is None:
+        args.column_chains = 2 if (world >= 8 and not weak and d % 2 == 0
+                                   and d // 2 in (8, 16, 32, 64, 128)) else 1
+    if args.exchange_parts is None:
+        args.exchange_parts = 1 if args.column_chains > 1 else 4
     xp = dict(exchange_parts=args.exchange_parts, frontier_parts=args.frontier_parts,
               vertex_order=args.vertex_order)
     if args.native_comm:
@@ -721,7 +734,9 @@ def main():
                                    + (" (sharded trainer)" if dist_mode and world == 1 else "")
                                    + (f", {args.column_chains} column chains"
                                       if dist_mode and not columns and args.column_chains > 1
-                                      else ""))},
+                                      else "")
+                                   + (f", {args.exchange_parts} item-row ranges per exchange"
+                                      if dist_mode and not columns else ""))},
         "bpr_steps_per_s": steps_per_s,
         "torch_gpu_reference": torch_ref,
         "dropin_module_step": dropin,

@@ -45,7 +45,8 @@ from ._lib import OP_SYM, call, ld, ptr, stream_handle
 from .bpr import bpr_args
 from .graph import BipartiteGraph, Scales
 from .optim import AdamRows, adam_step
-from .propagate import ORDER_GS, OperatorPair, backward, epilogue, forward, spmm
+from .propagate import (ORDER_GS, OperatorPair, backward, backward_steps, epilogue, forward,
+                        forward_steps, spmm)
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .scatter import RowScatter
 from .trainer import VARIANTS, FusedTrainer, _internal_rows, resolve_frontier
@@ -343,9 +344,9 @@ class ShardedTrainer(FusedTrainer):
         users per step on THIS rank. vertex_order="degree": local users by
         local degree, items by GLOBAL degree (identical on every rank).
         column_chains=C > 1: the propagation runs as C independent chains over
-        d/C-column slices of the tables, each on its own stream with its own
-        exchange group, so one chain's SpMMs overlap the other's item
-        all-reduces (see _Chain)."""
+        d/C-column slices of the tables, each on its own stream, their issue
+        interleaved one exchange at a time (_interleave), so one chain's SpMMs
+        overlap the other's item all-reduces."""
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}")
@@ -496,20 +497,19 @@ class ShardedTrainer(FusedTrainer):
         if n < 1 or emb_dim % n or emb_dim // n not in WIDTHS:
             raise ValueError(f"cannot run {n} column chains over {emb_dim} columns "
                              f"(slice widths must be one of {WIDTHS})")
-        ranks = dist.get_process_group_ranks(group if group is not None else dist.group.WORLD)
-        backend = dist.get_backend(group)
         w = emb_dim // n
         chains = []
         for c in range(n):
-            # each chain its own group: its collectives run on their own comm
-            # stream instead of queueing behind the other chain's (every rank
-            # creates the groups in the same order)
-            g = group if c == 0 else dist.new_group(ranks=ranks, backend=backend)
-            ex = self.exchange if c == 0 else ItemExchange(g, parts, frontier_parts)
+            # every chain on the ONE group (and one native communicator): the
+            # collectives run in issue order on its comm stream on every rank,
+            # and the chains' issue is interleaved per exchange (_interleave),
+            # so one chain's all-reduce is on the wire while the other computes
+            # (two communicators could start their kernels in different orders
+            # on different ranks)
+            ex = self.exchange if c == 0 else ItemExchange(group, parts, frontier_parts)
             if c > 0:
                 ex.balance_indptr = indptr_i
-                if native_comm:
-                    ex.native = RcclItemComm(g, dev)
+                ex.native = self.exchange.native
             chains.append(_Chain(c * w, (c + 1) * w, ex, torch.cuda.Stream(device=dev), {}))
         # the first-product slot values are built lazily on first use; build
         # them now, on this stream, before two chain streams could race for them
@@ -523,12 +523,13 @@ class ShardedTrainer(FusedTrainer):
         return [ch.exchange for ch in self.chains] if self.chains else [self.exchange]
 
     def close(self) -> None:
-        """Destroy the exchanges' own RCCL communicators (native_comm), if any;
+        """Destroy the exchange's own RCCL communicator (native_comm), if any;
         collective: every rank calls it before the process group goes."""
-        for ex in self._exchanges():
-            if ex.native is not None:
-                torch.cuda.synchronize(self.device)
-                ex.native.close()
+        native = self.exchange.native
+        if native is not None:
+            torch.cuda.synchronize(self.device)
+            native.close()
+            for ex in self._exchanges():
                 ex.native = None
 
     # -- batching ------------------------------------------------------------
@@ -663,25 +664,34 @@ class ShardedTrainer(FusedTrainer):
 
 
     # -- column chains -------------------------------------------------------
-    def _run_chains(self, body) -> None:
-        """body(chain, cols) on every chain's stream, after this stream's work
-        so far; this stream then waits for all of them. Host issue order is the
-        same on every rank, so each chain group sees its collectives in the
-        same order everywhere."""
+    def _interleave(self, steps) -> None:
+        """steps(chain, cols) -> a forward_steps / backward_steps generator per
+        chain, each advanced on its chain's stream (after this stream's work so
+        far) one exchange at a time, round robin: chain 0's item product and
+        all-reduce, chain 1's, chain 0's next products, ... The host order is
+        the same on every rank, so the one comm stream runs the collectives in
+        the same order everywhere. This stream then waits for every chain."""
         main = torch.cuda.current_stream()
+        active = []
         for ch in self.chains:
             ch.stream.wait_stream(main)
-            with torch.cuda.stream(ch.stream):
-                body(ch, slice(ch.c0, ch.c1))
+            active.append((ch, steps(ch, slice(ch.c0, ch.c1))))
+        while active:
+            for item in list(active):
+                ch, gen = item
+                with torch.cuda.stream(ch.stream):
+                    try:
+                        next(gen)
+                    except StopIteration:
+                        active.remove(item)
         for ch in self.chains:
             main.wait_stream(ch.stream)
 
     def _forward_chains(self, final_rows) -> None:
-        def body(ch, cs):
-            forward(self.pair, self.user_w[:, cs], self.item_w[:, cs], self.K, self.order,
-                    out_u=self.uf[:, cs], out_i=self.itf[:, cs], ws=ch.ws,
-                    reduce=ch.exchange, final_rows=final_rows)
-        self._run_chains(body)
+        self._interleave(lambda ch, cs: forward_steps(
+            self.pair, self.user_w[:, cs], self.item_w[:, cs], self.K, self.order,
+            out_u=self.uf[:, cs], out_i=self.itf[:, cs], ws=ch.ws, reduce=ch.exchange,
+            final_rows=final_rows))
 
     def _backward_chains(self, users, masks, alpha: float) -> None:
         """The backward of every chain on its column slice, then (on this
@@ -692,11 +702,10 @@ class ShardedTrainer(FusedTrainer):
         gl = 1.0 / (self.K + 1)
         a_gl = alpha / gl
         if not self.fuse_adam:
-            def body(ch, cs):
-                backward(self.pair, self.g_uf[:, cs], self.g_if[:, cs], self.K, self.order,
-                         out_u=self.g_u0[:, cs], out_i=self.g_i0[:, cs], ws=ch.ws,
-                         reduce=ch.exchange, grad_support=masks)
-            self._run_chains(body)
+            self._interleave(lambda ch, cs: backward_steps(
+                self.pair, self.g_uf[:, cs], self.g_if[:, cs], self.K, self.order,
+                out_u=self.g_u0[:, cs], out_i=self.g_i0[:, cs], ws=ch.ws, reduce=ch.exchange,
+                grad_support=masks))
             st = stream_handle()
             call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
                  ptr(self.g_u0), ld(self.g_u0), self.d, st)
@@ -709,7 +718,7 @@ class ShardedTrainer(FusedTrainer):
         done = self._item_adam_beside() if self.overlap_item_adam else None
         self.step_count += 1
 
-        def body(ch, cs):
+        def steps(ch, cs):
             w = ch.c1 - ch.c0
             adam_u = AdamRows(self.user_w[:, cs], self.m_u[:, cs], self.v_u[:, cs],
                               self.step_count, self.lr)
@@ -717,11 +726,11 @@ class ShardedTrainer(FusedTrainer):
             def before_last():
                 call("bbgr_rows_axpy", B, ptr(users), a_gl, ptr(self.user_w[:, cs]),
                      ld(self.user_w), ptr(self.g_uf[:, cs]), ld(self.g_uf), w, stream_handle())
-            backward(self.pair, self.g_uf[:, cs], self.g_if[:, cs], self.K, self.order,
-                     out_u=self.g_u0[:, cs], ws=ch.ws, grad_support=masks,
-                     grad_i0_dense=False, adam_u=adam_u, before_last=before_last,
-                     reduce=ch.exchange)
-        self._run_chains(body)
+            return backward_steps(self.pair, self.g_uf[:, cs], self.g_if[:, cs], self.K,
+                                  self.order, out_u=self.g_u0[:, cs], ws=ch.ws,
+                                  grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
+                                  before_last=before_last, reduce=ch.exchange)
+        self._interleave(steps)
         if done is not None:
             torch.cuda.current_stream().wait_event(done)
         else:
@@ -730,7 +739,8 @@ class ShardedTrainer(FusedTrainer):
 
 class _Chain:
     """One column chain of a ShardedTrainer: columns [c0, c1) of every table,
-    its stream, its item exchange (own process group) and its workspaces."""
+    its stream, its item exchange (the trainer's group; its own compaction
+    buffers and ratio cache) and its workspaces."""
 
     def __init__(self, c0: int, c1: int, exchange: ItemExchange, stream, ws: dict):
         self.c0, self.c1, self.exchange, self.stream, self.ws = c0, c1, exchange, stream, ws

@@ -362,11 +362,23 @@ def _buffers(ws: dict | None, device, d: int):
     return new
 
 
-def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
-            order: str = ORDER_GS, out_u: torch.Tensor | None = None,
-            out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None,
-            final_rows=None):
+def drain(steps):
+    """Run a *_steps generator to its end and return its value."""
+    try:
+        while True:
+            next(steps)
+    except StopIteration as stop:
+        return stop.value
+
+
+def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
+                  order: str = ORDER_GS, out_u: torch.Tensor | None = None,
+                  out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None,
+                  final_rows=None):
     """Final (layer-mean) user and item tables. u0 [U,d], i0 [I,d] fp32.
+    A generator: it yields after issuing each item-row product (with `reduce`,
+    each exchange point), so the caller can interleave the issue of several
+    chains (ShardedTrainer column chains); `drain()` / `forward()` run it whole.
     `reduce(t)`: in-place sum over ranks of item-row partial sums (sharded mode).
     `final_rows=(user_mask, item_mask[, user_list])`: only the flagged rows of the final
     tables are needed (a training step reads batch rows only). The last layer
@@ -398,6 +410,7 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
                           y_scale=pair.feed_fwd_iu, acc_in=i0 if k == 1 else acc_i,
                           acc_out=acc_i, acc_scale=FI.out_scale, gamma=g,
                           row_mask=mi if last else None, acc_mask=mi)
+            yield
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
                  acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
@@ -414,6 +427,7 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
                           acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
                           acc_scale=FI.out_scale, gamma=g, row_mask=mi if last else None,
                           acc_mask=mi)
+            yield
             spmm(FU, i0 if k == 1 else bufI[cur], k == 1,
                  y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
@@ -425,12 +439,22 @@ def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: 
     return acc_u, acc_i
 
 
-def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
-             order: str = ORDER_GS, out_u: torch.Tensor | None = None,
-             out_i: torch.Tensor | None = None, ws: dict | None = None,
-             grad_i0_dense: bool = True, reduce=None, grad_support=None,
-             adam_u=None, before_last=None, adam_i=None):
-    """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final).
+def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
+            order: str = ORDER_GS, out_u: torch.Tensor | None = None,
+            out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None,
+            final_rows=None):
+    """forward_steps run to completion: the final (u, i) tables."""
+    return drain(forward_steps(pair, u0, i0, num_layers, order, out_u, out_i, ws, reduce,
+                               final_rows))
+
+
+def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
+                   order: str = ORDER_GS, out_u: torch.Tensor | None = None,
+                   out_i: torch.Tensor | None = None, ws: dict | None = None,
+                   grad_i0_dense: bool = True, reduce=None, grad_support=None,
+                   adam_u=None, before_last=None, adam_i=None):
+    """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final); a
+    generator yielding after each item-row product, like forward_steps.
     `adam_u` (optim.AdamRows) fuses the user-table Adam step into the last
     (user-row) product, which then writes no gradient table (out_u is left
     untouched); `before_last()` runs just before the last products, after
@@ -470,6 +494,7 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
                           add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
                           src_mask=su if first else None,
                           row_mask=si if first else None)
+            yield
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
                      add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl,
@@ -507,6 +532,7 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
                 _item_product(BI, xi, first, reduce, new, y=bufI[nxt],
                               y_scale=pair.feed_bwd_iu, y_scale_s=ys,
                               add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl, src_mask=mi_)
+                yield
             else:
                 if before_last is not None and adam_u is not None:
                     before_last()
@@ -519,10 +545,22 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
                 if adam_i is not None:
                     ik["adam"] = adam_i
                 _item_product(BI, xi, first, reduce, new, **ik)
+                yield
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")
     return gu0, gi0
+
+
+def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
+             order: str = ORDER_GS, out_u: torch.Tensor | None = None,
+             out_i: torch.Tensor | None = None, ws: dict | None = None,
+             grad_i0_dense: bool = True, reduce=None, grad_support=None,
+             adam_u=None, before_last=None, adam_i=None):
+    """backward_steps run to completion: (grad u0, grad i0)."""
+    return drain(backward_steps(pair, gU, gI, num_layers, order, out_u, out_i, ws,
+                                grad_i0_dense, reduce, grad_support, adam_u, before_last,
+                                adam_i))
 
 
 def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,

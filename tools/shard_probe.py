@@ -7,6 +7,7 @@ compute plus the exchange machinery's launch / range overheads without the
 wire time (DESIGN §6 model: compute(N)). Swept over exchange_parts.
 
     python tools/shard_probe.py [--config C4] [--parts-of 8] [--exchange-parts 1,2,4,8]
+                                [--column-chains 1,2]
 """
 from __future__ import annotations
 
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("--parts-of", type=int, default=8)
     ap.add_argument("--exchange-parts", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--column-chains", default="1")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29581")
@@ -47,11 +49,13 @@ def main():
     local = shard_edges(e, lo, hi)
     cred = synthetic_credibility(U, CONFIG_SEED[a.config])[lo:hi]
     del e
-    for xp in (int(x) for x in a.exchange_parts.split(",")):
+    runs = [(int(x), int(ch)) for ch in a.column_chains.split(",")
+            for x in a.exchange_parts.split(",")]
+    for xp, chains in runs:
         tr = ShardedTrainer(local, hi - lo, I, "v2_pop", cred=cred, emb_dim=d, num_layers=K,
                             batch_size=max(1, B // a.parts_of), device="cuda",
                             vertex_order="degree", exchange_parts=xp,
-                            overlap_item_adam=True)
+                            overlap_item_adam=True, column_chains=chains)
         for _ in range(3):
             tr.step()
         torch.cuda.synchronize()
@@ -62,6 +66,7 @@ def main():
         ms = 1000.0 * (time.perf_counter() - t0) / a.steps
         print(json.dumps({"config": a.config, "rank_of": a.parts_of, "users": hi - lo,
                           "edges": int(local.shape[1]), "exchange_parts": xp,
+                          "column_chains": chains,
                           "ms_per_step": ms}), flush=True)
         tr.close()
         del tr
