@@ -410,7 +410,7 @@ def main():
                     help="users partition: run the propagation as this many column chains "
                          "(d/C columns each, own stream, issue interleaved per exchange) so "
                          "one chain's SpMMs overlap another's item all-reduces. Default: 2 "
-                         "for strong scaling at N >= 8 (small per-rank shards: one C4 rank "
+                         "for strong scaling at N >= 8 with <= 20M edges per rank (one C4 rank "
                          "of 8 computes in 3.38 ms with 2 chains and no ranges, as with 1 "
                          "chain and 4 ranges), else 1")
     ap.add_argument("--frontier-parts", type=int, default=2,
@@ -510,7 +510,10 @@ def main():
         f"scaling={scaling} generated in {time.perf_counter() - t0:.1f}s")
 
     if args.column_chains is None:
-        args.column_chains = 2 if (world >= 8 and not weak and d % 2 == 0
+        # small per-rank shards only: there the exchange outlasts the rank's
+        # item products; a big shard's item product hides it by itself (C5)
+        small = cfg["num_edges"] // max(world, 1) <= 20_000_000
+        args.column_chains = 2 if (world >= 8 and not weak and small and d % 2 == 0
                                    and d // 2 in (8, 16, 32, 64, 128)) else 1
     if args.exchange_parts is None:
         args.exchange_parts = 1 if args.column_chains > 1 else 4
