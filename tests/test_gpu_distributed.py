@@ -201,16 +201,19 @@ def test_column_sharded_step_matches_single_gpu(tmp_path, variant, frontier, ord
         np.testing.assert_array_equal(rk["user_w"], ranks[0]["user_w"])   # same gather
 
 
-@pytest.mark.parametrize("partition", ["columns", "users"])
+@pytest.mark.parametrize("partition", ["columns", "users", "users+chains"])
 def test_bench_two_ranks_on_c2(tmp_path, partition):
     """bench.py's N > 1 path end to end (the driver's multi-GPU run) with both
-    partitions, 2 gloo ranks sharing the device, on C2: one JSON line from
-    rank 0 with the whole job's graph and the partition named."""
+    partitions (and the user-row partition with two interleaved column chains,
+    the N >= 8 default), 2 gloo ranks sharing the device, on C2: one JSON line
+    from rank 0 with the whole job's graph and the partition named."""
+    chains = partition.endswith("+chains")
+    partition = partition.split("+")[0]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "3",
            "--warmup", "1", "--dense-check", "1", "--frontier", "on", "--partition", partition,
-           "--weak-beside", "2"]
+           "--weak-beside", "2"] + (["--column-chains", "2"] if chains else [])
     env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -220,6 +223,8 @@ def test_bench_two_ranks_on_c2(tmp_path, partition):
     assert j["n_gpus"] == 2 and j["scaling"] == "strong" and j["partition"] == partition
     assert j["config"]["num_edges"] == 1_000_000 and j["value"] > 0
     assert j["roofline"]["bound"] == "hbm" and j["dense_ms_per_step"] > 0
+    if chains:
+        assert "2 column chains, 1 item-row ranges" in j["config"]["parallelism"]
     if partition == "users":
         assert j["weak_beside"]["num_edges"] == 2_000_000
     else:
