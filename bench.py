@@ -733,6 +733,7 @@ def main():
                                    "rank, whole graph on every rank)" if columns else
                                    f"one column shard of {emulate} ({d // emulate} columns): "
                                    "single-GPU stand-in for one rank" if emulate else
+                                   "single GPU (fused trainer)" if not dist_mode else
                                    f"user-rows x{world}"
                                    + (" (sharded trainer)" if dist_mode and world == 1 else "")
                                    + (f", {args.column_chains} column chains"
@@ -778,7 +779,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch_corrected"),
-                     "kernel": "bbgr::spmm_kernel (+ spmm_fixup_kernel): full-CSR item<-user "
+                     "kernel": "bbgr::spmm_kernel (split rows finished in-launch): full-CSR item<-user "
                                "product, the largest share of step time",
                      "algorithmic_bytes_per_launch": dom_bytes,
                      "algorithmic_model": "gather model E*(4+4+4d) + R*(4+4d) (SURVEY §8(d))",
