@@ -66,10 +66,18 @@ class Product:
 
     def workspace(self, d: int):
         """Split-row partials and arrival counters, one set per (width, stream):
-        launches on two streams (column chains) must not share counters."""
+        launches on two streams (column chains) must not share counters. A
+        graph capture uses the default stream's set (see below)."""
         if self.csr.n_split == 0:
             return None
-        key = (d, torch.cuda.current_stream(self.csr.device).cuda_stream)
+        dev = self.csr.device
+        stream = torch.cuda.current_stream(dev)
+        if torch.cuda.is_current_stream_capturing():
+            # a captured step (GraphedStep) replays on its caller's stream, in
+            # order with that stream's eager launches: it shares their buffer
+            # rather than allocating (and zero-filling on every replay) its own
+            stream = torch.cuda.default_stream(dev)
+        key = (d, stream.cuda_stream)
         w = self.partial.get(key)
         if w is None:
             w = self.csr.partial_workspace(d)
