@@ -413,7 +413,7 @@ def main():
                          "for strong scaling at N >= 8 with <= 20M edges per rank (one C4 rank "
                          "of 8 computes in 3.38 ms with 2 chains and no ranges, as with 1 "
                          "chain and 4 ranges), else 1")
-    ap.add_argument("--frontier-parts", type=int, default=2,
+    ap.add_argument("--frontier-parts", type=int, default=None,
                     help="N>1: item-row ranges per frontier (row-list) exchange")
     ap.add_argument("--dense-check", type=int, default=5,
                     help="after the timed steps, time this many steps with frontier sparsity "
@@ -517,6 +517,8 @@ def main():
                                    and d // 2 in (8, 16, 32, 64, 128)) else 1
     if args.exchange_parts is None:
         args.exchange_parts = 1 if args.column_chains > 1 else 4
+    if args.frontier_parts is None:   # with chains the other chain hides the wire time
+        args.frontier_parts = 1 if args.column_chains > 1 else 2
     xp = dict(exchange_parts=args.exchange_parts, frontier_parts=args.frontier_parts,
               vertex_order=args.vertex_order)
     if args.native_comm:

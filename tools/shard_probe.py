@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--exchange-parts", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--column-chains", default="1")
+    ap.add_argument("--frontier-parts", default="2")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29581")
@@ -49,13 +50,14 @@ def main():
     local = shard_edges(e, lo, hi)
     cred = synthetic_credibility(U, CONFIG_SEED[a.config])[lo:hi]
     del e
-    runs = [(int(x), int(ch)) for ch in a.column_chains.split(",")
-            for x in a.exchange_parts.split(",")]
-    for xp, chains in runs:
+    runs = [(int(x), int(ch), int(fp)) for ch in a.column_chains.split(",")
+            for x in a.exchange_parts.split(",") for fp in a.frontier_parts.split(",")]
+    for xp, chains, fparts in runs:
         tr = ShardedTrainer(local, hi - lo, I, "v2_pop", cred=cred, emb_dim=d, num_layers=K,
                             batch_size=max(1, B // a.parts_of), device="cuda",
                             vertex_order="degree", exchange_parts=xp,
-                            overlap_item_adam=True, column_chains=chains)
+                            overlap_item_adam=True, column_chains=chains,
+                            frontier_parts=fparts)
         for _ in range(3):
             tr.step()
         torch.cuda.synchronize()
@@ -66,7 +68,7 @@ def main():
         ms = 1000.0 * (time.perf_counter() - t0) / a.steps
         print(json.dumps({"config": a.config, "rank_of": a.parts_of, "users": hi - lo,
                           "edges": int(local.shape[1]), "exchange_parts": xp,
-                          "column_chains": chains,
+                          "column_chains": chains, "frontier_parts": fparts,
                           "ms_per_step": ms}), flush=True)
         tr.close()
         del tr
