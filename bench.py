@@ -335,7 +335,7 @@ def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> d
     cred = synthetic_credibility(U, seed + 7919 * rank, args.cred)
     # full config-sized shards: the item products hide the exchange themselves
     # (range pipeline); column chains would only add compute
-    xpw = dict(xp, column_chains=1, exchange_parts=4)
+    xpw = dict(xp, column_chains=1, exchange_parts=4, frontier_parts=2)
     tr = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d, num_layers=K,
                         batch_size=B, device=dev, user_offset=rank * U, frontier=frontier,
                         **xpw)
