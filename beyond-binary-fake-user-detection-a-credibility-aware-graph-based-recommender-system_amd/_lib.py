@@ -182,6 +182,14 @@ _SIGNATURES = {
                            c_int32),
     "bbgr_mask_to_list": ([c_int64, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_rows_gather": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
+    # blueprint names, thin forms of the entry points above
+    "bbgr_spmm_f32": ([ctypes.POINTER(CsrStruct), _P, c_int64, _P, c_int64, c_int32, _P, _P,
+                       _P, c_float, _P], c_int32),
+    "bbgr_bpr_fwd_bwd": ([ctypes.POINTER(BprArgs), _P], c_int32),
+    "bbgr_adam_f32": ([c_int64, _P, _P, _P, _P, c_float, c_float, c_float, c_float,
+                       c_float, c_float, c_float, c_float, _P], c_int32),
+    "bbgr_negsample": ([c_int64, _P, _P, _P, c_int32, _P, c_float, c_int32, c_uint64,
+                        c_uint64, _P, _P, _P, _P], c_int32),
 }
 
 _lib = None

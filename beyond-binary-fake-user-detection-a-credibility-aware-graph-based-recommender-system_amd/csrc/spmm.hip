@@ -20,6 +20,8 @@
 #include <stdarg.h>
 #include <stdlib.h>
 
+#include <cstring>
+
 #include "common.h"
 
 namespace bbgr {
@@ -1041,9 +1043,8 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
     n_split = r[5] - r[4];
   }
   BBGR_REQUIRE(!a->row_list || a->n_row_list >= 0, "bbgr_spmm: negative n_row_list");
-  // chunk workgroups of a list launch compute only rows flagged in row_mask
-  // (and the fix-up sums only those): without the mask, long listed rows
-  // would be skipped and the fix-up would sum stale partials
+  // chunk workgroups of a list launch compute only rows flagged in row_mask:
+  // without the mask, long listed rows would be skipped
   BBGR_REQUIRE(!a->row_list || a->row_mask || csr->n_chunks == 0,
                "bbgr_spmm: row_list needs row_mask when the plan has long-row chunks");
   P.pair_rows = d >= 64 && pair_rows(csr);
@@ -1058,4 +1059,60 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
     case 128: return dispatch_wmode<128>(P, a->weight_mode, n_split, st);
     default: return dispatch_wmode<256>(P, a->weight_mode, n_split, st);
   }
+}
+
+// ---------------------------------------------------------------------------
+// The entry-point names of SURVEY §8(b)'s ABI sketch, kept as thin forms of
+// the entry points above (include/bbgr.h, "Blueprint names").
+// ---------------------------------------------------------------------------
+extern "C" int bbgr_spmm_f32(const bbgr_csr *A, const float *X, int64_t ldx, float *Y,
+                             int64_t ldy, int32_t d, const float *row_scale,
+                             const float *col_scale, float *acc, float acc_scale,
+                             bbgr_stream_t stream) {
+  BBGR_REQUIRE(A, "bbgr_spmm_f32: null csr");
+  BBGR_REQUIRE(A->n_split == 0,
+               "bbgr_spmm_f32: the plan has split rows; use bbgr_spmm with a partial workspace");
+  bbgr_spmm_args a;
+  std::memset(&a, 0, sizeof a);
+  a.d = d;
+  a.x = X;
+  a.ldx = ldx;
+  a.weight_mode = col_scale ? 2 : 0;
+  a.col_scale = col_scale;
+  a.col_scale_s = 1.f;
+  a.y = Y;
+  a.ldy = ldy;
+  a.y_scale = row_scale;
+  a.y_scale_s = 1.f;
+  if (acc) {   // acc += acc_scale * Y: the epilogue adds acc_scale * row_scale * T
+    a.acc_in = acc;
+    a.ldacc_in = ldy;
+    a.acc_out = acc;
+    a.ldacc_out = ldy;
+    a.acc_scale = row_scale;
+    a.acc_scale_s = acc_scale;
+  }
+  a.gamma = 1.f;
+  return bbgr_spmm(A, &a, stream);
+}
+
+extern "C" int bbgr_bpr_fwd_bwd(const bbgr_bpr_args *args, bbgr_stream_t stream) {
+  return bbgr_bpr(args, stream);
+}
+
+extern "C" int bbgr_adam_f32(int64_t n, float *param, const float *grad, float *exp_avg,
+                             float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                             float weight_decay, float grad_scale, float bias_correction1,
+                             float bias_correction2_sqrt, bbgr_stream_t stream) {
+  return bbgr_adam(n, param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                   grad_scale, bias_correction1, bias_correction2_sqrt, stream);
+}
+
+extern "C" int bbgr_negsample(int64_t batch, const int64_t *users, const int32_t *indptr,
+                              const int32_t *indices, int32_t n_items, const double *cdf,
+                              float mix_pop, int32_t max_tries, uint64_t seed, uint64_t counter,
+                              int64_t *pos, int64_t *neg, int32_t *fail_count,
+                              bbgr_stream_t stream) {
+  return bbgr_sample(batch, users, indptr, indices, n_items, cdf, mix_pop, max_tries, seed,
+                     counter, pos, neg, fail_count, stream);
 }

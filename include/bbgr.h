@@ -583,6 +583,29 @@ int bbgr_eval_sampled(const bbgr_eval_args *args, void *workspace, size_t *works
 int bbgr_eval_full(const bbgr_eval_args *args, void *workspace, size_t *workspace_bytes,
                    bbgr_stream_t stream);
 
+/* ------------------------------------------------------------------------- */
+/* Blueprint names (SURVEY §8(b)'s ABI sketch), thin forms of the above.      */
+/* ------------------------------------------------------------------------- */
+/* Y = diag(row_scale) A diag(col_scale) X (either scale NULL = ones), one    */
+/* fused launch; acc (nullable, leading dimension ldy): acc += acc_scale * Y  */
+/* (the layer-mean accumulation). For plans without split rows               */
+/* (A->n_split == 0); otherwise use bbgr_spmm with a partial workspace.       */
+int bbgr_spmm_f32(const bbgr_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                  int32_t d, const float *row_scale, const float *col_scale, float *acc,
+                  float acc_scale, bbgr_stream_t stream);
+/* = bbgr_bpr (loss parts and gradients in one launch). */
+int bbgr_bpr_fwd_bwd(const bbgr_bpr_args *args, bbgr_stream_t stream);
+/* = bbgr_adam. */
+int bbgr_adam_f32(int64_t n, float *param, const float *grad, float *exp_avg,
+                  float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, float grad_scale, float bias_correction1,
+                  float bias_correction2_sqrt, bbgr_stream_t stream);
+/* = bbgr_sample (pop-mix negatives + uniform positives). */
+int bbgr_negsample(int64_t batch, const int64_t *users, const int32_t *indptr,
+                   const int32_t *indices, int32_t n_items, const double *cdf,
+                   float mix_pop, int32_t max_tries, uint64_t seed, uint64_t counter,
+                   int64_t *pos, int64_t *neg, int32_t *fail_count, bbgr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,6 +98,15 @@ int main(void) {
                                                                (const int32_t *)f4, NULL, NULL,
                                                                NULL));
   expect_ok("row_support empty", bbgr_row_support(0, 64, NULL, 64, NULL, NULL, NULL, NULL, NULL));
+  expect_error("spmm_f32 null csr", bbgr_spmm_f32(NULL, f4, 64, f4, 64, 64, NULL, NULL, NULL,
+                                                   0.f, NULL));
+  csr.n_split = 1;
+  expect_error("spmm_f32 split rows", bbgr_spmm_f32(&csr, f4, 64, f4, 64, 64, NULL, NULL, NULL,
+                                                     0.f, NULL));
+  csr.n_split = 0;
+  expect_error("bpr_fwd_bwd null", bbgr_bpr_fwd_bwd(NULL, NULL));
+  expect_error("adam_f32 negative n", bbgr_adam_f32(-1, f4, f4, f4, f4, 1e-3f, 0.9f, 0.999f,
+                                                    1e-8f, 0.f, 1.f, 1.f, 1.f, NULL));
   expect_error("allreduce null comm", bbgr_allreduce_items(NULL, f4, 4, NULL));
   expect_error("eval sampled null", bbgr_eval_sampled(NULL, NULL, NULL, NULL));
   expect_error("eval full null", bbgr_eval_full(NULL, NULL, NULL, NULL));

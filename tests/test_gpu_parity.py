@@ -182,6 +182,38 @@ def test_column_shard_forward_equals_full_width_columns():
             assert_parity(si, itf[:, c0:c1], f"items {parts}/{idx}")
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_spmm_f32_blueprint_entry_point(d):
+    """bbgr_spmm_f32 (SURVEY §8(b)'s flat form): Y = diag(rs) A diag(cs) X and
+    acc += a * Y, against float64; a plan with split rows is refused."""
+    import ctypes
+    from bbgr._lib import call, ld, ptr, stream_handle
+    import scipy.sparse as sp
+    U, I = 900, 400
+    e = synthetic_edges(U, I, 12000, 17, items="zipf")
+    c = Csr(e[1], e[0], I, U, DEV, long_threshold=1 << 30)   # no split rows
+    assert c.n_split == 0
+    rng = np.random.default_rng(d)
+    x = rng.normal(size=(U, d)).astype(np.float32)
+    rs = rng.uniform(0.5, 1.5, I).astype(np.float32)
+    cs = rng.uniform(0.5, 1.5, U).astype(np.float32)
+    acc0 = rng.normal(size=(I, d)).astype(np.float32)
+    X, RS, CS = t(x), t(rs), t(cs)
+    Y = torch.empty(I, d, device=DEV)
+    acc = t(acc0)
+    call("bbgr_spmm_f32", ctypes.byref(c._struct), ptr(X), ld(X), ptr(Y), ld(Y), d, ptr(RS),
+         ptr(CS), ptr(acc), 0.25, stream_handle())
+    A = sp.csr_matrix((np.ones(e.shape[1]), (e[1], e[0])), shape=(I, U))
+    ref = (rs[:, None].astype(np.float64) * (A @ (cs[:, None].astype(np.float64) * x)))
+    assert_parity(Y, ref, "spmm_f32 Y")
+    assert_parity(acc, acc0 + 0.25 * ref, "spmm_f32 acc")
+    split = Csr(e[1], e[0], I, U, DEV, long_threshold=8, chunk_edges=16)
+    assert split.n_split > 0
+    with pytest.raises(RuntimeError, match="split rows"):
+        call("bbgr_spmm_f32", ctypes.byref(split._struct), ptr(X), ld(X), ptr(Y), ld(Y), d,
+             None, None, None, 0.0, stream_handle())
+
+
 def test_spmm_deterministic():
     from bbgr.propagate import Product, spmm
     e = synthetic_edges(3000, 500, 60000, 9, items="zipf")
