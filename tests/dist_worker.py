@@ -138,9 +138,12 @@ def rccl_single_rank(out_dir, variant, order="input"):
     nat = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
                          vertex_order=order, native_comm=True, **kw)   # bbgr_allreduce_items
     chains = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
-                            vertex_order=order, column_chains=2, **kw)   # two RCCL groups
+                            vertex_order=order, column_chains=2, **kw)   # interleaved chains
+    chains_nat = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=1,
+                                vertex_order=order, column_chains=2, native_comm=True, **kw)
     out = {}
-    for tag, tr in (("sharded", sh), ("single", one), ("native", nat), ("chains", chains)):
+    for tag, tr in (("sharded", sh), ("single", one), ("native", nat), ("chains", chains),
+                    ("chains_native", chains_nat)):
         out[f"{tag}_loss"] = np.array([float(tr.step()) for _ in range(3)])
         out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
         out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
@@ -148,6 +151,7 @@ def rccl_single_rank(out_dir, variant, order="input"):
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, "rccl1.npz"), **out)
     nat.close()   # bbgr_comm_destroy
+    chains_nat.close()
     dist.destroy_process_group()
 
 

@@ -165,10 +165,13 @@ def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, 
         assert err < 1e-6, (key, err)
         # the C ABI's own RCCL communicator (bbgr_allreduce_items) == torch's
         np.testing.assert_array_equal(z[f"native_{key}"], z[f"sharded_{key}"])
-        # two column chains on two RCCL groups and streams
-        err = np.linalg.norm(z[f"chains_{key}"] - b) / np.linalg.norm(b)
-        assert err < 1e-6, ("chains", key, err)
+        # two interleaved column chains on their own streams, through torch's
+        # collectives and through the C ABI's communicator (shared by the chains)
+        for tag in ("chains", "chains_native"):
+            err = np.linalg.norm(z[f"{tag}_{key}"] - b) / np.linalg.norm(b)
+            assert err < 1e-6, (tag, key, err)
     np.testing.assert_allclose(z["chains_loss"], z["single_loss"], rtol=1e-6)
+    np.testing.assert_allclose(z["chains_native_loss"], z["single_loss"], rtol=1e-6)
     np.testing.assert_array_equal(z["native_loss"], z["sharded_loss"])
 
 
