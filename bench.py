@@ -690,7 +690,8 @@ def main():
         log("[bench] timing the stock-torch reference step on the GPU ...")
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from torch_sparse_step import run as torch_reference_run
-        torch_ref = torch_reference_run(args.config, edges, cred, device=dev)
+        torch_ref = torch_reference_run(args.config, edges, cred, device=dev,
+                                        variant=args.variant)
         torch_ref["speedup_vs_torch"] = torch_ref["step_ms"] / (1000.0 * elapsed / args.steps)
         torch_ref["note"] = ("the reference's V2 step written with its own torch calls "
                              "(sparse_coo_tensor.coalesce, torch.sparse.mm, stack.mean, "

@@ -7,7 +7,10 @@ torch.sparse.mm per layer in Gauss-Seidel order and stack().mean(0)
 torch.optim.Adam(lr=1e-3) (:793, :858-863) — all on cuda. This is what the
 reference's own code does on this GPU, the like-for-like GPU baseline for
 the HIP path (bench.py / tools/dropin_probe.py). Batches are uniform draws
-made up front (the sampler is not what this times).
+made up front (the sampler is not what this times). variant="cu_fair" runs
+lightgcn_cu.py's step instead: its operators (`lightgcn_cu.py:383-397`,
+credibility on the item<-user side, 1/sqrt(deg_u*deg_i)), Jacobi layers
+(:429-447) and the fairness term (:583-584, 637-648).
 
     python tools/torch_sparse_step.py [--config C4] [--steps 5]
 """
@@ -28,6 +31,18 @@ import bbgr  # noqa: E402,F401
 from bbgr.synthetic import CONFIGS, CONFIG_SEED, config_edges, synthetic_credibility  # noqa: E402
 
 
+def operators_cu(e: np.ndarray, U: int, I: int, cred: torch.Tensor, dev):
+    """(item<-user [I,U], user<-item [U,I], deg_i) of lightgcn_cu.py."""
+    u = torch.as_tensor(e[0], dtype=torch.int64, device=dev)
+    i = torch.as_tensor(e[1], dtype=torch.int64, device=dev)
+    du = torch.bincount(u, minlength=U).float()
+    di = torch.bincount(i, minlength=I).float()
+    w = 1.0 / torch.sqrt(torch.clamp(du[u] * di[i], min=1e-12))
+    M_item = torch.sparse_coo_tensor(torch.stack([i, u]), cred[u] * w, (I, U)).coalesce()
+    M_user = torch.sparse_coo_tensor(torch.stack([u, i]), w, (U, I)).coalesce()
+    return M_item, M_user, di
+
+
 def operators(e: np.ndarray, U: int, I: int, cred: torch.Tensor, dev):
     u = torch.as_tensor(e[0], dtype=torch.int64, device=dev)
     i = torch.as_tensor(e[1], dtype=torch.int64, device=dev)
@@ -40,9 +55,11 @@ def operators(e: np.ndarray, U: int, I: int, cred: torch.Tensor, dev):
 
 
 class Model(torch.nn.Module):
-    def __init__(self, U, I, d, K, M_ui, M_iu):
+    def __init__(self, U, I, d, K, M_ui, M_iu, jacobi: bool = False, pop=None,
+                 lambda_fair: float = 0.0):
         super().__init__()
         self.K, self.M_ui, self.M_iu = K, M_ui, M_iu
+        self.jacobi, self.pop, self.lambda_fair = jacobi, pop, lambda_fair
         self.user_emb = torch.nn.Embedding(U, d)
         self.item_emb = torch.nn.Embedding(I, d)
         torch.nn.init.xavier_uniform_(self.user_emb.weight)
@@ -53,8 +70,11 @@ class Model(torch.nn.Module):
         i = self.item_emb.weight
         us, is_ = [u], [i]
         for _ in range(self.K):
-            i = torch.sparse.mm(self.M_iu, u)
-            u = torch.sparse.mm(self.M_ui, i)
+            if self.jacobi:   # both from the previous layer (M_iu: item<-user here)
+                i, u = torch.sparse.mm(self.M_iu, us[-1]), torch.sparse.mm(self.M_ui, is_[-1])
+            else:
+                i = torch.sparse.mm(self.M_iu, u)
+                u = torch.sparse.mm(self.M_ui, i)
             us.append(u)
             is_.append(i)
         return torch.stack(us, 0).mean(0), torch.stack(is_, 0).mean(0)
@@ -66,7 +86,10 @@ class Model(torch.nn.Module):
         ue, ie = self.user_emb.weight, self.item_emb.weight
         r = (ue[users].norm(2, dim=1).pow(2) + ie[pos].norm(2, dim=1).pow(2)
              + ie[neg].norm(2, dim=1).pow(2)).mean()
-        return loss + reg * r
+        loss = loss + reg * r
+        if self.pop is not None:
+            loss = loss + self.lambda_fair * (self.pop[pos] * (u * p).sum(1)).mean()
+        return loss
 
 
 def timed(fn, steps: int) -> float:
@@ -79,7 +102,7 @@ def timed(fn, steps: int) -> float:
 
 
 def run(cfg_name: str, edges: np.ndarray | None = None, cred_np=None, steps: int = 5,
-        warmup: int = 2, device=None) -> dict:
+        warmup: int = 2, device=None, variant: str = "v2_pop") -> dict:
     """Times of the stock-torch reference step at `cfg_name` (edges / cred
     drawn if not given). Frees its tensors before returning."""
     c = CONFIGS[cfg_name]
@@ -90,9 +113,14 @@ def run(cfg_name: str, edges: np.ndarray | None = None, cred_np=None, steps: int
         cred_np = synthetic_credibility(U, CONFIG_SEED[cfg_name])
     cred = torch.as_tensor(np.asarray(cred_np, np.float32), device=dev)
     t0 = time.perf_counter()
-    M_ui, M_iu = operators(e, U, I, cred, dev)
     torch.manual_seed(42)
-    model = Model(U, I, d, K, M_ui, M_iu).to(dev)
+    if variant == "cu_fair":
+        M_item, M_user, di = operators_cu(e, U, I, cred, dev)
+        model = Model(U, I, d, K, M_user, M_item, jacobi=True,
+                      pop=di / di.max().clamp(min=1.0), lambda_fair=0.05).to(dev)
+    else:
+        M_ui, M_iu = operators(e, U, I, cred, dev)
+        model = Model(U, I, d, K, M_ui, M_iu).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
@@ -120,13 +148,14 @@ def run(cfg_name: str, edges: np.ndarray | None = None, cred_np=None, steps: int
 
     for _ in range(warmup):
         step()
-    out = {"config": cfg_name, "torch": torch.__version__, "setup_s": setup_s,
+    out = {"config": cfg_name, "variant": "cu_fair" if variant == "cu_fair" else "v2_pop",
+           "torch": torch.__version__, "setup_s": setup_s,
            "num_edges": int(e.shape[1]), "steps": steps,
            "step_ms": timed(step, steps), "forward_ms": timed(fwd, steps),
            "forward_backward_ms": timed(fwd_bwd, steps),
            "adam_ms": timed(opt.step, steps)}
     out["edges_per_s_4KE"] = 4 * K * int(e.shape[1]) / (out["step_ms"] / 1e3)
-    del model, opt, M_ui, M_iu, users, pos, neg
+    del model, opt, users, pos, neg
     torch.cuda.empty_cache()
     return out
 
@@ -136,8 +165,10 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--variant", default="v2_pop", choices=["v2_pop", "cu_fair"])
     a = ap.parse_args()
-    print(json.dumps(run(a.config, steps=a.steps, warmup=a.warmup)), flush=True)
+    print(json.dumps(run(a.config, steps=a.steps, warmup=a.warmup, variant=a.variant)),
+          flush=True)
 
 
 if __name__ == "__main__":
