@@ -60,14 +60,86 @@ def bpr_loss_value(users, pos, neg, uf, itf, ue, ie, reg, pop=None, lambda_fair=
     return out
 
 
+def _receives_dense_grad(final: torch.Tensor, weight: torch.Tensor) -> bool:
+    """True when `final` is an output of a graph node that hands `weight` (a
+    leaf) its gradient directly — the drop-in's propagate op, whose backward
+    returns a dense table for it. Eager autograd only: not while compiling
+    (dynamo traces this function) nor while a CUDA graph is being captured."""
+    if torch.compiler.is_compiling() or not torch.is_grad_enabled():
+        return False
+    plain = (torch.Tensor, torch.nn.Parameter)   # not a fake / functional tensor
+    if type(final) not in plain or type(weight) not in plain:
+        return False
+    if not weight.requires_grad or weight.grad_fn is not None:
+        return False
+    if weight.is_cuda and torch.cuda.is_current_stream_capturing():
+        return False
+    fn = final.grad_fn
+    if fn is None:
+        return False
+    return any(nf is not None and getattr(nf, "variable", None) is weight
+               for nf, _ in fn.next_functions)
+
+
+def _first_slot(ids: torch.Tensor) -> torch.Tensor:
+    """slot[b] = position of the first occurrence of ids[b] (device-only, fixed
+    shape: stable sort, segment starts by cummax)."""
+    n = ids.numel()
+    srt, perm = torch.sort(ids, stable=True)
+    pos = torch.arange(n, dtype=torch.int64, device=ids.device)
+    start = torch.ones(n, dtype=torch.bool, device=ids.device)
+    start[1:] = srt[1:] != srt[:-1]
+    head = torch.cummax(torch.where(start, pos, 0), 0).values   # sorted position of the group head
+    slot = torch.empty_like(perm)
+    slot[perm] = perm[head]
+    return slot
+
+
+def ego_grad_rows(dloss, users, pos, neg, ue, ie, reg):
+    """The ego-L2 gradient as compact rows: ([B, d] user rows, [2B, d]
+    pos-then-neg item rows) and their table row ids, for a sparse COO
+    gradient. Every occurrence of a row adds into the row of its FIRST
+    occurrence, the others stay +0.0, so each table row's sum is formed exactly
+    as in the dense path (the bbgr_bpr kernel's own atomics of the identical
+    per-occurrence values 2·reg·dloss/B · e, computed in-kernel: one launch over
+    the gathered ego rows with slot indices). A triple the kernel drops (an id
+    out of range, e.g. the sampler's -1) adds nothing, as in the dense path."""
+    B, d = users.numel(), ue.shape[1]
+    U, I = ue.shape[0], ie.shape[0]
+    valid = (users >= 0) & (users < U) & (pos >= 0) & (pos < I) & (neg >= 0) & (neg < I)
+    iu = users.clamp(0, U - 1)
+    ii = torch.cat([pos, neg]).clamp(0, I - 1)
+    su, si = _first_slot(iu), _first_slot(ii)
+    ue_c = ue.index_select(0, iu)
+    ie_c = ie.index_select(0, ii)
+    cu = torch.where(valid, su, -1)
+    gu = torch.zeros(B, d, dtype=torch.float32, device=ue.device)
+    gi = torch.zeros(2 * B, d, dtype=torch.float32, device=ue.device)
+    a = bpr_args(cu, si[:B], si[B:], ue_c, ie_c, ue_c, ie_c, reg, None, 0.0,
+                 dloss=dloss, g_ue=gu, g_ie=gi)
+    call("bbgr_bpr", ctypes.byref(a), stream_handle())
+    return gu, gi, iu, ii
+
+
 def bpr_loss(users, pos_items, neg_items, user_final, item_final, user_ego, item_ego,
              reg_weight: float, pop: torch.Tensor | None = None, lambda_fair: float = 0.0):
     """Differentiable fused BPR loss (0-d tensor): the registered operator
-    bbgr::bpr_loss (ops.py), backward bbgr::bpr_loss_backward."""
+    bbgr::bpr_loss (ops.py), backward bbgr::bpr_loss_backward.
+
+    When the final tables come straight out of a node that already returns a
+    dense gradient for the ego tables (the drop-in's propagate op, eager mode),
+    the ego-L2 gradient is handed back as a sparse COO tensor of the batch rows
+    (bbgr::bpr_loss_sparse_ego, as nn.Embedding(sparse=True) does): autograd
+    adds it into propagate's dense table in place, so no zero-filled ego table
+    is written and no dense table sum runs. `.grad` stays dense."""
     dev = user_final.device
     users, pos_items, neg_items = (_idx(t, dev) for t in (users, pos_items, neg_items))
     if not (users.numel() == pos_items.numel() == neg_items.numel()):
         raise ValueError("users, pos_items, neg_items must have equal length")
     from . import ops
-    return ops.bpr_loss(user_final, item_final, user_ego, item_ego, users, pos_items,
-                        neg_items, float(reg_weight), pop, float(lambda_fair))
+    op = ops.bpr_loss
+    if (_receives_dense_grad(user_final, user_ego)
+            and _receives_dense_grad(item_final, item_ego)):
+        op = ops.bpr_loss_sparse_ego
+    return op(user_final, item_final, user_ego, item_ego, users, pos_items,
+              neg_items, float(reg_weight), pop, float(lambda_fair))

@@ -289,3 +289,46 @@ def _bpr_bwd(ctx, gloss):
 
 
 bpr_loss.register_autograd(_bpr_bwd, setup_context=_bpr_setup)
+
+
+# -- BPR loss, ego gradient as sparse batch rows (eager drop-in step) -------------
+@custom_op("bbgr::bpr_loss_sparse_ego", mutates_args=())
+def bpr_loss_sparse_ego(uf: Tensor, itf: Tensor, ue: Tensor, ie: Tensor, users: Tensor,
+                        pos: Tensor, neg: Tensor, reg: float, pop: Optional[Tensor],
+                        lambda_fair: float) -> Tensor:
+    """bbgr::bpr_loss whose backward returns the ego-table gradients as sparse
+    COO batch rows (bpr.bpr_loss picks it only when the final tables' node
+    returns dense gradients for the same ego tables; autograd then adds the
+    rows into that dense table in place)."""
+    from .bpr import bpr_loss_value
+    _lib.require_gpu(uf)
+    return bpr_loss_value(users, pos, neg, uf.contiguous(), itf.contiguous(), ue.contiguous(),
+                          ie.contiguous(), reg, pop, lambda_fair)
+
+
+@bpr_loss_sparse_ego.register_fake
+def _(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair):
+    return uf.new_empty(())
+
+
+def _bpr_se_bwd(ctx, gloss):
+    from .bpr import bpr_args, ego_grad_rows
+    from .scatter import index_add_rows
+    uf, itf, ue, ie, users, pos, neg = ctx.saved_tensors
+    uf, itf, ue, ie = (t.contiguous() for t in (uf, itf, ue, ie))
+    B = users.numel()
+    d = gloss.to(torch.float32).contiguous().reshape(())
+    g_uf, g_if = torch.zeros_like(uf), torch.zeros_like(itf)
+    contrib = torch.empty(3 * B, uf.shape[1], dtype=torch.float32, device=uf.device)
+    a = bpr_args(users, pos, neg, uf, itf, ue, ie, ctx.reg, ctx.pop, ctx.lam, dloss=d,
+                 contrib=contrib)
+    call("bbgr_bpr", ctypes.byref(a), stream_handle())
+    index_add_rows(g_uf, users, contrib[:B])
+    index_add_rows(g_if, torch.cat([pos, neg]), contrib[B:])
+    ru, ri, iu, ii = ego_grad_rows(d, users, pos, neg, ue, ie, ctx.reg)
+    g_ue = torch.sparse_coo_tensor(iu.unsqueeze(0), ru, ue.shape)
+    g_ie = torch.sparse_coo_tensor(ii.unsqueeze(0), ri, ie.shape)
+    return g_uf, g_if, g_ue, g_ie, None, None, None, None, None, None
+
+
+bpr_loss_sparse_ego.register_autograd(_bpr_se_bwd, setup_context=_bpr_setup)

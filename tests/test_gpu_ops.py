@@ -191,3 +191,40 @@ def test_backward_op_support_masks_are_bitwise_dense(order):
     a_u, a_i = ops.propagate_backward(gU, gI, ops.pair_key(pair), K, order)
     b_u, b_i = backward(pair, gU, gI, K, order)
     assert torch.equal(a_u, b_u) and torch.equal(a_i, b_i)
+
+
+@pytest.mark.parametrize("family", ["v2", "cu"])
+def test_sparse_ego_gradient_is_bitwise_dense(family, monkeypatch):
+    """Eager drop-in step: bpr_loss picks bbgr::bpr_loss_sparse_ego (the final
+    tables come from the propagate op, which returns dense gradients for the
+    same weights); .grad stays dense and equals the dense-ego op's bit for bit,
+    with repeated users / items and a dropped triple (neg = -1)."""
+    from bbgr import bpr
+    users, pos, neg = _batch(5)
+    neg = neg.clone()
+    neg[7] = -1
+    grads = {}
+    for mode in ("sparse", "dense"):
+        if mode == "dense":
+            monkeypatch.setattr(bpr, "_receives_dense_grad", lambda *a: False)
+        m = _model(family)
+        loss = _loss(m, users, pos, neg)
+        assert ("bpr_loss_sparse_ego" in loss.grad_fn.name()) == (mode == "sparse")
+        loss.backward()
+        grads[mode] = (float(loss), [p.grad for p in m.parameters()])
+        assert all(p.grad.layout == torch.strided for p in m.parameters())
+    assert grads["sparse"][0] == grads["dense"][0]
+    for a, b in zip(grads["sparse"][1], grads["dense"][1]):
+        assert torch.equal(a, b)
+
+
+def test_sparse_ego_not_chosen_without_dense_path():
+    """bpr_loss on tables that do not come from the propagate node keeps the
+    dense ego gradient (so .grad never turns sparse)."""
+    m = _model("v2")
+    uf, itf = m.get_user_item_emb()
+    users, pos, neg = _batch(6)
+    loss = m.bpr_loss(users, pos, neg, uf.detach(), itf.detach(), 1e-4)
+    assert "sparse" not in str(loss.grad_fn.name())
+    loss.backward()
+    assert m.user_emb.weight.grad.layout == torch.strided
