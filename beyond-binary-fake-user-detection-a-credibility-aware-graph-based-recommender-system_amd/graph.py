@@ -273,6 +273,14 @@ def _degree_count(ids: torch.Tensor, n: int) -> torch.Tensor:
     return deg[:n]
 
 
+def _non_increasing(deg: torch.Tensor) -> bool:
+    """True when a degree vector never increases (one device reduction and a
+    host read, at graph build)."""
+    if deg.numel() < 2:
+        return False
+    return bool((deg[1:] <= deg[:-1]).all())
+
+
 def _relabel(ids: torch.Tensor, order: VertexOrder) -> torch.Tensor:
     out = torch.empty_like(ids)
     call("bbgr_relabel", ids.numel(), ptr(ids), ptr(order.rank), ptr(out), stream_handle())
@@ -328,9 +336,16 @@ class BipartiteGraph:
                             long_threshold=long_threshold, chunk_edges=chunk_edges)
         self.item_csr = Csr(i, u, num_items, num_users, device,
                             long_threshold=long_threshold, chunk_edges=chunk_edges)
-        ordered = vertex_order == "degree"
-        for c in (self.user_csr, self.item_csr):
-            c.cols_by_degree = c.rows_by_degree = ordered
+        if vertex_order == "degree":
+            users_ordered = items_ordered = True
+        else:
+            # ids handed over already in descending-degree order (e.g. by
+            # ingest.degree_relabel) get the same hot-prefix / streaming cache
+            # policy; it changes no value, only which loads are streamed
+            users_ordered = _non_increasing(self.user_csr.degrees())
+            items_ordered = _non_increasing(self.item_csr.degrees())
+        self.user_csr.rows_by_degree = self.item_csr.cols_by_degree = users_ordered
+        self.item_csr.rows_by_degree = self.user_csr.cols_by_degree = items_ordered
         self._scales: dict = {}
 
     def scales(self, kind: int, cred: torch.Tensor | None = None) -> Scales:

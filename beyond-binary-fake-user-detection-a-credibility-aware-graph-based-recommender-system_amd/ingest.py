@@ -81,6 +81,30 @@ def edges_to_device(edges, device):
     return to_device_i32(np.asarray(src), device), to_device_i32(np.asarray(dst), device)
 
 
+def degree_relabel(edges, num_users: int, num_items: int):
+    """Renumber users and items by descending degree (ties keep ascending id,
+    as BipartiteGraph(vertex_order="degree") orders them) once, at ingest.
+
+    Returns (edges', user_ids, item_ids): int32 [2, E] edges in the new ids,
+    and int64 maps new id -> original id (user_ids[new] = old), so tables and
+    id lists of a model trained on edges' map back with `table[argsort(ids)]`
+    / `ids[new]`. The reference's ids are arbitrary index maps built at load
+    time, so a caller that can renumber them gets the degree-order gathers
+    (hot prefix cached, cold rows streamed: BipartiteGraph detects ordered
+    ids) in the drop-in module path too (`dropin_module_step`)."""
+    src, dst = np.asarray(edges[0]), np.asarray(edges[1])
+    out, maps = [], []
+    for ids, n in ((src, num_users), (dst, num_items)):
+        if ids.size and (int(ids.min()) < 0 or int(ids.max()) >= n):
+            raise ValueError("edge index out of range")
+        old = np.argsort(-np.bincount(ids, minlength=n), kind="stable")   # new -> old
+        rank = np.empty(n, np.int64)
+        rank[old] = np.arange(n)
+        out.append(rank[ids].astype(np.int32))
+        maps.append(old.astype(np.int64))
+    return np.stack(out), maps[0], maps[1]
+
+
 def load_credibility_csv(path, num_users: int, user2idx: dict | None = None) -> np.ndarray:
     """cred[num_users] float32 in [0, 1]; users absent from the file keep 1.0."""
     cred = np.ones((num_users,), dtype=np.float32)

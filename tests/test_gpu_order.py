@@ -207,3 +207,25 @@ def test_ordered_graph_edge_cases():
     tr.step()
     sd = tr.state_dict()   # isolated users are never in a batch: untouched by the step
     np.testing.assert_array_equal(sd["user_emb.weight"][U - 40:].cpu().numpy(), u0[U - 40:])
+
+
+def test_input_order_graph_detects_degree_ordered_ids():
+    """A graph handed over already in descending-degree order (ingest.
+    degree_relabel) gets the hot-prefix / streaming policy without
+    vertex_order="degree"; per side, and only when that side is ordered."""
+    from bbgr.ingest import degree_relabel
+    U, I = 3000, 700
+    e = synthetic_edges(U, I, 30000, 11, items="zipf")
+    g = BipartiteGraph(e, U, I, DEV)
+    assert not (g.user_csr.cols_by_degree or g.item_csr.cols_by_degree
+                or g.user_csr.rows_by_degree or g.item_csr.rows_by_degree)
+    e2, _, _ = degree_relabel(e, U, I)
+    g2 = BipartiteGraph(e2, U, I, DEV)
+    assert g2.user_csr.rows_by_degree and g2.user_csr.cols_by_degree
+    assert g2.item_csr.rows_by_degree and g2.item_csr.cols_by_degree
+    g2.user_csr.hot_bytes = g2.item_csr.hot_bytes = 1 << 12
+    assert g2.user_csr.stream_from(64) > 0 and g2.item_csr.stream_from(64) > 0
+    e3 = np.stack([e[0], e2[1]]).astype(np.int32)   # items ordered, users not
+    g3 = BipartiteGraph(e3, U, I, DEV)
+    assert g3.item_csr.rows_by_degree and g3.user_csr.cols_by_degree
+    assert not (g3.user_csr.rows_by_degree or g3.item_csr.cols_by_degree)

@@ -64,3 +64,25 @@ def test_credibility_npy(tmp_path):
     np.testing.assert_allclose(ingest.load_credibility_npy(tmp_path / "c.npy", 3), [0.5, 1, 0])
     with pytest.raises(ValueError):
         ingest.load_credibility_npy(tmp_path / "c.npy", 4)
+
+
+def test_degree_relabel_orders_and_maps_back():
+    """ingest.degree_relabel: degrees non-increasing in the new ids, ties by
+    ascending original id, the maps invert the renumbering, and the edge
+    multiset is the original one under the maps."""
+    U, I = 300, 120
+    e = synthetic_edges(U, I, 4000, 7, items="zipf")
+    e2, uid, iid = ingest.degree_relabel(e, U, I)
+    assert e2.dtype == np.int32 and e2.shape == e.shape
+    du = np.bincount(e2[0], minlength=U)
+    di = np.bincount(e2[1], minlength=I)
+    assert (np.diff(du) <= 0).all() and (np.diff(di) <= 0).all()
+    np.testing.assert_array_equal(uid[e2[0]], e[0])
+    np.testing.assert_array_equal(iid[e2[1]], e[1])
+    assert sorted(uid.tolist()) == list(range(U)) and sorted(iid.tolist()) == list(range(I))
+    d0 = np.bincount(e[0], minlength=U)
+    for a in range(U - 1):   # equal degrees keep ascending original ids
+        if d0[uid[a]] == d0[uid[a + 1]]:
+            assert uid[a] < uid[a + 1]
+    with pytest.raises(ValueError):
+        ingest.degree_relabel(e, U - 1, I)

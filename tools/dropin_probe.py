@@ -35,26 +35,14 @@ def timed(fn, steps: int) -> float:
     return 1000.0 * (time.perf_counter() - t0) / steps
 
 
-def degree_relabel(e, U: int, I: int):
-    """The edge list with users and items renumbered by descending degree
-    (stable): what a graph handed over already in degree order looks like."""
-    import numpy as np
-    out = []
-    for row, n in ((np.asarray(e[0]), U), (np.asarray(e[1]), I)):
-        order = np.argsort(-np.bincount(row, minlength=n), kind="stable")
-        rank = np.empty(n, np.int64)
-        rank[order] = np.arange(n)
-        out.append(rank[row].astype(np.int32))
-    return np.stack(out)
-
-
 def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
         adam: str = "foreach", device=None, pre_ordered: bool = False) -> dict:
     c = CONFIGS[cfg_name]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
     e = config_edges(cfg_name) if edges is None else edges
-    if pre_ordered:
-        e = degree_relabel(e, U, I)
+    if pre_ordered:   # ids renumbered once at ingest (the graph detects the order)
+        from bbgr.ingest import degree_relabel
+        e = degree_relabel(e, U, I)[0]
     if cred_np is None:
         cred_np = synthetic_credibility(U, CONFIG_SEED[cfg_name])
     cred = torch.as_tensor(cred_np)
@@ -62,9 +50,8 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
     t0 = time.perf_counter()
     M_ui, M_iu = V2.build_message_passing_mats(e, U, I, cred, dev)
     model = V2.LightGCN(U, I, d, K, M_ui, M_iu).to(dev)
-    if pre_ordered:   # ids are degree ranks: enable the hot-prefix / streaming policy
-        for csr in (M_ui.graph.user_csr, M_ui.graph.item_csr):
-            csr.cols_by_degree = csr.rows_by_degree = True
+    if pre_ordered:
+        assert M_ui.graph.user_csr.cols_by_degree and M_ui.graph.item_csr.cols_by_degree
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
     if adam == "bbgr":   # bbgr.optim.FusedAdam (bbgr_adam per parameter)
