@@ -86,9 +86,9 @@ def degree_relabel(edges, num_users: int, num_items: int):
     as BipartiteGraph(vertex_order="degree") orders them) once, at ingest.
 
     Returns (edges', user_ids, item_ids): int32 [2, E] edges in the new ids,
-    and int64 maps new id -> original id (user_ids[new] = old), so tables and
-    id lists of a model trained on edges' map back with `table[argsort(ids)]`
-    / `ids[new]`. The reference's ids are arbitrary index maps built at load
+    and int64 maps new id -> original id (user_ids[new] = old). Per-vertex
+    inputs follow as `cred[user_ids]`; tables and id lists of a model trained
+    on edges' map back with `table[argsort(user_ids)]` / `user_ids[new]`. The reference's ids are arbitrary index maps built at load
     time, so a caller that can renumber them gets the degree-order gathers
     (hot prefix cached, cold rows streamed: BipartiteGraph detects ordered
     ids) in the drop-in module path too (`dropin_module_step`)."""
