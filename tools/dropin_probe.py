@@ -17,6 +17,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -36,13 +37,17 @@ def timed(fn, steps: int) -> float:
 
 
 def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
-        adam: str = "foreach", device=None, pre_ordered: bool = False) -> dict:
+        adam: str = "foreach", device=None, pre_ordered: bool = False,
+        items_ordered: bool = False) -> dict:
     c = CONFIGS[cfg_name]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
     e = config_edges(cfg_name) if edges is None else edges
     if pre_ordered:   # ids renumbered once at ingest (the graph detects the order)
         from bbgr.ingest import degree_relabel
         e = degree_relabel(e, U, I)[0]
+    elif items_ordered:   # only the item ids renumbered by degree
+        from bbgr.ingest import degree_relabel
+        e = np.stack([np.asarray(e[0]), degree_relabel(e, U, I)[0][1]]).astype(np.int32)
     if cred_np is None:
         cred_np = synthetic_credibility(U, CONFIG_SEED[cfg_name])
     cred = torch.as_tensor(cred_np)
@@ -85,6 +90,7 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
     for _ in range(warmup):
         step()
     out = {"config": cfg_name, "adam": adam, "pre_ordered": pre_ordered,
+           "items_ordered": items_ordered,
            "setup_s": setup_s, "steps": steps,
            "step_ms": timed(step, steps), "forward_ms": timed(fwd, steps),
            "forward_backward_ms": timed(fwd_bwd, steps)}
@@ -103,9 +109,12 @@ def main():
     ap.add_argument("--adam", default="foreach", choices=["foreach", "fused", "bbgr"])
     ap.add_argument("--pre-ordered", action="store_true",
                     help="hand the model an edge list already in descending-degree order")
+    ap.add_argument("--items-ordered", action="store_true",
+                    help="only the item ids handed over in descending-degree order")
     a = ap.parse_args()
     print(json.dumps(run(a.config, steps=a.steps, warmup=a.warmup, adam=a.adam,
-                         pre_ordered=a.pre_ordered)), flush=True)
+                         pre_ordered=a.pre_ordered, items_ordered=a.items_ordered)),
+          flush=True)
 
 
 if __name__ == "__main__":
