@@ -229,3 +229,40 @@ def test_input_order_graph_detects_degree_ordered_ids():
     g3 = BipartiteGraph(e3, U, I, DEV)
     assert g3.item_csr.rows_by_degree and g3.user_csr.cols_by_degree
     assert not (g3.user_csr.rows_by_degree or g3.item_csr.cols_by_degree)
+
+
+def test_dropin_on_degree_relabelled_ids_matches_original():
+    """The drop-in model on ingest.degree_relabel'd ids (weights and
+    credibility permuted alike) gives the original model's final tables and
+    weight gradients, rows mapped back (fp32 rounding: the neighbour order
+    inside a row follows the ids)."""
+    from bbgr import lightgcn_cu_pop as V2
+    from bbgr.ingest import degree_relabel
+    U, I, d, K = 3000, 700, 64, 3
+    e = synthetic_edges(U, I, 30000, 11, items="zipf")
+    cred = torch.as_tensor(synthetic_credibility(U, 3))
+    e2, uid, iid = degree_relabel(e, U, I)
+    uid_t, iid_t = torch.as_tensor(uid, device=DEV), torch.as_tensor(iid, device=DEV)
+    a = V2.LightGCN(U, I, d, K, *V2.build_message_passing_mats(e, U, I, cred, DEV)).to(DEV)
+    b = V2.LightGCN(U, I, d, K, *V2.build_message_passing_mats(
+        e2, U, I, cred[torch.as_tensor(uid)], DEV)).to(DEV)
+    assert b.M_ui.graph.user_csr.cols_by_degree and b.M_ui.graph.user_csr.rows_by_degree
+    with torch.no_grad():
+        b.user_emb.weight.copy_(a.user_emb.weight[uid_t])
+        b.item_emb.weight.copy_(a.item_emb.weight[iid_t])
+    g = torch.Generator().manual_seed(2)
+    users = torch.randint(0, U, (256,), generator=g).to(DEV)
+    pos = torch.randint(0, I, (256,), generator=g).to(DEV)
+    neg = torch.randint(0, I, (256,), generator=g).to(DEV)
+    ru = torch.argsort(uid_t)   # original id -> new id
+    ri = torch.argsort(iid_t)
+    def rel(x, y):
+        return float((x - y).detach().norm() / y.detach().norm())
+
+    ua, ia = a.get_user_item_emb()
+    ub, ib = b.get_user_item_emb()
+    assert rel(ub[ru], ua) < 1e-6 and rel(ib[ri], ia) < 1e-6
+    a.bpr_loss(users, pos, neg, ua, ia, 1e-4).backward()
+    b.bpr_loss(ru[users], ri[pos], ri[neg], ub, ib, 1e-4).backward()
+    assert rel(b.user_emb.weight.grad[ru], a.user_emb.weight.grad) < 1e-6
+    assert rel(b.item_emb.weight.grad[ri], a.item_emb.weight.grad) < 1e-6
