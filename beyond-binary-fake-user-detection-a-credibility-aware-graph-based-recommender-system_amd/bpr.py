@@ -95,6 +95,13 @@ def _first_slot(ids: torch.Tensor) -> torch.Tensor:
     return slot
 
 
+def _from_propagate_op(final: torch.Tensor) -> bool:
+    """`final` is an output of bbgr::propagate itself, whose backward takes a
+    sparse dL/d(u_final) (ops.propagate_backward_rows)."""
+    fn = final.grad_fn
+    return fn is not None and type(fn).__name__ == "GeneratedBackwardFor_bbgr_propagate_defaultBackward"
+
+
 def ego_grad_rows(dloss, users, pos, neg, ue, ie, reg):
     """The ego-L2 gradient as compact rows: ([B, d] user rows, [2B, d]
     pos-then-neg item rows) and their table row ids, for a sparse COO
@@ -137,9 +144,9 @@ def bpr_loss(users, pos_items, neg_items, user_final, item_final, user_ego, item
     if not (users.numel() == pos_items.numel() == neg_items.numel()):
         raise ValueError("users, pos_items, neg_items must have equal length")
     from . import ops
-    op = ops.bpr_loss
+    args = (user_final, item_final, user_ego, item_ego, users, pos_items, neg_items,
+            float(reg_weight), pop, float(lambda_fair))
     if (_receives_dense_grad(user_final, user_ego)
             and _receives_dense_grad(item_final, item_ego)):
-        op = ops.bpr_loss_sparse_ego
-    return op(user_final, item_final, user_ego, item_ego, users, pos_items,
-              neg_items, float(reg_weight), pop, float(lambda_fair))
+        return ops.bpr_loss_sparse_ego(*args, _from_propagate_op(user_final))
+    return ops.bpr_loss(*args)

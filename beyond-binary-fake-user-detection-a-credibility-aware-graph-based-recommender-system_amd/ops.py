@@ -115,8 +115,58 @@ def _propagate_setup(ctx, inputs, output):
     ctx.shapes = (u0.shape, i0.shape)
 
 
+@custom_op("bbgr::propagate_backward_rows", mutates_args=())
+def propagate_backward_rows(iu: Tensor, vu: Tensor, gI: Tensor, num_users: int, pair_key: int,
+                            num_layers: int, order: str) -> tuple[Tensor, Tensor]:
+    """propagate_backward with dL/d(u_final) given as rows: vu[k] adds to user
+    iu[k] (a sparse COO gradient's indices and values, e.g. a BPR batch). The
+    dense gU is formed on the listed rows only (zeroed, then the rows summed in
+    ascending k — bbgr_scatter_add_rows, as the dense BPR backward forms them)
+    and the masks come from the list (bbgr_mark_rows / bbgr_mark_neighbors)
+    instead of a pass over a zero-filled table: every read of gU in the
+    backward chain is masked to those rows, so the rest is never touched.
+    The masks are a superset of the value-derived ones: bitwise the same."""
+    from .propagate import ORDER_GS, backward
+    from .scatter import index_add_rows
+    _lib.require_gpu(vu)
+    pair = _pair(pair_key)
+    U, I, d = pair.num_users, pair.num_items, vu.shape[1]
+    if num_users != U:
+        raise ValueError("propagate_backward_rows: num_users does not match the operator pair")
+    st = stream_handle()
+    iu = iu.to(torch.int64).contiguous()
+    gI = gI.contiguous()
+    gU = torch.empty(max(U, 1), d, dtype=torch.float32, device=vu.device)[:U]
+    gU.index_fill_(0, iu, 0.0)
+    index_add_rows(gU, iu, vu.contiguous())
+    mu = torch.zeros(max(U, 1), dtype=torch.uint8, device=vu.device)
+    mi = torch.empty(max(I, 1), dtype=torch.uint8, device=vu.device)
+    call("bbgr_mark_rows", iu.numel(), _lib.ptr(iu), 1, _lib.ptr(mu), U, st)
+    call("bbgr_row_support", I, d, _lib.ptr(gI), _lib.ld(gI), _lib.ptr(mi), None, None, None, st)
+    if order == ORDER_GS:   # the first item product's output support: N(listed users)
+        uc = pair.fwd_user.csr
+        call("bbgr_mark_neighbors", iu.numel(), _lib.ptr(iu), _lib.ptr(uc.indptr),
+             _lib.ptr(uc.indices), 1, _lib.ptr(mi), st)
+    return backward(pair, gU, gI, num_layers, order, grad_support=(mu[:U], mi[:I]))
+
+
+@propagate_backward_rows.register_fake
+def _(iu, vu, gI, num_users, pair_key, num_layers, order):
+    return vu.new_empty((num_users, vu.shape[1])), gI.new_empty(gI.shape)
+
+
 def _propagate_bwd(ctx, gU, gI):
     (su, si) = ctx.shapes
+    if gU is not None and gU.layout == torch.sparse_coo and (gI is None or not gI.is_sparse):
+        # BPR-shaped gradient handed over as rows (bbgr::bpr_loss_sparse_ego)
+        gI = gU._values().new_zeros(si) if gI is None else gI
+        gu0, gi0 = propagate_backward_rows(gU._indices()[0], gU._values(), gI, su[0],
+                                           ctx.key, ctx.K, ctx.order)
+        return gu0, gi0, None, None, None
+    if gU is not None and gU.is_sparse:
+        gU = gU.to_dense()
+    if gI is not None and gI.is_sparse:
+        gI = gI.to_dense()
     ref = gU if gU is not None else gI
     if gU is None:
         gU = ref.new_zeros(su)
@@ -295,11 +345,13 @@ bpr_loss.register_autograd(_bpr_bwd, setup_context=_bpr_setup)
 @custom_op("bbgr::bpr_loss_sparse_ego", mutates_args=())
 def bpr_loss_sparse_ego(uf: Tensor, itf: Tensor, ue: Tensor, ie: Tensor, users: Tensor,
                         pos: Tensor, neg: Tensor, reg: float, pop: Optional[Tensor],
-                        lambda_fair: float) -> Tensor:
+                        lambda_fair: float, sparse_uf: bool) -> Tensor:
     """bbgr::bpr_loss whose backward returns the ego-table gradients as sparse
     COO batch rows (bpr.bpr_loss picks it only when the final tables' node
     returns dense gradients for the same ego tables; autograd then adds the
-    rows into that dense table in place)."""
+    rows into that dense table in place). `sparse_uf` (uf is bbgr::propagate's
+    output): dL/d(uf) goes back as sparse batch rows too, which propagate's
+    backward consumes without a zero-filled table (propagate_backward_rows)."""
     from .bpr import bpr_loss_value
     _lib.require_gpu(uf)
     return bpr_loss_value(users, pos, neg, uf.contiguous(), itf.contiguous(), ue.contiguous(),
@@ -307,8 +359,13 @@ def bpr_loss_sparse_ego(uf: Tensor, itf: Tensor, ue: Tensor, ie: Tensor, users: 
 
 
 @bpr_loss_sparse_ego.register_fake
-def _(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair):
+def _(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair, sparse_uf):
     return uf.new_empty(())
+
+
+def _bpr_se_setup(ctx, inputs, output):
+    _bpr_setup(ctx, inputs[:10], output)
+    ctx.sparse_uf = inputs[10]
 
 
 def _bpr_se_bwd(ctx, gloss):
@@ -318,17 +375,22 @@ def _bpr_se_bwd(ctx, gloss):
     uf, itf, ue, ie = (t.contiguous() for t in (uf, itf, ue, ie))
     B = users.numel()
     d = gloss.to(torch.float32).contiguous().reshape(())
-    g_uf, g_if = torch.zeros_like(uf), torch.zeros_like(itf)
     contrib = torch.empty(3 * B, uf.shape[1], dtype=torch.float32, device=uf.device)
     a = bpr_args(users, pos, neg, uf, itf, ue, ie, ctx.reg, ctx.pop, ctx.lam, dloss=d,
                  contrib=contrib)
     call("bbgr_bpr", ctypes.byref(a), stream_handle())
-    index_add_rows(g_uf, users, contrib[:B])
+    g_if = torch.zeros_like(itf)
     index_add_rows(g_if, torch.cat([pos, neg]), contrib[B:])
     ru, ri, iu, ii = ego_grad_rows(d, users, pos, neg, ue, ie, ctx.reg)
+    if ctx.sparse_uf:   # rows for bbgr::propagate's backward (propagate_backward_rows);
+        # a dropped triple's row is +0.0 (the kernel zeroes it), so clamped ids add nothing
+        g_uf = torch.sparse_coo_tensor(iu.unsqueeze(0), contrib[:B], uf.shape)
+    else:
+        g_uf = torch.zeros_like(uf)
+        index_add_rows(g_uf, users, contrib[:B])
     g_ue = torch.sparse_coo_tensor(iu.unsqueeze(0), ru, ue.shape)
     g_ie = torch.sparse_coo_tensor(ii.unsqueeze(0), ri, ie.shape)
-    return g_uf, g_if, g_ue, g_ie, None, None, None, None, None, None
+    return g_uf, g_if, g_ue, g_ie, None, None, None, None, None, None, None
 
 
-bpr_loss_sparse_ego.register_autograd(_bpr_se_bwd, setup_context=_bpr_setup)
+bpr_loss_sparse_ego.register_autograd(_bpr_se_bwd, setup_context=_bpr_se_setup)

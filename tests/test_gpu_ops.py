@@ -197,20 +197,29 @@ def test_backward_op_support_masks_are_bitwise_dense(order):
 def test_sparse_ego_gradient_is_bitwise_dense(family, monkeypatch):
     """Eager drop-in step: bpr_loss picks bbgr::bpr_loss_sparse_ego (the final
     tables come from the propagate op, which returns dense gradients for the
-    same weights); .grad stays dense and equals the dense-ego op's bit for bit,
-    with repeated users / items and a dropped triple (neg = -1)."""
-    from bbgr import bpr
+    same weights), whose backward hands the ego gradient and dL/d(u_final) back
+    as sparse rows (propagate_backward_rows); .grad stays dense and equals the
+    dense op's bit for bit, with repeated users / items and a dropped triple
+    (neg = -1)."""
+    from bbgr import bpr, ops
     users, pos, neg = _batch(5)
     neg = neg.clone()
     neg[7] = -1
     grads = {}
+    rows_calls = []
+    real_rows = ops.propagate_backward_rows
+    monkeypatch.setattr(ops, "propagate_backward_rows",
+                        lambda *a: rows_calls.append(1) or real_rows(*a))
     for mode in ("sparse", "dense"):
         if mode == "dense":
             monkeypatch.setattr(bpr, "_receives_dense_grad", lambda *a: False)
         m = _model(family)
         loss = _loss(m, users, pos, neg)
         assert ("bpr_loss_sparse_ego" in loss.grad_fn.name()) == (mode == "sparse")
+        n0 = len(rows_calls)
         loss.backward()
+        # sparse mode: dL/d(u_final) reaches propagate's backward as rows too
+        assert len(rows_calls) - n0 == (1 if mode == "sparse" else 0)
         grads[mode] = (float(loss), [p.grad for p in m.parameters()])
         assert all(p.grad.layout == torch.strided for p in m.parameters())
     assert grads["sparse"][0] == grads["dense"][0]
