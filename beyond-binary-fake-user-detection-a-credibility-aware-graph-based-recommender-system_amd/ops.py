@@ -15,6 +15,10 @@ on torch's current stream).
   bbgr::bpr_loss(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair) -> loss
   bbgr::bpr_loss_backward(dloss, uf, itf, ue, ie, users, pos, neg, reg, pop,
                           lambda_fair) -> (g_uf, g_if, g_ue, g_ie)
+  bbgr::bpr_loss_sparse_ego(..., sparse_uf) -> loss   (eager drop-in step: the
+      ego gradients, and with sparse_uf dL/d(u_final), go back as sparse rows)
+  bbgr::propagate_backward_rows(iu, vu, gI, num_users, pair_key, num_layers,
+                                order) -> (grad_u0, grad_i0)   (gU given as rows)
 
 The sparse operators are not tensors: an OperatorPair is registered once
 (`pair_key`) and the ops look it up; shapes for the fake kernels come from
