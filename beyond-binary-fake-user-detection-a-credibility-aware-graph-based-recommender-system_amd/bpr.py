@@ -61,10 +61,13 @@ def bpr_loss_value(users, pos, neg, uf, itf, ue, ie, reg, pop=None, lambda_fair=
 
 
 def _receives_dense_grad(final: torch.Tensor, weight: torch.Tensor) -> bool:
-    """True when `final` is an output of a graph node that hands `weight` (a
-    leaf) its gradient directly — the drop-in's propagate op, whose backward
-    returns a dense table for it. Eager autograd only: not while compiling
-    (dynamo traces this function) nor while a CUDA graph is being captured."""
+    """True when `final` is an output of the drop-in's propagate op
+    (bbgr::propagate, whose backward returns a dense table) and that node hands
+    `weight` (a leaf) its gradient directly. Any other node — an Add, an
+    nn.Embedding(sparse=True) lookup — may return a sparse gradient, which with
+    the sparse ego rows would leave .grad sparse: not accepted.
+    Eager autograd only: not while compiling (dynamo traces this function) nor
+    while a CUDA graph is being captured."""
     if torch.compiler.is_compiling() or not torch.is_grad_enabled():
         return False
     plain = (torch.Tensor, torch.nn.Parameter)   # not a fake / functional tensor
@@ -75,7 +78,7 @@ def _receives_dense_grad(final: torch.Tensor, weight: torch.Tensor) -> bool:
     if weight.is_cuda and torch.cuda.is_current_stream_capturing():
         return False
     fn = final.grad_fn
-    if fn is None:
+    if fn is None or not _from_propagate_op(final):
         return False
     return any(nf is not None and getattr(nf, "variable", None) is weight
                for nf, _ in fn.next_functions)
@@ -95,11 +98,15 @@ def _first_slot(ids: torch.Tensor) -> torch.Tensor:
     return slot
 
 
+# autograd node types whose backward returns dense gradients for their leaf
+# inputs and takes a sparse dL/d(u_final) (ops.propagate_backward_rows)
+PROPAGATE_NODES = {"GeneratedBackwardFor_bbgr_propagate_defaultBackward"}
+
+
 def _from_propagate_op(final: torch.Tensor) -> bool:
-    """`final` is an output of bbgr::propagate itself, whose backward takes a
-    sparse dL/d(u_final) (ops.propagate_backward_rows)."""
+    """`final` is an output of bbgr::propagate itself."""
     fn = final.grad_fn
-    return fn is not None and type(fn).__name__ == "GeneratedBackwardFor_bbgr_propagate_defaultBackward"
+    return fn is not None and type(fn).__name__ in PROPAGATE_NODES
 
 
 def ego_grad_rows(dloss, users, pos, neg, ue, ie, reg):
@@ -148,5 +155,5 @@ def bpr_loss(users, pos_items, neg_items, user_final, item_final, user_ego, item
             float(reg_weight), pop, float(lambda_fair))
     if (_receives_dense_grad(user_final, user_ego)
             and _receives_dense_grad(item_final, item_ego)):
-        return ops.bpr_loss_sparse_ego(*args, _from_propagate_op(user_final))
+        return ops.bpr_loss_sparse_ego(*args, True)
     return ops.bpr_loss(*args)

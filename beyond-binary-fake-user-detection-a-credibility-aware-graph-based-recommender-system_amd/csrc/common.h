@@ -124,4 +124,14 @@ __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v,
   p = fmaf(-c.step, m / denom, p);             // p - lr/bc1 * m / denom
 }
 
+// Device step state {t, counter, next counter, table length} (bbgr_step_begin):
+// the step t clamped into the bias-correction table [1, state[3]]. Exact: in
+// fp32 both 1 - beta1^t and sqrt(1 - beta2^t) reach 1.0f long before any table
+// length the host builds (2^20 steps), so every t past the end reads the same
+// constants its own entry would hold; a replayed graph can never read past it.
+__device__ __forceinline__ long clamp_step(const long *state) {
+  const long t = state[0], n = state[3];
+  return t < 1 ? 1 : (t > n ? n : t);
+}
+
 }  // namespace bbgr

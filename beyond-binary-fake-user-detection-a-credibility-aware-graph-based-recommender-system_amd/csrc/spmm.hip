@@ -478,7 +478,7 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
 __device__ __forceinline__ AdamConsts launch_adam_consts(const SpmmParams &P) {
   AdamConsts c = P.adam;
   if (P.adam_state) {
-    const long t = P.adam_state[0];
+    const long t = clamp_step(P.adam_state);
     c.step = P.adam_lr / P.adam_bc[2 * (t - 1)];
     c.bc2s = P.adam_bc[2 * (t - 1) + 1];
   }

@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void bpr_reduce_kernel(long batch,
 __device__ __forceinline__ AdamConsts device_step_consts(AdamConsts c, float lr,
                                                          const float *bc, const long *state) {
   if (state) {
-    const long t = state[0];
+    const long t = clamp_step(state);
     c.step = lr / bc[2 * (t - 1)];
     c.bc2s = bc[2 * (t - 1) + 1];
   }

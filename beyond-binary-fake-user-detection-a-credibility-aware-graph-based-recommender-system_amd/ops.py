@@ -140,8 +140,12 @@ def propagate_backward_rows(iu: Tensor, vu: Tensor, gI: Tensor, num_users: int, 
     st = stream_handle()
     iu = iu.to(torch.int64).contiguous()
     gI = gI.contiguous()
-    gU = torch.empty(max(U, 1), d, dtype=torch.float32, device=vu.device)[:U]
-    gU.index_fill_(0, iu, 0.0)
+    if num_layers == 0:   # K = 0: backward copies gU whole (grad_u0 = gU), so no
+        # row may stay uninitialised
+        gU = torch.zeros(max(U, 1), d, dtype=torch.float32, device=vu.device)[:U]
+    else:   # every read of gU in the K >= 1 chain is masked to the listed rows
+        gU = torch.empty(max(U, 1), d, dtype=torch.float32, device=vu.device)[:U]
+        gU.index_fill_(0, iu, 0.0)
     index_add_rows(gU, iu, vu.contiguous())
     mu = torch.zeros(max(U, 1), dtype=torch.uint8, device=vu.device)
     mi = torch.empty(max(I, 1), dtype=torch.uint8, device=vu.device)

@@ -28,17 +28,34 @@ def bias_corrections(n: int, beta1: float = 0.9, beta2: float = 0.999) -> np.nda
     return bc.astype(np.float32)
 
 
+def exact_table_steps(beta1: float = 0.9, beta2: float = 0.999) -> int:
+    """A bias-correction table length past whose end every step's fp32
+    constants are exactly (1.0f, 1.0f): beta^t < 2^-25 for both betas makes
+    1 - beta1^t and sqrt(1 - beta2^t) round to 1.0f (0.9 / 0.999: ~17k steps).
+    The kernels clamp t to the table's end, so a table at least this long
+    holds every step's constants (tests/test_oracle.py checks it)."""
+    n = 1
+    for b in (beta1, beta2):
+        if 0.0 < b < 1.0:
+            n = max(n, int(math.ceil(-25.0 * math.log(2.0) / math.log(b))) + 1)
+    return n
+
+
 class DeviceStepState:
     """Device-resident step scalars of a graph-captured training step
-    (include/bbgr.h, bbgr_step_begin): state = int64 {t, counter, next counter}
-    and the bias-correction table bc[t-1] = (1 - beta1^t, sqrt(1 - beta2^t)),
-    computed here in double exactly as the host path does (then float)."""
+    (include/bbgr.h, bbgr_step_begin): state = int64 {t, counter, next counter,
+    table length} and the bias-correction table bc[t-1] = (1 - beta1^t,
+    sqrt(1 - beta2^t)), computed here in double exactly as the host path does
+    (then float). The kernels clamp t to the table (exact past its end)."""
 
     def __init__(self, device, step: int, counter: int, max_steps: int = 1 << 20,
                  beta1: float = 0.9, beta2: float = 0.999):
-        self.max_steps = int(max_steps)
+        # at least exact_table_steps() entries, so the kernels' clamp of t to
+        # the table end is exact (every later step's corrections round to 1.0f)
+        self.max_steps = max(int(max_steps), exact_table_steps(beta1, beta2))
         self.beta1, self.beta2 = beta1, beta2
-        self.state = torch.tensor([step, counter - 1, counter], dtype=torch.int64, device=device)
+        self.state = torch.tensor([step, counter - 1, counter, self.max_steps],
+                                  dtype=torch.int64, device=device)
         self.bc_table = torch.from_numpy(bias_corrections(self.max_steps, beta1, beta2)).to(device)
 
     def begin(self) -> None:

@@ -67,22 +67,27 @@ class Product:
     def workspace(self, d: int):
         """Split-row partials and arrival counters, one set per (width, stream):
         launches on two streams (column chains) must not share counters. A
-        graph capture uses the default stream's set (see below)."""
+        graph capture gets a set of its own, so a replay on any stream never
+        races eager launches over shared counters: prepared before
+        capture by `prepare_graph` (GraphedStep), else allocated inside the
+        capture (its zero fill is then part of the graph, re-run per replay)."""
         if self.csr.n_split == 0:
             return None
         dev = self.csr.device
-        stream = torch.cuda.current_stream(dev)
         if torch.cuda.is_current_stream_capturing():
-            # a captured step (GraphedStep) replays on its caller's stream, in
-            # order with that stream's eager launches: it shares their buffer
-            # rather than allocating (and zero-filling on every replay) its own
-            stream = torch.cuda.default_stream(dev)
-        key = (d, stream.cuda_stream)
+            key = (d, "graph")
+        else:
+            key = (d, torch.cuda.current_stream(dev).cuda_stream)
         w = self.partial.get(key)
         if w is None:
             w = self.csr.partial_workspace(d)
             self.partial[key] = w
         return w
+
+    def prepare_graph(self, d: int) -> None:
+        """Allocate the captured launches' workspace (call outside capture)."""
+        if self.csr.n_split and (d, "graph") not in self.partial:
+            self.partial[(d, "graph")] = self.csr.partial_workspace(d)
 
 
 class OperatorPair:
@@ -99,6 +104,11 @@ class OperatorPair:
         # feed vectors: output scale of a product x input scale of the next one
         self.feed_fwd_iu, self.feed_fwd_ui = feed_fwd_iu, feed_fwd_ui
         self.feed_bwd_iu, self.feed_bwd_ui = feed_bwd_iu, feed_bwd_ui
+
+    def prepare_graph(self, d: int) -> None:
+        """Workspaces of a graph capture of this pair's products (width d)."""
+        for p in (self.fwd_item, self.fwd_user, self.bwd_item, self.bwd_user):
+            p.prepare_graph(d)
 
     @classmethod
     def factored(cls, graph: BipartiteGraph, sc: Scales) -> "OperatorPair":

@@ -178,9 +178,7 @@ class FusedTrainer:
     def _step(self, users: torch.Tensor, listed: bool) -> torch.Tensor:
         """The step on internal user ids (`listed`: no repeated user). Issues
         device work only, so it can be captured (GraphedStep)."""
-        if self.dev_state is not None:
-            if self.step_count + 1 > self.dev_state.max_steps:
-                raise RuntimeError("device step state: bias-correction table exhausted")
+        if self.dev_state is not None:   # (the kernels clamp t to the exact table)
             self.dev_state.begin()
         self._last_users = users
         B = users.numel()
@@ -357,6 +355,7 @@ class GraphedStep:
         host = (trainer.step_count, trainer.sampler.counter)
         # the graph records the launches of THIS configuration
         self._captured = (trainer.frontier, trainer.fuse_adam, trainer.B)
+        trainer.pair.prepare_graph(trainer.d)   # the graph's own split-row workspaces
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):

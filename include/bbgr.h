@@ -371,15 +371,17 @@ int bbgr_adam(int64_t n, float *param, const float *grad, float *exp_avg,
 /* Device-resident step state (graph-captured training steps)                 */
 /*   A training step captured once into a hipGraph (torch.cuda.CUDAGraph) and */
 /*   replayed must not bake the host's per-step scalars into kernel args.     */
-/*   state[3] int64 on the device: state[0] = Adam step t, state[1] = this    */
-/*   step's sampler counter, state[2] = the next one. bbgr_step_begin (one    */
-/*   lane): t += 1; state[1] = state[2]; state[2] += 1 -- the same sequence   */
-/*   the host keeps for an eager step (counter used, then incremented).       */
+/*   state[4] int64 on the device: state[0] = Adam step t, state[1] = this    */
+/*   step's sampler counter, state[2] = the next one, state[3] = the number   */
+/*   of steps bc_table holds (>= 1). bbgr_step_begin (one lane): t += 1;      */
+/*   state[1] = state[2]; state[2] += 1 -- the same sequence the host keeps   */
+/*   for an eager step (counter used, then incremented).                      */
 /*   bc_table[2(t-1)] = 1 - beta1^t, bc_table[2(t-1)+1] = sqrt(1 - beta2^t),  */
 /*   computed on the host in double as torch does, rounded to float: the     */
 /*   device constants are then bit-identical to the host ones.               */
 /*   bbgr_adam_dev / bbgr_sample_dev: bbgr_adam / bbgr_sample with t and the  */
-/*   counter read from state (t must not exceed the table's length).          */
+/*   counter read from state. Every reader clamps t to [1, state[3]]: a table */
+/*   of >= ~20k steps is exact past its end (both corrections are 1.0f).      */
 /* ------------------------------------------------------------------------- */
 int bbgr_step_begin(int64_t *state, bbgr_stream_t stream);
 int bbgr_adam_dev(int64_t n, float *param, const float *grad, float *exp_avg,

@@ -2,10 +2,12 @@
 
 bpr._receives_dense_grad decides from the autograd graph alone (no kernels),
 so it is checked here on CPU with a stand-in two-output op shaped like
-bbgr::propagate: the sparse form is chosen only when the final tables come
-straight out of a node that also returns a dense gradient for the same leaf
-weights, never for detached / derived tables, under no_grad, or while
-dynamo compiles."""
+bbgr::propagate (registered as a propagate node for these tests): the sparse
+form is chosen only when the final tables come straight out of that node and
+it also returns a dense gradient for the same leaf weights, never for
+detached / derived tables, other nodes with a direct edge to the weight
+(ADVICE r2), under no_grad, or while dynamo compiles."""
+import pytest
 import torch
 from torch.library import custom_op
 
@@ -26,6 +28,12 @@ two_tables.register_autograd(lambda ctx, gu, gi: (gu * 2, gi * 3),
                              setup_context=lambda ctx, inputs, output: None)
 
 
+@pytest.fixture(autouse=True)
+def _stand_in_is_a_propagate_node(monkeypatch):
+    monkeypatch.setattr(bpr, "PROPAGATE_NODES", bpr.PROPAGATE_NODES |
+                        {"GeneratedBackwardFor_bbgr_test_two_tables_defaultBackward"})
+
+
 def _weights():
     return torch.nn.Embedding(6, 4).weight, torch.nn.Embedding(5, 4).weight
 
@@ -41,6 +49,7 @@ def test_other_tables_keep_the_dense_form():
     uf, itf = two_tables(wu, wi)
     assert not bpr._receives_dense_grad(uf.detach(), wu)      # no graph
     assert not bpr._receives_dense_grad(uf * 1.0, wu)         # a derived table
+    assert not bpr._receives_dense_grad(wu + uf.detach(), wu)  # Add with a leaf edge
     other, _ = _weights()
     assert not bpr._receives_dense_grad(two_tables(other, wi)[0], wu)
     with torch.no_grad():

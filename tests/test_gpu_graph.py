@@ -50,7 +50,7 @@ def test_device_state_eager_matches_host_scalars(variant, fuse):
         assert float(a.step()) == float(b.step())
     _assert_same(a, b)
     st = b.dev_state.state.cpu().tolist()
-    assert st == [4, 3, 4]          # t, this step's counter, next counter
+    assert st == [4, 3, 4, b.dev_state.max_steps]   # t, this counter, next counter, table
 
 
 @pytest.mark.parametrize("variant,fuse,frontier", [("v2_pop", True, True),

@@ -25,21 +25,21 @@ DEV = "cuda"
 U, I, E, D, K, B = 1500, 700, 20000, 64, 3, 512
 
 
-def _model(family, seed=0):
+def _model(family, seed=0, layers=K):
     e = synthetic_edges(U, I, E, seed=4, items="zipf")
     torch.manual_seed(seed)
     if family == "v2":
         cred = torch.as_tensor(synthetic_credibility(U, 4))
         M_ui, M_iu = V2.build_message_passing_mats(e, U, I, cred, DEV)
-        m = V2.LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+        m = V2.LightGCN(U, I, D, layers, M_ui, M_iu).to(DEV)
     elif family == "cu":
         cred = torch.as_tensor(synthetic_credibility(U, 4))
         M_ui, M_iu, deg_i = J.build_cred_weighted_mats(e, U, I, cred, DEV)
-        m = J.CredLightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+        m = J.CredLightGCN(U, I, D, layers, M_ui, M_iu).to(DEV)
         m.pop = torch.as_tensor(deg_i / max(deg_i.max(), 1.0), device=DEV)
     else:
         A = L.build_norm_adj(e, U, I, DEV)
-        m = L.LightGCN(U, I, D, K, A).to(DEV)
+        m = L.LightGCN(U, I, D, layers, A).to(DEV)
     return m
 
 
@@ -193,14 +193,15 @@ def test_backward_op_support_masks_are_bitwise_dense(order):
     assert torch.equal(a_u, b_u) and torch.equal(a_i, b_i)
 
 
-@pytest.mark.parametrize("family", ["v2", "cu"])
-def test_sparse_ego_gradient_is_bitwise_dense(family, monkeypatch):
+@pytest.mark.parametrize("family,layers", [("v2", K), ("cu", K), ("v2", 0), ("cu", 0)])
+def test_sparse_ego_gradient_is_bitwise_dense(family, layers, monkeypatch):
     """Eager drop-in step: bpr_loss picks bbgr::bpr_loss_sparse_ego (the final
     tables come from the propagate op, which returns dense gradients for the
     same weights), whose backward hands the ego gradient and dL/d(u_final) back
     as sparse rows (propagate_backward_rows); .grad stays dense and equals the
     dense op's bit for bit, with repeated users / items and a dropped triple
-    (neg = -1)."""
+    (neg = -1). K = 0 (the reference's layer loop runs zero times) included:
+    grad_u0 is then gU itself, every row of it."""
     from bbgr import bpr, ops
     users, pos, neg = _batch(5)
     neg = neg.clone()
@@ -213,7 +214,7 @@ def test_sparse_ego_gradient_is_bitwise_dense(family, monkeypatch):
     for mode in ("sparse", "dense"):
         if mode == "dense":
             monkeypatch.setattr(bpr, "_receives_dense_grad", lambda *a: False)
-        m = _model(family)
+        m = _model(family, layers=layers)
         loss = _loss(m, users, pos, neg)
         assert ("bpr_loss_sparse_ego" in loss.grad_fn.name()) == (mode == "sparse")
         n0 = len(rows_calls)
@@ -234,6 +235,15 @@ def test_sparse_ego_not_chosen_without_dense_path():
     uf, itf = m.get_user_item_emb()
     users, pos, neg = _batch(6)
     loss = m.bpr_loss(users, pos, neg, uf.detach(), itf.detach(), 1e-4)
+    assert "sparse" not in str(loss.grad_fn.name())
+    loss.backward()
+    assert m.user_emb.weight.grad.layout == torch.strided
+    # a node with a direct edge to the weight that is NOT the propagate op (an
+    # Add here; an nn.Embedding(sparse=True) lookup alike) keeps the dense form
+    m.zero_grad()
+    uf2 = m.user_emb.weight + uf.detach()
+    itf2 = m.item_emb.weight + itf.detach()
+    loss = m.bpr_loss(users, pos, neg, uf2, itf2, 1e-4)
     assert "sparse" not in str(loss.grad_fn.name())
     loss.backward()
     assert m.user_emb.weight.grad.layout == torch.strided

@@ -200,6 +200,22 @@ def test_adam_matches_torch():
     assert nrel(tp.detach().numpy(), p) < 1e-12
 
 
+@pytest.mark.parametrize("betas", [(0.9, 0.999), (0.8, 0.99), (0.9, 0.9999)])
+def test_bias_correction_table_is_exact_past_its_end(betas):
+    """The device step state's kernels clamp t to the table end:
+    exact because from exact_table_steps() on every step's fp32 constants are
+    (1.0f, 1.0f), the value the host computes for any later t."""
+    import math
+    from bbgr.optim import bias_corrections, exact_table_steps
+    b1, b2 = betas
+    n = exact_table_steps(b1, b2)
+    tab = bias_corrections(n + 64, b1, b2)
+    assert np.all(tab[n - 1:] == np.float32(1.0))
+    for t in (n, n + 1, 10 * n, 1 << 40):      # the host path's scalars for a later step
+        assert np.float32(1.0 - b1 ** t) == tab[n - 1, 0]
+        assert np.float32(math.sqrt(1.0 - b2 ** t)) == tab[n - 1, 1]
+
+
 def test_reference_style_sampler_never_returns_positive():
     e, _, _, _ = _random_case(9, U=50, I=30, E=600, dup=0)
     indptr, indices = R.edges_to_user_csr(e, 50)
