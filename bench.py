@@ -18,6 +18,7 @@ cpu_baseline = the reference's CPU path (oracle/ref_torch.py: the same torch
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -436,6 +437,12 @@ def main():
                     help="N>1 strong runs: afterwards time this many weak-scaled steps "
                          "(each rank a full config-sized shard) and report them beside "
                          "the strong line (0 = skip)")
+    ap.add_argument("--dist-timeout", type=float, default=180.0,
+                    help="N>1: seconds before a stuck collective aborts the run (every rank "
+                         "draws its graph in parallel first: C4 ~25 s)")
+    ap.add_argument("--partition-beside", type=int, default=1,
+                    help="strong N > 1: also time the other partition (columns / users) on "
+                         "the same graph and report the faster as the line (0 = off)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="N>1: strong (default) = the config's one graph cut into N user "
                          "ranges (the metric's |E|); weak = every rank owns a full "
@@ -469,14 +476,19 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         backend = os.environ.get("BBGR_DIST_BACKEND", "nccl")
+        # a collective stuck on one rank aborts the job after --dist-timeout
+        # seconds (torch's watchdog names the op, its sequence number and size)
+        # instead of sitting until the driver kills the run
+        timeout = datetime.timedelta(seconds=args.dist_timeout)
         if backend == "nccl":
             # high-priority RCCL stream: its kernels get CUs while the SpMM of the
             # next item range floods the queue (range_probe: 2.07 -> 1.96 ms / product)
             opts = torch.distributed.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = True
-            torch.distributed.init_process_group("nccl", device_id=dev, pg_options=opts)
+            torch.distributed.init_process_group("nccl", device_id=dev, pg_options=opts,
+                                                 timeout=timeout)
         else:
-            torch.distributed.init_process_group(backend)
+            torch.distributed.init_process_group(backend, timeout=timeout)
 
     U, I, d, K = cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"]
     B = cfg["batch"]
@@ -528,132 +540,169 @@ def main():
     frontier = {"auto": "auto", "on": True, "off": False}[args.frontier]
     if args.dense:
         frontier = False
-    if emulate:
-        from bbgr.columns import ColumnShardedTrainer
-        trainer = ColumnShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
-                                       num_layers=K, batch_size=B, device=dev,
-                                       vertex_order=args.vertex_order, frontier=frontier,
-                                       column_parts=emulate, column_index=0)
-    elif not dist_mode:
-        from bbgr.graph import BipartiteGraph
-        from bbgr.trainer import FusedTrainer
-        graph = BipartiteGraph(edges, U, I, dev, vertex_order=args.vertex_order)
-        trainer = FusedTrainer(graph, args.variant, cred=cred, emb_dim=d, num_layers=K,
-                               batch_size=B, frontier=frontier)
-    elif columns:
-        from bbgr.columns import ColumnShardedTrainer
-        trainer = ColumnShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
-                                       num_layers=K, batch_size=B, device=dev,
-                                       vertex_order=args.vertex_order, frontier=frontier)
-    elif weak:
+    def build(part: str):
+        """The trainer of one partition ("columns" / "users" at N > 1)."""
+        if emulate:
+            from bbgr.columns import ColumnShardedTrainer
+            return ColumnShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
+                                        num_layers=K, batch_size=B, device=dev,
+                                        vertex_order=args.vertex_order, frontier=frontier,
+                                        column_parts=emulate, column_index=0)
+        if not dist_mode:
+            from bbgr.graph import BipartiteGraph
+            from bbgr.trainer import FusedTrainer
+            graph = BipartiteGraph(edges, U, I, dev, vertex_order=args.vertex_order)
+            return FusedTrainer(graph, args.variant, cred=cred, emb_dim=d, num_layers=K,
+                                batch_size=B, frontier=frontier)
+        if part == "columns":
+            from bbgr.columns import ColumnShardedTrainer
+            return ColumnShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
+                                        num_layers=K, batch_size=B, device=dev,
+                                        vertex_order=args.vertex_order, frontier=frontier)
         from bbgr.distributed import ShardedTrainer
-        trainer = ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
-                                 num_layers=K, batch_size=B, device=dev, user_offset=rank * U,
-                                 frontier=frontier, **xp)
-    elif sharded_gen:
-        from bbgr.distributed import ShardedTrainer
-        trainer = ShardedTrainer(edges, hi - lo, I, args.variant, cred=cred, emb_dim=d,
-                                 num_layers=K, batch_size=max(1, B // world), device=dev,
-                                 user_offset=lo, frontier=frontier, **xp)
-    else:
-        from bbgr.distributed import ShardedTrainer
-        trainer = ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
-                                                   emb_dim=d, num_layers=K, batch_size=B,
-                                                   device=dev, frontier=frontier, **xp)
-    # edges of the whole job's graph: the sum of the ranks' shards (column
-    # shards all hold the whole graph)
-    E_local = trainer.graph.item_csr.nnz
-    E = int(_allreduce(E_local, dev, torch.distributed.ReduceOp.SUM)) if dist_mode and \
-        not columns else E_local
-    U_job = U * (world if weak else 1)
-    if dist_mode:
-        del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
-    torch.cuda.synchronize()
-    log(f"[bench] rank {rank}: setup done, E={E} (local {E_local}), frontier="
-        f"{trainer.frontier}, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
+        if weak:
+            return ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
+                                  num_layers=K, batch_size=B, device=dev, user_offset=rank * U,
+                                  frontier=frontier, **xp)
+        if sharded_gen:
+            return ShardedTrainer(edges, hi - lo, I, args.variant, cred=cred, emb_dim=d,
+                                  num_layers=K, batch_size=max(1, B // world), device=dev,
+                                  user_offset=lo, frontier=frontier, **xp)
+        return ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
+                                                emb_dim=d, num_layers=K, batch_size=B,
+                                                device=dev, frontier=frontier, **xp)
 
     from bbgr.trainer import FRONTIER_MIN_EDGES
-    use_graph = not dist_mode and (args.graph == "on" or (args.graph == "auto"
-                                                          and E < FRONTIER_MIN_EDGES))
-    step_fn = trainer.step
-    if use_graph:
-        from bbgr.trainer import GraphedStep
-        step_fn = GraphedStep(trainer).step
-    for _ in range(args.warmup):
-        step_fn()
-    timer = P.SpmmTimer()
-    if dist_mode:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    # Per-launch HIP events for the roofline. On one GPU they ride inside the
-    # timed steps (cost ~0.1 ms/step). In the sharded step, events recorded
-    # between launches interleave with the collectives' cross-stream waits and
-    # cost 1.4-3 ms/step, so there the events are recorded over
-    # `--roofline-steps` extra steps right after the timed region instead.
-    # A captured graph replays its launches without the host: its per-launch
-    # events are taken over eager steps after the timed region, as for sharded.
-    events_in_loop = not dist_mode and not use_graph
-    if events_in_loop:
-        P.set_spmm_timer(timer)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step_fn()
-    torch.cuda.synchronize()
-    if dist_mode:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    P.set_spmm_timer(None)
-    timer_steps = args.steps
-    if not events_in_loop:
-        timer_steps = max(1, args.roofline_steps)
-        P.set_spmm_timer(timer)
-        for _ in range(timer_steps):
+    count_steps = max(1, args.count_steps)
+
+    def measure(trainer, part: str, dense_check: int) -> dict:
+        """Warm-up, then EXACTLY args.steps timed steps (barrier + sync on both
+        sides, max over ranks); per-launch events, device edge counts and the
+        dense (frontier off) step after the timed region."""
+        cols = dist_mode and part == "columns"
+        # edges of the whole job's graph: the sum of the ranks' shards (column
+        # shards all hold the whole graph)
+        E_local = trainer.graph.item_csr.nnz
+        E = int(_allreduce(E_local, dev, torch.distributed.ReduceOp.SUM)) if dist_mode and \
+            not cols else E_local
+        torch.cuda.synchronize()
+        log(f"[bench] rank {rank}: {part} setup done, E={E} (local {E_local}), frontier="
+            f"{trainer.frontier}, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
+        use_graph = not dist_mode and (args.graph == "on" or (args.graph == "auto"
+                                                              and E < FRONTIER_MIN_EDGES))
+        step_fn = trainer.step
+        if use_graph:
+            from bbgr.trainer import GraphedStep
+            step_fn = GraphedStep(trainer).step
+        for _ in range(args.warmup):
+            step_fn()
+        timer = P.SpmmTimer()
+        if dist_mode:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        # Per-launch HIP events for the roofline. On one GPU they ride inside the
+        # timed steps (cost ~0.1 ms/step). In the sharded step, events recorded
+        # between launches interleave with the collectives' cross-stream waits and
+        # cost 1.4-3 ms/step (DESIGN §6), so there the events are recorded over
+        # `--roofline-steps` extra steps right after the timed region instead.
+        # A captured graph replays its launches without the host: its per-launch
+        # events are taken over eager steps after the timed region, as for sharded.
+        events_in_loop = not dist_mode and not use_graph
+        if events_in_loop:
+            P.set_spmm_timer(timer)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step_fn()
+        torch.cuda.synchronize()
+        if dist_mode:
+            torch.distributed.barrier()
+        elapsed = time.perf_counter() - t0
+        P.set_spmm_timer(None)
+        timer_steps = args.steps
+        if not events_in_loop:
+            timer_steps = max(1, args.roofline_steps)
+            P.set_spmm_timer(timer)
+            for _ in range(timer_steps):
+                trainer.step()
+            torch.cuda.synchronize()
+            P.set_spmm_timer(None)
+        if dist_mode:
+            elapsed = _allreduce(elapsed, dev, torch.distributed.ReduceOp.MAX)
+        final_loss = float(loss)
+        # rows / edges every launch actually processes (frontier masks make them
+        # data-dependent), counted on the device over extra steps
+        counter = P.SpmmTimer(count=True)
+        P.set_spmm_timer(counter)
+        for _ in range(count_steps):
             trainer.step()
         torch.cuda.synchronize()
         P.set_spmm_timer(None)
-    if dist_mode:
-        elapsed = _allreduce(elapsed, dev, torch.distributed.ReduceOp.MAX)
-    final_loss = float(loss)
-    # rows / edges every launch actually processes (frontier masks make them
-    # data-dependent), counted on the device over extra steps
-    counter = P.SpmmTimer(count=True)
-    count_steps = max(1, args.count_steps)
-    P.set_spmm_timer(counter)
-    for _ in range(count_steps):
-        trainer.step()
-    torch.cuda.synchronize()
-    P.set_spmm_timer(None)
-    counts = counter.edge_counts()
-    gathered_step, visited_step = edges_per_step(counts, d, count_steps)
-    if dist_mode:
-        gathered_step = _allreduce(gathered_step, dev, torch.distributed.ReduceOp.SUM)
-        visited_step = _allreduce(visited_step, dev, torch.distributed.ReduceOp.SUM)
-    dense_ms = None
-    if trainer.frontier and args.dense_check > 0:
-        # the same trainer with frontier sparsity off (every product over the
-        # full CSR): what the masks save, reported next to the value
-        trainer.frontier = False
-        trainer.step()
+        counts = counter.edge_counts()
+        gathered_step, visited_step = edges_per_step(counts, d, count_steps)
         if dist_mode:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.dense_check):
+            gathered_step = _allreduce(gathered_step, dev, torch.distributed.ReduceOp.SUM)
+            visited_step = _allreduce(visited_step, dev, torch.distributed.ReduceOp.SUM)
+        dense_ms = None
+        if trainer.frontier and dense_check > 0:
+            # the same trainer with frontier sparsity off (every product over the
+            # full CSR): what the masks save, reported next to the value
+            trainer.frontier = False
             trainer.step()
-        torch.cuda.synchronize()
-        if dist_mode:
-            torch.distributed.barrier()
-        dense_s = time.perf_counter() - t1
-        if dist_mode:
-            dense_s = _allreduce(dense_s, dev, torch.distributed.ReduceOp.MAX)
-        dense_ms = 1000.0 * dense_s / args.dense_check
-        trainer.frontier = True
-    frontier_on = bool(trainer.frontier)
+            if dist_mode:
+                torch.distributed.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(dense_check):
+                trainer.step()
+            torch.cuda.synchronize()
+            if dist_mode:
+                torch.distributed.barrier()
+            dense_s = time.perf_counter() - t1
+            if dist_mode:
+                dense_s = _allreduce(dense_s, dev, torch.distributed.ReduceOp.MAX)
+            dense_ms = 1000.0 * dense_s / dense_check
+            trainer.frontier = True
+        return dict(part=part, columns=cols, E=E, use_graph=use_graph, timer=timer,
+                    timer_steps=timer_steps, events_in_loop=events_in_loop, elapsed=elapsed,
+                    final_loss=final_loss, counts=counts, gathered_step=gathered_step,
+                    visited_step=visited_step, dense_ms=dense_ms,
+                    frontier_on=bool(trainer.frontier),
+                    value=gathered_step * args.steps / elapsed,
+                    ms_per_step=1000.0 * elapsed / args.steps)
+
+    trainer = build(partition)
+    res = measure(trainer, partition, args.dense_check)
+    U_job = U * (world if weak else 1)
+    partition_beside = None
+    other = {"columns": "users", "users": "columns"}.get(partition)
+    if (dist_mode and world > 1 and not weak and not sharded_gen and args.partition_beside
+            and (other == "users" or can_shard_columns(d, world))):
+        # strong N > 1: the other partition, measured the same way right after;
+        # the faster one is the line, the other is reported beside it (the
+        # per-link exchange model cannot settle N = 2 / 4 without the links)
+        trainer.close()
+        del trainer
+        torch.cuda.empty_cache()
+        trainer = build(other)
+        res_other = measure(trainer, other, 0)
+        if res_other["elapsed"] < res["elapsed"]:
+            res, res_other = res_other, res
+        partition_beside = {k: res_other[k] for k in ("part", "ms_per_step", "value", "E",
+                                                       "final_loss")}
+        partition_beside["note"] = ("the other strong-scaling partition of the same graph, "
+                                    "timed the same way in the same run; the faster one is "
+                                    "the line")
+    columns = res["columns"]
+    E, use_graph, timer, timer_steps = res["E"], res["use_graph"], res["timer"], res["timer_steps"]
+    events_in_loop, elapsed, final_loss = res["events_in_loop"], res["elapsed"], res["final_loss"]
+    counts, gathered_step, visited_step = res["counts"], res["gathered_step"], res["visited_step"]
+    dense_ms, frontier_on = res["dense_ms"], res["frontier_on"]
     if dist_mode:
+        del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
         trainer.close()                    # the native exchange's communicator, if any
     groups = roofline_groups(timer, counts, timer_steps, count_steps, I)
     weak_beside = None
-    if world > 1 and not weak and not columns and args.weak_beside > 0 and not sharded_gen:
+    if world > 1 and not weak and args.weak_beside > 0 and not sharded_gen:
         # the same machinery at fixed per-GPU work, beside the strong line:
         # every rank a full config-sized user shard over the shared items
         del trainer
@@ -748,6 +797,7 @@ def main():
         "torch_gpu_reference": torch_ref,
         "dropin_module_step": dropin,
         "weak_beside": weak_beside,
+        "partition_beside": partition_beside,
         "partition": ("columns" if columns else "users") if dist_mode else
                      (f"one column shard of {emulate}" if emulate else "single GPU"),
         "graph_replay": use_graph,

@@ -85,6 +85,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_bias_correction1", c_float), ("adam_bias_correction2_sqrt", c_float),
         ("stream_from", c_int32), ("stream_out_from", c_int32),
         ("adam_bc_table", c_void_p), ("adam_state", c_void_p),
+        ("y_map", c_void_p), ("acc_map", c_void_p), ("add_map", c_void_p),
     ]
 
 
@@ -163,6 +164,8 @@ _SIGNATURES = {
     "bbgr_scatter_add_rows": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P,
                                ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
+    "bbgr_mark_neighbors_of_mask": ([c_int64, _P, _P, _P, _P, ctypes.c_uint8, _P, _P],
+                                    c_int32),
     "bbgr_row_support": ([c_int64, c_int32, _P, c_int64, _P, _P, _P, _P, _P], c_int32),
     "bbgr_rows_zero": ([c_int64, _P, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_rows_axpy": ([c_int64, _P, c_float, _P, c_int64, _P, c_int64, c_int32, _P],
@@ -215,7 +218,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 3:
+        if handle.bbgr_abi_version() != 4:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

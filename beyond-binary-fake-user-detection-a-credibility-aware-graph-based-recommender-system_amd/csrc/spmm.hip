@@ -75,6 +75,10 @@ struct SpmmParams {
   float adam_lr;
   const float *adam_bc;        // device step state (nullable): bias corrections by step t
   const long *adam_state;
+  // row maps of the epilogue's tables (nullable; args.y_map / acc_map / add_map):
+  // CSR row r reads / writes row map[r] of y (and the fused Adam's rows), of
+  // acc_in / acc_out, of add; the masks of those tables index the same rows
+  const int *y_map, *acc_map, *add_map;
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -486,7 +490,7 @@ __device__ __forceinline__ AdamConsts launch_adam_consts(const SpmmParams &P) {
 }
 
 template <int D>
-__device__ __forceinline__ void adam_row(const SpmmParams &P, int row, int lane,
+__device__ __forceinline__ void adam_row(const SpmmParams &P, long row, int lane,
                                          const float4 (&G)[RowShape<D>::V]) {
   constexpr int V = RowShape<D>::V;
   const AdamConsts ac = launch_adam_consts(P);
@@ -523,18 +527,19 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
   if (P.y || P.adam_p) {
     const float ys = (P.y_scale ? P.y_scale[row] : 1.f) * P.y_scale_s;
     float4 G[V];
-    if (P.add && (!P.add_mask || P.add_mask[row])) {
+    const long ra = P.add_map ? (long)P.add_map[row] : (long)row;
+    if (P.add && (!P.add_mask || P.add_mask[ra])) {
       const float as = (P.add_scale ? P.add_scale[row] : 1.f) * P.add_scale_s;
-      const float4 *ad =
-          reinterpret_cast<const float4 *>(P.add + (long)row * P.ldadd) + lane;
+      const float4 *ad = reinterpret_cast<const float4 *>(P.add + ra * P.ldadd) + lane;
 #pragma unroll
       for (int k = 0; k < V; ++k) G[k] = f4_fma(as, ad[16 * k], f4_mul(ys, T[k]));
     } else {
 #pragma unroll
       for (int k = 0; k < V; ++k) G[k] = f4_mul(ys, T[k]);
     }
+    const long ry = P.y_map ? (long)P.y_map[row] : (long)row;
     if (P.y) {
-      float4 *dst = reinterpret_cast<float4 *>(P.y + (long)row * P.ldy) + lane;
+      float4 *dst = reinterpret_cast<float4 *>(P.y + ry * P.ldy) + lane;
       if (row >= P.nt_out_from) {
 #pragma unroll
         for (int k = 0; k < V; ++k) st_nt(dst + 16 * k, G[k]);
@@ -543,16 +548,15 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
         for (int k = 0; k < V; ++k) dst[16 * k] = G[k];
       }
     }
-    if (P.adam_p) adam_row<D>(P, row, lane, G);
+    if (P.adam_p) adam_row<D>(P, ry, lane, G);
   }
-  if (P.acc_out && (!P.acc_mask || P.acc_mask[row])) {
+  const long rc = P.acc_map ? (long)P.acc_map[row] : (long)row;
+  if (P.acc_out && (!P.acc_mask || P.acc_mask[rc])) {
     const float cs = (P.acc_scale ? P.acc_scale[row] : 1.f) * P.acc_scale_s;
-    float4 *dst =
-        reinterpret_cast<float4 *>(P.acc_out + (long)row * P.ldacc_out) + lane;
+    float4 *dst = reinterpret_cast<float4 *>(P.acc_out + rc * P.ldacc_out) + lane;
     if (P.acc_in) {
       const float4 *ai =
-          reinterpret_cast<const float4 *>(P.acc_in + (long)row * P.ldacc_in) +
-          lane;
+          reinterpret_cast<const float4 *>(P.acc_in + rc * P.ldacc_in) + lane;
 #pragma unroll
       for (int k = 0; k < V; ++k)
         dst[16 * k] = f4_mul(P.gamma, f4_fma(cs, T[k], ai[16 * k]));
@@ -922,6 +926,9 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.adam = adam_consts(a->adam_lr, a->adam_beta1, a->adam_beta2, a->adam_eps,
                        a->adam_weight_decay, dev ? 1.f : a->adam_bias_correction1,
                        dev ? 1.f : a->adam_bias_correction2_sqrt);
+  P.y_map = a->y_map;
+  P.acc_map = a->acc_map;
+  P.add_map = a->add_map;
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {

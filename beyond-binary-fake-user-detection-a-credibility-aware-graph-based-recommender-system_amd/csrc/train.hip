@@ -304,6 +304,18 @@ __global__ void mark_neighbors_kernel(long n, const long *rows, const int *indpt
     mask[indices[e]] = v;
 }
 
+// every neighbour of a row flagged in row_mask (indexed through row_map when
+// given: CSR row r is flagged by row_mask[row_map[r]]) is set to v in mask
+__global__ void mark_neighbors_of_mask_kernel(long n_rows, const unsigned char *row_mask,
+                                              const int *row_map, const int *indptr,
+                                              const int *indices, unsigned char v,
+                                              unsigned char *mask) {
+  const long r = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (r >= n_rows || !row_mask[row_map ? (long)row_map[r] : r]) return;
+  for (int e = indptr[r] + (threadIdx.x & 15); e < indptr[r + 1]; e += 16)
+    mask[indices[e]] = v;
+}
+
 // mask[r] = 1 if row r of x holds a nonzero (a -0.0 counts as zero: skipping
 // a signed-zero source row leaves every sum unchanged), else 0; with a CSR,
 // every neighbour of a flagged row is also set in nbr. One 16-lane group per
@@ -628,6 +640,21 @@ extern "C" int bbgr_mark_neighbors(int64_t n, const int64_t *rows,
                      as_stream(stream), (long)n, (const long *)rows, indptr, indices, value,
                      mask);
   BBGR_LAUNCHED("mark_neighbors_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_mark_neighbors_of_mask(int64_t n_rows, const uint8_t *row_mask,
+                                           const int32_t *row_map, const int32_t *indptr,
+                                           const int32_t *indices, uint8_t value,
+                                           uint8_t *mask, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n_rows >= 0, "bbgr_mark_neighbors_of_mask: negative n_rows");
+  if (n_rows == 0) return BBGR_OK;
+  BBGR_REQUIRE(row_mask && indptr && indices && mask,
+               "bbgr_mark_neighbors_of_mask: null arrays");
+  hipLaunchKernelGGL(mark_neighbors_of_mask_kernel, dim3((unsigned)((n_rows + 15) / 16)),
+                     dim3(256), 0, as_stream(stream), (long)n_rows, row_mask, row_map, indptr,
+                     indices, value, mask);
+  BBGR_LAUNCHED("mark_neighbors_of_mask_kernel");
   return BBGR_OK;
 }
 

@@ -68,6 +68,8 @@ class Csr:
     """Row-sorted CSR on the device (int32 indptr/indices, columns sorted in
     each row, duplicates kept) plus the SpMM load-balance plan."""
 
+    cols_sorted = True   # columns ascending inside each row (membership searches)
+
     def __init__(self, rows, cols, n_rows: int, n_cols: int, device,
                  edge_values: torch.Tensor | None = None,
                  long_threshold: int | None = DEFAULT_LONG_THRESHOLD,
@@ -301,7 +303,7 @@ class BipartiteGraph:
     def __init__(self, train_edges_2xE, num_users: int, num_items: int, device,
                  long_threshold: int | None = DEFAULT_LONG_THRESHOLD,
                  chunk_edges: int = DEFAULT_CHUNK_EDGES, vertex_order: str = "input",
-                 item_degree_hook=None):
+                 item_degree_hook=None, input_col_order: bool = False):
         device = torch.device(device)
         if isinstance(train_edges_2xE, tuple):        # graph.py's (u2i_src, u2i_dst)
             src, dst = train_edges_2xE
@@ -331,11 +333,30 @@ class BipartiteGraph:
                 deg_i = item_degree_hook(deg_i)
             self.user_order = VertexOrder(_degree_count(u, self.num_users))
             self.item_order = VertexOrder(deg_i)
-            u, i = _relabel(u, self.user_order), _relabel(i, self.item_order)
-        self.user_csr = Csr(u, i, num_users, num_items, device,
-                            long_threshold=long_threshold, chunk_edges=chunk_edges)
-        self.item_csr = Csr(i, u, num_items, num_users, device,
-                            long_threshold=long_threshold, chunk_edges=chunk_edges)
+            u_int, i_int = _relabel(u, self.user_order), _relabel(i, self.item_order)
+            if input_col_order:
+                # rows renumbered, each row's columns kept in ascending INPUT id
+                # (the input-order CSR's slot order, then relabelled): every row
+                # sums its edges exactly as the input-order graph does, so the
+                # drop-in's results are bitwise those of an input-order build;
+                # the input-id copies stay for the products that gather the
+                # caller's input-order tables (Product.input_struct)
+                self.user_csr = Csr(u_int, i, num_users, num_items, device,
+                                    long_threshold=long_threshold, chunk_edges=chunk_edges)
+                self.item_csr = Csr(i_int, u, num_items, num_users, device,
+                                    long_threshold=long_threshold, chunk_edges=chunk_edges)
+                for c, order in ((self.user_csr, self.item_order), (self.item_csr,
+                                                                    self.user_order)):
+                    c.cols_sorted = False   # (no binary search over these rows)
+                    c._input_indices = c.indices.clone()
+                    call("bbgr_relabel", c.nnz, ptr(c._input_indices), ptr(order.rank),
+                         ptr(c.indices), stream_handle())
+            u, i = u_int, i_int
+        if not (vertex_order == "degree" and input_col_order):
+            self.user_csr = Csr(u, i, num_users, num_items, device,
+                                long_threshold=long_threshold, chunk_edges=chunk_edges)
+            self.item_csr = Csr(i, u, num_items, num_users, device,
+                                long_threshold=long_threshold, chunk_edges=chunk_edges)
         if vertex_order == "degree":
             users_ordered = items_ordered = True
         else:

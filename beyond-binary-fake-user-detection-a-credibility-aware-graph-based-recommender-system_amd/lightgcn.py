@@ -19,16 +19,14 @@ import torch
 
 from . import bpr as _bpr
 from ._lib import OP_SYM
-from .graph import BipartiteGraph
-from .operators import NormAdjOperator, square_from_torch_sparse
+from .operators import NormAdjOperator, build_pair, square_from_torch_sparse
 from .propagate import (ORDER_J, OperatorPair, _SquareFn, backward as _bwd,
                         forward as _fwd)
 
 
 def build_norm_adj(train_edges, num_users: int, num_items: int, device):
-    graph = BipartiteGraph(train_edges, num_users, num_items, device)
-    sc = graph.scales(OP_SYM, None)
-    return NormAdjOperator(OperatorPair.factored(graph, sc), graph)
+    graph, sc, pair = build_pair(train_edges, num_users, num_items, OP_SYM, None, device)
+    return NormAdjOperator(pair, graph)
 
 
 class LightGCN(torch.nn.Module):

@@ -18,22 +18,18 @@ import torch
 
 from . import bpr as _bpr
 from ._lib import OP_J
-from .graph import BipartiteGraph
-from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator,
-                        resolve_pair, to_device_cred)
+from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator, build_pair,
+                        input_order_vector, resolve_pair)
 from .propagate import ORDER_J, OperatorPair, propagate as _propagate
 
 
 def build_cred_weighted_mats(train_edges, num_users: int, num_items: int,
                              cred_u: np.ndarray, device: str):
     """Eq 3.23: M_ui[i,u] = c_u / sqrt(deg_u deg_i); Eq 3.24: M_iu[u,i] = 1/sqrt(..)."""
-    graph = BipartiteGraph(train_edges, num_users, num_items, device)
-    cred = to_device_cred(cred_u, num_users, graph.device)
-    sc = graph.scales(OP_J, cred)
-    pair = OperatorPair.factored(graph, sc)
+    graph, sc, pair = build_pair(train_edges, num_users, num_items, OP_J, cred_u, device)
     M_ui = BipartiteOperator(pair, ITEM_FROM_USER, graph, OP_J)   # [I, U]
     M_iu = BipartiteOperator(pair, USER_FROM_ITEM, graph, OP_J)   # [U, I]
-    deg_i = sc.deg_i.detach().cpu().numpy().astype(np.float32)
+    deg_i = input_order_vector(graph, sc.deg_i, "item").detach().cpu().numpy().astype(np.float32)
     return M_ui, M_iu, deg_i
 
 

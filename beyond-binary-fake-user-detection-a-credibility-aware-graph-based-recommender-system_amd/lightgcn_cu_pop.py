@@ -13,7 +13,9 @@ Same names, signatures, attributes and state_dict keys as the reference:
   attributes, not buffers, as in the reference).
 
 The operators are built ON the device from the int32 [2, E] edge array; no
-numpy weight math, no COO coalesce. Torch sparse COO operators are also
+numpy weight math, no COO coalesce. The graph inside is numbered by
+descending degree (operators.DROPIN_VERTEX_ORDER) while the embedding tables,
+the final tables and the gradients stay in the caller's ids. Torch sparse COO operators are also
 accepted by LightGCN (converted once to explicit-value CSRs).
 """
 from __future__ import annotations
@@ -22,17 +24,13 @@ import torch
 
 from . import bpr as _bpr
 from ._lib import OP_GS
-from .graph import BipartiteGraph
-from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator,
-                        resolve_pair, to_device_cred)
+from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator, build_pair,
+                        resolve_pair)
 from .propagate import ORDER_GS, OperatorPair, propagate as _propagate
 
 
 def _build(train_edges_2xE, num_users, num_items, cred_u, device, kind):
-    graph = BipartiteGraph(train_edges_2xE, num_users, num_items, device)
-    cred = to_device_cred(cred_u, num_users, graph.device)
-    sc = graph.scales(kind, cred)
-    pair = OperatorPair.factored(graph, sc)
+    graph, sc, pair = build_pair(train_edges_2xE, num_users, num_items, kind, cred_u, device)
     M_ui = BipartiteOperator(pair, USER_FROM_ITEM, graph, kind)
     M_iu = BipartiteOperator(pair, ITEM_FROM_USER, graph, kind)
     return M_ui, M_iu

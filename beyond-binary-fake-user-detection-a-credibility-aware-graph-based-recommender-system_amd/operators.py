@@ -9,6 +9,8 @@ working.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -56,8 +58,13 @@ class BipartiteOperator:
         _lib.require_gpu(x)
         x = x.contiguous()
         y = torch.empty(self.shape[0], x.shape[1], dtype=torch.float32, device=x.device)
-        # diag(out) A diag(in) x: first-layer form applies `in` per gathered row
-        spmm(prod, x, True, y=y, y_scale=prod.out_scale)
+        # diag(out) A diag(in) x: first-layer form applies `in` per gathered row;
+        # an input-order pair gathers x by input id and places y's rows by map
+        io = self.pair.io
+        y_map = None if io is None else (io.item_map if self.role == ITEM_FROM_USER
+                                         else io.user_map)
+        spmm(prod, x, True, y=y, y_scale=prod.out_scale, src_input=io is not None,
+             y_map=y_map)
         return y
 
     __matmul__ = mm
@@ -74,6 +81,11 @@ class BipartiteOperator:
             vals = prod.vals[: csr.nnz]
         else:
             vals = prod.out_scale[rows] * prod.in_scale[cols]
+        io = self.pair.io
+        if io is not None:   # internal ids -> the caller's input ids
+            rmap, cmap = ((io.item_map64, io.user_map64) if self.role == ITEM_FROM_USER
+                          else (io.user_map64, io.item_map64))
+            rows, cols = rmap[rows], cmap[cols]
         return torch.sparse_coo_tensor(torch.stack([rows, cols]), vals,
                                        size=self.shape).coalesce()
 
@@ -101,6 +113,37 @@ class NormAdjOperator:
         idx = torch.cat([torch.stack([ai[0] + U, ai[1]]), torch.stack([bi[0], bi[1] + U])], 1)
         vals = torch.cat([a.values(), b.values()])
         return torch.sparse_coo_tensor(idx, vals, size=self.shape).coalesce()
+
+
+# Vertex order of the graphs the drop-in builders make: "degree" numbers users
+# and items by descending degree inside the graph (hot rows cached, cold rows
+# streamed) while every table the caller sees stays in its input
+# order (OperatorPair.set_input_order); each row keeps its input-order column
+# sequence, so results are bitwise those of an input-order build. "input":
+# the graph in the caller's numbering (BBGR_DROPIN_ORDER=input, A/B runs).
+DROPIN_VERTEX_ORDER = os.environ.get("BBGR_DROPIN_ORDER", "degree")
+
+
+def build_pair(train_edges, num_users: int, num_items: int, kind: int, cred_u, device):
+    """(graph, scales, pair) of a drop-in builder: the device graph, the
+    operator family's scale vectors and the factored pair, with the caller's
+    input-order credibility vector (None: no credibility)."""
+    graph = BipartiteGraph(train_edges, num_users, num_items, device,
+                           vertex_order=DROPIN_VERTEX_ORDER, input_col_order=True)
+    cred = to_device_cred(cred_u, num_users, graph.device)
+    if cred is not None and graph.user_order is not None:
+        cred = cred[graph.user_order._perm64].contiguous()   # internal order
+    sc = graph.scales(kind, cred)
+    pair = OperatorPair.factored(graph, sc)
+    if graph.user_order is not None:
+        pair.set_input_order(graph.user_order, graph.item_order)
+    return graph, sc, pair
+
+
+def input_order_vector(graph: BipartiteGraph, v: torch.Tensor, side: str) -> torch.Tensor:
+    """A per-item / per-user vector of the graph (internal order) by input id."""
+    order = graph.item_order if side == "item" else graph.user_order
+    return v if order is None else v[order._rank64]
 
 
 def _coo_parts(M: torch.Tensor):

@@ -90,12 +90,39 @@ def grad_support(pair, gU: Tensor, gI: Tensor, order: str):
     mi = torch.empty(max(I, 1), dtype=torch.uint8, device=gU.device)
     d = gU.shape[1]
     call("bbgr_row_support", I, d, _lib.ptr(gI), _lib.ld(gI), _lib.ptr(mi), None, None, None, st)
+    if pair.io is not None:   # input-order tables over a degree-ordered graph
+        call("bbgr_row_support", U, d, _lib.ptr(gU), _lib.ld(gU), _lib.ptr(mu), None, None,
+             None, st)
+        return _io_support(pair, mu[:U], mi[:I], order)
     uc = pair.fwd_user.csr if order == ORDER_GS else None   # user rows -> item neighbours
     call("bbgr_row_support", U, d, _lib.ptr(gU), _lib.ld(gU), _lib.ptr(mu),
          None if uc is None else _lib.ptr(uc.indptr),
          None if uc is None else _lib.ptr(uc.indices),
          None if uc is None else _lib.ptr(mi), st)
     return mu[:U], mi[:I]
+
+
+def _io_support(pair, mu: Tensor, mi: Tensor, order: str, users: Optional[Tensor] = None):
+    """grad_support of an input-order pair (propagate.backward_steps): (user mask,
+    item mask) in the caller's input order plus the item mask in the graph's
+    internal order (the first item product's row mask); GS adds the item
+    neighbours of every flagged user (of `users`, input ids, when given) to both
+    item masks."""
+    from .propagate import ORDER_GS
+    io = pair.io
+    if order != ORDER_GS:
+        return mu, mi, None
+    st = stream_handle()
+    mi_int = mi[io.item_map64]
+    uc = pair.fwd_user.csr
+    if users is not None:
+        ui = io.user_rank64[users]
+        call("bbgr_mark_neighbors", ui.numel(), _lib.ptr(ui), _lib.ptr(uc.indptr),
+             _lib.ptr(uc.indices), 1, _lib.ptr(mi_int), st)
+    else:
+        call("bbgr_mark_neighbors_of_mask", pair.num_users, _lib.ptr(mu), _lib.ptr(io.user_map),
+             _lib.ptr(uc.indptr), _lib.ptr(uc.indices), 1, _lib.ptr(mi_int), st)
+    return mu, mi_int[io.item_rank64], mi_int
 
 
 @custom_op("bbgr::propagate_backward", mutates_args=())
@@ -151,6 +178,9 @@ def propagate_backward_rows(iu: Tensor, vu: Tensor, gI: Tensor, num_users: int, 
     mi = torch.empty(max(I, 1), dtype=torch.uint8, device=vu.device)
     call("bbgr_mark_rows", iu.numel(), _lib.ptr(iu), 1, _lib.ptr(mu), U, st)
     call("bbgr_row_support", I, d, _lib.ptr(gI), _lib.ld(gI), _lib.ptr(mi), None, None, None, st)
+    if pair.io is not None:   # input-order tables over a degree-ordered graph
+        return backward(pair, gU, gI, num_layers, order,
+                        grad_support=_io_support(pair, mu[:U], mi[:I], order, users=iu))
     if order == ORDER_GS:   # the first item product's output support: N(listed users)
         uc = pair.fwd_user.csr
         call("bbgr_mark_neighbors", iu.numel(), _lib.ptr(iu), _lib.ptr(uc.indptr),
@@ -197,8 +227,11 @@ def jacobi_layer(u: Tensor, i: Tensor, pair_key: int) -> tuple[Tensor, Tensor]:
     FI, FU = pair.fwd_item, pair.fwd_user
     new_i = torch.empty(pair.num_items, u.shape[1], device=u.device)
     new_u = torch.empty(pair.num_users, u.shape[1], device=u.device)
-    spmm(FI, u, True, y=new_i, y_scale=FI.out_scale)
-    spmm(FU, i, True, y=new_u, y_scale=FU.out_scale)
+    io = pair.io   # input-order layer tables: input-id gathers, mapped output rows
+    spmm(FI, u, True, y=new_i, y_scale=FI.out_scale, src_input=io is not None,
+         y_map=None if io is None else io.item_map)
+    spmm(FU, i, True, y=new_u, y_scale=FU.out_scale, src_input=io is not None,
+         y_map=None if io is None else io.user_map)
     return new_i, new_u
 
 
@@ -215,8 +248,11 @@ def jacobi_layer_backward(g_i: Tensor, g_u: Tensor, pair_key: int) -> tuple[Tens
     BI, BU = pair.bwd_item, pair.bwd_user
     gu = torch.empty(pair.num_users, g_i.shape[1], device=g_i.device)
     gi = torch.empty(pair.num_items, g_u.shape[1], device=g_u.device)
-    spmm(BU, g_i.contiguous(), True, y=gu, y_scale=BU.out_scale)
-    spmm(BI, g_u.contiguous(), True, y=gi, y_scale=BI.out_scale)
+    io = pair.io
+    spmm(BU, g_i.contiguous(), True, y=gu, y_scale=BU.out_scale, src_input=io is not None,
+         y_map=None if io is None else io.user_map)
+    spmm(BI, g_u.contiguous(), True, y=gi, y_scale=BI.out_scale, src_input=io is not None,
+         y_map=None if io is None else io.item_map)
     return gu, gi
 
 

@@ -52,6 +52,27 @@ class Product:
     out_scale: torch.Tensor | None
     partial: dict
     first_vals: torch.Tensor | None = None
+    col_input_map: torch.Tensor | None = None   # internal column id -> input id (int32)
+
+    def input_struct(self):
+        """The CSR with INPUT-id column indices (built once, 4 B/edge, shared by
+        the products over the same CSR): a first product of an input-order pair
+        gathers the caller's input-order table through it."""
+        c = self.csr
+        st = c.__dict__.get("_input_struct")
+        if st is None:
+            idx = c.__dict__.get("_input_indices")   # kept by the graph build
+            if idx is None:
+                if self.col_input_map is None:
+                    raise RuntimeError("product has no input-id column map")
+                idx = torch.empty(max(c.nnz, 1), dtype=torch.int32, device=c.device)
+                call("bbgr_relabel", c.nnz, ptr(c.indices), ptr(self.col_input_map), ptr(idx),
+                     stream_handle())
+                c.__dict__["_input_indices"] = idx
+            st = c.struct(with_plan=True)
+            st.indices = ptr(idx)
+            c.__dict__["_input_struct"] = st
+        return st
 
     def first_layer_values(self) -> torch.Tensor:
         """in_scale[col] per CSR slot (built once, 4 B/edge): the first product of
@@ -90,6 +111,20 @@ class Product:
             self.partial[(d, "graph")] = self.csr.partial_workspace(d)
 
 
+@dataclass
+class InputOrder:
+    """Vertex maps of an input-order pair: *_map[internal] = input id,
+    *_rank[input id] = internal (int32, graph.VertexOrder perm / rank)."""
+    user_map: torch.Tensor
+    item_map: torch.Tensor
+    user_rank: torch.Tensor
+    item_rank: torch.Tensor
+
+    def __post_init__(self):   # int64 copies for torch indexing (built once)
+        self.user_map64, self.item_map64 = self.user_map.long(), self.item_map.long()
+        self.user_rank64, self.item_rank64 = self.user_rank.long(), self.item_rank.long()
+
+
 class OperatorPair:
     """The four products of one bipartite operator pair (fwd item<-user,
     fwd user<-item, and their transposes for the backward)."""
@@ -104,6 +139,20 @@ class OperatorPair:
         # feed vectors: output scale of a product x input scale of the next one
         self.feed_fwd_iu, self.feed_fwd_ui = feed_fwd_iu, feed_fwd_ui
         self.feed_bwd_iu, self.feed_bwd_ui = feed_bwd_iu, feed_bwd_ui
+        self.io: InputOrder | None = None
+
+    def set_input_order(self, user_order, item_order) -> None:
+        """The pair's graph is numbered by descending degree (graph.VertexOrder
+        per side) but its callers' tables — u0 / i0, the final tables, the
+        gradients — stay in INPUT order: the first products gather through
+        input-id column indices and the epilogues place input-order rows
+        through row maps (bbgr_spmm_args.y_map / acc_map / add_map). The drop-in
+        modules get the hot-prefix / streaming policy of the degree order
+        without a permute of any table."""
+        self.io = InputOrder(user_order.perm, item_order.perm, user_order.rank,
+                             item_order.rank)
+        self.fwd_item.col_input_map = self.bwd_item.col_input_map = self.io.user_map
+        self.fwd_user.col_input_map = self.bwd_user.col_input_map = self.io.item_map
 
     def prepare_graph(self, d: int) -> None:
         """Workspaces of a graph capture of this pair's products (width d)."""
@@ -210,7 +259,7 @@ class SpmmTimer:
         return out
 
     def count_launch(self, prod: "Product", kind: str, d: int, rng, src_mask, row_mask,
-                     row_list) -> None:
+                     row_list, src_input: bool = False) -> None:
         """Device-side count of the rows / edges one launch processes (stream-
         ordered torch ops on the launch's own masks, read after the steps)."""
         c = prod.csr
@@ -231,7 +280,8 @@ class SpmmTimer:
         if src_mask is None:
             gathered = visited
         else:
-            live = src_mask[c.indices[:c.nnz].long()].bool()
+            cols = c.__dict__["_input_indices"] if src_input else c.indices
+            live = src_mask[cols[:c.nnz].long()].bool()
             gathered = (live & torch.repeat_interleave(sel, deg)).sum()
         self.counts.append((kind, mask_signature(src_mask, row_mask, row_list), c.n_rows,
                             c.n_cols, d, sel.sum(), visited, gathered))
@@ -255,9 +305,13 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          y_scale_s: float = 1.0, add=None, add_scale=None, add_scale_s: float = 1.0,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
-         add_mask=None, row_list=None, rng=None, adam=None) -> None:
+         add_mask=None, row_list=None, rng=None, adam=None, y_map=None, acc_map=None,
+         add_map=None, src_input: bool = False) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream. `adam`
-    (optim.AdamRows): apply Adam to each row's y value in the epilogue."""
+    (optim.AdamRows): apply Adam to each row's y value in the epilogue.
+    `y_map` / `acc_map` / `add_map`: row maps of those tables (input-order
+    tables of a degree-ordered pair); `src_input`: x is gathered through the
+    CSR's input-id column indices (Product.input_struct)."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
     a.d = d
@@ -287,20 +341,23 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
             a.range[k] = rng[k]
     if adam is not None:
         adam.fill(a)
-    a.stream_from = prod.csr.stream_from(d)
-    a.stream_out_from = prod.csr.stream_out_from(d)
+    a.y_map, a.acc_map, a.add_map = ptr(y_map), ptr(acc_map), ptr(add_map)
+    # input-order source rows carry no hot prefix; mapped output rows neither
+    a.stream_from = 0 if src_input else prod.csr.stream_from(d)
+    a.stream_out_from = 0 if y_map is not None else prod.csr.stream_out_from(d)
+    cs = prod.input_struct() if src_input else prod.csr._struct
     if _timer is None:
-        call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
+        call("bbgr_spmm", ctypes.byref(cs), ctypes.byref(a), stream_handle())
         return
     masked = src_mask is not None or row_mask is not None or row_list is not None
     kind = "masked" if masked else ("adam" if adam is not None else "full")
     if _timer.count:
-        call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
-        _timer.count_launch(prod, kind, d, rng, src_mask, row_mask, row_list)
+        call("bbgr_spmm", ctypes.byref(cs), ctypes.byref(a), stream_handle())
+        _timer.count_launch(prod, kind, d, rng, src_mask, row_mask, row_list, src_input)
         return
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    call("bbgr_spmm", ctypes.byref(prod.csr._struct), ctypes.byref(a), stream_handle())
+    call("bbgr_spmm", ctypes.byref(cs), ctypes.byref(a), stream_handle())
     ev1.record()
     rows, nnz = prod.csr.n_rows, prod.csr.nnz
     if rng is not None and row_list is None:   # a row range: its own rows and edges
@@ -345,6 +402,9 @@ def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw
     if reduce is None:
         spmm(prod, x, first, **kw)
         return
+    for key in ("y_map", "acc_map", "add_map", "src_input"):   # input-order pairs only
+        if kw.pop(key, None):
+            raise ValueError("sharded item products take no input-order maps")
     if hasattr(reduce, "item_product"):   # chunked / overlapped exchange
         reduce.item_product(prod, x, first, new, kw)
         return
@@ -419,6 +479,13 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
     FI, FU = pair.fwd_item, pair.fwd_user
     new = _buffers(ws, u0.device, d)
     mu, mi, ulist = (tuple(final_rows) + (None,))[:3] if final_rows is not None else (None,) * 3
+    io = pair.io   # input-order tables over a degree-ordered graph (set_input_order)
+    if io is not None and (reduce is not None or final_rows is not None):
+        raise ValueError("an input-order pair takes neither a reduce hook nor final_rows")
+    # the layer-mean accumulators hold the caller's (input-order) rows: every
+    # epilogue places them through the side's map; the first products gather
+    # the input-order u0 / i0 through input-id column indices
+    am_u, am_i = (io.user_map, io.item_map) if io is not None else (None, None)
     if order == ORDER_GS:
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(1, K + 1):
@@ -427,12 +494,13 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
             _item_product(FI, u0 if k == 1 else bufU, k == 1, reduce, new, y=bufI,
                           y_scale=pair.feed_fwd_iu, acc_in=i0 if k == 1 else acc_i,
                           acc_out=acc_i, acc_scale=FI.out_scale, gamma=g,
-                          row_mask=mi if last else None, acc_mask=mi)
+                          row_mask=mi if last else None, acc_mask=mi, acc_map=am_i,
+                          src_input=io is not None and k == 1)
             yield
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
                  acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
-                 acc_mask=mu, row_list=ulist if last else None)
+                 acc_mask=mu, row_list=ulist if last else None, acc_map=am_u)
     elif order == ORDER_J:
         bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
         cur = 0
@@ -444,13 +512,14 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
                           y=bufI[nxt] if k < K else None, y_scale=pair.feed_fwd_iu,
                           acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
                           acc_scale=FI.out_scale, gamma=g, row_mask=mi if last else None,
-                          acc_mask=mi)
+                          acc_mask=mi, acc_map=am_i, src_input=io is not None and k == 1)
             yield
             spmm(FU, i0 if k == 1 else bufI[cur], k == 1,
                  y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
                  acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
-                 acc_mask=mu, row_list=ulist if last else None)
+                 acc_mask=mu, row_list=ulist if last else None, acc_map=am_u,
+                 src_input=io is not None and k == 1)
             cur = nxt
     else:
         raise ValueError(f"unknown propagation order {order!r}")
@@ -499,7 +568,22 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     gl = 1.0 / (K + 1)
     BI, BU = pair.bwd_item, pair.bwd_user
     new = _buffers(ws, gU.device, d)
-    su, si = grad_support if grad_support is not None else (None, None)
+    io = pair.io
+    if io is not None and reduce is not None:
+        raise ValueError("an input-order pair takes no reduce hook")
+    # input-order pair: gU / gI / the outputs are in the caller's order (row
+    # maps on add / y, input-id gathers in the first products); grad_support
+    # is then (su, si, si_internal): su / si index input-order rows (the add
+    # tables' and the first products' sources), si_internal the item CSR rows
+    if grad_support is None:
+        su = si = si_int = None
+    elif io is not None:
+        su, si, si_int = grad_support
+    else:
+        su, si = grad_support
+        si_int = si
+    um, im = (io.user_map, io.item_map) if io is not None else (None, None)
+    inp = io is not None
     if order == ORDER_GS:
         bufU, bufI = new("u0", U), new("i0", I)
         for k in range(K, 0, -1):
@@ -511,20 +595,21 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                           y_scale=pair.feed_bwd_iu, y_scale_s=gl if first else 1.0,
                           add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
                           src_mask=su if first else None,
-                          row_mask=si if first else None)
+                          row_mask=si_int if first else None, add_map=im,
+                          src_input=inp and first)
             yield
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
                      add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl,
-                     src_mask=si if first else None)
+                     src_mask=si_int if first else None, add_map=um)
             else:
                 if before_last is not None:
                     before_last()
-                src = si if first else None
+                src = si_int if first else None
                 fused = adam_u is not None and src is None   # fused Adam needs every row
                 spmm(BU, bufI, False, y=None if fused else gu0, y_scale=BU.out_scale,
                      add=gU, add_mask=su, add_scale=None, add_scale_s=gl,
-                     src_mask=src, adam=adam_u if fused else None)
+                     src_mask=src, adam=adam_u if fused else None, add_map=um, y_map=um)
                 if adam_u is not None and not fused:   # K == 1: masked product, Adam apart
                     adam_u.apply(gu0)
         if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
@@ -544,22 +629,25 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
             xi = gU if first else bufU[cur]   # input of BI (user table)
             mu_ = si if first else None     # BU reads gI (items), BI reads gU (users)
             mi_ = su if first else None
+            src_in = inp and first           # gI / gU: input order
             if k > 1:
                 spmm(BU, xu, first, y=bufU[nxt], y_scale=pair.feed_bwd_ui, y_scale_s=ys,
-                     add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl, src_mask=mu_)
+                     add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl, src_mask=mu_,
+                     add_map=um, src_input=src_in)
                 _item_product(BI, xi, first, reduce, new, y=bufI[nxt],
                               y_scale=pair.feed_bwd_iu, y_scale_s=ys,
-                              add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl, src_mask=mi_)
+                              add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
+                              src_mask=mi_, add_map=im, src_input=src_in)
                 yield
             else:
                 if before_last is not None and adam_u is not None:
                     before_last()
                 spmm(BU, xu, first, y=None if adam_u is not None else gu0, y_scale=BU.out_scale,
                      y_scale_s=ys, add=gU, add_mask=su, add_scale=None, add_scale_s=gl,
-                     src_mask=mu_, adam=adam_u)
+                     src_mask=mu_, adam=adam_u, add_map=um, y_map=um, src_input=src_in)
                 ik = dict(y=None if adam_i is not None else gi0, y_scale=BI.out_scale,
                           y_scale_s=ys, add=gI, add_mask=si, add_scale=None, add_scale_s=gl,
-                          src_mask=mi_)
+                          src_mask=mi_, add_map=im, y_map=im, src_input=src_in)
                 if adam_i is not None:
                     ik["adam"] = adam_i
                 _item_product(BI, xi, first, reduce, new, **ik)

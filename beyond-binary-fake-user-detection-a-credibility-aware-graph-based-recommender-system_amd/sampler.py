@@ -36,6 +36,8 @@ class PopMixSampler:
                  mix_pop: float = 0.7, gamma: float | None = 0.75, max_tries: int = 50,
                  seed: int = 42):
         _lib.require_gpu()
+        if not user_csr.cols_sorted:
+            raise ValueError("the sampler's membership search needs column-sorted CSR rows")
         self.csr = user_csr
         self.num_items = int(num_items)
         self.mix_pop = float(mix_pop)

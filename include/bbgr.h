@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 3
+#define BBGR_ABI_VERSION 4
 
 typedef enum {
   BBGR_OK = 0,
@@ -219,6 +219,16 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   from device memory (bbgr_step_begin's state[0]) and its bias corrections */
 /*   from adam_bc_table[2(t-1)], [2(t-1)+1] instead of the two float fields,  */
 /*   so a captured step (hipGraph) replays with the right t every time.       */
+/* y_map / acc_map / add_map (nullable, int32 [n_rows]): row maps of the      */
+/*   epilogue's tables. CSR row r writes row y_map[r] of y (and updates row   */
+/*   y_map[r] of the fused Adam's tables), reads / writes row acc_map[r] of    */
+/*   acc_in / acc_out and reads row add_map[r] of add; acc_mask / add_mask    */
+/*   index the mapped rows. Scale vectors stay indexed by r. Lets a graph      */
+/*   numbered by descending degree serve tables the caller holds in its own    */
+/*   (input) order: the drop-in modules' first products gather input-order    */
+/*   rows through input-id column indices, and these maps place every        */
+/*   input-order output row, so no table is permuted. stream_out_from must be */
+/*   0 when y_map is set.                                                      */
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
@@ -272,6 +282,9 @@ typedef struct {
   int32_t stream_out_from;
   const float *adam_bc_table;
   const int64_t *adam_state;
+  const int32_t *y_map;
+  const int32_t *acc_map;
+  const int32_t *add_map;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -450,6 +463,13 @@ int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value, uint8_t *mask,
 int bbgr_mark_neighbors(int64_t n, const int64_t *rows, const int32_t *indptr,
                         const int32_t *indices, uint8_t value, uint8_t *mask,
                         bbgr_stream_t stream);
+/* The same for every CSR row r < n_rows flagged in row_mask: row_mask[r], or
+ * row_mask[row_map[r]] when row_map is given (a mask kept in the caller's
+ * vertex order over a CSR numbered by descending degree). */
+int bbgr_mark_neighbors_of_mask(int64_t n_rows, const uint8_t *row_mask,
+                                const int32_t *row_map, const int32_t *indptr,
+                                const int32_t *indices, uint8_t value, uint8_t *mask,
+                                bbgr_stream_t stream);
 
 /* mask[r] = 1 if row r of x [n_rows, d] (leading dimension ldx) holds a
  * nonzero, else 0 (every row written; -0.0 counts as zero). With a CSR

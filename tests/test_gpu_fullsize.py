@@ -1,33 +1,41 @@
 """Full-size parity at the BASELINE workloads (north_star:
-"layer-K embeddings match the reference forward to 1e-5 rel").
+"layer-K embeddings match the reference CPU/PyTorch forward to 1e-5 rel on
+identical inputs").
 
-The float64 oracle cannot hold a 50M/500M-edge propagation in host memory,
-so each product is checked on sampled output rows instead: the GPU computes
-layer k from its own layer k-1 (the drop-in operators' products, the
-torch.sparse.mm calls of the reference's propagate loop), and the oracle
-recomputes ~10k of layer k's rows in float64 from their CSR neighbourhoods
-in the host edge list, with the reference's fp32 operator values
-(oracle/ref_numpy.edge_weights, from host-side degrees). Every layer and
-side is checked; then the fused training-path forward (degree-ordered graph,
-the bench's layout) is checked against the float64 layer mean of the same
-rows; at C4 the first training step's weight gradients are checked the same
-way through every backward product.
+Every GPU result here is compared with a float64 chain computed on the host
+from the SAME u0 / i0 (oracle/chain64.py over oracle/csrc/chain64.c): the
+reference's K-layer propagation (Version-2/lighgcn_cu_pop.py:472-490,
+lightgcn_cu.py:420-448) with the reference's fp32 operator values
+(oracle/ref_numpy.edge_weights, host-side degrees), in float64, every layer.
+No assertion compares the GPU with its own intermediates. Checked per config:
 
-Sampled rows: random rows of each side, plus high-degree rows (the chunked,
-fixed-order long-row path) up to an edge budget, plus (gradient test) the
-batch rows. Tolerance: normwise relative <= 1e-5 and max-abs <= 1e-5*max|ref|
-over the sampled rows.
+  * every layer k and side of the drop-in operators' chain (the
+    torch.sparse.mm calls of the reference's propagate loop, BipartiteOperator.mm);
+  * the drop-in module's final tables (LightGCN.propagate() /
+    CredLightGCN.final_embeddings(), i.e. the bbgr::propagate op);
+  * the fused training path's forward (degree-ordered graph, the bench layout);
+  * C4: the first fused training step's loss (float64 BPR of the step's batch
+    on the float64 final tables) and grad(u0) / grad(i0) (float64 adjoint chain
+    of that BPR gradient, Version-2:862 autograd).
+
+Compared rows: random rows of each side, the heaviest rows up to an edge
+budget (the chunked, fixed-order long-row path) and (C4 gradients) the batch
+rows. Tolerance: normwise relative <= 1e-5 and max-abs <= 1e-5*max|ref| over
+the compared rows. C5 (500M edges, d=256) runs its float64 chain on 16 of the
+256 columns (propagation acts on each column alone, so those columns are the
+whole chain's; all 256 columns at 500M edges would take ~10 min of host time).
 
   C1  lightgcn.py symmetric path, 943 x 1682, 100K edges, d=64, K=3:
       whole tables against tests/golden/golden_c1.npz (every layer, final,
       BPR loss, gradient of emb.weight)
   C3  lightgcn_cu.py Jacobi path, Beta credibility, 5M x 1M, 50M edges, d=128, K=3
   C4  Version-2 GS path, Beta credibility, 5M x 1M, 50M edges, d=64, K=3
-      (+ the first training step's gradients, B=8192)
+      (+ the first training step's loss and gradients, B=8192)
   C5  GS path, 10M x 2M, 500M edges, d=256, K=4 (the 8-GPU config, on one GPU)
 """
 import multiprocessing as mp
 import os
+import time
 
 import numpy as np
 import pytest
@@ -38,6 +46,7 @@ pytestmark = pytest.mark.gpu
 from bbgr.synthetic import (CONFIGS, CONFIG_SEED, config_edges,  # noqa: E402
                             shard_edges_strong, synthetic_credibility)
 from oracle import ref_numpy as R  # noqa: E402
+from oracle.chain64 import Chain64  # noqa: E402
 
 DEV = "cuda"
 TOL = 1e-5
@@ -67,24 +76,14 @@ def _c5_shard(rank_world):
     return e
 
 
-_EDGES = {}
-
-
 def workload_edges(name: str) -> np.ndarray:
     """The config's synthetic graph. C5 (500M edges) is drawn as the union of
-    its 8 user shards (the graph the 8-GPU run trains on), in parallel. C4's
-    graph is kept for the gradient test."""
-    if name in _EDGES:
-        return _EDGES[name]
+    its 8 user shards (the graph the 8-GPU run trains on), in parallel."""
     if name != "C5":
-        e = config_edges(name)
-    else:
-        with mp.get_context("spawn").Pool(8) as pool:
-            parts = pool.map(_c5_shard, [(r, 8) for r in range(8)])
-        e = np.concatenate(parts, axis=1)
-    if name == "C4":
-        _EDGES[name] = e
-    return e
+        return config_edges(name)
+    with mp.get_context("spawn").Pool(8) as pool:
+        parts = pool.map(_c5_shard, [(r, 8) for r in range(8)])
+    return np.concatenate(parts, axis=1)
 
 
 def device_tables(U, I, d, seed=42):
@@ -112,42 +111,26 @@ def sample_rows(deg: np.ndarray, rng, n: int, budget: int, extra=None) -> np.nda
     return np.unique(np.concatenate(parts))
 
 
-class SideEdges:
-    """The host edges whose OUTPUT row (on one side) is in a sampled set."""
-
-    def __init__(self, out_ids: np.ndarray, src_ids: np.ndarray, n_out: int, sel: np.ndarray,
-                 w_all_fn):
-        m = np.zeros(n_out, bool)
-        m[sel] = True
-        k = np.flatnonzero(m[out_ids])
-        self.sel = sel
-        self.rows = out_ids[k].astype(np.int64)
-        self.cols = src_ids[k].astype(np.int64)
-        self.k = k
-        self.w = w_all_fn(k)     # fp32 values of these edges (oracle expressions)
+def gpu_rows(t: torch.Tensor, sel: np.ndarray, cols=None) -> np.ndarray:
+    r = t[torch.from_numpy(np.asarray(sel, np.int64)).to(t.device)]
+    if cols is not None:
+        r = r[:, torch.from_numpy(cols).to(t.device)]
+    return r.double().cpu().numpy()
 
 
-def oracle_rows(side: SideEdges, x_gpu: torch.Tensor, chunk: int = 1 << 20) -> np.ndarray:
-    """float64 rows side.sel of (M x) from the GPU's x (its fp32 values)."""
-    out = np.zeros((side.sel.size, x_gpu.shape[1]), np.float64)
-    for a in range(0, side.rows.size, chunk):
-        cols = side.cols[a:a + chunk]
-        uniq, inv = np.unique(cols, return_inverse=True)
-        xs = x_gpu[torch.from_numpy(uniq).to(x_gpu.device)].cpu().numpy()
-        out += R.rows_product(side.sel, side.rows[a:a + chunk], cols,
-                              side.w[a:a + chunk], xs[inv])
-    return out
+def host_cols(t: torch.Tensor, cols=None) -> np.ndarray:
+    """The fp32 device table (or its `cols` columns) as a float64 host array."""
+    if cols is not None:
+        t = t[:, torch.from_numpy(cols).to(t.device)]
+    return t.double().cpu().numpy()
 
 
-def gpu_rows(t: torch.Tensor, sel: np.ndarray) -> np.ndarray:
-    return t[torch.from_numpy(sel).to(t.device)].double().cpu().numpy()
-
-
-KINDS = {   # config -> operator family, drop-in builder, fused-trainer variant
-    "C3": ("j", "cu_fair"),
-    "C4": ("gs", "v2_pop"),
-    "C5": ("gs", "v2_pop"),
+KINDS = {   # config -> operator family, propagation order, fused-trainer variant
+    "C3": ("j", "jacobi", "cu_fair"),
+    "C4": ("gs", "gs", "v2_pop"),
+    "C5": ("gs", "gs", "v2_pop"),
 }
+CHAIN_COLS = {"C5": 16}   # float64 chain on a column subset (see the docstring)
 
 
 def drop_in_operators(kind, e, U, I, cred):
@@ -163,47 +146,83 @@ def drop_in_operators(kind, e, U, I, cred):
     raise ValueError(kind)
 
 
-def run_layers(name, check_grads=False):
+def drop_in_model(kind, e, U, I, d, K, cred, u0, i0):
+    """The reference-named module (Version-2 LightGCN / lightgcn_cu
+    CredLightGCN) on its own builders, weights set to u0 / i0; returns its
+    final tables (the caller's propagate() / final_embeddings())."""
+    if kind == "gs":
+        from bbgr.lightgcn_cu_pop import LightGCN as Model, build_message_passing_mats
+        ops = build_message_passing_mats(e, U, I, torch.from_numpy(cred).to(DEV), DEV)
+    else:
+        from bbgr.lightgcn_cu import CredLightGCN as Model, build_cred_weighted_mats
+        ops = build_cred_weighted_mats(e, U, I, cred, DEV)[:2]
+    with torch.device(DEV):   # (the module's own xavier init on the device: C5 is 12 GB)
+        m = Model(U, I, d, K, *ops)
+    with torch.no_grad():
+        m.user_emb.weight.copy_(u0)
+        m.item_emb.weight.copy_(i0)
+        uf, itf = m.propagate() if kind == "gs" else m.final_embeddings()
+    return m, uf, itf
+
+
+def _progress(t0, what):
+    """A line per stage (a C5 run takes minutes; run with -s to see them)."""
+    print(f"[fullsize {time.perf_counter() - t0:7.1f} s] {what}", flush=True)
+
+
+def run_full(name, check_grads=False):
+    """Every GPU form of the config's forward against the float64 chain from
+    the same u0 / i0; returns the state the gradient check continues from."""
+    t0 = time.perf_counter()
     c = CONFIGS[name]
     U, I, d, K = c["num_users"], c["num_items"], c["emb_dim"], c["num_layers"]
-    kind, variant = KINDS[name]
+    kind, order, variant = KINDS[name]
     e = workload_edges(name)
     assert e.shape[1] == c["num_edges"]
     cred = synthetic_credibility(U, CONFIG_SEED[name], "beta")
-    deg_u, deg_i = R.degrees(e, U, I)
     rng = np.random.default_rng(CONFIG_SEED[name])
+    cols = None
+    if name in CHAIN_COLS:
+        cols = np.sort(rng.choice(d, CHAIN_COLS[name], replace=False))
+    _progress(t0, f"{name}: graph drawn ({e.shape[1]} edges)")
+    chain = Chain64(e, U, I, kind, cred)
+    _progress(t0, f"{name}: float64 operator CSRs built")
     budget = 2_000_000 if d <= 128 else 1_000_000
-    sel_u = sample_rows(deg_u.astype(np.int64), rng, N_SAMPLE, budget)
-    sel_i = sample_rows(deg_i.astype(np.int64), rng, N_SAMPLE, budget)
-
-    def w_fn(k):
-        return R.edge_weights(kind, e[0, k], e[1, k], deg_u, deg_i, cred)
-
-    ue = SideEdges(e[0], e[1], U, sel_u, lambda k: w_fn(k)[0])   # user rows <- items
-    ie = SideEdges(e[1], e[0], I, sel_i, lambda k: w_fn(k)[1])   # item rows <- users
-    item_op, user_op = drop_in_operators(kind, e, U, I, cred)
+    sel_u = sample_rows(chain.deg_u.astype(np.int64), rng, N_SAMPLE, budget)
+    sel_i = sample_rows(chain.deg_i.astype(np.int64), rng, N_SAMPLE, budget)
     u0, i0 = device_tables(U, I, d)
-    us, is_ = [gpu_rows(u0, sel_u)], [gpu_rows(i0, sel_i)]
+    u0h, i0h = host_cols(u0, cols), host_cols(i0, cols)
+    ruf, ritf, lay_u, lay_i = chain.forward(u0h, i0h, K, order, keep_u=sel_u, keep_i=sel_i)
+    _progress(t0, f"{name}: float64 chain done ({'all' if cols is None else len(cols)} columns)")
+    tag = f"{name} {kind}"
+
+    # (1) the drop-in operators' layer chain (the reference's propagate loop)
+    item_op, user_op = drop_in_operators(kind, e, U, I, cred)
     u, i = u0, i0
     for k in range(1, K + 1):
-        if kind == "gs":     # Version-2:482-487: items first, users from the NEW items
+        if order == "gs":      # Version-2:482-487: items first, users from the NEW items
             i_new = item_op.mm(u)
             u_new = user_op.mm(i_new)
-            want_i, want_u = oracle_rows(ie, u), oracle_rows(ue, i_new)
-        else:                # lightgcn_cu.py:429-447: both sides from layer k-1
+        else:                  # lightgcn_cu.py:429-447: both sides from layer k-1
             i_new, u_new = item_op.mm(u), user_op.mm(i)
-            want_i, want_u = oracle_rows(ie, u), oracle_rows(ue, i)
-        got_i, got_u = gpu_rows(i_new, sel_i), gpu_rows(u_new, sel_u)
-        assert_parity(got_i, want_i, f"{name} {kind} item layer {k}")
-        assert_parity(got_u, want_u, f"{name} {kind} user layer {k}")
-        us.append(got_u)
-        is_.append(got_i)
+        assert_parity(gpu_rows(i_new, sel_i, cols), lay_i[k], f"{tag} item layer {k}")
+        assert_parity(gpu_rows(u_new, sel_u, cols), lay_u[k], f"{tag} user layer {k}")
         if k > 1:
             del u, i
         u, i = u_new, i_new
     del u, i, item_op, user_op
     torch.cuda.empty_cache()
-    # the fused training-path forward on the degree-ordered graph (bench layout)
+    _progress(t0, f"{name}: drop-in operator layers checked")
+
+    # (2) the drop-in module's final tables (bbgr::propagate)
+    m, uf, itf = drop_in_model(kind, e, U, I, d, K, cred, u0, i0)
+    assert_parity(gpu_rows(uf, sel_u, cols), ruf[sel_u], f"{tag} drop-in module u_final")
+    assert_parity(gpu_rows(itf, sel_i, cols), ritf[sel_i], f"{tag} drop-in module i_final")
+    del m, uf, itf
+    torch.cuda.empty_cache()
+    _progress(t0, f"{name}: drop-in module finals checked")
+
+    # (3) the fused training path's forward (degree-ordered graph, bench layout)
     from bbgr.graph import BipartiteGraph
     from bbgr.trainer import FusedTrainer
     graph = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
@@ -211,90 +230,56 @@ def run_layers(name, check_grads=False):
                       batch_size=c["batch"], u0=u0, i0=i0, fuse_adam=not check_grads)
     del u0, i0
     uf, itf = tr.forward()
-    assert_parity(gpu_rows(uf, sel_u), np.mean(us, 0), f"{name} fused forward u_final")
-    assert_parity(gpu_rows(itf, sel_i), np.mean(is_, 0), f"{name} fused forward i_final")
-    out = dict(e=e, cred=cred, U=U, I=I, d=d, K=K, kind=kind, tr=tr, uf=uf, itf=itf,
-               deg_u=deg_u, deg_i=deg_i, rng=rng, budget=budget)
-    return out
+    assert_parity(gpu_rows(uf, sel_u, cols), ruf[sel_u], f"{tag} fused forward u_final")
+    assert_parity(gpu_rows(itf, sel_i, cols), ritf[sel_i], f"{tag} fused forward i_final")
+    del uf, itf
+    _progress(t0, f"{name}: fused-trainer forward checked")
+    if not check_grads:
+        return None
+    return dict(e=e, U=U, I=I, d=d, K=K, tr=tr, chain=chain, ruf=ruf, ritf=ritf,
+                u0h=u0h, i0h=i0h, rng=rng, budget=budget)
 
 
-@pytest.mark.parametrize("name", ["C3", "C4", "C5"])
-def test_every_layer_and_fused_forward_full_size(name):
-    run_layers(name)
+@pytest.mark.parametrize("name", ["C3", "C5"])
+def test_full_chain_every_layer_and_finals(name):
+    run_full(name)
     torch.cuda.empty_cache()
 
 
-def test_c4_first_training_step_gradients_full_size():
-    """The first fused training step at C4 (frontier masks, degree order,
-    B=8192 pop-mix batch): loss vs the float64 BPR of the step's batch on the
-    GPU final tables, and grad(u0) / grad(i0) on sampled + batch rows vs the
-    backward chain evaluated product by product (each product checked against
-    the float64 oracle from its GPU input)."""
-    from bbgr.lightgcn_cu_pop import build_message_passing_mats
-    from bbgr.propagate import spmm
+def test_c4_full_chain_and_first_training_step():
+    """C4 forward as above, then the first fused training step (frontier masks,
+    degree order, B=8192 pop-mix batch): its loss against the float64 BPR
+    (Version-2:495-508) of the step's batch on the float64 final tables, and
+    grad(u0) / grad(i0) on sampled + batch rows against the float64 adjoint
+    chain of that BPR gradient plus the ego-L2 rows."""
     from bbgr.trainer import _input_rows
-    w = run_layers("C4", check_grads=True)
-    tr, e, cred, U, I, d, K = (w[k] for k in ("tr", "e", "cred", "U", "I", "d", "K"))
-    deg_u, deg_i, rng, budget = w["deg_u"], w["deg_i"], w["rng"], w["budget"]
-    uf, itf = w["uf"], w["itf"]                      # forward of the step's weights (input ids)
-    u0 = _input_rows(tr.graph.user_order, tr.user_w).clone()
-    i0 = _input_rows(tr.graph.item_order, tr.item_w).clone()
+    w = run_full("C4", check_grads=True)
+    tr, chain, U, I, d, K = (w[k] for k in ("tr", "chain", "U", "I", "d", "K"))
+    ruf, ritf, u0h, i0h = w["ruf"], w["ritf"], w["u0h"], w["i0h"]
     loss = float(tr.step())
     users, pos, neg = (x.cpu().numpy() for x in tr.batch())
     g_u0 = _input_rows(tr.graph.user_order, tr.g_u0)
     g_i0 = _input_rows(tr.graph.item_order, tr.g_i0)
-    # float64 BPR on compact tables of the batch rows (Version-2:495-508)
     bu, inv_u = np.unique(users, return_inverse=True)
     bi, inv_i = np.unique(np.concatenate([pos, neg]), return_inverse=True)
     B = users.size
-    want_loss, g = R.bpr_loss(gpu_rows(uf, bu), gpu_rows(itf, bi), gpu_rows(u0, bu),
-                              gpu_rows(i0, bi), inv_u, inv_i[:B], inv_i[B:], tr.reg)
+    want_loss, g = R.bpr_loss(ruf[bu], ritf[bi], u0h[bu], i0h[bi], inv_u, inv_i[:B],
+                              inv_i[B:], tr.reg)
     assert abs(loss - want_loss) <= TOL * abs(want_loss), (loss, want_loss)
-    gU = torch.zeros(U, d, device=DEV)
-    gI = torch.zeros(I, d, device=DEV)
-    gU[torch.from_numpy(bu).to(DEV)] = torch.from_numpy(g["g_uf"]).float().to(DEV)
-    gI[torch.from_numpy(bi).to(DEV)] = torch.from_numpy(g["g_if"]).float().to(DEV)
-    # sampled rows now include the batch rows (the BPR terms land there)
-    sel_u = sample_rows(deg_u.astype(np.int64), rng, N_SAMPLE, budget, extra=bu[:2000])
-    sel_i = sample_rows(deg_i.astype(np.int64), rng, N_SAMPLE, budget, extra=bi[:2000])
-
-    def w_fn(k):
-        return R.edge_weights("gs", e[0, k], e[1, k], deg_u, deg_i, cred)
-
-    # transposed products: M_ui^T (item rows <- users, values of M_ui) and
-    # M_iu^T (user rows <- items, values of M_iu)
-    it_side = SideEdges(e[1], e[0], I, sel_i, lambda k: w_fn(k)[0])
-    us_side = SideEdges(e[0], e[1], U, sel_u, lambda k: w_fn(k)[1])
-    M_ui, M_iu = build_message_passing_mats(e, U, I, torch.from_numpy(cred).to(DEV), DEV)
-    pair = M_iu.pair
-
-    def T(prod, x):
-        y = torch.empty(prod.csr.n_rows, d, device=DEV)
-        spmm(prod, x, True, y=y, y_scale=prod.out_scale)
-        return y
-
-    gl = 1.0 / (K + 1)
-    gUs, gIs = gU * gl, gI * gl
-    Gu = gUs
-    for k in range(K, 0, -1):      # autograd of Version-2:482-489 (SURVEY §3.3)
-        t_i = T(pair.bwd_item, Gu)
-        assert_parity(gpu_rows(t_i, sel_i), oracle_rows(it_side, Gu), f"C4 M_ui^T product {k}")
-        Gi = gIs + t_i
-        t_u = T(pair.bwd_user, Gi)
-        assert_parity(gpu_rows(t_u, sel_u), oracle_rows(us_side, Gi), f"C4 M_iu^T product {k}")
-        Gu = gUs + t_u
-    ego_u = np.zeros((sel_u.size, d))
-    ego_i = np.zeros((sel_i.size, d))
-    pu = {int(r): j for j, r in enumerate(bu)}
-    pi = {int(r): j for j, r in enumerate(bi)}
-    for j, r in enumerate(sel_u):
-        if int(r) in pu:
-            ego_u[j] = g["g_ue"][pu[int(r)]]
-    for j, r in enumerate(sel_i):
-        if int(r) in pi:
-            ego_i[j] = g["g_ie"][pi[int(r)]]
-    assert_parity(gpu_rows(g_u0, sel_u), gpu_rows(Gu, sel_u) + ego_u, "C4 grad u0")
-    assert_parity(gpu_rows(g_i0, sel_i), gpu_rows(gIs, sel_i) + ego_i, "C4 grad i0")
+    gU = np.zeros((U, d))
+    gI = np.zeros((I, d))
+    gU[bu] = g["g_uf"]
+    gI[bi] = g["g_if"]
+    Gu, Gi = chain.backward(gU, gI, K, "gs")
+    del gU, gI
+    Gu[bu] += g["g_ue"]
+    Gi[bi] += g["g_ie"]
+    sel_u = sample_rows(chain.deg_u.astype(np.int64), w["rng"], N_SAMPLE, w["budget"],
+                        extra=bu[:2000])
+    sel_i = sample_rows(chain.deg_i.astype(np.int64), w["rng"], N_SAMPLE, w["budget"],
+                        extra=bi[:2000])
+    assert_parity(gpu_rows(g_u0, sel_u), Gu[sel_u], "C4 grad u0")
+    assert_parity(gpu_rows(g_i0, sel_i), Gi[sel_i], "C4 grad i0")
 
 
 # ---------------------------------------------------------------------------

@@ -266,3 +266,77 @@ def test_dropin_on_degree_relabelled_ids_matches_original():
     b.bpr_loss(ru[users], ri[pos], ri[neg], ub, ib, 1e-4).backward()
     assert rel(b.user_emb.weight.grad[ru], a.user_emb.weight.grad) < 1e-6
     assert rel(b.item_emb.weight.grad[ri], a.item_emb.weight.grad) < 1e-6
+
+
+@pytest.mark.parametrize("family", ["v2", "method_a", "cu", "sym"])
+def test_dropin_degree_graph_is_bitwise_the_input_order_graph(family, monkeypatch):
+    """The drop-in builders number their graph by descending degree
+    (operators.DROPIN_VERTEX_ORDER) while every table the caller sees stays in
+    input order (first products gather through input-id columns, epilogues
+    place rows through maps). Each row keeps its input-order column sequence,
+    so the operators' products, the final tables, the per-layer Jacobi op, the
+    loss and every weight gradient — through the sparse-rows backward and the
+    dense propagate_backward op — are bitwise those of an input-order graph."""
+    from bbgr import lightgcn as L
+    from bbgr import lightgcn_cu as J
+    from bbgr import lightgcn_cu_pop as V2
+    from bbgr import lightgcn_cu_pop_long_tail_exposure as MA
+    from bbgr import operators, ops
+    U, I, d, K, B = 3000, 700, 64, 3, 512
+    e = synthetic_edges(U, I, 30000, 11, items="zipf", duplicates=40)
+    cred = torch.as_tensor(synthetic_credibility(U, 3))
+    g = torch.Generator().manual_seed(5)
+    users = torch.randint(0, U, (B,), generator=g).to(DEV)
+    pos = torch.randint(0, I, (B,), generator=g).to(DEV)
+    neg = torch.randint(0, I, (B,), generator=g).to(DEV)
+    gU = torch.zeros(U, d, device=DEV)
+    gI = torch.zeros(I, d, device=DEV)
+    gU[users] = torch.randn(B, d, generator=g).to(DEV)
+    gI[pos] = torch.randn(B, d, generator=g).to(DEV)
+    x_u = torch.randn(U, d, generator=g).to(DEV)
+    x_i = torch.randn(I, d, generator=g).to(DEV)
+    out = {}
+    for order in ("input", "degree"):
+        monkeypatch.setattr(operators, "DROPIN_VERTEX_ORDER", order)
+        torch.manual_seed(0)
+        r = []
+        if family in ("v2", "method_a"):
+            mod = V2 if family == "v2" else MA
+            M_ui, M_iu = mod.build_message_passing_mats(e, U, I, cred, DEV)
+            m = mod.LightGCN(U, I, d, K, M_ui, M_iu).to(DEV)
+            ops_ = (M_iu, M_ui)
+            uf, itf = m.propagate()
+            loss = m.bpr_loss(users, pos, neg, uf, itf, 1e-4)
+        elif family == "cu":
+            a, b, deg_i = J.build_cred_weighted_mats(e, U, I, cred, DEV)
+            m = J.CredLightGCN(U, I, d, K, a, b).to(DEV)
+            ops_ = (a, b)
+            r.append(torch.as_tensor(deg_i))
+            us, is_ = m.propagate_all_layers()
+            r += list(us) + list(is_)
+            uf, itf = m.final_embeddings()
+            pop = torch.as_tensor(deg_i / deg_i.max(), device=DEV)
+            loss = m.bpr_fair_loss(users, pos, neg, uf, itf, pop, 0.05, 1e-4) + \
+                sum(t.sum() for t in us[1:]) * 1e-3
+        else:
+            A = L.build_norm_adj(e, U, I, DEV)
+            m = L.LightGCN(U, I, d, K, A).to(DEV)
+            ops_ = ()
+            r.append(A.to_torch_sparse().to_dense())
+            uf, itf = m.get_user_item_emb()
+            loss = m.bpr_loss(users, pos, neg, uf, itf, 1e-4)
+        graph = getattr(ops_[0], "graph", None) if ops_ else m.norm_adj.graph
+        assert (graph.user_order is not None) == (order == "degree")
+        for op in ops_:
+            r.append(op.mm(x_u if op.shape[1] == U else x_i))
+            r.append(op.to_torch_sparse().to_dense())
+        loss.backward()
+        r += [uf.detach(), itf.detach(), loss.detach()] + [p.grad for p in m.parameters()]
+        if family != "sym":   # the dense (registered) backward op, its own masks
+            pair = m._operator_pair()
+            r += list(ops.propagate_backward(gU, gI, ops.pair_key(pair), K,
+                                             "jacobi" if family == "cu" else "gs"))
+        out[order] = r
+    assert len(out["input"]) == len(out["degree"])
+    for k, (a, b) in enumerate(zip(out["input"], out["degree"])):
+        assert torch.equal(a.cpu(), b.cpu()), f"{family}: result {k} differs"

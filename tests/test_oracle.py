@@ -384,3 +384,31 @@ def test_edge_weights_match_operator_builders():
     S = R.sym_values(e, U, I)
     a, _ = R.edge_weights("sym", e[0], e[1], deg_u, deg_i)
     np.testing.assert_allclose(a, np.asarray(S[e[0], e[1] + U]).ravel(), rtol=1e-7)
+
+
+@pytest.mark.parametrize("kind,order", [("gs", "gs"), ("method_a", "gs"), ("j", "jacobi")])
+def test_chain64_matches_scipy_restatement(kind, order):
+    """oracle/chain64 (the C float64 chain the full-size GPU parity tests use)
+    equals the scipy restatement (propagate_* / backward_*) on a graph with
+    duplicate edges and a hub item: every layer, finals and both gradients."""
+    from bbgr.synthetic import synthetic_credibility, synthetic_edges
+    from oracle.chain64 import Chain64
+    U, I, K = 300, 200, 3
+    e = synthetic_edges(U, I, 4000, seed=3, items="zipf", duplicates=30)
+    cred = synthetic_credibility(U, 3)
+    rng = np.random.default_rng(0)
+    u0, i0 = rng.standard_normal((U, 16)), rng.standard_normal((I, 16))
+    ch = Chain64(e, U, I, kind, cred)
+    uf, itf, lu, li = ch.forward(u0, i0, K, order, keep_u=np.arange(U), keep_i=np.arange(I))
+    gu, gi = ch.backward(u0, i0, K, order)
+    if kind == "j":
+        a, b, _ = R.j_mats(e, U, I, cred)
+        ruf, ritf, us, is_ = R.propagate_j(a, b, u0, i0, K)
+        rgu, rgi = R.backward_j(a, b, u0, i0, K)
+    else:
+        a, b = R.gs_mats(e, U, I, cred, method_a=kind == "method_a")
+        ruf, ritf, us, is_ = R.propagate_gs(a, b, u0, i0, K)
+        rgu, rgi = R.backward_gs(a, b, u0, i0, K)
+    for got, want in [(uf, ruf), (itf, ritf), (gu, rgu), (gi, rgi)] + list(zip(lu, us)) \
+            + list(zip(li, is_)):
+        assert nrel(got, want) < 1e-13
