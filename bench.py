@@ -71,19 +71,27 @@ def _median_s(fn, reps: int = 5, warmup: int = 1):
     return float(np.median(ts)), ts
 
 
-def _reference_step_s(cfg_name: str, reps: int = 5):
+def _spread(ts) -> dict:
+    """Run-to-run spread of a list of timings: interquartile range and full
+    range, each relative to the median."""
+    q25, q50, q75 = np.percentile(ts, [25, 50, 75])
+    return {"iqr_rel": float((q75 - q25) / q50), "range_rel": float((max(ts) - min(ts)) / q50)}
+
+
+def _reference_step_s(cfg_name: str, variant: str = "v2_pop", reps: int = 11):
     """Median seconds of one whole reference-style training step at a small
-    config (Version-2/lighgcn_cu_pop.py:826-866: the per-user sampler loop
-    :835-849, then propagate -> bpr_loss -> backward -> Adam :858-863)."""
+    config, the variant's own family (oracle/ref_torch.reference_model):
+    the per-user sampler loop (pop-mix: Version-2/lighgcn_cu_pop.py:835-849;
+    uniform: lightgcn_cu.py:611-621 / lightgcn.py:565-575), then propagate ->
+    bpr_loss -> backward -> Adam (V2:858-863, cu:632-652, lightgcn.py:584-589)."""
     from oracle import ref_numpy as R
     from oracle import ref_torch as T
     c = CONFIGS[cfg_name]
     U, I, d, K, B = c["num_users"], c["num_items"], c["emb_dim"], c["num_layers"], c["batch"]
     e = config_edges(cfg_name)
     cred = synthetic_credibility(U, CONFIG_SEED[cfg_name])
-    M_ui, M_iu = T.gs_operators(e, U, I, cred)
     torch.manual_seed(42)
-    model = T.GSModel(U, I, d, K, M_ui, M_iu)
+    model, popmix = T.reference_model(variant, e, U, I, d, K, cred)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     indptr, indices = R.edges_to_user_csr(e, U)
     pp = R.pop_prob(e, I)
@@ -96,7 +104,10 @@ def _reference_step_s(cfg_name: str, reps: int = 5):
         lo = pos_in_perm[0] % max(len(perm) - B, 1)
         pos_in_perm[0] += B
         users = perm[lo:lo + B]
-        us, ps, ns = R.sample_batch_reference_style(indptr, indices, users, I, rng, pp)
+        if popmix:
+            us, ps, ns = R.sample_batch_reference_style(indptr, indices, users, I, rng, pp)
+        else:
+            us, ps, ns = R.sample_batch_uniform_reference_style(indptr, indices, users, I, rng)
         T.train_step(model, opt, torch.as_tensor(us), torch.as_tensor(ps),
                      torch.as_tensor(ns), 1e-4)
 
@@ -143,24 +154,25 @@ def numa_local_cpus(n: int) -> list[int]:
     return (best or sorted(allowed))[:n]
 
 
-def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
-                 whole_steps=("C2", "C1")):
+def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop", every: int = 16,
+                 reps: int = 5, whole_steps=("C2", "C1"), whole_reps: int = 11,
+                 small_edges: int = 4_000_000):
     """The reference's CPU path (oracle/ref_torch.py: the same torch calls as
-    Version-2/lighgcn_cu_pop.py:441-450, 482-489, 858-863) timed on this host,
-    SURVEY §8(d): every figure is the median of `reps` runs after one warm-up.
+    Version-2/lighgcn_cu_pop.py:441-450, 482-489, 858-863, lightgcn_cu.py:
+    420-448, 632-652, lightgcn.py:318-349) timed on this host, SURVEY §8(d),
+    for the bench's own variant.
 
-    Bounded sample of the C4 step: each of the four products of a step is timed
-    on the rows of every `every`-th output vertex (all their edges, the FULL
-    source table gathered, so cache behaviour is the real one) and scaled by
-    E / sampled edges:
-      forward  item<-user  M_iu[items % every == 0, :] @ u
-      forward  user<-item  M_ui[users % every == 0, :] @ i
-      backward grad u      autograd of M_iu[:, users % every == 0] @ u_s
-                           (the reference's transposed product incl. its coalesce)
-      backward grad i      autograd of M_ui[:, items % every == 0] @ i_s
-    plus torch Adam over all (U+I) x d parameters and the reference's per-user
-    pop-mix sampler loop on B/every users (scaled by `every`). A whole reference
-    step is timed end to end at C2 (and C1) beside it."""
+    C1 / C2 (small graphs): whole reference steps end to end (sampler loop,
+    propagate, loss, backward, Adam), median of `whole_reps` after one warm-up,
+    with the run-to-run spread.
+
+    C3 / C4 (50M edges): ONE full forward propagate() over the whole graph
+    (2K torch.sparse.mm, every row; one run: 25-60 s on 16 host cores), plus
+    the backward's products timed on the rows of every `every`-th output
+    vertex (all their edges, the FULL source table gathered) and scaled by
+    edges, torch Adam over all (U+I) x d parameters and the variant's sampler
+    loop on B/`every` users (scaled). Whole reference steps of the same
+    variant at C2 and C1 are timed beside."""
     from oracle import ref_numpy as R
     from oracle import ref_torch as T
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
@@ -169,20 +181,41 @@ def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
     U, I, d, K, B = (cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"],
                      cfg["batch"])
     E = edges.shape[1]
+    popmix = variant == "v2_pop"
+    if E <= small_edges:   # C1 / C2: the whole step, end to end
+        med, ts, work = _reference_step_s(cfg_name, variant, whole_reps)
+        return {"value": work / med, "unit": "edges/s", "cores": cores, "kind": "port",
+                "bpr_steps_per_s": 1.0 / med, "step_s": med,
+                "sample": (f"whole {cfg_name} reference steps ({variant}: sampler loop, "
+                           f"propagate, BPR, backward, Adam), median of {whole_reps} after "
+                           f"1 warm-up: {med:.3f}s"),
+                "whole_step_s": {cfg_name: {"median": med, "runs": ts, "edges_per_s": work / med,
+                                            **_spread(ts)}}}
     t_setup = time.perf_counter()
-    u, i, w_ui, w_iu = R.gs_values(edges, U, I, cred)
+    torch.manual_seed(42)
+    model, _ = T.reference_model(variant, edges, U, I, d, K, cred)
+    t_setup = time.perf_counter() - t_setup
+    # one full forward propagate() ("one forward for C3/C4")
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        model.finals()
+        t_fwd = time.perf_counter() - t0
+    del model
+    # the backward's products on sampled rows
+    kind = {"cu_fair": "j", "plain": "j"}.get(variant, "gs")
+    if kind == "gs":
+        u, i, w_ui, w_iu = R.gs_values(edges, U, I, cred, method_a=variant == "method_a")
+    else:
+        u, i, w_ui, w_iu, _ = R.j_values(edges, U, I, cred)
     g = torch.Generator().manual_seed(0)
     x_u = torch.rand(U, d, generator=g) - 0.5
     x_i = torch.rand(I, d, generator=g) - 0.5
     su, si = (u % every) == 0, (i % every) == 0
     Us, Is = (U + every - 1) // every, (I + every - 1) // every
-    A_f_iu = T.coo(i[si] // every, u[si], w_iu[si], (Is, U))      # item rows sampled
-    A_f_ui = T.coo(u[su] // every, i[su], w_ui[su], (Us, I))      # user rows sampled
     A_b_u = T.coo(i[su], u[su] // every, w_iu[su], (I, Us))       # grad-u rows sampled
     A_b_i = T.coo(u[si], i[si] // every, w_ui[si], (U, Is))       # grad-i rows sampled
     e_iu, e_ui = int(si.sum()), int(su.sum())
     del u, i, w_ui, w_iu, su, si
-    t_setup = time.perf_counter() - t_setup
 
     def bwd(A, x_s, gy):
         xs = x_s.clone().requires_grad_()
@@ -191,52 +224,53 @@ def cpu_baseline(edges, cfg, cfg_name, cred, every: int = 16, reps: int = 5,
         y.backward(gy)
         return time.perf_counter() - t0
 
-    # the sampled products are short (~0.3 s): 2 more runs each steady their
-    # medians (r26: two bench runs 6 % apart with 5)
-    pr = reps + 2
-    t_f_iu, _ = _median_s(lambda: torch.sparse.mm(A_f_iu, x_u), pr)
-    t_f_ui, _ = _median_s(lambda: torch.sparse.mm(A_f_ui, x_i), pr)
+    pr = reps + 2   # short (~0.3 s) runs: 2 more steady their medians
     gi, gu = torch.rand(I, d, generator=g), torch.rand(U, d, generator=g)
     t_b_u, _ = _median_s(lambda: bwd(A_b_u, x_u[::every].contiguous(), gi), pr)
     t_b_i, _ = _median_s(lambda: bwd(A_b_i, x_i[::every].contiguous(), gu), pr)
-    del A_f_iu, A_f_ui, A_b_u, A_b_i, gi, gu
+    del A_b_u, A_b_i, gi, gu
     s_iu, s_ui = E / max(e_iu, 1), E / max(e_ui, 1)
-    t_prop = K * (t_f_iu * s_iu + t_f_ui * s_ui + t_b_u * s_ui + t_b_i * s_iu)
+    t_bwd = K * (t_b_u * s_ui + t_b_i * s_iu)
     # torch Adam over every parameter row (the reference's dense gradients)
     pu, pi = torch.nn.Parameter(x_u), torch.nn.Parameter(x_i)
     opt = torch.optim.Adam([pu, pi], lr=1e-3)
     pu.grad, pi.grad = torch.full_like(x_u, 1e-3), torch.full_like(x_i, 1e-3)
     t_adam, _ = _median_s(opt.step, reps)
     del opt, pu, pi, x_u, x_i
-    # the reference's per-user pop-mix sampler loop on B/every users
+    # the variant's per-user sampler loop on B/every users
     indptr, indices = R.edges_to_user_csr(edges, U)
     pp = R.pop_prob(edges, I)
     rng = np.random.default_rng(42)
     nonempty = np.flatnonzero(np.diff(indptr) > 0)
     n_s = max(1, B // every)
-    t_samp, _ = _median_s(lambda: R.sample_batch_reference_style(
-        indptr, indices, rng.choice(nonempty, n_s, replace=False), I, rng, pp), reps)
+    if popmix:
+        samp = lambda: R.sample_batch_reference_style(  # noqa: E731
+            indptr, indices, rng.choice(nonempty, n_s, replace=False), I, rng, pp)
+    else:
+        samp = lambda: R.sample_batch_uniform_reference_style(  # noqa: E731
+            indptr, indices, rng.choice(nonempty, n_s, replace=False), I, rng)
+    t_samp, _ = _median_s(samp, reps)
     t_samp *= B / n_s
-    t_step = t_prop + t_adam + t_samp
-    whole = {n: _reference_step_s(n, reps) for n in whole_steps}
+    t_step = t_fwd + t_bwd + t_adam + t_samp
+    whole = {n: _reference_step_s(n, variant, whole_reps) for n in whole_steps}
     return {
         "value": 4 * K * E / t_step, "unit": "edges/s", "cores": cores, "kind": "port",
         "bpr_steps_per_s": 1.0 / t_step,
-        "sample": (f"{cfg_name_global} step from sampled products (median of {pr} after 1 "
-                   f"warm-up, rows of every {every}th output vertex, scaled by edges): "
-                   f"fwd item<-user {t_f_iu * s_iu:.2f}s, fwd user<-item {t_f_ui * s_ui:.2f}s, "
-                   f"bwd grad-u {t_b_u * s_ui:.2f}s, bwd grad-i {t_b_i * s_iu:.2f}s per layer "
-                   f"(x K={K}); torch Adam on {U + I} rows {t_adam:.2f}s; reference pop-mix "
-                   f"sampler loop {t_samp:.2f}s for B={B} (timed on {n_s} users); "
-                   f"est. {t_step:.1f}s/step. Whole reference steps, median of {reps}: "
+        "sample": (f"{cfg_name} {variant} step: ONE full forward propagate() {t_fwd:.1f}s "
+                   f"(2K={2 * K} torch.sparse.mm over all {E} edges); backward products from "
+                   f"the rows of every {every}th output vertex, scaled by edges (median of "
+                   f"{pr} after 1 warm-up): grad-u {t_b_u * s_ui:.2f}s, grad-i "
+                   f"{t_b_i * s_iu:.2f}s per layer (x K={K}); torch Adam on {U + I} rows "
+                   f"{t_adam:.2f}s; reference {'pop-mix' if popmix else 'uniform'} sampler "
+                   f"loop {t_samp:.2f}s for B={B} (timed on {n_s} users); est. "
+                   f"{t_step:.1f}s/step. Whole reference steps, median of {whole_reps}: "
                    + ", ".join(f"{n} {w[0]:.3f}s ({w[2] / w[0] / 1e6:.1f} M edges/s)"
                                for n, w in whole.items())),
         "step_s": t_step,
-        "components_s": {"fwd_item_from_user": t_f_iu * s_iu, "fwd_user_from_item": t_f_ui * s_ui,
-                         "bwd_grad_u": t_b_u * s_ui, "bwd_grad_i": t_b_i * s_iu,
-                         "adam": t_adam, "sampler": t_samp},
-        "whole_step_s": {n: {"median": w[0], "runs": w[1], "edges_per_s": w[2] / w[0]}
-                         for n, w in whole.items()},
+        "components_s": {"forward_full": t_fwd, "bwd_grad_u": t_b_u * s_ui * K,
+                         "bwd_grad_i": t_b_i * s_iu * K, "adam": t_adam, "sampler": t_samp},
+        "whole_step_s": {n: {"median": w[0], "runs": w[1], "edges_per_s": w[2] / w[0],
+                             **_spread(w[1])} for n, w in whole.items()},
         "setup_s": t_setup,
     }
 
@@ -728,7 +762,7 @@ def main():
     if not args.no_cpu_baseline and not dist_mode and not sharded_gen:
         log("[bench] timing the reference CPU path (bounded sample) ...")
         t_cpu = time.perf_counter()
-        cpu = cpu_baseline(edges, cfg, args.config, cred)
+        cpu = cpu_baseline(edges, cfg, args.config, cred, args.variant)
         if pinned is not None:
             cpu["cpus"] = _cpu_list_text(pinned)
         log(f"[bench] cpu baseline took {time.perf_counter() - t_cpu:.1f}s")

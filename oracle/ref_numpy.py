@@ -94,6 +94,21 @@ def sample_batch_reference_style(indptr, indices, users, num_items, rng, pop_pro
     return np.array(used), np.array(pos), np.array(neg)
 
 
+def sample_batch_uniform_reference_style(indptr, indices, users, num_items, rng):
+    """The per-user host loop of lightgcn_cu.py:611-621 (== lightgcn.py:565-575):
+    a uniform positive from the row, a uniform negative rejected while the user
+    has it (sample_neg_item)."""
+    used, pos, neg = [], [], []
+    for u in users:
+        p = sample_pos_item(indptr, indices, int(u), rng)
+        if p is None:
+            continue
+        used.append(int(u))
+        pos.append(p)
+        neg.append(sample_neg_item(indptr, indices, int(u), num_items, rng))
+    return np.array(used), np.array(pos), np.array(neg)
+
+
 # ---------------------------------------------------------------------------
 # Operator values (fp32, as the reference computes them)
 # ---------------------------------------------------------------------------

@@ -115,6 +115,61 @@ class GSModel(torch.nn.Module):
         return bpr(uf, itf, self.user_emb.weight, self.item_emb.weight, users, pos, neg, reg)
 
 
+class JModel(GSModel):
+    """lightgcn_cu.py CredLightGCN restated: Jacobi layers (:420-448), the BPR
+    loss + lambda_fair * L_fair (pop[pos] * s+) + reg * ego L2 (:632-648)."""
+
+    def __init__(self, U, I, d, K, M_item_from_user, M_user_from_item, pop, lambda_fair):
+        super().__init__(U, I, d, K, M_user_from_item, M_item_from_user)
+        self.pop, self.lambda_fair = pop, lambda_fair
+
+    def finals(self):
+        return propagate_j(self.M_iu, self.M_ui, self.user_emb.weight, self.item_emb.weight,
+                           self.K)
+
+    def loss(self, users, pos, neg, reg):
+        uf, itf = self.finals()
+        return bpr(uf, itf, self.user_emb.weight, self.item_emb.weight, users, pos, neg, reg,
+                   self.pop, self.lambda_fair)
+
+
+class SymModel(torch.nn.Module):
+    """lightgcn.py LightGCN restated: one emb [N, d] (:306-316), x_{k+1} = A_hat
+    x_k (:318-325), the BPR loss with the ego rows at offset U (:333-349)."""
+
+    def __init__(self, U, I, d, K, A):
+        super().__init__()
+        self.U, self.K, self.A = U, K, A
+        self.emb = torch.nn.Embedding(U + I, d)
+        torch.nn.init.xavier_uniform_(self.emb.weight)
+
+    def finals(self):
+        x = propagate_sym(self.A, self.emb.weight, self.K)
+        return x[: self.U], x[self.U:]
+
+    def loss(self, users, pos, neg, reg):
+        uf, itf = self.finals()
+        W = self.emb.weight
+        return bpr(uf, itf, W[: self.U], W[self.U:], users, pos, neg, reg)
+
+
+def reference_model(variant: str, edges, U, I, d, K, cred=None, lambda_fair=0.05):
+    """(model, uses popularity-mix negatives) of one reference family, with the
+    family's own operator builder: "v2_pop" / "cu_message" (Version-2 /
+    version_1 GS), "method_a", "cu_fair" (lightgcn_cu.py), "plain" (lightgcn.py)."""
+    if variant in ("v2_pop", "cu_message", "method_a"):
+        M_ui, M_iu = gs_operators(edges, U, I, cred, method_a=variant == "method_a")
+        return GSModel(U, I, d, K, M_ui, M_iu), variant == "v2_pop"
+    if variant == "cu_fair":
+        a, b = j_operators(edges, U, I, cred)
+        deg_i = np.bincount(edges[1].astype(np.int64), minlength=I).astype(np.float32)
+        pop = torch.as_tensor(deg_i / max(float(deg_i.max()), 1.0))
+        return JModel(U, I, d, K, a, b, pop, lambda_fair), False
+    if variant == "plain":
+        return SymModel(U, I, d, K, sym_operator(edges, U, I)), False
+    raise ValueError(f"unknown variant {variant!r}")
+
+
 def train_step(model: GSModel, opt: torch.optim.Optimizer, users, pos, neg, reg):
     """One reference training step (Version-2/lighgcn_cu_pop.py:858-865)."""
     loss = model.loss(users, pos, neg, reg)

@@ -68,24 +68,38 @@ def test_roofline_groups_models(bench):
     assert m["gather_model_bytes"] == 1000 * 8 + 600 * 4 * d + 100 * (4 + 4 * d)
 
 
-def test_cpu_baseline_small_graph(bench):
-    """The sampled-product baseline runs end to end and scales each sampled
-    product by its own edge fraction; the whole-step timing uses the
-    reference-style step (sampler loop + torch autograd + Adam)."""
+@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair", "plain"])
+def test_cpu_baseline_large_path_on_small_graph(bench, variant):
+    """The C3 / C4 form end to end on a small graph: one full forward of the
+    variant's reference model, the backward's sampled products scaled by their
+    own edge fractions, Adam and the variant's sampler loop; whole reference
+    steps of the same variant beside, with their spread."""
     from bbgr.synthetic import synthetic_credibility, synthetic_edges
     U, I, E = 4000, 1000, 40000
     cfg = dict(num_users=U, num_items=I, num_edges=E, emb_dim=16, num_layers=2, batch=256)
     e = synthetic_edges(U, I, E, seed=3, items="zipf")
-    r = bench.cpu_baseline(e, cfg, "X", synthetic_credibility(U, 3), every=4, reps=2,
-                           whole_steps=("C1",))
+    r = bench.cpu_baseline(e, cfg, "X", synthetic_credibility(U, 3), variant, every=4, reps=2,
+                           whole_steps=("C1",), whole_reps=3, small_edges=0)
     assert r["kind"] == "port" and r["unit"] == "edges/s" and r["cores"] >= 1
     comp = r["components_s"]
     assert all(v > 0 for v in comp.values())
-    K = 2   # the four products run once per layer
-    step = K * (comp["fwd_item_from_user"] + comp["fwd_user_from_item"] + comp["bwd_grad_u"]
-                + comp["bwd_grad_i"]) + comp["adam"] + comp["sampler"]
-    assert r["value"] == pytest.approx(4 * 2 * E / step, rel=1e-9)
-    assert r["whole_step_s"]["C1"]["median"] > 0 and len(r["whole_step_s"]["C1"]["runs"]) == 2
+    assert r["value"] == pytest.approx(4 * 2 * E / sum(comp.values()), rel=1e-9)
+    w = r["whole_step_s"]["C1"]
+    assert w["median"] > 0 and len(w["runs"]) == 3 and w["iqr_rel"] >= 0
+    assert ("pop-mix" in r["sample"]) == (variant == "v2_pop")
+
+
+def test_cpu_baseline_small_config_is_whole_steps(bench):
+    """C1 / C2: the baseline IS the whole reference step of the bench's variant
+    (C1: lightgcn.py's symmetric model with uniform negatives, --variant plain)."""
+    from bbgr.synthetic import CONFIGS, config_edges, synthetic_credibility
+    cfg = CONFIGS["C1"]
+    r = bench.cpu_baseline(config_edges("C1"), cfg, "C1",
+                           synthetic_credibility(cfg["num_users"], 1), "plain", whole_reps=3)
+    w = r["whole_step_s"]["C1"]
+    assert r["step_s"] == w["median"] and len(w["runs"]) == 3
+    assert r["value"] == pytest.approx(4 * cfg["num_layers"] * cfg["num_edges"] / w["median"])
+    assert "plain" in r["sample"]
 
 
 def test_median_uses_returned_interval(bench):
