@@ -718,7 +718,7 @@ def main():
         del trainer
         torch.cuda.empty_cache()
         trainer = build(other)
-        res_other = measure(trainer, other, 0)
+        res_other = measure(trainer, other, args.dense_check)
         if res_other["elapsed"] < res["elapsed"]:
             res, res_other = res_other, res
         partition_beside = {k: res_other[k] for k in ("part", "ms_per_step", "value", "E",

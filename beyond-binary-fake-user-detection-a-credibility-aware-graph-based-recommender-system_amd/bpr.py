@@ -98,15 +98,17 @@ def _first_slot(ids: torch.Tensor) -> torch.Tensor:
     return slot
 
 
-# autograd node types whose backward returns dense gradients for their leaf
-# inputs and takes a sparse dL/d(u_final) (ops.propagate_backward_rows)
-PROPAGATE_NODES = {"GeneratedBackwardFor_bbgr_propagate_defaultBackward"}
+# autograd nodes whose backward returns dense gradients for their leaf inputs
+# and takes a sparse dL/d(u_final) (bbgr::propagate_backward_rows): the C++
+# bbgr::propagate node (ops.PROPAGATE_NODE)
+PROPAGATE_NODES = {"torch::autograd::CppNode<bbgr_torch::PropagateFn>"}
 
 
 def _from_propagate_op(final: torch.Tensor) -> bool:
     """`final` is an output of bbgr::propagate itself."""
     fn = final.grad_fn
-    return fn is not None and type(fn).__name__ in PROPAGATE_NODES
+    return fn is not None and (fn.name() in PROPAGATE_NODES
+                               or type(fn).__name__ in PROPAGATE_NODES)
 
 
 def ego_grad_rows(dloss, users, pos, neg, ue, ie, reg):

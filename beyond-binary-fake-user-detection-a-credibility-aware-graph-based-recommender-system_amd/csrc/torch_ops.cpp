@@ -1,0 +1,1122 @@
+// torch_ops.cpp — the drop-in path's operators registered from C++
+// (TORCH_LIBRARY(bbgr)): libbbgr_torch.so, loaded by bbgr/ops.py with
+// torch.ops.load_library. The reference's models call torch.sparse.mm inside
+// their propagate() and rely on autograd for the backward
+// (Version-2/lighgcn_cu_pop.py:472-508, lightgcn_cu.py:420-463,
+// lightgcn.py:318-349, the step at Version-2:858-863); these operators are the
+// drop-in for exactly that surface:
+//
+//   bbgr::propagate(u0, i0, pair_key, num_layers, order) -> (u_final, i_final)
+//   bbgr::propagate_backward(gU, gI, pair_key, num_layers, order) -> (grad_u0, grad_i0)
+//   bbgr::propagate_backward_rows(iu, vu, gI, num_users, pair_key, num_layers, order)
+//   bbgr::jacobi_layer(u, i, pair_key) -> (new_i, new_u)          (+ _backward)
+//   bbgr::propagate_sym(x0, pair_key, num_layers) -> x_final       (+ _backward)
+//   bbgr::bpr_loss(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair) -> loss
+//   bbgr::bpr_loss_backward(...) -> (g_uf, g_if, g_ue, g_ie)
+//   bbgr::bpr_loss_sparse_ego(..., sparse_uf) -> loss
+//   bbgr::_register_pair / _unregister_pair / _counters            (host bookkeeping)
+//
+// Each has a CUDA(=HIP) kernel that issues libbbgr launches on torch's current
+// stream (graph-capturable, no host sync), a Meta kernel (torch.compile traces
+// through it) and, for the forward ops, an Autograd kernel whose backward is
+// itself a registered op. The sparse operators are not tensors: an operator
+// pair (four CSR products + scale vectors, bbgr/propagate.OperatorPair) is
+// registered once from Python and the ops look it up by key.
+#include <ATen/ATen.h>
+#include <ATen/core/dispatch/Dispatcher.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <torch/autograd.h>
+#include <torch/library.h>
+
+#include <atomic>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "bbgr.h"
+
+using at::Tensor;
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+
+namespace bbgr_torch {
+
+static void check(int rc, const char *what) {
+  TORCH_CHECK(rc == BBGR_OK, "bbgr: ", what, " failed (", rc, "): ", bbgr_last_error());
+}
+
+static hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+static bool capturing() {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(cur_stream(), &st) != hipSuccess) return false;
+  return st != hipStreamCaptureStatusNone;
+}
+
+template <class T>
+static T *p(const Tensor &t) {
+  return t.defined() ? t.data_ptr<T>() : nullptr;
+}
+static const float *cf(const c10::optional<Tensor> &t) {
+  return t && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+static int64_t ld(const Tensor &t) {
+  if (!t.defined()) return 0;
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "bbgr: tables must be 2-D with unit column stride");
+  return t.stride(0);
+}
+static void check_table(const char *name, const Tensor &t, int64_t rows, int64_t d) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.dim() == 2 && t.size(0) == rows && t.size(1) == d, name, " has shape ",
+              t.sizes(), ", expected [", rows, ", ", d, "]");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have unit column stride");
+}
+
+// -- operator pairs (registered from Python) ----------------------------------
+struct Product {
+  bbgr_csr csr{};      // internal ids
+  bbgr_csr csr_in{};   // input-id column indices (input-order pairs)
+  bool has_in = false;
+  const float *vals = nullptr, *in_scale = nullptr, *out_scale = nullptr;
+  const float *first_vals = nullptr;
+  bool cols_by_degree = false, rows_by_degree = false;
+  int64_t hot_bytes = 192LL << 20;
+
+  // propagate.Csr.stream_from / stream_out_from
+  int32_t stream_from(int d) const {
+    if (!cols_by_degree) return 0;
+    if ((int64_t)csr.n_cols * 4 * d <= hot_bytes) return 0;
+    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(csr.n_cols / 8, hot_bytes / (4 * d)));
+  }
+  int32_t stream_out_from(int d) const {
+    if (!rows_by_degree) return 0;
+    if ((int64_t)csr.n_rows * 4 * d <= hot_bytes) return 0;
+    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(csr.n_rows / 8, hot_bytes / (4 * d)));
+  }
+};
+
+struct Pair {
+  Product fi, fu, bi, bu;   // fwd item<-user, fwd user<-item, their transposes
+  int64_t U = 0, I = 0;
+  const float *feed_fwd_iu = nullptr, *feed_fwd_ui = nullptr;
+  const float *feed_bwd_iu = nullptr, *feed_bwd_ui = nullptr;
+  bool io = false;   // input-order tables over a degree-ordered graph
+  Tensor user_map, item_map, user_rank64, item_rank64, item_map64;
+  std::vector<Tensor> keep;   // every registered tensor, alive while registered
+};
+
+static std::mutex g_mu;
+static std::unordered_map<int64_t, std::shared_ptr<Pair>> g_pairs;
+// split-row workspaces: (indptr, d, stream or -1 for graph captures) -> buffer
+static std::map<std::tuple<const void *, int, int64_t>, Tensor> g_ws;
+static std::atomic<int64_t> g_rows_backward{0}, g_dense_backward{0};
+
+static std::shared_ptr<Pair> pair_of(int64_t key) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_pairs.find(key);
+  TORCH_CHECK(it != g_pairs.end(), "bbgr ops: no operator pair registered under key ", key);
+  return it->second;
+}
+
+// partial workspace of a product's split rows (n_chunks*(d+1) floats, zeroed
+// once; every launch leaves the arrival counters zero). A graph capture gets a
+// set of its own, allocated inside the capture (its zero fill then replays).
+static float *workspace(const Product &pr, int d, const at::Device &dev) {
+  if (pr.csr.n_split == 0) return nullptr;
+  const int64_t skey = capturing() ? -1 : (int64_t)(intptr_t)cur_stream();
+  auto key = std::make_tuple((const void *)pr.csr.indptr, d, skey);
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_ws.find(key);
+  if (it == g_ws.end()) {
+    Tensor w = at::zeros({(int64_t)pr.csr.n_chunks * (d + 1)},
+                         at::TensorOptions().dtype(at::kFloat).device(dev));
+    it = g_ws.emplace(key, w).first;
+  }
+  return it->second.data_ptr<float>();
+}
+
+// -- one fused SpMM launch (propagate.spmm) ------------------------------------
+struct Opts {
+  Tensor y;
+  const float *y_scale = nullptr;
+  float y_scale_s = 1.f;
+  Tensor add;
+  const float *add_scale = nullptr;
+  float add_scale_s = 1.f;
+  Tensor acc_in, acc_out;
+  const float *acc_scale = nullptr;
+  float acc_scale_s = 1.f;
+  float gamma = 1.f;
+  const uint8_t *src_mask = nullptr, *row_mask = nullptr, *add_mask = nullptr;
+  const int32_t *y_map = nullptr, *acc_map = nullptr, *add_map = nullptr;
+  bool src_input = false;
+};
+
+static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) {
+  bbgr_spmm_args a;
+  std::memset(&a, 0, sizeof a);
+  const int d = (int)x.size(1);
+  a.d = d;
+  a.x = x.data_ptr<float>();
+  a.ldx = ld(x);
+  if (pr.vals) {
+    a.weight_mode = 1;
+    a.edge_val = pr.vals;
+  } else if (first && pr.in_scale) {
+    TORCH_CHECK(pr.first_vals, "bbgr: first-layer edge values not registered");
+    a.weight_mode = 1;
+    a.edge_val = pr.first_vals;
+  }
+  a.col_scale_s = 1.f;
+  a.y = p<float>(o.y);
+  a.ldy = ld(o.y);
+  a.y_scale = o.y_scale;
+  a.y_scale_s = o.y_scale_s;
+  a.add = p<float>(o.add);
+  a.ldadd = ld(o.add);
+  a.add_scale = o.add_scale;
+  a.add_scale_s = o.add_scale_s;
+  a.acc_in = p<float>(o.acc_in);
+  a.ldacc_in = ld(o.acc_in);
+  a.acc_out = p<float>(o.acc_out);
+  a.ldacc_out = ld(o.acc_out);
+  a.acc_scale = o.acc_scale;
+  a.acc_scale_s = o.acc_scale_s;
+  a.gamma = o.gamma;
+  a.partial = workspace(pr, d, x.device());
+  a.src_mask = o.src_mask;
+  a.row_mask = o.row_mask;
+  a.add_mask = o.add_mask;
+  a.y_map = o.y_map;
+  a.acc_map = o.acc_map;
+  a.add_map = o.add_map;
+  // input-order source rows carry no hot prefix; mapped output rows neither
+  a.stream_from = o.src_input ? 0 : pr.stream_from(d);
+  a.stream_out_from = o.y_map ? 0 : pr.stream_out_from(d);
+  TORCH_CHECK(!o.src_input || pr.has_in, "bbgr: product has no input-id columns");
+  check(bbgr_spmm(o.src_input ? &pr.csr_in : &pr.csr, &a, cur_stream()), "bbgr_spmm");
+}
+
+static at::TensorOptions f32(const Tensor &like) {
+  return at::TensorOptions().dtype(at::kFloat).device(like.device());
+}
+static at::TensorOptions u8(const Tensor &like) {
+  return at::TensorOptions().dtype(at::kByte).device(like.device());
+}
+
+// -- K-layer chains (propagate.forward_steps / backward_steps, no sharding) ----
+static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0, const Tensor &i0,
+                                                int64_t K, bool gs, Tensor acc_u = Tensor(),
+                                                Tensor acc_i = Tensor()) {
+  const int64_t U = P.U, I = P.I, d = u0.size(1);
+  check_table("user table", u0, U, d);
+  check_table("item table", i0, I, d);
+  if (!acc_u.defined()) acc_u = at::empty({U, d}, f32(u0));
+  if (!acc_i.defined()) acc_i = at::empty({I, d}, f32(u0));
+  if (K == 0) {
+    acc_u.copy_(u0);
+    acc_i.copy_(i0);
+    return {acc_u, acc_i};
+  }
+  const float gl = (float)(1.0 / (double)(K + 1));   // as the Python float
+  const int32_t *am_u = P.io ? P.user_map.data_ptr<int32_t>() : nullptr;
+  const int32_t *am_i = P.io ? P.item_map.data_ptr<int32_t>() : nullptr;
+  if (gs) {   // Version-2:482-487: i_k = M_iu u_{k-1}; u_k = M_ui i_k
+    Tensor bufU = at::empty({U, d}, f32(u0)), bufI = at::empty({I, d}, f32(u0));
+    for (int64_t k = 1; k <= K; ++k) {
+      const float g = k == K ? gl : 1.f;
+      Opts oi;
+      oi.y = bufI;
+      oi.y_scale = P.feed_fwd_iu;
+      oi.acc_in = k == 1 ? i0 : acc_i;
+      oi.acc_out = acc_i;
+      oi.acc_scale = P.fi.out_scale;
+      oi.gamma = g;
+      oi.acc_map = am_i;
+      oi.src_input = P.io && k == 1;
+      spmm(P.fi, k == 1 ? u0 : bufU, k == 1, oi);
+      Opts ou;
+      if (k < K) ou.y = bufU;
+      ou.y_scale = P.feed_fwd_ui;
+      ou.acc_in = k == 1 ? u0 : acc_u;
+      ou.acc_out = acc_u;
+      ou.acc_scale = P.fu.out_scale;
+      ou.gamma = g;
+      ou.acc_map = am_u;
+      spmm(P.fu, bufI, false, ou);
+    }
+  } else {    // lightgcn_cu.py:429-447: both sides from layer k-1
+    Tensor bufU[2] = {at::empty({U, d}, f32(u0)), at::empty({U, d}, f32(u0))};
+    Tensor bufI[2] = {at::empty({I, d}, f32(u0)), at::empty({I, d}, f32(u0))};
+    int cur = 0;
+    for (int64_t k = 1; k <= K; ++k) {
+      const float g = k == K ? gl : 1.f;
+      const int nxt = 1 - cur;
+      Opts oi;
+      if (k < K) oi.y = bufI[nxt];
+      oi.y_scale = P.feed_fwd_iu;
+      oi.acc_in = k == 1 ? i0 : acc_i;
+      oi.acc_out = acc_i;
+      oi.acc_scale = P.fi.out_scale;
+      oi.gamma = g;
+      oi.acc_map = am_i;
+      oi.src_input = P.io && k == 1;
+      spmm(P.fi, k == 1 ? u0 : bufU[cur], k == 1, oi);
+      Opts ou;
+      if (k < K) ou.y = bufU[nxt];
+      ou.y_scale = P.feed_fwd_ui;
+      ou.acc_in = k == 1 ? u0 : acc_u;
+      ou.acc_out = acc_u;
+      ou.acc_scale = P.fu.out_scale;
+      ou.gamma = g;
+      ou.acc_map = am_u;
+      ou.src_input = P.io && k == 1;
+      spmm(P.fu, k == 1 ? i0 : bufI[cur], k == 1, ou);
+      cur = nxt;
+    }
+  }
+  return {acc_u, acc_i};
+}
+
+// grad_support: (su, si, si_int) — su / si index the rows of gU / gI (input
+// order for an input-order pair), si_int the item CSR rows (GS: the first
+// item product's output support). Undefined = no masks.
+struct Support {
+  Tensor su, si, si_int;
+};
+
+static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU, const Tensor &gI,
+                                                 int64_t K, bool gs, const Support &s,
+                                                 Tensor gu0 = Tensor(), Tensor gi0 = Tensor()) {
+  const int64_t U = P.U, I = P.I, d = gU.size(1);
+  check_table("user grad", gU, U, d);
+  check_table("item grad", gI, I, d);
+  if (!gu0.defined()) gu0 = at::empty({U, d}, f32(gU));
+  if (!gi0.defined()) gi0 = at::empty({I, d}, f32(gU));
+  if (K == 0) {
+    gu0.copy_(gU);
+    gi0.copy_(gI);
+    return {gu0, gi0};
+  }
+  const float gl = (float)(1.0 / (double)(K + 1));   // as the Python float
+  const uint8_t *su = p<uint8_t>(s.su), *si = p<uint8_t>(s.si);
+  const uint8_t *si_int = s.si_int.defined() ? p<uint8_t>(s.si_int) : si;
+  const int32_t *um = P.io ? P.user_map.data_ptr<int32_t>() : nullptr;
+  const int32_t *im = P.io ? P.item_map.data_ptr<int32_t>() : nullptr;
+  if (gs) {   // Gi_k = gI' + M_ui^T Gu_k ; Gu_{k-1} = gU' + M_iu^T Gi_k ; Gu_K = gU'
+    Tensor bufU = at::empty({U, d}, f32(gU)), bufI = at::empty({I, d}, f32(gU));
+    for (int64_t k = K; k >= 1; --k) {
+      const bool first = k == K;
+      Opts oi;
+      oi.y = bufI;
+      oi.y_scale = P.feed_bwd_iu;
+      oi.y_scale_s = first ? gl : 1.f;
+      oi.add = gI;
+      oi.add_mask = si;
+      oi.add_scale = P.bu.in_scale;
+      oi.add_scale_s = gl;
+      oi.src_mask = first ? su : nullptr;
+      oi.row_mask = first ? si_int : nullptr;
+      oi.add_map = im;
+      oi.src_input = P.io && first;
+      spmm(P.bi, first ? gU : bufU, first, oi);
+      Opts ou;
+      ou.add = gU;
+      ou.add_mask = su;
+      ou.add_map = um;
+      ou.src_mask = first ? si_int : nullptr;
+      ou.add_scale_s = gl;
+      if (k > 1) {
+        ou.y = bufU;
+        ou.y_scale = P.feed_bwd_ui;
+        ou.add_scale = P.bi.in_scale;
+      } else {
+        ou.y = gu0;
+        ou.y_scale = P.bu.out_scale;
+        ou.y_map = um;
+      }
+      spmm(P.bu, bufI, false, ou);
+    }
+    at::mul_out(gi0, gI, gl);   // GS: i0 only feeds the layer mean
+  } else {    // Jacobi: Gu_{k-1} = gU' + M_iu^T Gi_k ; Gi_{k-1} = gI' + M_ui^T Gu_k
+    Tensor bufU[2] = {at::empty({U, d}, f32(gU)), at::empty({U, d}, f32(gU))};
+    Tensor bufI[2] = {at::empty({I, d}, f32(gU)), at::empty({I, d}, f32(gU))};
+    int cur = 0;
+    for (int64_t k = K; k >= 1; --k) {
+      const bool first = k == K;
+      const int nxt = 1 - cur;
+      const float ys = first ? gl : 1.f;
+      const Tensor &xu = first ? gI : bufI[cur];   // input of BU (item table)
+      const Tensor &xi = first ? gU : bufU[cur];   // input of BI (user table)
+      Opts ou, oi;
+      ou.y_scale_s = oi.y_scale_s = ys;
+      ou.add = gU;
+      ou.add_mask = su;
+      ou.add_map = um;
+      ou.add_scale_s = gl;
+      ou.src_mask = first ? si : nullptr;
+      ou.src_input = P.io && first;
+      oi.add = gI;
+      oi.add_mask = si;
+      oi.add_map = im;
+      oi.add_scale_s = gl;
+      oi.src_mask = first ? su : nullptr;
+      oi.src_input = P.io && first;
+      if (k > 1) {
+        ou.y = bufU[nxt];
+        ou.y_scale = P.feed_bwd_ui;
+        ou.add_scale = P.bi.in_scale;
+        oi.y = bufI[nxt];
+        oi.y_scale = P.feed_bwd_iu;
+        oi.add_scale = P.bu.in_scale;
+      } else {
+        ou.y = gu0;
+        ou.y_scale = P.bu.out_scale;
+        ou.y_map = um;
+        oi.y = gi0;
+        oi.y_scale = P.bi.out_scale;
+        oi.y_map = im;
+      }
+      spmm(P.bu, xu, first, ou);
+      spmm(P.bi, xi, first, oi);
+      cur = nxt;
+    }
+  }
+  return {gu0, gi0};
+}
+
+// -- gradient supports (ops.grad_support / the rows path) ----------------------
+static Support io_support(const Pair &P, const Tensor &mu, const Tensor &mi, bool gs,
+                          const Tensor &users /* input ids or undefined */) {
+  Support s{mu, mi, Tensor()};
+  if (!gs) return s;
+  Tensor mi_int = mi.index_select(0, P.item_map64);
+  const bbgr_csr &uc = P.fu.csr;
+  if (users.defined()) {
+    Tensor ui = P.user_rank64.index_select(0, users).contiguous();
+    check(bbgr_mark_neighbors(ui.numel(), ui.data_ptr<int64_t>(), uc.indptr, uc.indices, 1,
+                              mi_int.data_ptr<uint8_t>(), cur_stream()),
+          "bbgr_mark_neighbors");
+  } else {
+    check(bbgr_mark_neighbors_of_mask(P.U, mu.data_ptr<uint8_t>(), P.user_map.data_ptr<int32_t>(),
+                                      uc.indptr, uc.indices, 1, mi_int.data_ptr<uint8_t>(),
+                                      cur_stream()),
+          "bbgr_mark_neighbors_of_mask");
+  }
+  s.si = mi_int.index_select(0, P.item_rank64);
+  s.si_int = mi_int;
+  return s;
+}
+
+// the gradients' row support, read off the tables (bbgr_row_support): users
+// with a nonzero gU row; items with a nonzero gI row plus, for GS, every
+// neighbour of a flagged user. Bitwise the dense chain (skipped rows are zero).
+static Support grad_support(const Pair &P, const Tensor &gU, const Tensor &gI, bool gs) {
+  const int64_t U = P.U, I = P.I, d = gU.size(1);
+  Tensor mu = at::empty({std::max<int64_t>(U, 1)}, u8(gU));
+  Tensor mi = at::empty({std::max<int64_t>(I, 1)}, u8(gU));
+  check(bbgr_row_support(I, (int32_t)d, gI.data_ptr<float>(), ld(gI), mi.data_ptr<uint8_t>(),
+                         nullptr, nullptr, nullptr, cur_stream()),
+        "bbgr_row_support");
+  if (P.io) {
+    check(bbgr_row_support(U, (int32_t)d, gU.data_ptr<float>(), ld(gU), mu.data_ptr<uint8_t>(),
+                           nullptr, nullptr, nullptr, cur_stream()),
+          "bbgr_row_support");
+    return io_support(P, mu.narrow(0, 0, U), mi.narrow(0, 0, I), gs, Tensor());
+  }
+  const bbgr_csr &uc = P.fu.csr;
+  check(bbgr_row_support(U, (int32_t)d, gU.data_ptr<float>(), ld(gU), mu.data_ptr<uint8_t>(),
+                         gs ? uc.indptr : nullptr, gs ? uc.indices : nullptr,
+                         gs ? mi.data_ptr<uint8_t>() : nullptr, cur_stream()),
+        "bbgr_row_support");
+  return Support{mu.narrow(0, 0, U), mi.narrow(0, 0, I), Tensor()};
+}
+
+// dst.index_add_(0, index, src) summed per destination in ascending source
+// order (bbgr_scatter_add_rows; deterministic)
+static void index_add_rows(Tensor &dst, const Tensor &index, const Tensor &src) {
+  Tensor idx = index.to(at::kLong).contiguous();
+  const int64_t n = idx.numel();
+  TORCH_CHECK(src.size(0) >= n && src.size(1) == dst.size(1), "index_add_rows: shapes");
+  size_t need = 0;
+  const int32_t d = (int32_t)dst.size(1);
+  check(bbgr_scatter_add_rows(n, idx.data_ptr<int64_t>(), src.data_ptr<float>(), ld(src),
+                              dst.data_ptr<float>(), ld(dst), d, dst.size(0), nullptr, &need,
+                              cur_stream()),
+        "bbgr_scatter_add_rows (size)");
+  Tensor ws = at::empty({(int64_t)std::max<size_t>(need, 1)}, u8(dst));
+  size_t have = (size_t)ws.numel();
+  check(bbgr_scatter_add_rows(n, idx.data_ptr<int64_t>(), src.data_ptr<float>(), ld(src),
+                              dst.data_ptr<float>(), ld(dst), d, dst.size(0), ws.data_ptr(),
+                              &have, cur_stream()),
+        "bbgr_scatter_add_rows");
+}
+
+static bool is_gs(c10::string_view order) {
+  if (order == "gs") return true;
+  TORCH_CHECK(order == "jacobi", "unknown propagation order ", order);
+  return false;
+}
+
+// -- CUDA (HIP) kernels ---------------------------------------------------------
+static std::tuple<Tensor, Tensor> propagate_cuda(const Tensor &u0, const Tensor &i0, int64_t key,
+                                                 int64_t K, c10::string_view order) {
+  auto P = pair_of(key);
+  return forward_chain(*P, u0.contiguous(), i0.contiguous(), K, is_gs(order));
+}
+
+static std::tuple<Tensor, Tensor> propagate_backward_cuda(const Tensor &gU_, const Tensor &gI_,
+                                                          int64_t key, int64_t K,
+                                                          c10::string_view order) {
+  auto P = pair_of(key);
+  const bool gs = is_gs(order);
+  Tensor gU = gU_.contiguous(), gI = gI_.contiguous();
+  g_dense_backward++;
+  return backward_chain(*P, gU, gI, K, gs, grad_support(*P, gU, gI, gs));
+}
+
+// dL/d(u_final) given as rows: vu[k] adds to user iu[k]. The dense gU is
+// formed on the listed rows only (zeroed, then summed in ascending k) and the
+// masks come from the list: every read of gU in a K >= 1 chain is masked to
+// those rows, so the rest is never touched (K = 0 copies gU whole: zeroed).
+static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
+    const Tensor &iu_, const Tensor &vu, const Tensor &gI_, int64_t num_users, int64_t key,
+    int64_t K, c10::string_view order) {
+  auto P = pair_of(key);
+  const bool gs = is_gs(order);
+  TORCH_CHECK(num_users == P->U, "propagate_backward_rows: num_users does not match the pair");
+  const int64_t U = P->U, I = P->I, d = vu.size(1);
+  Tensor iu = iu_.to(at::kLong).contiguous();
+  Tensor gI = gI_.contiguous();
+  Tensor gU;
+  if (K == 0) {
+    gU = at::zeros({std::max<int64_t>(U, 1), d}, f32(vu)).narrow(0, 0, U);
+  } else {
+    gU = at::empty({std::max<int64_t>(U, 1), d}, f32(vu)).narrow(0, 0, U);
+    gU.index_fill_(0, iu, 0.0);
+  }
+  index_add_rows(gU, iu, vu.contiguous());
+  Tensor mu = at::zeros({std::max<int64_t>(U, 1)}, u8(vu));
+  Tensor mi = at::empty({std::max<int64_t>(I, 1)}, u8(vu));
+  check(bbgr_mark_rows(iu.numel(), iu.data_ptr<int64_t>(), 1, mu.data_ptr<uint8_t>(), U,
+                       cur_stream()),
+        "bbgr_mark_rows");
+  check(bbgr_row_support(I, (int32_t)d, gI.data_ptr<float>(), ld(gI), mi.data_ptr<uint8_t>(),
+                         nullptr, nullptr, nullptr, cur_stream()),
+        "bbgr_row_support");
+  g_rows_backward++;
+  Support s;
+  if (P->io) {
+    s = io_support(*P, mu.narrow(0, 0, U), mi.narrow(0, 0, I), gs, iu);
+  } else {
+    if (gs) {   // the first item product's output support: N(listed users)
+      const bbgr_csr &uc = P->fu.csr;
+      check(bbgr_mark_neighbors(iu.numel(), iu.data_ptr<int64_t>(), uc.indptr, uc.indices, 1,
+                                mi.data_ptr<uint8_t>(), cur_stream()),
+            "bbgr_mark_neighbors");
+    }
+    s = Support{mu.narrow(0, 0, U), mi.narrow(0, 0, I), Tensor()};
+  }
+  return backward_chain(*P, gU, gI, K, gs, s);
+}
+
+static std::tuple<Tensor, Tensor> jacobi_layer_cuda(const Tensor &u_, const Tensor &i_, int64_t key) {
+  auto P = pair_of(key);
+  Tensor u = u_.contiguous(), i = i_.contiguous();
+  const int64_t d = u.size(1);
+  check_table("user table", u, P->U, d);
+  check_table("item table", i, P->I, d);
+  Tensor new_i = at::empty({P->I, d}, f32(u)), new_u = at::empty({P->U, d}, f32(u));
+  Opts oi, ou;
+  oi.y = new_i;
+  oi.y_scale = P->fi.out_scale;
+  oi.src_input = P->io;
+  oi.y_map = P->io ? P->item_map.data_ptr<int32_t>() : nullptr;
+  ou.y = new_u;
+  ou.y_scale = P->fu.out_scale;
+  ou.src_input = P->io;
+  ou.y_map = P->io ? P->user_map.data_ptr<int32_t>() : nullptr;
+  spmm(P->fi, u, true, oi);
+  spmm(P->fu, i, true, ou);
+  return {new_i, new_u};
+}
+
+// (d/du, d/di): M_iu^T g_i on the user rows, M_ui^T g_u on the item rows
+static std::tuple<Tensor, Tensor> jacobi_layer_backward_cuda(const Tensor &g_i, const Tensor &g_u,
+                                                             int64_t key) {
+  auto P = pair_of(key);
+  const int64_t d = g_i.size(1);
+  Tensor gu = at::empty({P->U, d}, f32(g_i)), gi = at::empty({P->I, d}, f32(g_i));
+  Opts ou, oi;
+  ou.y = gu;
+  ou.y_scale = P->bu.out_scale;
+  ou.src_input = P->io;
+  ou.y_map = P->io ? P->user_map.data_ptr<int32_t>() : nullptr;
+  oi.y = gi;
+  oi.y_scale = P->bi.out_scale;
+  oi.src_input = P->io;
+  oi.y_map = P->io ? P->item_map.data_ptr<int32_t>() : nullptr;
+  spmm(P->bu, g_i.contiguous(), true, ou);
+  spmm(P->bi, g_u.contiguous(), true, oi);
+  return {gu, gi};
+}
+
+// lightgcn.py's one stacked [users; items] table: Jacobi on the two blocks
+static Tensor propagate_sym_cuda(const Tensor &x0_, int64_t key, int64_t K) {
+  auto P = pair_of(key);
+  Tensor x0 = x0_.contiguous();
+  Tensor out = at::empty_like(x0);
+  forward_chain(*P, x0.narrow(0, 0, P->U), x0.narrow(0, P->U, P->I), K, false,
+                out.narrow(0, 0, P->U), out.narrow(0, P->U, P->I));
+  return out;
+}
+
+static Tensor propagate_sym_backward_cuda(const Tensor &g_, int64_t key, int64_t K) {
+  auto P = pair_of(key);
+  Tensor g = g_.contiguous();
+  Tensor gx = at::empty_like(g);
+  Tensor gU = g.narrow(0, 0, P->U), gI = g.narrow(0, P->U, P->I);
+  g_dense_backward++;
+  backward_chain(*P, gU, gI, K, false, grad_support(*P, gU, gI, false), gx.narrow(0, 0, P->U),
+                 gx.narrow(0, P->U, P->I));
+  return gx;
+}
+
+// -- BPR --------------------------------------------------------------------
+static bbgr_bpr_args bpr_args(const Tensor &users, const Tensor &pos, const Tensor &neg,
+                              const Tensor &uf, const Tensor &itf, const Tensor &ue,
+                              const Tensor &ie, double reg, const c10::optional<Tensor> &pop,
+                              double lambda_fair) {
+  TORCH_CHECK(users.numel() == pos.numel() && pos.numel() == neg.numel(),
+              "users, pos_items, neg_items must have equal length");
+  TORCH_CHECK(!ue.defined() || ue.size(0) == uf.size(0), "ego and final tables differ in rows");
+  TORCH_CHECK(!ie.defined() || ie.size(0) == itf.size(0), "ego and final tables differ in rows");
+  bbgr_bpr_args a;
+  std::memset(&a, 0, sizeof a);
+  a.batch = users.numel();
+  a.d = (int32_t)uf.size(1);
+  a.n_users = uf.size(0);
+  a.n_items = itf.size(0);
+  a.users = users.data_ptr<int64_t>();
+  a.pos = pos.data_ptr<int64_t>();
+  a.neg = neg.data_ptr<int64_t>();
+  a.uf = uf.data_ptr<float>();
+  a.lduf = ld(uf);
+  a.itf = itf.data_ptr<float>();
+  a.ldif = ld(itf);
+  a.ue = p<float>(ue);
+  a.ldue = ld(ue);
+  a.ie = p<float>(ie);
+  a.ldie = ld(ie);
+  a.pop = cf(pop);
+  a.reg = (float)reg;
+  a.lambda_fair = (float)lambda_fair;
+  return a;
+}
+
+static Tensor idx64(const Tensor &t) { return t.to(at::kLong).contiguous(); }
+
+static Tensor bpr_loss_cuda(const Tensor &uf_, const Tensor &itf_, const Tensor &ue_,
+                            const Tensor &ie_, const Tensor &users_, const Tensor &pos_,
+                            const Tensor &neg_, double reg, const c10::optional<Tensor> &pop,
+                            double lambda_fair) {
+  Tensor uf = uf_.contiguous(), itf = itf_.contiguous(), ue = ue_.contiguous(),
+         ie = ie_.contiguous();
+  Tensor users = idx64(users_), pos = idx64(pos_), neg = idx64(neg_);
+  const int64_t B = users.numel();
+  TORCH_CHECK(B > 0, "empty batch");
+  Tensor parts = at::empty({3 * B}, f32(uf));
+  Tensor out = at::empty({}, f32(uf));
+  bbgr_bpr_args a = bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop, lambda_fair);
+  a.parts = parts.data_ptr<float>();
+  check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr");
+  check(bbgr_bpr_reduce(B, parts.data_ptr<float>(), (float)reg, (float)lambda_fair,
+                        out.data_ptr<float>(), cur_stream()),
+        "bbgr_bpr_reduce");
+  return out;
+}
+
+// deterministic: per-triple gradient rows of the final tables (contrib), each
+// destination summed in ascending triple order (bbgr_scatter_add_rows)
+static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_cuda(
+    const Tensor &dloss, const Tensor &uf_, const Tensor &itf_, const Tensor &ue_,
+    const Tensor &ie_, const Tensor &users_, const Tensor &pos_, const Tensor &neg_, double reg,
+    const c10::optional<Tensor> &pop, double lambda_fair) {
+  Tensor uf = uf_.contiguous(), itf = itf_.contiguous(), ue = ue_.contiguous(),
+         ie = ie_.contiguous();
+  Tensor users = idx64(users_), pos = idx64(pos_), neg = idx64(neg_);
+  Tensor g_uf = at::zeros_like(uf), g_if = at::zeros_like(itf), g_ue = at::zeros_like(ue),
+         g_ie = at::zeros_like(ie);
+  const int64_t B = users.numel();
+  Tensor contrib = at::empty({3 * B, uf.size(1)}, f32(uf));
+  Tensor dl = dloss.to(at::kFloat).contiguous().reshape({});
+  bbgr_bpr_args a = bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop, lambda_fair);
+  a.dloss = dl.data_ptr<float>();
+  a.g_ue = g_ue.data_ptr<float>();
+  a.ldgue = ld(g_ue);
+  a.g_ie = g_ie.data_ptr<float>();
+  a.ldgie = ld(g_ie);
+  a.contrib = contrib.data_ptr<float>();
+  a.ldcontrib = ld(contrib);
+  check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr");
+  index_add_rows(g_uf, users, contrib.narrow(0, 0, B));
+  index_add_rows(g_if, at::cat({pos, neg}), contrib.narrow(0, B, 2 * B));
+  return {g_uf, g_if, g_ue, g_ie};
+}
+
+// slot[b] = position of the first occurrence of ids[b] (device-only)
+static Tensor first_slot(const Tensor &ids) {
+  const int64_t n = ids.numel();
+  auto sorted = at::sort(ids, /*stable=*/true, /*dim=*/0, /*descending=*/false);
+  const Tensor &srt = std::get<0>(sorted);
+  const Tensor &perm = std::get<1>(sorted);
+  Tensor posn = at::arange(n, ids.options().dtype(at::kLong));
+  Tensor start = at::ones({n}, ids.options().dtype(at::kBool));
+  if (n > 1) start.narrow(0, 1, n - 1).copy_(srt.narrow(0, 1, n - 1) != srt.narrow(0, 0, n - 1));
+  Tensor head = std::get<0>(at::cummax(at::where(start, posn, at::zeros_like(posn)), 0));
+  Tensor slot = at::empty_like(perm);
+  slot.index_put_({perm}, perm.index_select(0, head));
+  return slot;
+}
+
+// the ego-L2 gradient as compact rows (bpr.ego_grad_rows): every occurrence of
+// a row adds into the row of its FIRST occurrence (the others stay +0.0), so
+// each table row's sum is formed exactly as in the dense path
+static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl,
+                                                                const Tensor &users,
+                                                                const Tensor &pos,
+                                                                const Tensor &neg,
+                                                                const Tensor &ue,
+                                                                const Tensor &ie, double reg) {
+  const int64_t B = users.numel(), d = ue.size(1), U = ue.size(0), I = ie.size(0);
+  Tensor valid = (users >= 0) & (users < U) & (pos >= 0) & (pos < I) & (neg >= 0) & (neg < I);
+  Tensor iu = users.clamp(0, U - 1);
+  Tensor ii = at::cat({pos, neg}).clamp(0, I - 1);
+  Tensor su = first_slot(iu), si = first_slot(ii);
+  Tensor ue_c = ue.index_select(0, iu).contiguous(), ie_c = ie.index_select(0, ii).contiguous();
+  Tensor cu = at::where(valid, su, at::full_like(su, -1)).contiguous();
+  Tensor gu = at::zeros({B, d}, f32(ue)), gi = at::zeros({2 * B, d}, f32(ue));
+  Tensor sp = si.narrow(0, 0, B).contiguous(), sn = si.narrow(0, B, B).contiguous();
+  bbgr_bpr_args a = bpr_args(cu, sp, sn, ue_c, ie_c, ue_c, ie_c, reg, c10::nullopt, 0.0);
+  a.dloss = dl.data_ptr<float>();
+  a.g_ue = gu.data_ptr<float>();
+  a.ldgue = ld(gu);
+  a.g_ie = gi.data_ptr<float>();
+  a.ldgie = ld(gi);
+  check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr (ego rows)");
+  return {gu, gi, iu, ii};
+}
+
+// -- Meta kernels (shapes only; torch.compile traces through them) ---------------
+static std::tuple<Tensor, Tensor> propagate_meta(const Tensor &u0, const Tensor &i0, int64_t,
+                                                 int64_t, c10::string_view) {
+  return {at::empty_like(u0), at::empty_like(i0)};
+}
+static std::tuple<Tensor, Tensor> propagate_backward_rows_meta(const Tensor &, const Tensor &vu,
+                                                               const Tensor &gI, int64_t num_users,
+                                                               int64_t, int64_t,
+                                                               c10::string_view) {
+  return {at::empty({num_users, vu.size(1)}, vu.options()), at::empty_like(gI)};
+}
+static std::tuple<Tensor, Tensor> jacobi_layer_meta(const Tensor &u, const Tensor &i, int64_t) {
+  return {at::empty_like(i), at::empty_like(u)};
+}
+static std::tuple<Tensor, Tensor> jacobi_layer_backward_meta(const Tensor &g_i, const Tensor &g_u,
+                                                             int64_t) {
+  return {at::empty_like(g_u), at::empty_like(g_i)};
+}
+static Tensor propagate_sym_meta(const Tensor &x0, int64_t, int64_t) { return at::empty_like(x0); }
+static Tensor bpr_loss_meta(const Tensor &uf, const Tensor &, const Tensor &, const Tensor &,
+                            const Tensor &, const Tensor &, const Tensor &, double,
+                            const c10::optional<Tensor> &, double) {
+  return at::empty({}, uf.options());
+}
+static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_meta(
+    const Tensor &, const Tensor &uf, const Tensor &itf, const Tensor &ue, const Tensor &ie,
+    const Tensor &, const Tensor &, const Tensor &, double, const c10::optional<Tensor> &,
+    double) {
+  return {at::empty_like(uf), at::empty_like(itf), at::empty_like(ue), at::empty_like(ie)};
+}
+static Tensor bpr_loss_sparse_ego_meta(const Tensor &uf, const Tensor &, const Tensor &,
+                                       const Tensor &, const Tensor &, const Tensor &,
+                                       const Tensor &, double, const c10::optional<Tensor> &,
+                                       double, bool) {
+  return at::empty({}, uf.options());
+}
+static Tensor bpr_loss_sparse_ego_cuda(const Tensor &uf, const Tensor &itf, const Tensor &ue,
+                                       const Tensor &ie, const Tensor &users, const Tensor &pos,
+                                       const Tensor &neg, double reg,
+                                       const c10::optional<Tensor> &pop, double lambda_fair, bool) {
+  return bpr_loss_cuda(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair);
+}
+
+// -- dispatcher handles (autograd kernels call below the Autograd key) ----------
+template <class Sig>
+static c10::TypedOperatorHandle<Sig> op(const char *name) {
+  return c10::Dispatcher::singleton().findSchemaOrThrow(name, "").typed<Sig>();
+}
+using PropSig = std::tuple<Tensor, Tensor>(const Tensor &, const Tensor &, int64_t, int64_t,
+                                           c10::string_view);
+using RowsSig = std::tuple<Tensor, Tensor>(const Tensor &, const Tensor &, const Tensor &, int64_t,
+                                           int64_t, int64_t, c10::string_view);
+using LayerSig = std::tuple<Tensor, Tensor>(const Tensor &, const Tensor &, int64_t);
+using SymSig = Tensor(const Tensor &, int64_t, int64_t);
+using BprSig = Tensor(const Tensor &, const Tensor &, const Tensor &, const Tensor &,
+                      const Tensor &, const Tensor &, const Tensor &, double,
+                      const c10::optional<Tensor> &, double);
+using BprBwdSig = std::tuple<Tensor, Tensor, Tensor, Tensor>(
+    const Tensor &, const Tensor &, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
+    const Tensor &, const Tensor &, double, const c10::optional<Tensor> &, double);
+using BprSeSig = Tensor(const Tensor &, const Tensor &, const Tensor &, const Tensor &,
+                        const Tensor &, const Tensor &, const Tensor &, double,
+                        const c10::optional<Tensor> &, double, bool);
+
+// -- autograd -------------------------------------------------------------------
+struct PropagateFn : public torch::autograd::Function<PropagateFn> {
+  static variable_list forward(AutogradContext *ctx, const Tensor &u0, const Tensor &i0,
+                               int64_t key, int64_t K, c10::string_view order) {
+    ctx->saved_data["key"] = key;
+    ctx->saved_data["K"] = K;
+    ctx->saved_data["order"] = std::string(order);
+    ctx->saved_data["su"] = u0.sizes().vec();
+    ctx->saved_data["si"] = i0.sizes().vec();
+    at::AutoDispatchBelowADInplaceOrView g;
+    static auto h = op<PropSig>("bbgr::propagate");
+    auto r = h.call(u0, i0, key, K, order);
+    return {std::get<0>(r), std::get<1>(r)};
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list go) {
+    const int64_t key = ctx->saved_data["key"].toInt(), K = ctx->saved_data["K"].toInt();
+    const std::string order = ctx->saved_data["order"].toStringRef();
+    const auto su = ctx->saved_data["su"].toIntVector(), si = ctx->saved_data["si"].toIntVector();
+    Tensor gU = go[0], gI = go[1];
+    if (gU.defined() && gU.layout() == at::kSparse && !(gI.defined() && gI.is_sparse())) {
+      // a BPR-shaped gradient handed over as rows (bbgr::bpr_loss_sparse_ego)
+      Tensor vals = gU._values();
+      if (!gI.defined()) gI = at::zeros(si, vals.options());
+      static auto h = op<RowsSig>("bbgr::propagate_backward_rows");
+      auto r = h.call(gU._indices().select(0, 0), vals, gI, su[0], key, K, order);
+      return {std::get<0>(r), std::get<1>(r), Tensor(), Tensor(), Tensor()};
+    }
+    if (gU.defined() && gU.is_sparse()) gU = gU.to_dense();
+    if (gI.defined() && gI.is_sparse()) gI = gI.to_dense();
+    const Tensor &ref = gU.defined() ? gU : gI;
+    if (!gU.defined()) gU = at::zeros(su, ref.options());
+    if (!gI.defined()) gI = at::zeros(si, ref.options());
+    static auto h = op<PropSig>("bbgr::propagate_backward");
+    auto r = h.call(gU, gI, key, K, order);
+    return {std::get<0>(r), std::get<1>(r), Tensor(), Tensor(), Tensor()};
+  }
+};
+
+struct JacobiLayerFn : public torch::autograd::Function<JacobiLayerFn> {
+  static variable_list forward(AutogradContext *ctx, const Tensor &u, const Tensor &i,
+                               int64_t key) {
+    ctx->saved_data["key"] = key;
+    ctx->saved_data["su"] = u.sizes().vec();
+    ctx->saved_data["si"] = i.sizes().vec();
+    at::AutoDispatchBelowADInplaceOrView g;
+    static auto h = op<LayerSig>("bbgr::jacobi_layer");
+    auto r = h.call(u, i, key);
+    return {std::get<0>(r), std::get<1>(r)};
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list go) {
+    const int64_t key = ctx->saved_data["key"].toInt();
+    const auto su = ctx->saved_data["su"].toIntVector(), si = ctx->saved_data["si"].toIntVector();
+    Tensor g_i = go[0], g_u = go[1];
+    const Tensor &ref = g_i.defined() ? g_i : g_u;
+    if (!g_i.defined()) g_i = at::zeros(si, ref.options());
+    if (!g_u.defined()) g_u = at::zeros(su, ref.options());
+    if (g_i.is_sparse()) g_i = g_i.to_dense();
+    if (g_u.is_sparse()) g_u = g_u.to_dense();
+    static auto h = op<LayerSig>("bbgr::jacobi_layer_backward");
+    auto r = h.call(g_i, g_u, key);
+    return {std::get<0>(r), std::get<1>(r), Tensor()};
+  }
+};
+
+struct PropagateSymFn : public torch::autograd::Function<PropagateSymFn> {
+  static Tensor forward(AutogradContext *ctx, const Tensor &x0, int64_t key, int64_t K) {
+    ctx->saved_data["key"] = key;
+    ctx->saved_data["K"] = K;
+    at::AutoDispatchBelowADInplaceOrView g;
+    static auto h = op<SymSig>("bbgr::propagate_sym");
+    return h.call(x0, key, K);
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list go) {
+    Tensor g = go[0].is_sparse() ? go[0].to_dense() : go[0];
+    static auto h = op<SymSig>("bbgr::propagate_sym_backward");
+    return {h.call(g, ctx->saved_data["key"].toInt(), ctx->saved_data["K"].toInt()), Tensor(),
+            Tensor()};
+  }
+};
+
+struct BprFn : public torch::autograd::Function<BprFn> {
+  static Tensor forward(AutogradContext *ctx, const Tensor &uf, const Tensor &itf,
+                        const Tensor &ue, const Tensor &ie, const Tensor &users,
+                        const Tensor &pos, const Tensor &neg, double reg,
+                        const c10::optional<Tensor> &pop, double lambda_fair) {
+    ctx->save_for_backward({uf, itf, ue, ie, users, pos, neg});
+    ctx->saved_data["reg"] = reg;
+    ctx->saved_data["lam"] = lambda_fair;
+    ctx->saved_data["pop"] = pop ? c10::IValue(*pop) : c10::IValue();
+    at::AutoDispatchBelowADInplaceOrView g;
+    static auto h = op<BprSig>("bbgr::bpr_loss");
+    return h.call(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair);
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list go) {
+    auto s = ctx->get_saved_variables();
+    c10::optional<Tensor> pop;
+    if (!ctx->saved_data["pop"].isNone()) pop = ctx->saved_data["pop"].toTensor();
+    static auto h = op<BprBwdSig>("bbgr::bpr_loss_backward");
+    auto r = h.call(go[0], s[0], s[1], s[2], s[3], s[4], s[5], s[6],
+                    ctx->saved_data["reg"].toDouble(), pop, ctx->saved_data["lam"].toDouble());
+    return {std::get<0>(r), std::get<1>(r), std::get<2>(r), std::get<3>(r), Tensor(), Tensor(),
+            Tensor(), Tensor(), Tensor(), Tensor()};
+  }
+};
+
+// bbgr::bpr_loss whose backward returns the ego-table gradients as sparse COO
+// batch rows (eager drop-in step; autograd adds them into propagate's dense
+// table in place) and, with sparse_uf, dL/d(u_final) as sparse rows too
+// (consumed by propagate's backward without a zero-filled table)
+struct BprSparseEgoFn : public torch::autograd::Function<BprSparseEgoFn> {
+  static Tensor forward(AutogradContext *ctx, const Tensor &uf, const Tensor &itf,
+                        const Tensor &ue, const Tensor &ie, const Tensor &users,
+                        const Tensor &pos, const Tensor &neg, double reg,
+                        const c10::optional<Tensor> &pop, double lambda_fair, bool sparse_uf) {
+    ctx->save_for_backward({uf, itf, ue, ie, users, pos, neg});
+    ctx->saved_data["reg"] = reg;
+    ctx->saved_data["lam"] = lambda_fair;
+    ctx->saved_data["pop"] = pop ? c10::IValue(*pop) : c10::IValue();
+    ctx->saved_data["sparse_uf"] = sparse_uf;
+    at::AutoDispatchBelowADInplaceOrView g;
+    static auto h = op<BprSeSig>("bbgr::bpr_loss_sparse_ego");
+    return h.call(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair, sparse_uf);
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list go) {
+    auto s = ctx->get_saved_variables();
+    Tensor uf = s[0].contiguous(), itf = s[1].contiguous(), ue = s[2].contiguous(),
+           ie = s[3].contiguous();
+    Tensor users = idx64(s[4]), pos = idx64(s[5]), neg = idx64(s[6]);
+    c10::optional<Tensor> pop;
+    if (!ctx->saved_data["pop"].isNone()) pop = ctx->saved_data["pop"].toTensor();
+    const double reg = ctx->saved_data["reg"].toDouble();
+    const int64_t B = users.numel();
+    Tensor dl = go[0].to(at::kFloat).contiguous().reshape({});
+    Tensor contrib = at::empty({3 * B, uf.size(1)}, f32(uf));
+    bbgr_bpr_args a = bpr_args(users, pos, neg, uf, itf, ue, ie, reg, pop,
+                               ctx->saved_data["lam"].toDouble());
+    a.dloss = dl.data_ptr<float>();
+    a.contrib = contrib.data_ptr<float>();
+    a.ldcontrib = ld(contrib);
+    check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr");
+    Tensor g_if = at::zeros_like(itf);
+    index_add_rows(g_if, at::cat({pos, neg}), contrib.narrow(0, B, 2 * B));
+    auto eg = ego_grad_rows(dl, users, pos, neg, ue, ie, reg);
+    const Tensor &ru = std::get<0>(eg), &ri = std::get<1>(eg), &iu = std::get<2>(eg),
+                 &ii = std::get<3>(eg);
+    Tensor g_uf;
+    if (ctx->saved_data["sparse_uf"].toBool()) {
+      // a dropped triple's row is +0.0 (the kernel zeroes it): clamped ids add nothing
+      g_uf = at::sparse_coo_tensor(iu.unsqueeze(0), contrib.narrow(0, 0, B), uf.sizes());
+    } else {
+      g_uf = at::zeros_like(uf);
+      index_add_rows(g_uf, users, contrib.narrow(0, 0, B));
+    }
+    Tensor g_ue = at::sparse_coo_tensor(iu.unsqueeze(0), ru, ue.sizes());
+    Tensor g_ie = at::sparse_coo_tensor(ii.unsqueeze(0), ri, ie.sizes());
+    return {g_uf, g_if, g_ue, g_ie, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(),
+            Tensor()};
+  }
+};
+
+static std::tuple<Tensor, Tensor> propagate_autograd(const Tensor &u0, const Tensor &i0,
+                                                     int64_t key, int64_t K,
+                                                     c10::string_view order) {
+  auto r = PropagateFn::apply(u0, i0, key, K, order);
+  return {r[0], r[1]};
+}
+static std::tuple<Tensor, Tensor> jacobi_layer_autograd(const Tensor &u, const Tensor &i,
+                                                        int64_t key) {
+  auto r = JacobiLayerFn::apply(u, i, key);
+  return {r[0], r[1]};
+}
+static Tensor propagate_sym_autograd(const Tensor &x0, int64_t key, int64_t K) {
+  return PropagateSymFn::apply(x0, key, K);
+}
+static Tensor bpr_loss_autograd(const Tensor &uf, const Tensor &itf, const Tensor &ue,
+                                const Tensor &ie, const Tensor &users, const Tensor &pos,
+                                const Tensor &neg, double reg, const c10::optional<Tensor> &pop,
+                                double lambda_fair) {
+  return BprFn::apply(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair);
+}
+static Tensor bpr_loss_sparse_ego_autograd(const Tensor &uf, const Tensor &itf, const Tensor &ue,
+                                           const Tensor &ie, const Tensor &users,
+                                           const Tensor &pos, const Tensor &neg, double reg,
+                                           const c10::optional<Tensor> &pop, double lambda_fair,
+                                           bool sparse_uf) {
+  return BprSparseEgoFn::apply(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair,
+                               sparse_uf);
+}
+
+// -- registration of operator pairs ---------------------------------------------
+// tensors: per product (fwd_item, fwd_user, bwd_item, bwd_user) 9 entries
+//   [indptr, indices, chunks, split, vals, in_scale, out_scale, first_vals,
+//    input_indices], then feed_fwd_iu, feed_fwd_ui, feed_bwd_iu, feed_bwd_ui,
+//   then user_map, item_map, user_rank, item_rank (input-order pairs).
+// meta: per product 10 ints [n_rows, n_cols, nnz, long_threshold, chunk_edges,
+//   n_chunks, n_split, cols_by_degree, rows_by_degree, hot_bytes], then U, I.
+static constexpr int kTensPerProduct = 9, kMetaPerProduct = 10;
+
+static void register_pair(int64_t key, const std::vector<c10::optional<Tensor>> &t,
+                          const std::vector<int64_t> &m) {
+  TORCH_CHECK(t.size() == 4 * kTensPerProduct + 8, "_register_pair: tensor list of ", t.size());
+  TORCH_CHECK(m.size() == 4 * kMetaPerProduct + 2, "_register_pair: meta list of ", m.size());
+  auto P = std::make_shared<Pair>();
+  auto get = [&](size_t j) -> Tensor {
+    if (!t[j] || !t[j]->defined()) return Tensor();
+    P->keep.push_back(*t[j]);
+    return *t[j];
+  };
+  Product *prods[4] = {&P->fi, &P->fu, &P->bi, &P->bu};
+  for (int q = 0; q < 4; ++q) {
+    Product &pr = *prods[q];
+    const size_t b = (size_t)q * kTensPerProduct;
+    const int64_t *mm = m.data() + q * kMetaPerProduct;
+    Tensor indptr = get(b), indices = get(b + 1), chunks = get(b + 2), split = get(b + 3);
+    TORCH_CHECK(indptr.defined() && indices.defined() && indptr.scalar_type() == at::kInt &&
+                    indices.scalar_type() == at::kInt,
+                "_register_pair: int32 indptr / indices");
+    pr.csr.n_rows = (int32_t)mm[0];
+    pr.csr.n_cols = (int32_t)mm[1];
+    pr.csr.nnz = mm[2];
+    pr.csr.indptr = indptr.data_ptr<int32_t>();
+    pr.csr.indices = indices.data_ptr<int32_t>();
+    pr.csr.long_threshold = (int32_t)mm[3];
+    pr.csr.chunk_edges = (int32_t)mm[4];
+    pr.csr.n_chunks = (int32_t)mm[5];
+    pr.csr.n_split = (int32_t)mm[6];
+    pr.csr.chunks = chunks.defined() ? chunks.data_ptr<int32_t>() : nullptr;
+    pr.csr.split = split.defined() ? split.data_ptr<int32_t>() : nullptr;
+    pr.cols_by_degree = mm[7] != 0;
+    pr.rows_by_degree = mm[8] != 0;
+    pr.hot_bytes = mm[9];
+    Tensor vals = get(b + 4), in_scale = get(b + 5), out_scale = get(b + 6),
+           first = get(b + 7), in_idx = get(b + 8);
+    pr.vals = vals.defined() ? vals.data_ptr<float>() : nullptr;
+    pr.in_scale = in_scale.defined() ? in_scale.data_ptr<float>() : nullptr;
+    pr.out_scale = out_scale.defined() ? out_scale.data_ptr<float>() : nullptr;
+    pr.first_vals = first.defined() ? first.data_ptr<float>() : nullptr;
+    if (in_idx.defined()) {
+      pr.has_in = true;
+      pr.csr_in = pr.csr;
+      pr.csr_in.indices = in_idx.data_ptr<int32_t>();
+    }
+  }
+  const size_t f = 4 * kTensPerProduct;
+  Tensor a = get(f), b = get(f + 1), c = get(f + 2), d = get(f + 3);
+  P->feed_fwd_iu = a.defined() ? a.data_ptr<float>() : nullptr;
+  P->feed_fwd_ui = b.defined() ? b.data_ptr<float>() : nullptr;
+  P->feed_bwd_iu = c.defined() ? c.data_ptr<float>() : nullptr;
+  P->feed_bwd_ui = d.defined() ? d.data_ptr<float>() : nullptr;
+  Tensor um = get(f + 4), im = get(f + 5), ur = get(f + 6), ir = get(f + 7);
+  P->U = m[4 * kMetaPerProduct];
+  P->I = m[4 * kMetaPerProduct + 1];
+  if (um.defined()) {
+    TORCH_CHECK(im.defined() && ur.defined() && ir.defined(), "_register_pair: partial io maps");
+    P->io = true;
+    P->user_map = um;
+    P->item_map = im;
+    P->item_map64 = im.to(at::kLong);
+    P->user_rank64 = ur.to(at::kLong);
+    P->item_rank64 = ir.to(at::kLong);
+    TORCH_CHECK(P->fi.has_in && P->fu.has_in && P->bi.has_in && P->bu.has_in,
+                "_register_pair: input-order pair without input-id columns");
+  }
+  std::lock_guard<std::mutex> g(g_mu);
+  g_pairs[key] = P;
+}
+
+static void unregister_pair(int64_t key) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_pairs.find(key);
+  if (it == g_pairs.end()) return;
+  const Pair &P = *it->second;
+  for (const Product *pr : {&P.fi, &P.fu, &P.bi, &P.bu}) {   // its split-row workspaces
+    for (auto w = g_ws.begin(); w != g_ws.end();) {
+      if (std::get<0>(w->first) == (const void *)pr->csr.indptr) w = g_ws.erase(w);
+      else ++w;
+    }
+  }
+  g_pairs.erase(it);
+}
+
+// (rows-path backwards, dense backwards) issued so far: tests check which
+// backward the autograd graph took
+static std::vector<int64_t> counters() { return {g_rows_backward.load(), g_dense_backward.load()}; }
+
+}  // namespace bbgr_torch
+
+TORCH_LIBRARY(bbgr, m) {
+  m.def("propagate(Tensor u0, Tensor i0, int pair_key, int num_layers, str order) -> (Tensor, Tensor)");
+  m.def("propagate_backward(Tensor gU, Tensor gI, int pair_key, int num_layers, str order) -> (Tensor, Tensor)");
+  m.def("propagate_backward_rows(Tensor iu, Tensor vu, Tensor gI, int num_users, int pair_key, "
+        "int num_layers, str order) -> (Tensor, Tensor)");
+  m.def("jacobi_layer(Tensor u, Tensor i, int pair_key) -> (Tensor, Tensor)");
+  m.def("jacobi_layer_backward(Tensor g_i, Tensor g_u, int pair_key) -> (Tensor, Tensor)");
+  m.def("propagate_sym(Tensor x0, int pair_key, int num_layers) -> Tensor");
+  m.def("propagate_sym_backward(Tensor g, int pair_key, int num_layers) -> Tensor");
+  m.def("bpr_loss(Tensor uf, Tensor itf, Tensor ue, Tensor ie, Tensor users, Tensor pos, "
+        "Tensor neg, float reg, Tensor? pop, float lambda_fair) -> Tensor");
+  m.def("bpr_loss_backward(Tensor dloss, Tensor uf, Tensor itf, Tensor ue, Tensor ie, "
+        "Tensor users, Tensor pos, Tensor neg, float reg, Tensor? pop, float lambda_fair) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("bpr_loss_sparse_ego(Tensor uf, Tensor itf, Tensor ue, Tensor ie, Tensor users, "
+        "Tensor pos, Tensor neg, float reg, Tensor? pop, float lambda_fair, bool sparse_uf) "
+        "-> Tensor");
+  m.def("_register_pair(int key, Tensor?[] tensors, int[] meta) -> ()",
+        &bbgr_torch::register_pair);
+  m.def("_unregister_pair(int key) -> ()", &bbgr_torch::unregister_pair);
+  m.def("_counters() -> int[]", &bbgr_torch::counters);
+}
+
+TORCH_LIBRARY_IMPL(bbgr, CUDA, m) {
+  m.impl("propagate", &bbgr_torch::propagate_cuda);
+  m.impl("propagate_backward", &bbgr_torch::propagate_backward_cuda);
+  m.impl("propagate_backward_rows", &bbgr_torch::propagate_backward_rows_cuda);
+  m.impl("jacobi_layer", &bbgr_torch::jacobi_layer_cuda);
+  m.impl("jacobi_layer_backward", &bbgr_torch::jacobi_layer_backward_cuda);
+  m.impl("propagate_sym", &bbgr_torch::propagate_sym_cuda);
+  m.impl("propagate_sym_backward", &bbgr_torch::propagate_sym_backward_cuda);
+  m.impl("bpr_loss", &bbgr_torch::bpr_loss_cuda);
+  m.impl("bpr_loss_backward", &bbgr_torch::bpr_loss_backward_cuda);
+  m.impl("bpr_loss_sparse_ego", &bbgr_torch::bpr_loss_sparse_ego_cuda);
+}
+
+TORCH_LIBRARY_IMPL(bbgr, Meta, m) {
+  m.impl("propagate", &bbgr_torch::propagate_meta);
+  m.impl("propagate_backward", &bbgr_torch::propagate_meta);
+  m.impl("propagate_backward_rows", &bbgr_torch::propagate_backward_rows_meta);
+  m.impl("jacobi_layer", &bbgr_torch::jacobi_layer_meta);
+  m.impl("jacobi_layer_backward", &bbgr_torch::jacobi_layer_backward_meta);
+  m.impl("propagate_sym", &bbgr_torch::propagate_sym_meta);
+  m.impl("propagate_sym_backward", &bbgr_torch::propagate_sym_meta);
+  m.impl("bpr_loss", &bbgr_torch::bpr_loss_meta);
+  m.impl("bpr_loss_backward", &bbgr_torch::bpr_loss_backward_meta);
+  m.impl("bpr_loss_sparse_ego", &bbgr_torch::bpr_loss_sparse_ego_meta);
+}
+
+TORCH_LIBRARY_IMPL(bbgr, Autograd, m) {
+  m.impl("propagate", &bbgr_torch::propagate_autograd);
+  m.impl("jacobi_layer", &bbgr_torch::jacobi_layer_autograd);
+  m.impl("propagate_sym", &bbgr_torch::propagate_sym_autograd);
+  m.impl("bpr_loss", &bbgr_torch::bpr_loss_autograd);
+  m.impl("bpr_loss_sparse_ego", &bbgr_torch::bpr_loss_sparse_ego_autograd);
+}

@@ -216,7 +216,8 @@ def test_bench_two_ranks_on_c2(tmp_path, partition):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "3",
            "--warmup", "1", "--dense-check", "1", "--frontier", "on", "--partition", partition,
-           "--weak-beside", "2"] + (["--column-chains", "2"] if chains else [])
+           "--weak-beside", "2", "--partition-beside", "0"] + \
+        (["--column-chains", "2"] if chains else [])
     env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -228,7 +229,23 @@ def test_bench_two_ranks_on_c2(tmp_path, partition):
     assert j["roofline"]["bound"] == "hbm" and j["dense_ms_per_step"] > 0
     if chains:
         assert "2 column chains, 1 item-row ranges" in j["config"]["parallelism"]
-    if partition == "users":
-        assert j["weak_beside"]["num_edges"] == 2_000_000
-    else:
-        assert j["weak_beside"] is None
+    assert j["weak_beside"]["num_edges"] == 2_000_000   # every strong partition
+    assert j["partition_beside"] is None
+
+
+def test_bench_two_ranks_measures_both_partitions(tmp_path):
+    """--partition-beside (the N > 1 default): the other partition of the same
+    graph is timed the same way in the same run; the faster is the line and the
+    other is reported beside it."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "3",
+           "--warmup", "1", "--dense-check", "1", "--frontier", "on", "--weak-beside", "0"]
+    env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    j = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    b = j["partition_beside"]
+    assert {j["partition"], b["part"]} == {"columns", "users"}
+    assert j["ms_per_step"] <= b["ms_per_step"] and b["E"] == 1_000_000
+    assert j["weak_beside"] is None and j["dense_ms_per_step"] > 0

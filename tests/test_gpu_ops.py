@@ -174,6 +174,34 @@ def test_row_support_kernel(d, ld):
     assert torch.equal(nbr.cpu().bool(), want_nbr)
 
 
+@pytest.mark.parametrize("family", ["v2", "cu", "sym"])
+def test_cpp_operators_equal_the_python_chain(family):
+    """torch.ops.bbgr.* (csrc/torch_ops.cpp) issue the same launches as the
+    Python chain (propagate.forward / backward): bitwise equal outputs."""
+    from bbgr import ops
+    from bbgr.propagate import ORDER_GS, ORDER_J, backward, forward
+    m = _model(family)
+    pair = m.norm_adj.pair if family == "sym" else m._operator_pair()
+    order = ORDER_GS if family == "v2" else ORDER_J
+    if family == "sym":
+        u0, i0 = m.emb.weight[:U].detach(), m.emb.weight[U:].detach()
+    else:
+        u0, i0 = m.user_emb.weight.detach(), m.item_emb.weight.detach()
+    key = ops.pair_key(pair)
+    a = ops.propagate(u0, i0, key, K, order)
+    b = forward(pair, u0, i0, K, order)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    g = torch.Generator().manual_seed(9)
+    gU, gI = torch.randn(U, D, generator=g).to(DEV), torch.randn(I, D, generator=g).to(DEV)
+    a = ops.propagate_backward(gU, gI, key, K, order)
+    b = backward(pair, gU, gI, K, order)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    if family == "sym":
+        x0 = m.emb.weight.detach()
+        assert torch.equal(ops.propagate_sym(x0, key, K), torch.cat(forward(pair, u0, i0, K,
+                                                                           ORDER_J)))
+
+
 @pytest.mark.parametrize("order", ["gs", "jacobi"])
 def test_backward_op_support_masks_are_bitwise_dense(order):
     """bbgr::propagate_backward reads the gradients' row support and masks the
@@ -207,20 +235,18 @@ def test_sparse_ego_gradient_is_bitwise_dense(family, layers, monkeypatch):
     neg = neg.clone()
     neg[7] = -1
     grads = {}
-    rows_calls = []
-    real_rows = ops.propagate_backward_rows
-    monkeypatch.setattr(ops, "propagate_backward_rows",
-                        lambda *a: rows_calls.append(1) or real_rows(*a))
     for mode in ("sparse", "dense"):
         if mode == "dense":
             monkeypatch.setattr(bpr, "_receives_dense_grad", lambda *a: False)
         m = _model(family, layers=layers)
         loss = _loss(m, users, pos, neg)
-        assert ("bpr_loss_sparse_ego" in loss.grad_fn.name()) == (mode == "sparse")
-        n0 = len(rows_calls)
+        assert ("sparseego" in loss.grad_fn.name().lower()) == (mode == "sparse")
+        n0 = ops.counters()
         loss.backward()
+        n1 = ops.counters()
         # sparse mode: dL/d(u_final) reaches propagate's backward as rows too
-        assert len(rows_calls) - n0 == (1 if mode == "sparse" else 0)
+        assert n1["rows"] - n0["rows"] == (1 if mode == "sparse" else 0)
+        assert n1["dense"] - n0["dense"] == (0 if mode == "sparse" else 1)
         grads[mode] = (float(loss), [p.grad for p in m.parameters()])
         assert all(p.grad.layout == torch.strided for p in m.parameters())
     assert grads["sparse"][0] == grads["dense"][0]
@@ -235,7 +261,7 @@ def test_sparse_ego_not_chosen_without_dense_path():
     uf, itf = m.get_user_item_emb()
     users, pos, neg = _batch(6)
     loss = m.bpr_loss(users, pos, neg, uf.detach(), itf.detach(), 1e-4)
-    assert "sparse" not in str(loss.grad_fn.name())
+    assert "sparse" not in loss.grad_fn.name().lower()
     loss.backward()
     assert m.user_emb.weight.grad.layout == torch.strided
     # a node with a direct edge to the weight that is NOT the propagate op (an
@@ -244,6 +270,6 @@ def test_sparse_ego_not_chosen_without_dense_path():
     uf2 = m.user_emb.weight + uf.detach()
     itf2 = m.item_emb.weight + itf.detach()
     loss = m.bpr_loss(users, pos, neg, uf2, itf2, 1e-4)
-    assert "sparse" not in str(loss.grad_fn.name())
+    assert "sparse" not in loss.grad_fn.name().lower()
     loss.backward()
     assert m.user_emb.weight.grad.layout == torch.strided
