@@ -86,6 +86,7 @@ class SpmmArgs(ctypes.Structure):
         ("stream_from", c_int32), ("stream_out_from", c_int32),
         ("adam_bc_table", c_void_p), ("adam_state", c_void_p),
         ("y_map", c_void_p), ("acc_map", c_void_p), ("add_map", c_void_p),
+        ("src_bits", c_void_p),
     ]
 
 
@@ -142,6 +143,8 @@ _SIGNATURES = {
                               _P, _P, _P, _P, _P], c_int32),
     "bbgr_gather_scale": ([c_int64, _P, _P, _P, _P], c_int32),
     "bbgr_degree_count": ([c_int64, _P, c_int32, _P, _P], c_int32),
+    "bbgr_degree_count_ws": ([c_int64, _P, c_int32, _P, _P, ctypes.POINTER(c_size_t), _P],
+                             c_int32),
     "bbgr_degree_order": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_relabel": ([c_int64, _P, _P, _P, _P], c_int32),
     "bbgr_spmm": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(SpmmArgs), _P], c_int32),
@@ -164,6 +167,9 @@ _SIGNATURES = {
     "bbgr_scatter_add_rows": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P,
                                ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
+    "bbgr_mark_slots": ([c_int64, _P, _P, _P, _P, c_int32, _P], c_int32),
+    "bbgr_transpose_slots": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(CsrStruct), _P, _P],
+                             c_int32),
     "bbgr_mark_neighbors_of_mask": ([c_int64, _P, _P, _P, _P, ctypes.c_uint8, _P, _P],
                                     c_int32),
     "bbgr_row_support": ([c_int64, c_int32, _P, c_int64, _P, _P, _P, _P, _P], c_int32),

@@ -271,9 +271,50 @@ __global__ void gather_scale_kernel(long nnz, const int *indices, const float *s
 
 // Vertex order: degree histogram (integer atomics: exact), iota values for
 // the descending sort, inverse permutation, id relabelling.
+// For every slot s of CSR a (row r, column c): the slot of CSR b (the
+// transpose: row c, column-sorted) that holds the same edge; the k-th copy of
+// a duplicate pair maps to the k-th copy. One 16-lane group per row of a.
+__global__ void transpose_slots_kernel(int n_rows, const int *a_indptr, const int *a_indices,
+                                       const int *b_indptr, const int *b_indices, int *out) {
+  const long r = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (r >= n_rows) return;
+  for (int s = a_indptr[r] + (threadIdx.x & 15); s < a_indptr[r + 1]; s += 16) {
+    const int c = a_indices[s];
+    int k = 0;   // earlier copies of (r, c) in this row (a's columns are sorted)
+    while (s - k - 1 >= a_indptr[r] && a_indices[s - k - 1] == c) ++k;
+    int lo = b_indptr[c], hi = b_indptr[c + 1];   // first position holding r
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (b_indices[mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    out[s] = lo + k;
+  }
+}
+
 __global__ void degree_count_kernel(long n, const int *ids, int *deg) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < n) atomicAdd(deg + ids[e], 1);
+}
+
+// Replicated counters: workgroup b counts into copy b % DEG_COPIES. Workgroups
+// are dispatched round-robin to the 8 XCDs, so each copy takes the atomics
+// of one XCD and a power-law id (one item holds ~1 % of a Zipf graph's edges)
+// sees 1/8 of the same-address traffic; a second pass sums the copies.
+constexpr int DEG_COPIES = 8;
+__global__ void degree_count_copies_kernel(long n, const int *ids, int n_bins, int *copies) {
+  int *mine = copies + (long)(blockIdx.x % DEG_COPIES) * n_bins;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) atomicAdd(mine + ids[e], 1);
+}
+
+__global__ void degree_sum_copies_kernel(int n_bins, const int *copies, int *deg) {
+  const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_bins) return;
+  int s = 0;
+#pragma unroll
+  for (int c = 0; c < DEG_COPIES; ++c) s += copies[(long)c * n_bins + j];
+  deg[j] = s;
 }
 
 __global__ void iota_kernel(int n, int *out) {
@@ -618,6 +659,19 @@ extern "C" int bbgr_gather_scale(int64_t nnz, const int32_t *indices,
   return BBGR_OK;
 }
 
+extern "C" int bbgr_transpose_slots(const bbgr_csr *a, const bbgr_csr *b, int32_t *out,
+                                    bbgr_stream_t stream) {
+  BBGR_REQUIRE(a && b && out, "bbgr_transpose_slots: null args");
+  BBGR_REQUIRE(a->n_rows == b->n_cols && a->n_cols == b->n_rows && a->nnz == b->nnz,
+               "bbgr_transpose_slots: b is not the transpose of a");
+  if (a->n_rows == 0 || a->nnz == 0) return BBGR_OK;
+  hipLaunchKernelGGL(transpose_slots_kernel, dim3((unsigned)((a->n_rows + 15) / 16)), dim3(256),
+                     0, as_stream(stream), (int)a->n_rows, a->indptr, a->indices, b->indptr,
+                     b->indices, out);
+  BBGR_LAUNCHED("transpose_slots_kernel");
+  return BBGR_OK;
+}
+
 extern "C" int bbgr_nonempty_rows(int32_t n_rows, const int32_t *indptr,
                                   int64_t *out, int64_t *count, void *workspace,
                                   size_t *workspace_bytes, bbgr_stream_t stream) {
@@ -674,6 +728,35 @@ extern "C" int bbgr_mask_to_list(int64_t n, const uint8_t *mask, int64_t *out,
   }
   BBGR_HIP(hipcub::DeviceSelect::If(workspace, temp, it, (long *)out, (long *)count, (int)n,
                                     sel, st));
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_degree_count_ws(int64_t n_ids, const int32_t *ids, int32_t n,
+                                    int32_t *degree, void *workspace, size_t *workspace_bytes,
+                                    bbgr_stream_t stream) {
+  BBGR_REQUIRE(workspace_bytes && n_ids >= 0 && n >= 0, "bbgr_degree_count_ws: bad args");
+  const size_t need = (size_t)DEG_COPIES * 4 * (size_t)(n > 0 ? n : 1);
+  if (!workspace) {
+    *workspace_bytes = need;
+    return BBGR_OK;
+  }
+  if (*workspace_bytes < need) {
+    set_error("bbgr_degree_count_ws: workspace %zu < %zu", *workspace_bytes, need);
+    return BBGR_ERR_WORKSPACE;
+  }
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(degree && (n_ids == 0 || ids), "bbgr_degree_count_ws: null arrays");
+  hipStream_t st = as_stream(stream);
+  int *copies = static_cast<int *>(workspace);
+  BBGR_HIP(hipMemsetAsync(copies, 0, need, st));
+  if (n_ids > 0) {
+    hipLaunchKernelGGL(degree_count_copies_kernel, dim3(blocks_for(n_ids)), dim3(256), 0, st,
+                       (long)n_ids, ids, (int)n, copies);
+    BBGR_LAUNCHED("degree_count_copies_kernel");
+  }
+  hipLaunchKernelGGL(degree_sum_copies_kernel, dim3(blocks_for(n)), dim3(256), 0, st, (int)n,
+                     (const int *)copies, degree);
+  BBGR_LAUNCHED("degree_sum_copies_kernel");
   return BBGR_OK;
 }
 

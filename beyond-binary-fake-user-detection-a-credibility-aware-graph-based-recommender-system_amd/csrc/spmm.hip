@@ -79,6 +79,7 @@ struct SpmmParams {
   // CSR row r reads / writes row map[r] of y (and the fused Adam's rows), of
   // acc_in / acc_out, of add; the masks of those tables index the same rows
   const int *y_map, *acc_map, *add_map;
+  const unsigned *src_bits;    // slot bitmap of live edges (args.src_bits; d >= 64)
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -203,6 +204,14 @@ template <> struct Tune<256> {
 };
 #define BBGR_WAVES(n) __attribute__((amdgpu_waves_per_eu((n) ? (n) : 1, (n) ? (n) : 10)))
 
+// Bits [e, e + 64) of a slot bitmap (3 words of padding past the end).
+__device__ __forceinline__ unsigned long long slot_bits64(const unsigned *bits, int e) {
+  const int w = e >> 5, sh = e & 31;
+  const unsigned long long x =
+      (unsigned long long)bits[w] | ((unsigned long long)bits[w + 1] << 32);
+  return sh ? (x >> sh) | ((unsigned long long)bits[w + 2] << (64 - sh)) : x;
+}
+
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
 template <int D, int WMODE, bool MASKED>
 __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
@@ -211,17 +220,32 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
   constexpr int U = Tune<D>::row_u;   // source rows in flight per group per batch
   for (int e0 = eb; e0 < ee; e0 += 16) {
     const int n = min(16, ee - e0);
+    unsigned live = 0xffffu;   // slot-bitmap mode: this batch's live edges
+    if (MASKED && P.src_bits) {
+      // liveness from the bitmap, 64 edges per test: a dead window costs one
+      // (cached) 12-byte load instead of 64 index + mask loads; the live
+      // edges are exactly src_mask's, in the same order (bitwise identical)
+      unsigned long long win = slot_bits64(P.src_bits, e0);
+      const int span = ee - e0;
+      if (span < 64) win &= (1ull << span) - 1ull;
+      if (win == 0ull) {
+        e0 += 48;   // + 16 by the loop: the next 64-edge window
+        continue;
+      }
+      live = (unsigned)(win & 0xffffull);
+      if (live == 0u) continue;
+    }
     int my = -1;
     float mw = 0.f;
-    if (lane < n) {
+    if (lane < n && ((live >> lane) & 1u)) {
       my = P.indices[e0 + lane];
-      if (MASKED && P.src_mask && !P.src_mask[my]) my = -1;   // exact-zero source row
+      if (MASKED && P.src_mask && !P.src_bits && !P.src_mask[my]) my = -1;   // exact-zero source row
       if (my >= 0) {
         if (WMODE == 1) mw = P.edge_val[e0 + lane];
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
       }
     }
-    if (MASKED && P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
+    if (MASKED && P.src_mask && !P.src_bits) {   // skip 16-edge batches with no live source (group-uniform)
       const unsigned long long live = __ballot(my >= 0);
       if (((live >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
     }
@@ -929,6 +953,7 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.y_map = a->y_map;
   P.acc_map = a->acc_map;
   P.add_map = a->add_map;
+  P.src_bits = a->src_bits;
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {
@@ -998,6 +1023,8 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
                                "(16-byte aligned, adam_ld >= d) and bias corrections > 0");
   BBGR_REQUIRE(!a->adam_param || !(a->src_mask || a->row_mask || a->row_list || a->use_range),
                "bbgr_spmm: fused Adam needs every row (no masks, row list or range)");
+  BBGR_REQUIRE(!a->src_bits || a->src_mask,
+               "bbgr_spmm: src_bits needs src_mask (narrow and two-row kernels read the mask)");
   BBGR_REQUIRE(a->weight_mode != 1 || a->edge_val, "bbgr_spmm: weight_mode 1 needs edge_val");
   BBGR_REQUIRE(a->weight_mode != 2 || a->col_scale, "bbgr_spmm: weight_mode 2 needs col_scale");
   BBGR_REQUIRE(csr->n_chunks == 0 || csr->chunks, "bbgr_spmm: plan chunks missing");

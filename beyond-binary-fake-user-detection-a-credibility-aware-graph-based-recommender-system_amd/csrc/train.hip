@@ -304,6 +304,21 @@ __global__ void mark_neighbors_kernel(long n, const long *rows, const int *indpt
     mask[indices[e]] = v;
 }
 
+// slot bitmap of the listed rows' edges in the TRANSPOSE CSR: for every edge e
+// of row rows[k], bit tmap[e] of bits is set (set != 0, atomic OR) or its
+// whole word cleared (set == 0; a later launch, so no OR races the store)
+__global__ void mark_slots_kernel(long n, const long *rows, const int *indptr, const int *tmap,
+                                  unsigned *bits, int set) {
+  const long k = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (k >= n || rows[k] < 0) return;
+  const long r = rows[k];
+  for (int e = indptr[r] + (threadIdx.x & 15); e < indptr[r + 1]; e += 16) {
+    const int sl = tmap[e];
+    if (set) atomicOr(bits + (sl >> 5), 1u << (sl & 31));
+    else bits[sl >> 5] = 0u;
+  }
+}
+
 // every neighbour of a row flagged in row_mask (indexed through row_map when
 // given: CSR row r is flagged by row_mask[row_map[r]]) is set to v in mask
 __global__ void mark_neighbors_of_mask_kernel(long n_rows, const unsigned char *row_mask,
@@ -640,6 +655,18 @@ extern "C" int bbgr_mark_neighbors(int64_t n, const int64_t *rows,
                      as_stream(stream), (long)n, (const long *)rows, indptr, indices, value,
                      mask);
   BBGR_LAUNCHED("mark_neighbors_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_mark_slots(int64_t n, const int64_t *rows, const int32_t *indptr,
+                               const int32_t *tmap, uint32_t *bits, int32_t set,
+                               bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_mark_slots: negative n");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(rows && indptr && tmap && bits, "bbgr_mark_slots: null arrays");
+  hipLaunchKernelGGL(mark_slots_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)rows, indptr, tmap, bits, (int)set);
+  BBGR_LAUNCHED("mark_slots_kernel");
   return BBGR_OK;
 }
 

@@ -270,8 +270,15 @@ class VertexOrder:
 
 
 def _degree_count(ids: torch.Tensor, n: int) -> torch.Tensor:
+    """Exact occurrence counts (bbgr_degree_count_ws: per-XCD counter copies)."""
     deg = torch.empty(max(n, 1), dtype=torch.int32, device=ids.device)
-    call("bbgr_degree_count", ids.numel(), ptr(ids), n, ptr(deg), stream_handle())
+    st = stream_handle()
+    nb = _lib.workspace_query("bbgr_degree_count_ws", ids.numel(), ptr(ids), n, ptr(deg),
+                              args_after=(st,))
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=ids.device)
+    have = ctypes.c_size_t(nb)
+    call("bbgr_degree_count_ws", ids.numel(), ptr(ids), n, ptr(deg), ptr(ws),
+         ctypes.byref(have), st)
     return deg[:n]
 
 
@@ -388,6 +395,20 @@ class BipartiteGraph:
         sc._cred = cred  # keep alive
         self._scales[key] = sc
         return sc
+
+    def user_item_slots(self) -> torch.Tensor:
+        """int32 [nnz]: for every user-CSR slot, the item-CSR slot of the same
+        edge (bbgr_transpose_slots; built once). Feeds the slot bitmap of a
+        batch's user edges (bbgr_mark_slots -> bbgr_spmm_args.src_bits)."""
+        t = self.__dict__.get("_u2i_slots")
+        if t is None:
+            if not (self.user_csr.cols_sorted and self.item_csr.cols_sorted):
+                raise ValueError("user_item_slots needs column-sorted CSR rows")
+            t = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=self.device)
+            call("bbgr_transpose_slots", ctypes.byref(self.user_csr._struct),
+                 ctypes.byref(self.item_csr._struct), ptr(t), stream_handle())
+            self._u2i_slots = t
+        return t
 
     def nbytes(self) -> int:
         return self.user_csr.nbytes() + self.item_csr.nbytes()

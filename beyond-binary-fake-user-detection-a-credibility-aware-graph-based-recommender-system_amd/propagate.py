@@ -306,12 +306,13 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
          add_mask=None, row_list=None, rng=None, adam=None, y_map=None, acc_map=None,
-         add_map=None, src_input: bool = False) -> None:
+         add_map=None, src_input: bool = False, src_bits=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream. `adam`
     (optim.AdamRows): apply Adam to each row's y value in the epilogue.
     `y_map` / `acc_map` / `add_map`: row maps of those tables (input-order
     tables of a degree-ordered pair); `src_input`: x is gathered through the
-    CSR's input-id column indices (Product.input_struct)."""
+    CSR's input-id column indices (Product.input_struct). `src_bits`: the slot
+    bitmap of src_mask's live edges in this CSR (bbgr_spmm_args.src_bits)."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
     a.d = d
@@ -342,6 +343,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     if adam is not None:
         adam.fill(a)
     a.y_map, a.acc_map, a.add_map = ptr(y_map), ptr(acc_map), ptr(add_map)
+    if src_bits is not None and src_mask is not None:
+        a.src_bits = ptr(src_bits)
     # input-order source rows carry no hot prefix; mapped output rows neither
     a.stream_from = 0 if src_input else prod.csr.stream_from(d)
     a.stream_out_from = 0 if y_map is not None else prod.csr.stream_out_from(d)
@@ -405,6 +408,7 @@ def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw
     for key in ("y_map", "acc_map", "add_map", "src_input"):   # input-order pairs only
         if kw.pop(key, None):
             raise ValueError("sharded item products take no input-order maps")
+    kw.pop("src_bits", None)   # an index-scan shortcut only: the mask alone is exact
     if hasattr(reduce, "item_product"):   # chunked / overlapped exchange
         reduce.item_product(prod, x, first, new, kw)
         return
@@ -539,7 +543,7 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                    order: str = ORDER_GS, out_u: torch.Tensor | None = None,
                    out_i: torch.Tensor | None = None, ws: dict | None = None,
                    grad_i0_dense: bool = True, reduce=None, grad_support=None,
-                   adam_u=None, before_last=None, adam_i=None):
+                   adam_u=None, before_last=None, adam_i=None, src_bits=None):
     """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final); a
     generator yielding after each item-row product, like forward_steps.
     `adam_u` (optim.AdamRows) fuses the user-table Adam step into the last
@@ -553,7 +557,10 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     and, for GS, the first item product's output is zero outside the flagged
     items (GS: batch items and N(batch users); Jacobi: gI's own support). The
     first products of the chain then skip the exact-zero source rows; results
-    are bitwise identical to the dense chain (the skipped terms are +0.0)."""
+    are bitwise identical to the dense chain (the skipped terms are +0.0).
+    `src_bits`: the item-CSR slot bitmap of the flagged users' edges
+    (graph.user_item_slots + bbgr_mark_slots): the first item product then
+    tests liveness on it instead of scanning every index of its rows."""
     U, I = pair.num_users, pair.num_items
     d = gU.shape[1]
     _check_table("user grad", gU, U, d)
@@ -596,7 +603,7 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                           add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
                           src_mask=su if first else None,
                           row_mask=si_int if first else None, add_map=im,
-                          src_input=inp and first)
+                          src_input=inp and first, src_bits=src_bits if first else None)
             yield
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
@@ -637,7 +644,8 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                 _item_product(BI, xi, first, reduce, new, y=bufI[nxt],
                               y_scale=pair.feed_bwd_iu, y_scale_s=ys,
                               add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
-                              src_mask=mi_, add_map=im, src_input=src_in)
+                              src_mask=mi_, add_map=im, src_input=src_in,
+                              src_bits=src_bits if first else None)
                 yield
             else:
                 if before_last is not None and adam_u is not None:
@@ -647,7 +655,8 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                      src_mask=mu_, adam=adam_u, add_map=um, y_map=um, src_input=src_in)
                 ik = dict(y=None if adam_i is not None else gi0, y_scale=BI.out_scale,
                           y_scale_s=ys, add=gI, add_mask=si, add_scale=None, add_scale_s=gl,
-                          src_mask=mi_, add_map=im, y_map=im, src_input=src_in)
+                          src_mask=mi_, add_map=im, y_map=im, src_input=src_in,
+                          src_bits=src_bits if first else None)
                 if adam_i is not None:
                     ik["adam"] = adam_i
                 _item_product(BI, xi, first, reduce, new, **ik)
@@ -662,11 +671,11 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
              order: str = ORDER_GS, out_u: torch.Tensor | None = None,
              out_i: torch.Tensor | None = None, ws: dict | None = None,
              grad_i0_dense: bool = True, reduce=None, grad_support=None,
-             adam_u=None, before_last=None, adam_i=None):
+             adam_u=None, before_last=None, adam_i=None, src_bits=None):
     """backward_steps run to completion: (grad u0, grad i0)."""
     return drain(backward_steps(pair, gU, gI, num_layers, order, out_u, out_i, ws,
                                 grad_i0_dense, reduce, grad_support, adam_u, before_last,
-                                adam_i))
+                                adam_i, src_bits))
 
 
 def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,

@@ -129,6 +129,18 @@ class FusedTrainer:
         self.frontier = resolve_frontier(frontier, graph.item_csr.nnz)
         self.mask_u = torch.zeros(self.U, dtype=torch.uint8, device=dev)
         self.mask_i = torch.zeros(self.I, dtype=torch.uint8, device=dev)
+        # The first backward item product reads only the batch users' rows of
+        # gU (81k of 50M edges at C4) but would scan every index of its
+        # frontier rows (20.6M) to find them: a bitmap over the item-CSR slots
+        # of the batch users' edges (set with the masks, cleared after the
+        # step) lets it test 64 edges per load (bbgr_spmm_args.src_bits;
+        # bitwise the mask's result). Full-width tables only (narrow column
+        # shards keep the mask).
+        self.slot_map = self.slot_bits = None
+        if self.frontier and emb_dim >= 64:
+            self.slot_map = graph.user_item_slots()
+            self.slot_bits = torch.zeros(graph.item_csr.nnz // 32 + 4, dtype=torch.int32,
+                                         device=dev)
         # Fused optimizer (GS order): the user Adam runs inside the last backward
         # product's epilogue and the item Adam reads gI/(K+1) straight from the
         # sparse BPR gradient table (grad_scale), so neither weight-gradient
@@ -207,7 +219,8 @@ class FusedTrainer:
             self._backward_fused(users, self.posneg[: 2 * B], masks, alpha)
         else:
             backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
-                     out_i=self.g_i0, ws=self.ws, grad_support=masks)
+                     out_i=self.g_i0, ws=self.ws, grad_support=masks,
+                     src_bits=self._bits(masks))
             # ego L2 term goes straight to the weight grads (Version-2:503-507):
             # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
             call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
@@ -258,6 +271,7 @@ class FusedTrainer:
 
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
+                 src_bits=self._bits(masks),
                  before_last=before_last, reduce=reduce)
         if item_adam:
             self._item_adam(item_rows, self.g_if, a_gl, gl)
@@ -292,7 +306,8 @@ class FusedTrainer:
                  ld(self.item_w), ptr(self.g_if), ld(self.g_if), self.d, st)
 
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, ws=self.ws,
-                 grad_support=masks, adam_u=adam_u, adam_i=adam_i, before_last=before_last)
+                 grad_support=masks, adam_u=adam_u, adam_i=adam_i, before_last=before_last,
+                 src_bits=self._bits(masks))
 
     def _set_masks(self, users, pos, neg, value: int):
         """mask_u = batch users; mask_i = batch items (+ N(batch users) for GS,
@@ -302,11 +317,18 @@ class FusedTrainer:
         call("bbgr_mark_rows", B, ptr(users), value, ptr(self.mask_u), self.U, st)
         call("bbgr_mark_rows", B, ptr(pos), value, ptr(self.mask_i), self.I, st)
         call("bbgr_mark_rows", B, ptr(neg), value, ptr(self.mask_i), self.I, st)
+        uc = self.graph.user_csr
         if self.order == ORDER_GS:
-            uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), value,
                  ptr(self.mask_i), st)
+        if getattr(self, "slot_bits", None) is not None:   # set / clear the batch's bits
+            call("bbgr_mark_slots", B, ptr(users), ptr(uc.indptr), ptr(self.slot_map),
+                 ptr(self.slot_bits), value, st)
         return self.mask_u, self.mask_i
+
+    def _bits(self, masks):
+        """The slot bitmap for backward(src_bits=...) when the masks are on."""
+        return getattr(self, "slot_bits", None) if masks is not None else None
     def forward(self):
         """Final (layer-mean) tables, rows by input id."""
         uf, itf = forward(self.pair, self.user_w, self.item_w, self.K, self.order,

@@ -99,6 +99,12 @@ int bbgr_csr_plan_build(const bbgr_csr *csr, int32_t *chunks, int32_t *split,
                         void *workspace, size_t *workspace_bytes,
                         bbgr_stream_t stream);
 
+/* out[s] = the slot of b holding the edge of slot s of a, b being a's        */
+/* transpose with column-sorted rows (the k-th copy of a duplicate pair maps   */
+/* to the k-th copy). One-time; feeds bbgr_mark_slots.                         */
+int bbgr_transpose_slots(const bbgr_csr *a, const bbgr_csr *b, int32_t *out,
+                         bbgr_stream_t stream);
+
 /* ------------------------------------------------------------------------- */
 /* Vertex order (a one-time relabelling before the CSR build)                 */
 /*   The reference indexes users / items in id-map order (Version-2:227-303). */
@@ -111,6 +117,11 @@ int bbgr_csr_plan_build(const bbgr_csr *csr, int32_t *chunks, int32_t *split,
 /* degree[j] = number of e < n_ids with ids[e] == j, j < n (exact).           */
 int bbgr_degree_count(int64_t n_ids, const int32_t *ids, int32_t n, int32_t *degree,
                       bbgr_stream_t stream);
+/* The same with 8 replicated counter arrays (one per XCD's workgroups) summed */
+/* at the end: power-law ids contend 8x less (workspace: 32*n bytes; query     */
+/* with workspace == NULL).                                                    */
+int bbgr_degree_count_ws(int64_t n_ids, const int32_t *ids, int32_t n, int32_t *degree,
+                         void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
 /* perm[new] = old id, rank[old] = new id, by descending degree; equal degrees */
 /* keep ascending id (stable). Workspace query with workspace == NULL.        */
 int bbgr_degree_order(int32_t n, const int32_t *degree, int32_t *perm, int32_t *rank,
@@ -229,6 +240,13 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   rows through input-id column indices, and these maps place every        */
 /*   input-order output row, so no table is permuted. stream_out_from must be */
 /*   0 when y_map is set.                                                      */
+/* src_bits (nullable, with src_mask, d >= 64): a bitmap over this CSR's      */
+/*   slots, bit e set iff src_mask[indices[e]] != 0 (bbgr_mark_slots of the    */
+/*   source rows' edges). The gather then tests liveness on the bitmap (64     */
+/*   edges per test) and loads only live edges' indices: a first backward      */
+/*   product over a few batch rows' edges stops scanning every index of the  */
+/*   row. Results are bitwise those of src_mask alone (same edges, same      */
+/*   order); bits of padding: 3 words beyond nnz/32, readable.                 */
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
@@ -285,6 +303,7 @@ typedef struct {
   const int32_t *y_map;
   const int32_t *acc_map;
   const int32_t *add_map;
+  const uint32_t *src_bits;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -463,6 +482,13 @@ int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value, uint8_t *mask,
 int bbgr_mark_neighbors(int64_t n, const int64_t *rows, const int32_t *indptr,
                         const int32_t *indices, uint8_t value, uint8_t *mask,
                         bbgr_stream_t stream);
+/* Slot bitmaps (bbgr_spmm_args.src_bits). tmap = bbgr_transpose_slots of the  */
+/* CSR whose rows are listed: for every edge e of row rows[k] (k < n), bit     */
+/* tmap[e] of bits is set (set != 0), or its whole 32-bit word cleared          */
+/* (set == 0: restores an all-zero bitmap after use). Negative rows skipped.   */
+int bbgr_mark_slots(int64_t n, const int64_t *rows, const int32_t *indptr,
+                    const int32_t *tmap, uint32_t *bits, int32_t set,
+                    bbgr_stream_t stream);
 /* The same for every CSR row r < n_rows flagged in row_mask: row_mask[r], or
  * row_mask[row_map[r]] when row_map is given (a mask kept in the caller's
  * vertex order over a CSR numbered by descending degree). */

@@ -122,3 +122,41 @@ def test_split_rows_finish_in_launch_and_counters_reset():
     ref = (A @ x.double().cpu()).numpy()
     got = outs[0].double().cpu().numpy()
     assert np.linalg.norm(got - ref) <= 1e-5 * np.linalg.norm(ref)
+
+
+def test_transpose_slots_map_every_edge_once():
+    """bbgr_transpose_slots: every user-CSR slot maps to the item-CSR slot of
+    the same edge (duplicates: k-th copy to k-th copy), a permutation."""
+    U, I = 2000, 300
+    e = synthetic_edges(U, I, 40000, 6, items="zipf", duplicates=300)
+    g = BipartiteGraph(e, U, I, "cuda", vertex_order="degree")
+    t = g.user_item_slots().long().cpu()
+    uc_ptr, uc_idx = g.user_csr.indptr.long().cpu(), g.user_csr.indices.long().cpu()
+    ic_ptr, ic_idx = g.item_csr.indptr.long().cpu(), g.item_csr.indices.long().cpu()
+    E = uc_idx.numel()
+    assert torch.equal(torch.sort(t).values, torch.arange(E))
+    urow = torch.repeat_interleave(torch.arange(U), uc_ptr[1:] - uc_ptr[:-1])
+    irow = torch.repeat_interleave(torch.arange(I), ic_ptr[1:] - ic_ptr[:-1])
+    assert torch.equal(ic_idx[t], urow) and torch.equal(irow[t], uc_idx)
+
+
+@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair"])
+def test_slot_bitmap_first_item_product_is_bitwise_the_mask(variant):
+    """The first backward item product tests liveness on the batch users' slot
+    bitmap (bbgr_spmm_args.src_bits) instead of scanning indices: weights,
+    moments and losses over three steps equal the mask-only trainer bit for
+    bit (hub items: chunked and split rows), and the bitmap is all zero again
+    after every step."""
+    U, I = 20000, 3000
+    e = synthetic_edges(U, I, 300000, 8, items="zipf")
+    g = BipartiteGraph(e, U, I, "cuda", vertex_order="degree")
+    kw = dict(cred=synthetic_credibility(U, 8), emb_dim=64, num_layers=3, batch_size=2048,
+              frontier=True, seed=5)
+    a, b = FusedTrainer(g, variant, **kw), FusedTrainer(g, variant, **kw)
+    assert a.slot_bits is not None
+    b.slot_bits = b.slot_map = None          # the mask-only path
+    for _ in range(3):
+        assert float(a.step()) == float(b.step())
+        assert int(a.slot_bits.abs().sum()) == 0
+    for x, y in ((a.user_w, b.user_w), (a.item_w, b.item_w), (a.m_u, b.m_u), (a.v_i, b.v_i)):
+        assert torch.equal(x, y)
