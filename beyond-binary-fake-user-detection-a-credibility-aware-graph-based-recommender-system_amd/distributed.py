@@ -194,13 +194,21 @@ class ItemExchange:
         return self._ranges[1], self._ranges[2]
 
     def set_rows(self, csr, mask: torch.Tensor, row_list: torch.Tensor,
-                 offs_host: torch.Tensor) -> None:
+                 offs_host: torch.Tensor, like: "ItemExchange | None" = None) -> None:
         """The step's frontier: rows flagged in `mask` (global), listed ascending
         in `row_list` (bbgr_mask_to_list). The number of listed rows below each
         range boundary is computed here and copied to the host without
         blocking; it is read (one event wait, long complete by then) at the
-        first frontier product."""
+        first frontier product. `like`: an exchange of another column chain
+        whose rows were just set with the same ranges — its offsets are
+        shared instead of recomputed (one mask scan per step)."""
         _, bounds = self.ranges(csr)
+        if (like is not None and like._rows is not None
+                and like.frontier_parts == self.frontier_parts
+                and like.balance_indptr is self.balance_indptr):
+            self._rows = (row_list,) + like._rows[1:]
+            self._offs = None
+            return
         cum = torch.cumsum(mask.ne(0), 0)
         offs = torch.where(bounds > 0, cum[(bounds - 1).clamp(min=0)], torch.zeros_like(bounds))
         host = offs_host[: bounds.numel()]
@@ -577,8 +585,11 @@ class ShardedTrainer(FusedTrainer):
         have = ctypes.c_size_t(self._list_ws.numel())
         call("bbgr_mask_to_list", I, ptr(self.mask_i), ptr(self.item_list),
              ptr(self.item_count), ptr(self._list_ws), ctypes.byref(have), st)
-        for ex in self._exchanges():
-            ex.set_rows(self.graph.item_csr, self.mask_i, self.item_list, self.item_offs_host)
+        first = None
+        for ex in self._exchanges():   # the chains' ranges are identical: one mask scan
+            ex.set_rows(self.graph.item_csr, self.mask_i, self.item_list, self.item_offs_host,
+                        like=first)
+            first = first or ex
 
     def _item_adam_beside(self) -> torch.cuda.Event:
         """The item Adam of this step on the side stream: its gradient rows are

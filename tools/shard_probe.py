@@ -62,14 +62,18 @@ def main():
             tr.step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        issue = 0.0
         for _ in range(a.steps):
+            t1 = time.perf_counter()
             tr.step()
+            issue += time.perf_counter() - t1   # host time to enqueue one step
         torch.cuda.synchronize()
         ms = 1000.0 * (time.perf_counter() - t0) / a.steps
         print(json.dumps({"config": a.config, "rank_of": a.parts_of, "users": hi - lo,
                           "edges": int(local.shape[1]), "exchange_parts": xp,
                           "column_chains": chains, "frontier_parts": fparts,
-                          "ms_per_step": ms}), flush=True)
+                          "ms_per_step": ms, "host_issue_ms": 1000.0 * issue / a.steps}),
+              flush=True)
         tr.close()
         del tr
         torch.cuda.empty_cache()
