@@ -190,6 +190,8 @@ _SIGNATURES = {
     "bbgr_nonempty_rows": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P],
                            c_int32),
     "bbgr_mask_to_list": ([c_int64, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_list_offsets": ([c_int32, _P, _P, _P, _P, _P], c_int32),
+    "bbgr_list_positions": ([c_int64, _P, _P, _P, _P], c_int32),
     "bbgr_rows_gather": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
     # blueprint names, thin forms of the entry points above
     "bbgr_spmm_f32": ([ctypes.POINTER(CsrStruct), _P, c_int64, _P, c_int64, c_int32, _P, _P,

@@ -292,6 +292,30 @@ __global__ void transpose_slots_kernel(int n_rows, const int *a_indptr, const in
   }
 }
 
+// offs[k] = entries of the ascending list[0..*count) below bounds[k] (lower
+// bound); one thread per boundary, the list is read O(log count) times
+__global__ void list_offsets_kernel(int n_bounds, const long *bounds, const long *list,
+                                    const long *count, long *offs) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_bounds) return;
+  const long b = bounds[k];
+  long lo = 0, hi = *count;
+  while (lo < hi) {
+    const long mid = (lo + hi) >> 1;
+    if (list[mid] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  offs[k] = lo;
+}
+
+// pos[list[j]] = j for j < *count: the compact position of each listed row
+__global__ void list_positions_kernel(long n_max, const long *list, const long *count,
+                                      int *pos) {
+  const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_max || j >= *count) return;
+  pos[list[j]] = (int)j;
+}
+
 __global__ void degree_count_kernel(long n, const int *ids, int *deg) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < n) atomicAdd(deg + ids[e], 1);
@@ -728,6 +752,30 @@ extern "C" int bbgr_mask_to_list(int64_t n, const uint8_t *mask, int64_t *out,
   }
   BBGR_HIP(hipcub::DeviceSelect::If(workspace, temp, it, (long *)out, (long *)count, (int)n,
                                     sel, st));
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_list_offsets(int32_t n_bounds, const int64_t *bounds, const int64_t *list,
+                                 const int64_t *count, int64_t *offs, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n_bounds >= 0, "bbgr_list_offsets: bad args");
+  if (n_bounds == 0) return BBGR_OK;
+  BBGR_REQUIRE(bounds && list && count && offs, "bbgr_list_offsets: null arrays");
+  hipLaunchKernelGGL(list_offsets_kernel, dim3((unsigned)((n_bounds + 63) / 64)), dim3(64), 0,
+                     as_stream(stream), (int)n_bounds, (const long *)bounds, (const long *)list,
+                     (const long *)count, (long *)offs);
+  BBGR_LAUNCHED("list_offsets_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_list_positions(int64_t n_max, const int64_t *list, const int64_t *count,
+                                   int32_t *pos, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n_max >= 0 && n_max < (int64_t)1 << 31, "bbgr_list_positions: bad args");
+  if (n_max == 0) return BBGR_OK;
+  BBGR_REQUIRE(list && count && pos, "bbgr_list_positions: null arrays");
+  hipLaunchKernelGGL(list_positions_kernel, dim3((unsigned)((n_max + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), (long)n_max, (const long *)list, (const long *)count,
+                     (int *)pos);
+  BBGR_LAUNCHED("list_positions_kernel");
   return BBGR_OK;
 }
 

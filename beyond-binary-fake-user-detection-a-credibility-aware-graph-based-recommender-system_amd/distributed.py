@@ -141,7 +141,7 @@ class ItemExchange:
 
     Frontier products (a `row_mask`: the last forward item layer and the first
     backward item product of a training step) need only the step's item
-    frontier, a GLOBAL row set identical on every rank (`set_rows`). Only
+    frontier, a GLOBAL row set identical on every rank (`use_rows`). Only
     those rows are computed (row-list SpMM), compacted (bbgr_rows_gather) and
     all-reduced — pipelined over the same row ranges — and the compact
     epilogue finishes them: the payload is |frontier|*d*4 bytes instead of
@@ -193,43 +193,48 @@ class ItemExchange:
             self._ranges = (csr, rg, torch.tensor(b, dtype=torch.int64, device=csr.device))
         return self._ranges[1], self._ranges[2]
 
-    def set_rows(self, csr, mask: torch.Tensor, row_list: torch.Tensor,
-                 offs_host: torch.Tensor, like: "ItemExchange | None" = None) -> None:
-        """The step's frontier: rows flagged in `mask` (global), listed ascending
-        in `row_list` (bbgr_mask_to_list). The number of listed rows below each
-        range boundary is computed here and copied to the host without
-        blocking; it is read (one event wait, long complete by then) at the
-        first frontier product. `like`: an exchange of another column chain
-        whose rows were just set with the same ranges — its offsets are
-        shared instead of recomputed (one mask scan per step)."""
+    def list_rows(self, csr, row_list: torch.Tensor, count: torch.Tensor,
+                  offs: torch.Tensor, offs_host: torch.Tensor, positions=None):
+        """A frontier (rows listed ascending in `row_list`, *count of them:
+        bbgr_mask_to_list) split at this exchange's range boundaries on the
+        stream: offs[k] = listed rows below boundary k (bbgr_list_offsets),
+        copied to the pinned offs_host without blocking. `positions` (int32
+        [csr.n_rows]): filled with each listed row's list index
+        (bbgr_list_positions), the frontier SpMMs' y_map — they then write
+        their rows straight into the compact payload. Returns the rows
+        use_rows() takes; the host reads the offsets at the first frontier
+        product (one event wait). Every column chain's exchange has the same
+        ranges, so one split serves them all."""
         _, bounds = self.ranges(csr)
-        if (like is not None and like._rows is not None
-                and like.frontier_parts == self.frontier_parts
-                and like.balance_indptr is self.balance_indptr):
-            self._rows = (row_list,) + like._rows[1:]
-            self._offs = None
-            return
-        cum = torch.cumsum(mask.ne(0), 0)
-        offs = torch.where(bounds > 0, cum[(bounds - 1).clamp(min=0)], torch.zeros_like(bounds))
-        host = offs_host[: bounds.numel()]
-        host.copy_(offs, non_blocking=True)
+        n = bounds.numel()
+        st = stream_handle()
+        call("bbgr_list_offsets", n, ptr(bounds), ptr(row_list), ptr(count), ptr(offs), st)
+        if positions is not None:
+            call("bbgr_list_positions", csr.n_rows, ptr(row_list), ptr(count), ptr(positions),
+                 st)
+        host = offs_host[:n]
+        host.copy_(offs[:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._rows = (row_list, host, ev)
-        self._offs = None
+        return (row_list, host, ev, positions)
+
+    def use_rows(self, rows) -> None:
+        """The step's frontier (list_rows() of it) for the frontier products."""
+        self._rows, self._offs = rows, None
 
     def clear_rows(self) -> None:
         self._rows, self._offs = None, None
 
     def rows(self):
-        """(row list, [offsets into it at each range boundary]) or None."""
+        """(row list, [offsets into it at each range boundary], positions or
+        None) or None."""
         if self._rows is None:
             return None
+        lst, host, ev, positions = self._rows
         if self._offs is None:
-            lst, host, ev = self._rows
             ev.synchronize()
             self._offs = [int(v) for v in host.tolist()]
-        return self._rows[0], self._offs
+        return lst, self._offs, positions
 
     def _compact_buf(self, n: int, d: int, device) -> torch.Tensor:
         c = self._compact
@@ -240,23 +245,27 @@ class ItemExchange:
     def item_product(self, prod, x, first, new, kw) -> None:
         src_mask = kw.pop("src_mask", None)
         row_mask = kw.pop("row_mask", None)
-        t = new("partial", prod.csr.n_rows)
         fr = self.rows() if row_mask is not None else None
         works = []
         if fr is not None:
-            lst, offs = fr
+            lst, offs, positions = fr
             rgs, _ = self.ranges(prod.csr)
             d, n = x.shape[1], offs[-1]
             c = self._compact_buf(n, d, x.device)
+            t = None if positions is not None else new("partial", prod.csr.n_rows)
             for k, rg in enumerate(rgs):
                 a, b = offs[k], offs[k + 1]
                 if b <= a:
                     continue
                 part = lst[a:b]
-                spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask,
-                     row_list=part, rng=rg)
-                call("bbgr_rows_gather", b - a, ptr(part), ptr(t), ld(t), ptr(c[a:b]),
-                     ld(c), d, stream_handle())
+                if positions is not None:   # listed row lst[j] -> row j of c
+                    spmm(prod, x, first, y=c, y_map=positions, src_mask=src_mask,
+                         row_mask=row_mask, row_list=part, rng=rg)
+                else:
+                    spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask,
+                         row_list=part, rng=rg)
+                    call("bbgr_rows_gather", b - a, ptr(part), ptr(t), ld(t), ptr(c[a:b]),
+                         ld(c), d, stream_handle())
                 self._allreduce_async(c[a:b], works)
             self._wait(works)
             epilogue(c, row_list=lst[:n], n_rows=prod.csr.n_rows, **kw)
@@ -268,6 +277,7 @@ class ItemExchange:
                 and not (kw.get("add") is not None and kw.get("acc_out") is not None)):
             self._linear_product(prod, x, first, src_mask, y, kw)
             return
+        t = new("partial", prod.csr.n_rows)
         for rg in self._dense_order(prod.csr):
             spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask, rng=rg)
             self._allreduce_async(t[rg[0]:rg[1]], works)
@@ -444,13 +454,8 @@ class ShardedTrainer(FusedTrainer):
             max_tries=neg_max_tries, seed=seed + 7919 * self.rank)
         self.epoch, self.cursor, self.step_count = 0, 0, 0
         self.perm = None
-        self.posneg = torch.empty(2 * B, dtype=torch.int64, device=dev)
-        self.pos, self.neg = self.posneg[:B], self.posneg[B:]
-        self.all_items = torch.empty(2 * self.B_global, dtype=torch.int64, device=dev)
         # one decision for every rank: the size rule on the GLOBAL edge count
         self.frontier = resolve_frontier(frontier, int(indptr_i[-1]))
-        self.mask_u = torch.zeros(num_local_users, dtype=torch.uint8, device=dev)
-        self.mask_i = torch.zeros(num_items, dtype=torch.uint8, device=dev)
         self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
         self.dev_state = None   # host step scalars (the sharded step is not graph-captured)
         # GS item Adam on a side stream beside the backward chain: its gradient
@@ -466,11 +471,20 @@ class ShardedTrainer(FusedTrainer):
         self._adam_stream = torch.cuda.Stream(device=dev) if self.overlap_item_adam else None
         # sparse frontier exchange: the step's global item frontier as a row list
         self.sparse_exchange = bool(sparse_exchange) and self.frontier
-        self.item_list = torch.empty(max(num_items, 1), dtype=torch.int64, device=dev)
-        self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.item_offs_host = torch.zeros(max(exchange_parts, frontier_parts) + 2,
-                                          dtype=torch.int64).pin_memory()
+        # the step's batch and frontier, double-buffered: step t prepares step
+        # t+1's (users, negatives, global item mask, frontier row list and its
+        # range offsets) before its own forward. Nothing in it depends on the
+        # weights, so the values are those of preparing it at t+1; but the
+        # host read of the offsets at t+1's first frontier product then finds
+        # them copied a step ago instead of waiting for the GPU to get there
+        # (at N = 8 that wait serialised host issue and GPU work).
+        n_bounds = max(exchange_parts, frontier_parts) + 2
+        self._fronts = [_Front(B, self.B_global, num_local_users, num_items, n_bounds, dev)
+                        for _ in range(2)]
+        self._next = None
         self._list_ws = None
+        self._list_need = None
+        self._use(self._fronts[0])
 
     @classmethod
     def from_global_edges(cls, edges: np.ndarray, num_users: int, num_items: int,
@@ -556,40 +570,53 @@ class ShardedTrainer(FusedTrainer):
             users = torch.cat([users, self.perm[: self.B_local - users.numel()]])
         return users
 
-    def _masks(self, users, pos, neg):
-        """mask_u: my batch users. mask_i: every rank's batch items (+ every
-        rank's N(batch users) for GS), made global by a byte all-reduce; its
-        rows, listed, are the step's frontier for the sparse exchange."""
-        st = stream_handle()
+    def _use(self, f: "_Front") -> None:
+        """Point the step's batch / mask attributes at front f."""
+        self.posneg, self.all_items = f.posneg, f.all_items
+        B = f.posneg.numel() // 2
+        self.pos, self.neg = f.posneg[:B], f.posneg[B:]
+        self.mask_u, self.mask_i, self.item_list = f.mask_u, f.mask_i, f.item_list
+
+    def _prepare(self, f: "_Front") -> None:
+        """One step's batch and frontier into front f, on this stream (and
+        the group's): my users and their (pos, neg) items, every rank's (pos,
+        neg) ids (all-gather), and with the frontier on, the masks — mask_u:
+        my batch users; mask_i: every rank's batch items (+ every rank's
+        N(batch users) for GS), made global by a byte all-reduce — and, for
+        the sparse exchange, mask_i's rows listed and split at the ranges."""
+        users = self.next_users()
         B = users.numel()
-        call("bbgr_mark_rows", B, ptr(users), 1, ptr(self.mask_u), self.U, st)
-        call("bbgr_mark_rows", 2 * B, ptr(self.posneg), 1, ptr(self.mask_i), self.I, st)
+        f.users = users
+        self.sampler.sample(users, f.posneg[:B], f.posneg[B:])
+        _all_gather(f.all_items, f.posneg, self.group)
+        if not self.frontier:
+            return
+        st = stream_handle()
+        call("bbgr_mark_rows", B, ptr(users), 1, ptr(f.mask_u), self.U, st)
+        call("bbgr_mark_rows", 2 * B, ptr(f.posneg), 1, ptr(f.mask_i), self.I, st)
         if self.order == ORDER_GS:
             uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), 1,
-                 ptr(self.mask_i), st)
-        dist.all_reduce(self.mask_i, op=dist.ReduceOp.SUM, group=self.group)  # <= world: no wrap
+                 ptr(f.mask_i), st)
+        dist.all_reduce(f.mask_i, op=dist.ReduceOp.SUM, group=self.group)  # <= world: no wrap
         if self.sparse_exchange:
-            self._list_rows()
-        return self.mask_u, self.mask_i
+            self._list_rows(f)
 
-    def _list_rows(self) -> None:
+    def _list_rows(self, f: "_Front") -> None:
         st = stream_handle()
         I = self.I
-        need = ctypes.c_size_t(0)
-        call("bbgr_mask_to_list", I, ptr(self.mask_i), ptr(self.item_list),
-             ptr(self.item_count), None, ctypes.byref(need), st)
-        if self._list_ws is None or self._list_ws.numel() < need.value:
+        if self._list_need is None:   # hipcub's temp size depends on I only
+            need = ctypes.c_size_t(0)
+            call("bbgr_mask_to_list", I, ptr(f.mask_i), ptr(f.item_list), ptr(f.item_count),
+                 None, ctypes.byref(need), st)
+            self._list_need = need.value
             self._list_ws = torch.empty(max(need.value, 1), dtype=torch.uint8,
                                         device=self.device)
         have = ctypes.c_size_t(self._list_ws.numel())
-        call("bbgr_mask_to_list", I, ptr(self.mask_i), ptr(self.item_list),
-             ptr(self.item_count), ptr(self._list_ws), ctypes.byref(have), st)
-        first = None
-        for ex in self._exchanges():   # the chains' ranges are identical: one mask scan
-            ex.set_rows(self.graph.item_csr, self.mask_i, self.item_list, self.item_offs_host,
-                        like=first)
-            first = first or ex
+        call("bbgr_mask_to_list", I, ptr(f.mask_i), ptr(f.item_list), ptr(f.item_count),
+             ptr(self._list_ws), ctypes.byref(have), st)
+        f.rows = self.exchange.list_rows(self.graph.item_csr, f.item_list, f.item_count,
+                                         f.offs, f.offs_host, f.positions)
 
     def _item_adam_beside(self) -> torch.cuda.Event:
         """The item Adam of this step on the side stream: its gradient rows are
@@ -617,12 +644,22 @@ class ShardedTrainer(FusedTrainer):
         return done
 
     def step(self) -> torch.Tensor:
-        users = self.next_users()
+        f = self._next
+        if f is None:   # first step: nothing was prepared
+            f = self._fronts[0]
+            self._prepare(f)
+        nxt = self._fronts[1] if f is self._fronts[0] else self._fronts[0]
+        self._prepare(nxt)   # the next step's batch and frontier (see __init__)
+        self._next = nxt
+        self._use(f)
+        users, pos, neg = f.users, self.pos, self.neg
         self._last_users = users
         B = users.numel()
-        pos, neg = self.sampler.sample(users, self.pos, self.neg)
         st = stream_handle()
-        masks = self._masks(users, pos, neg) if self.frontier else None
+        masks = (self.mask_u, self.mask_i) if self.frontier else None
+        if f.rows is not None:
+            for ex in self._exchanges():
+                ex.use_rows(f.rows)
         final_rows = None if masks is None else (masks[0], masks[1], users)
         if self.chains:
             self._forward_chains(final_rows)
@@ -636,9 +673,9 @@ class ShardedTrainer(FusedTrainer):
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
         self.scatter(self.g_uf, users, self.contrib[:B])
-        # item gradient of the global batch: every rank's (pos, neg) rows and
-        # their per-triple gradient rows, summed in rank-major order
-        _all_gather(self.all_items, self.posneg, self.group)
+        # item gradient of the global batch: every rank's (pos, neg) rows
+        # (gathered with the batch) and their per-triple gradient rows, summed
+        # in rank-major order
         _all_gather(self.all_contrib, self.contrib[B: 3 * B], self.group)
         self.scatter(self.g_if, self.all_items, self.all_contrib)
         alpha = 2.0 * self.reg / self.B_global            # ego L2 (Version-2:503-507)
@@ -667,6 +704,7 @@ class ShardedTrainer(FusedTrainer):
         if masks is not None:
             call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), self.U, st)
             self.mask_i.zero_()
+        f.rows = None
         for ex in self._exchanges():
             ex.clear_rows()
         dist.all_reduce(self.loss, op=dist.ReduceOp.SUM, group=self.group)
@@ -755,6 +793,25 @@ class _Chain:
 
     def __init__(self, c0: int, c1: int, exchange: ItemExchange, stream, ws: dict):
         self.c0, self.c1, self.exchange, self.stream, self.ws = c0, c1, exchange, stream, ws
+
+
+class _Front:
+    """One step's batch and frontier (ShardedTrainer keeps two: the running
+    step's and the next one's). Masks are all-zero between uses."""
+
+    def __init__(self, B: int, B_global: int, U: int, I: int, n_bounds: int, dev):
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.users = None
+        self.posneg = torch.empty(2 * B, **i64)
+        self.all_items = torch.empty(2 * B_global, **i64)
+        self.mask_u = torch.zeros(U, dtype=torch.uint8, device=dev)
+        self.mask_i = torch.zeros(I, dtype=torch.uint8, device=dev)
+        self.item_list = torch.empty(max(I, 1), **i64)
+        self.item_count = torch.zeros(1, **i64)
+        self.positions = torch.zeros(max(I, 1), dtype=torch.int32, device=dev)
+        self.offs = torch.zeros(n_bounds, **i64)
+        self.offs_host = torch.zeros(n_bounds, dtype=torch.int64).pin_memory()
+        self.rows = None   # ItemExchange.list_rows() of the frontier
 
 
 class _GlobalItemCsr:

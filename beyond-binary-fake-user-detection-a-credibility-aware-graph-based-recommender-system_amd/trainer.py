@@ -329,6 +329,7 @@ class FusedTrainer:
     def _bits(self, masks):
         """The slot bitmap for backward(src_bits=...) when the masks are on."""
         return getattr(self, "slot_bits", None) if masks is not None else None
+
     def forward(self):
         """Final (layer-mean) tables, rows by input id."""
         uf, itf = forward(self.pair, self.user_w, self.item_w, self.K, self.order,

@@ -572,6 +572,20 @@ int bbgr_nonempty_rows(int32_t n_rows, const int32_t *indptr, int64_t *out,
 int bbgr_mask_to_list(int64_t n, const uint8_t *mask, int64_t *out, int64_t *count,
                       void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
 
+/* offs[k] = number of entries of the ascending list[0..*count) below
+ * bounds[k] (k < n_bounds; *count is a DEVICE int64): the split of a
+ * bbgr_mask_to_list row list at row-range boundaries, computed on the stream
+ * so the host copies n_bounds values instead of scanning the mask. */
+int bbgr_list_offsets(int32_t n_bounds, const int64_t *bounds, const int64_t *list,
+                      const int64_t *count, int64_t *offs, bbgr_stream_t stream);
+
+/* pos[list[j]] = j for j < *count (n_max >= *count: the launch size; list
+ * entries < the length of pos; other entries of pos are left alone). With
+ * pos as an SpMM's y_map, a row-list product writes listed row list[j]
+ * straight to row j of a compact table (the sparse item exchange's payload). */
+int bbgr_list_positions(int64_t n_max, const int64_t *list, const int64_t *count,
+                        int32_t *pos, bbgr_stream_t stream);
+
 /* ------------------------------------------------------------------------- */
 /* Evaluation                                            */
 /*   bbgr_eval_sampled replaces evaluate_sampled,                             */

@@ -858,6 +858,20 @@ def test_mask_to_list_rows_gather_and_compact_epilogue():
         want = np.flatnonzero(m)
         assert int(cnt.item()) == want.size
         np.testing.assert_array_equal(out[: want.size].cpu().numpy(), want)
+        # the list split at range boundaries (the sparse exchange's offsets);
+        # entries past *count (-7 here) must not be read
+        bounds = np.array([0, 1, 17, 2500, want[want.size // 2] if want.size else 9,
+                           n - 1, n], np.int64)
+        offs = torch.full((bounds.size,), -1, dtype=torch.int64, device=DEV)
+        call("bbgr_list_offsets", bounds.size, ptr(t(bounds, torch.int64)), ptr(out), ptr(cnt),
+             ptr(offs), stream_handle())
+        np.testing.assert_array_equal(offs.cpu().numpy(),
+                                      np.searchsorted(want, bounds, side="left"))
+        pos = torch.full((n,), -3, dtype=torch.int32, device=DEV)
+        call("bbgr_list_positions", n, ptr(out), ptr(cnt), ptr(pos), stream_handle())
+        ref = np.full(n, -3, np.int32)
+        ref[want] = np.arange(want.size)
+        np.testing.assert_array_equal(pos.cpu().numpy(), ref)
     src = t(rng.standard_normal((n, 68)).astype(np.float32))[:, :d]   # ld 68
     idx = t(np.concatenate([rng.integers(0, n, 300), [-1, 0, n - 1]]), torch.int64)
     dst = torch.full((idx.numel(), d), 5.0, device=DEV)

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--column-chains", default="1")
     ap.add_argument("--frontier-parts", default="2")
+    ap.add_argument("--profile", default="",
+                    help="cProfile the timed steps into <this>.c<chains>x<parts>f<fparts>")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29581")
@@ -61,6 +63,11 @@ def main():
         for _ in range(3):
             tr.step()
         torch.cuda.synchronize()
+        prof = None
+        if a.profile:   # host profile of the timed steps only
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         issue = 0.0
         for _ in range(a.steps):
@@ -69,6 +76,9 @@ def main():
             issue += time.perf_counter() - t1   # host time to enqueue one step
         torch.cuda.synchronize()
         ms = 1000.0 * (time.perf_counter() - t0) / a.steps
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(f"{a.profile}.c{chains}x{xp}f{fparts}")
         print(json.dumps({"config": a.config, "rank_of": a.parts_of, "users": hi - lo,
                           "edges": int(local.shape[1]), "exchange_parts": xp,
                           "column_chains": chains, "frontier_parts": fparts,
