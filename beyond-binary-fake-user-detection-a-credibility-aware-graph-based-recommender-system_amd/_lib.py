@@ -87,6 +87,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_bc_table", c_void_p), ("adam_state", c_void_p),
         ("y_map", c_void_p), ("acc_map", c_void_p), ("add_map", c_void_p),
         ("src_bits", c_void_p),
+        ("row_count", c_void_p),
     ]
 
 
@@ -168,6 +169,7 @@ _SIGNATURES = {
                                ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
     "bbgr_mark_slots": ([c_int64, _P, _P, _P, _P, c_int32, _P], c_int32),
+    "bbgr_mark_list": ([c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P], c_int32),
     "bbgr_transpose_slots": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(CsrStruct), _P, _P],
                              c_int32),
     "bbgr_mark_neighbors_of_mask": ([c_int64, _P, _P, _P, _P, ctypes.c_uint8, _P, _P],
@@ -226,7 +228,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 4:
+        if handle.bbgr_abi_version() != 5:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

@@ -80,6 +80,7 @@ struct SpmmParams {
   // acc_in / acc_out, of add; the masks of those tables index the same rows
   const int *y_map, *acc_map, *add_map;
   const unsigned *src_bits;    // slot bitmap of live edges (args.src_bits; d >= 64)
+  const long *row_count;       // device length of row_list (args.row_count; nullable)
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -213,7 +214,7 @@ __device__ __forceinline__ unsigned long long slot_bits64(const unsigned *bits, 
 }
 
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
-template <int D, int WMODE, bool MASKED>
+template <int D, int WMODE, bool MASKED, bool BITS = false>
 __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
                                              int lane, float4 (&acc)[D / 64]) {
   constexpr int V = D / 64;
@@ -221,7 +222,7 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
   for (int e0 = eb; e0 < ee; e0 += 16) {
     const int n = min(16, ee - e0);
     unsigned live = 0xffffu;   // slot-bitmap mode: this batch's live edges
-    if (MASKED && P.src_bits) {
+    if constexpr (MASKED && BITS) {
       // liveness from the bitmap, 64 edges per test: a dead window costs one
       // (cached) 12-byte load instead of 64 index + mask loads; the live
       // edges are exactly src_mask's, in the same order (bitwise identical)
@@ -239,13 +240,13 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     float mw = 0.f;
     if (lane < n && ((live >> lane) & 1u)) {
       my = P.indices[e0 + lane];
-      if (MASKED && P.src_mask && !P.src_bits && !P.src_mask[my]) my = -1;   // exact-zero source row
+      if (MASKED && !BITS && P.src_mask && !P.src_mask[my]) my = -1;   // exact-zero source row
       if (my >= 0) {
         if (WMODE == 1) mw = P.edge_val[e0 + lane];
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
       }
     }
-    if (MASKED && P.src_mask && !P.src_bits) {   // skip 16-edge batches with no live source (group-uniform)
+    if (MASKED && !BITS && P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
       const unsigned long long live = __ballot(my >= 0);
       if (((live >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
     }
@@ -394,13 +395,13 @@ __device__ __forceinline__ void gather_slot(const SpmmParams &P, int eb, int ee,
 }
 
 // A row's gather for any width: the narrow form below 64 columns.
-template <int D, int WMODE, bool MASKED>
+template <int D, int WMODE, bool MASKED, bool BITS = false>
 __device__ __forceinline__ void gather_row(const SpmmParams &P, int eb, int ee, int lane,
                                            float4 (&acc)[RowShape<D>::V]) {
   if constexpr (D < 64) {
     gather_range_narrow<D, WMODE, MASKED>(P, eb, ee, lane, acc[0]);
   } else {
-    gather_range<D, WMODE, MASKED>(P, eb, ee, lane, acc);
+    gather_range<D, WMODE, MASKED, BITS>(P, eb, ee, lane, acc);
   }
 }
 
@@ -694,59 +695,94 @@ __device__ __forceinline__ void split_row_arrive(const SpmmParams &P, int4 ch, f
   if (last) split_row_finish<D>(P, ch.x, base, c, red, g, lane);
 }
 
-template <int D, int WMODE, bool MASKED, bool PAIR>
-__device__ __forceinline__ void spmm_body(const SpmmParams &P) {
+// A single-chunk long row (deg in (long_threshold, chunk_edges]) of a slot-
+// bitmap launch, summed by ONE 16-lane group in the order of the chunk
+// workgroup that owns such a row elsewhere: lane group g's range
+// [eb + g*per, eb + (g+1)*per) from zero (gather_range), then the 16 range
+// sums added in group order (block_reduce16). Bitwise the workgroup's value;
+// with a few live edges per row the bitmap windows are nearly all dead, and a
+// workgroup per row (11k of them at C4) cost more than the scan.
+template <int D, int WMODE>
+__device__ __forceinline__ void chunk_row_serial(const SpmmParams &P, int eb, int ee, int lane,
+                                                 float4 (&s)[RowShape<D>::V]) {
   constexpr int V = RowShape<D>::V;
-  __shared__ float4 red[16 * (D / 4)];
-  const int g = threadIdx.x >> 4;
-  const int lane = threadIdx.x & 15;
+  const int len = ee - eb;
+  const int per = (((len + 15) >> 4) + 15) & ~15;   // the chunk workgroup's split
+  // lane g tests range g's bitmap windows (<= 2 of 64 edges), all lanes at
+  // once; only live ranges are gathered. A dead range's sum is +0.0 and
+  // s + 0.0 == s (s is never -0.0: a sum from +0.0), so skipping it keeps the
+  // workgroup's value bit for bit.
+  bool live = false;
+  {
+    const int gb = eb + lane * per, ge = min(ee, gb + per);
+#pragma unroll 1
+    for (int e = gb; e < ge && !live; e += 64) {
+      unsigned long long w = slot_bits64(P.src_bits, e);
+      if (ge - e < 64) w &= (1ull << (ge - e)) - 1ull;
+      live = w != 0ull;
+    }
+  }
+  unsigned segs = (unsigned)((__ballot(live) >> (threadIdx.x & 48)) & 0xffffull);
+#pragma unroll
+  for (int k = 0; k < V; ++k) s[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  bool first = true;
+#pragma unroll 1
+  while (segs) {
+    const int g = __ffs(segs) - 1;
+    segs &= segs - 1u;
+    float4 p[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) p[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int gb = eb + g * per;
+    gather_row<D, WMODE, true, true>(P, gb, min(ee, gb + per), lane, p);
+#pragma unroll
+    for (int k = 0; k < V; ++k) s[k] = first ? p[k] : f4_add(s[k], p[k]);
+    first = false;
+  }
+}
+
+// Long rows a slot-bitmap launch sums in its short-row groups (chunk_row_serial)
+// instead of chunk workgroups: the rows with a single chunk.
+template <int D, bool BITS>
+__device__ __forceinline__ bool serial_long(const SpmmParams &P, int len) {
+  if constexpr (BITS && D >= 64) return len <= P.chunk_edges;
+  return false;
+}
+
+// Short-row workgroup sb of a launch: rows sb*per_block.. of the row range or
+// of the row list (whose length is n_list).
+template <int D, int WMODE, bool MASKED, bool PAIR, bool BITS>
+__device__ __forceinline__ void short_rows(const SpmmParams &P, long sb, long n_list, int g,
+                                           int lane) {
+  constexpr int V = RowShape<D>::V;
   float4 acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  if ((int)blockIdx.x < P.n_chunks) {
-    // ---- one chunk of a long row: whole workgroup --------------------------
-    const int4 ch = P.chunks[P.chunk_begin + blockIdx.x];  // row, e_begin, e_end, slot
-    if (MASKED && P.row_mask && !P.row_mask[ch.x]) return;   // whole workgroup, uniform
-    if (MASKED && P.row_list && !P.row_mask) return;         // list mode: short rows only
-    const int len = ch.z - ch.y;
-    const int per = (((len + 15) >> 4) + 15) & ~15;  // multiple of 16
-    const int gb = ch.y + g * per;
-    const int ge = min(ch.z, gb + per);
-    if (gb < ge) gather_row<D, WMODE, MASKED>(P, gb, ge, lane, acc);
-    block_reduce16<D>(red, g, lane, acc);
-    if (ch.w < 0) {   // the row's only chunk
-      if (g == 0 && lane < RowShape<D>::LANES) {
-        float4 T[V];
-#pragma unroll
-        for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
-        epilogue<D>(P, ch.x, lane, T);
-      }
-      return;
-    }
-    split_row_arrive<D>(P, ch, red, g, lane);
-    return;
-  }
-
-  if constexpr (PAIR && D >= 64) {   // ---- short rows, two per 16-lane group (rows j, j + 16)
+  if constexpr (PAIR && D >= 64) {   // ---- two rows per 16-lane group (rows j, j + 16)
     long rr[2];
     int eb[2], ee[2];
+    bool ser[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * 32 + 16 * h + g;
+      long row = (long)P.row_begin + sb * 32 + 16 * h + g;
       if (MASKED && P.row_list) {
-        row = row < P.n_row_list ? P.row_list[row] : -1;
+        row = row < n_list ? P.row_list[row] : -1;
       } else if (row >= P.row_end) {
         row = -1;
       }
       if (row >= P.n_rows) row = -1;
       eb[h] = ee[h] = 0;
+      ser[h] = false;
       if (row >= 0) {
         eb[h] = P.indptr[row];
         ee[h] = P.indptr[row + 1];
-        if (ee[h] - eb[h] > P.long_threshold ||
-            (MASKED && !P.row_list && P.row_mask && !P.row_mask[row]))
+        if (MASKED && !P.row_list && P.row_mask && !P.row_mask[row]) {
           row = -1;
+        } else if (ee[h] - eb[h] > P.long_threshold) {
+          ser[h] = serial_long<D, BITS>(P, ee[h] - eb[h]);
+          if (!ser[h]) row = -1;
+        }
       }
       if (row < 0) eb[h] = ee[h] = 0;
       rr[h] = row;
@@ -754,17 +790,26 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     float4 accB[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) accB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    gather_pair<D, WMODE, MASKED>(P, eb[0], ee[0], eb[1], ee[1], lane, acc, accB);
-    if (rr[0] >= 0) epilogue<D>(P, (int)rr[0], lane, acc);
-    if (rr[1] >= 0) epilogue<D>(P, (int)rr[1], lane, accB);
+    gather_pair<D, WMODE, MASKED>(P, ser[0] ? 0 : eb[0], ser[0] ? 0 : ee[0],
+                                  ser[1] ? 0 : eb[1], ser[1] ? 0 : ee[1], lane, acc, accB);
+    if (rr[0] >= 0 && !ser[0]) epilogue<D>(P, (int)rr[0], lane, acc);
+    if (rr[1] >= 0 && !ser[1]) epilogue<D>(P, (int)rr[1], lane, accB);
+    if (ser[0] || ser[1]) {
+#pragma unroll 1
+      for (int h = 0; h < 2; ++h) {
+        if (!ser[h]) continue;
+        chunk_row_serial<D, WMODE>(P, eb[h], ee[h], lane, acc);
+        epilogue<D>(P, (int)rr[h], lane, acc);
+      }
+    }
     return;
   }
   if constexpr (D < 64) {   // ---- narrow short rows: 16/L per group, one per slot
     constexpr int L = D / 4, S = 16 / L;
     const int slot = lane / L, sub = lane - slot * L;
-    long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * (16 * S) + g * S + slot;
+    long row = (long)P.row_begin + sb * (16 * S) + g * S + slot;
     if (MASKED && P.row_list) {
-      row = row < P.n_row_list ? P.row_list[row] : -1;
+      row = row < n_list ? P.row_list[row] : -1;
     } else if (row >= P.row_end) {
       row = -1;
     }
@@ -783,9 +828,9 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     return;
   }
   // ---- short rows: one 16-lane group per row ------------------------------
-  long row = (long)P.row_begin + (long)(blockIdx.x - P.n_chunks) * 16 + g;
+  long row = (long)P.row_begin + sb * 16 + g;
   if (MASKED && P.row_list) {
-    if (row >= P.n_row_list) return;
+    if (row >= n_list) return;
     row = P.row_list[row];
     if (row < 0) return;
   } else if (row >= P.row_end) {
@@ -794,10 +839,56 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   if (row >= P.n_rows) return;
   const int eb = P.indptr[row];
   const int ee = P.indptr[row + 1];
-  if (ee - eb > P.long_threshold) return;  // owned by chunk blocks
   if (MASKED && !P.row_list && P.row_mask && !P.row_mask[row]) return;
-  gather_row<D, WMODE, MASKED>(P, eb, ee, lane, acc);
+  if (ee - eb > P.long_threshold) {
+    if (!serial_long<D, BITS>(P, ee - eb)) return;  // owned by chunk blocks
+    chunk_row_serial<D, WMODE>(P, eb, ee, lane, acc);
+  } else {
+    gather_row<D, WMODE, MASKED, BITS>(P, eb, ee, lane, acc);
+  }
   epilogue<D>(P, (int)row, lane, acc);
+}
+
+template <int D, int WMODE, bool MASKED, bool PAIR, bool BITS = false>
+__device__ __forceinline__ void spmm_body(const SpmmParams &P) {
+  constexpr int V = RowShape<D>::V;
+  __shared__ float4 red[16 * (D / 4)];
+  const int g = threadIdx.x >> 4;
+  const int lane = threadIdx.x & 15;
+
+  if ((int)blockIdx.x < P.n_chunks) {
+    // ---- one chunk of a long row: whole workgroup --------------------------
+    const int4 ch = P.chunks[P.chunk_begin + blockIdx.x];  // row, e_begin, e_end, slot
+    if (MASKED && P.row_mask && !P.row_mask[ch.x]) return;   // whole workgroup, uniform
+    if (MASKED && P.row_list && !P.row_mask) return;         // list mode: short rows only
+    if (ch.w < 0 && serial_long<D, BITS>(P, ch.z - ch.y)) return;   // short_rows sums it
+    float4 acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int len = ch.z - ch.y;
+    const int per = (((len + 15) >> 4) + 15) & ~15;  // multiple of 16
+    const int gb = ch.y + g * per;
+    const int ge = min(ch.z, gb + per);
+    if (gb < ge) gather_row<D, WMODE, MASKED, BITS>(P, gb, ge, lane, acc);
+    block_reduce16<D>(red, g, lane, acc);
+    if (ch.w < 0) {   // the row's only chunk
+      if (g == 0 && lane < RowShape<D>::LANES) {
+        float4 T[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) T[k] = red[lane + 16 * k];
+        epilogue<D>(P, ch.x, lane, T);
+      }
+      return;
+    }
+    split_row_arrive<D>(P, ch, red, g, lane);
+    return;
+  }
+  const long sb = (long)blockIdx.x - P.n_chunks;
+  long n = P.n_row_list;
+  // list length in device memory (a list built on the stream, e.g. inside a
+  // captured step; n_row_list is its capacity): workgroups past it exit
+  if (MASKED && P.row_list && P.row_count) n = min(n, *P.row_count);
+  short_rows<D, WMODE, MASKED, PAIR, BITS>(P, sb, n, g, lane);
 }
 
 // Full-CSR launches (the roofline kernel) and masked / row-list launches are
@@ -825,6 +916,16 @@ template <int D, int WMODE>
 __global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves_masked) void
 spmm_masked_pair_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true, true>(P);
+}
+
+// Slot-bitmap launches (args.src_bits, d >= 64, one row per group): liveness
+// from the bitmap, single-chunk long rows summed by their row's group
+// (chunk_row_serial). A symbol of its own so the plain masked kernels keep
+// their register budget.
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::masked_waves) void spmm_bits_kernel(
+    SpmmParams P) {
+  spmm_body<D, WMODE, true, false, true>(P);
 }
 
 // Full-CSR launch whose epilogue applies the fused Adam step (its bytes add the
@@ -877,6 +978,13 @@ static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
         if (masked) hipLaunchKernelGGL((spmm_masked_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
         else if (P.adam_p) hipLaunchKernelGGL((spmm_adam_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
         else hipLaunchKernelGGL((spmm_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+        BBGR_LAUNCHED("spmm_kernel");
+        return BBGR_OK;
+      }
+    }
+    if constexpr (D >= 64) {
+      if (P.src_bits) {
+        hipLaunchKernelGGL((spmm_bits_kernel<D, WMODE>), gd, bd, 0, st, P);
         BBGR_LAUNCHED("spmm_kernel");
         return BBGR_OK;
       }
@@ -1055,6 +1163,8 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   P.row_mask = a->row_mask;
   P.row_list = (const long *)a->row_list;
   P.n_row_list = a->n_row_list;
+  P.row_count = (const long *)a->row_count;
+  BBGR_REQUIRE(!a->row_count || a->row_list, "bbgr_spmm: row_count needs row_list");
   int n_split = csr->n_split;
   P.row_begin = 0;
   P.row_end = csr->n_rows;

@@ -304,6 +304,51 @@ __global__ void mark_neighbors_kernel(long n, const long *rows, const int *indpt
     mask[indices[e]] = v;
 }
 
+// Flag row r in a byte mask and, if this call set it first, append r to list:
+// an atomic OR on r's 4-byte word tells who set the byte; the new rows of a
+// wave take consecutive list slots from ONE atomic add on the count.
+__device__ __forceinline__ void mark_append(long r, bool on, unsigned char *mask, long *list,
+                                            unsigned long long *count) {
+  bool fresh = false;
+  if (on) {
+    unsigned *w = reinterpret_cast<unsigned *>(mask + (r & ~3L));
+    const unsigned sh = 8u * (unsigned)(r & 3);
+    fresh = (atomicOr(w, 1u << sh) & (0xffu << sh)) == 0u;
+  }
+  const unsigned long long m = __ballot(fresh);
+  if (m == 0ull) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader);
+  if (fresh) list[base + __popcll(m & ((1ull << lane) - 1ull))] = r;
+}
+
+__global__ void mark_list_rows_kernel(long n, const long *idx, unsigned char *mask, long n_rows,
+                                      long *list, unsigned long long *count) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long r = k < n ? idx[k] : -1;
+  mark_append(r, r >= 0 && r < n_rows, mask, list, count);
+}
+
+// one 16-lane group per listed row, its edges 16 at a time
+__global__ void mark_list_neighbors_kernel(long n, const long *rows, const int *indptr,
+                                           const int *indices, unsigned char *mask, long *list,
+                                           unsigned long long *count) {
+  const long k = (long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  const long r = k < n ? rows[k] : -1;
+  const int eb = r >= 0 ? indptr[r] : 0, ee = r >= 0 ? indptr[r + 1] : 0;
+  // every lane of the wave runs the same trip count (the ballot needs them all)
+  int len = ee - eb;
+#pragma unroll
+  for (int off = 16; off < 64; off <<= 1) len = max(len, __shfl_xor(len, off));
+  for (int o = (int)(threadIdx.x & 15); o < ((len + 15) & ~15); o += 16) {
+    const int e = eb + o;
+    mark_append(e < ee ? (long)indices[e] : -1L, e < ee, mask, list, count);
+  }
+}
+
 // slot bitmap of the listed rows' edges in the TRANSPOSE CSR: for every edge e
 // of row rows[k], bit tmap[e] of bits is set (set != 0, atomic OR) or its
 // whole word cleared (set == 0; a later launch, so no OR races the store)
@@ -655,6 +700,29 @@ extern "C" int bbgr_mark_neighbors(int64_t n, const int64_t *rows,
                      as_stream(stream), (long)n, (const long *)rows, indptr, indices, value,
                      mask);
   BBGR_LAUNCHED("mark_neighbors_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_mark_list(int64_t n, const int64_t *rows, const int32_t *indptr,
+                              const int32_t *indices, uint8_t *mask, int64_t n_rows,
+                              int64_t *list, int64_t *count, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n_rows >= 0, "bbgr_mark_list: negative n / n_rows");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(rows && mask && list && count && (!indptr || indices),
+               "bbgr_mark_list: null arrays");
+  BBGR_REQUIRE(((uintptr_t)mask & 3) == 0, "bbgr_mark_list: mask must be 4-byte aligned");
+  hipStream_t st = as_stream(stream);
+  if (!indptr) {
+    hipLaunchKernelGGL(mark_list_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, (long)n, (const long *)rows, mask, (long)n_rows, (long *)list,
+                       (unsigned long long *)count);
+    BBGR_LAUNCHED("mark_list_rows_kernel");
+  } else {
+    hipLaunchKernelGGL(mark_list_neighbors_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256),
+                       0, st, (long)n, (const long *)rows, indptr, indices, mask, (long *)list,
+                       (unsigned long long *)count);
+    BBGR_LAUNCHED("mark_list_neighbors_kernel");
+  }
   return BBGR_OK;
 }
 

@@ -142,10 +142,10 @@ class ItemExchange:
     Frontier products (a `row_mask`: the last forward item layer and the first
     backward item product of a training step) need only the step's item
     frontier, a GLOBAL row set identical on every rank (`use_rows`). Only
-    those rows are computed (row-list SpMM), compacted (bbgr_rows_gather) and
-    all-reduced — pipelined over the same row ranges — and the compact
-    epilogue finishes them: the payload is |frontier|*d*4 bytes instead of
-    I*d*4."""
+    those rows are computed (row-list SpMM writing listed row list[j] straight
+    to row j of a compact table: y_map = bbgr_list_positions) and all-reduced
+    — pipelined over the same row ranges — and the compact epilogue finishes
+    them: the payload is |frontier|*d*4 bytes instead of I*d*4."""
 
     def __init__(self, group=None, parts: int = 4, frontier_parts: int = 2):
         self.group, self.parts = group, max(1, int(parts))
@@ -154,7 +154,7 @@ class ItemExchange:
         # little overlap, so they are cut coarser than the dense ones
         self.frontier_parts = max(1, int(frontier_parts))
         self.balance_indptr = None   # global item indptr: identical cuts on every rank
-        self._rows = None            # (device list, host offsets, event) of the step
+        self._rows = None            # (device list, host offsets, event, positions)
         self._offs = None
         self._compact = None
         self._ranges = None          # (csr, ranges, device boundary rows)
@@ -575,7 +575,8 @@ class ShardedTrainer(FusedTrainer):
         self.posneg, self.all_items = f.posneg, f.all_items
         B = f.posneg.numel() // 2
         self.pos, self.neg = f.posneg[:B], f.posneg[B:]
-        self.mask_u, self.mask_i, self.item_list = f.mask_u, f.mask_i, f.item_list
+        self.mask_u, self.mask_i = f.mask_u, f.mask_i
+        self.item_list, self.item_count = f.item_list, f.item_count
 
     def _prepare(self, f: "_Front") -> None:
         """One step's batch and frontier into front f, on this stream (and

@@ -306,13 +306,16 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
          add_mask=None, row_list=None, rng=None, adam=None, y_map=None, acc_map=None,
-         add_map=None, src_input: bool = False, src_bits=None) -> None:
+         add_map=None, src_input: bool = False, src_bits=None, row_count=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream. `adam`
     (optim.AdamRows): apply Adam to each row's y value in the epilogue.
     `y_map` / `acc_map` / `add_map`: row maps of those tables (input-order
     tables of a degree-ordered pair); `src_input`: x is gathered through the
     CSR's input-id column indices (Product.input_struct). `src_bits`: the slot
-    bitmap of src_mask's live edges in this CSR (bbgr_spmm_args.src_bits)."""
+    bitmap of src_mask's live edges in this CSR (bbgr_spmm_args.src_bits).
+    `row_count` (device int64): row_list holds that many rows (its numel() is
+    the capacity; bbgr_spmm_args.row_count) — a list built on the stream, the
+    rows row_mask flags."""
     d = x.shape[1]
     a = _lib.SpmmArgs()
     a.d = d
@@ -336,6 +339,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
     if row_list is not None:
         a.row_list, a.n_row_list = ptr(row_list), row_list.numel()
+        if row_count is not None:
+            a.row_count = ptr(row_count)
     if rng is not None:   # (row0, row1, chunk0, chunk1, split0, split1): Csr.row_ranges
         a.use_range = 1
         for k in range(6):
@@ -354,6 +359,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
         return
     masked = src_mask is not None or row_mask is not None or row_list is not None
     kind = "masked" if masked else ("adam" if adam is not None else "full")
+    if row_count is not None:   # the list is row_mask's rows; its length is on the device
+        row_list = None
     if _timer.count:
         call("bbgr_spmm", ctypes.byref(cs), ctypes.byref(a), stream_handle())
         _timer.count_launch(prod, kind, d, rng, src_mask, row_mask, row_list, src_input)
@@ -462,12 +469,15 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
     each exchange point), so the caller can interleave the issue of several
     chains (ShardedTrainer column chains); `drain()` / `forward()` run it whole.
     `reduce(t)`: in-place sum over ranks of item-row partial sums (sharded mode).
-    `final_rows=(user_mask, item_mask[, user_list])`: only the flagged rows of the final
+    `final_rows=(user_mask, item_mask[, user_list[, (item_list, item_count)]])`:
+    only the flagged rows of the final
     tables are needed (a training step reads batch rows only). The last layer
     then computes only those rows; the item mask must cover every item the
     flagged users' last-layer rows read (GS: N(batch users) and the batch
     items; Jacobi: the batch items). Flagged rows are bitwise identical to a
-    full pass; the others are left stale."""
+    full pass; the others are left stale. The item list (GS, no `reduce`):
+    item_mask's rows with their count in device memory (bbgr_mark_list) — the
+    last item product visits them instead of testing every row's mask byte."""
     U, I = pair.num_users, pair.num_items
     d = u0.shape[1]
     _check_table("user table", u0, U, d)
@@ -482,7 +492,8 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
     gl = 1.0 / (K + 1)
     FI, FU = pair.fwd_item, pair.fwd_user
     new = _buffers(ws, u0.device, d)
-    mu, mi, ulist = (tuple(final_rows) + (None,))[:3] if final_rows is not None else (None,) * 3
+    mu, mi, ulist, ilist = ((tuple(final_rows) + (None, None))[:4] if final_rows is not None
+                            else (None,) * 4)
     io = pair.io   # input-order tables over a degree-ordered graph (set_input_order)
     if io is not None and (reduce is not None or final_rows is not None):
         raise ValueError("an input-order pair takes neither a reduce hook nor final_rows")
@@ -492,6 +503,9 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
     am_u, am_i = (io.user_map, io.item_map) if io is not None else (None, None)
     if order == ORDER_GS:
         bufU, bufI = new("u0", U), new("i0", I)
+        il = {}
+        if ilist is not None and reduce is None and mi is not None:
+            il = dict(row_list=ilist[0], row_count=ilist[1])
         for k in range(1, K + 1):
             g = gl if k == K else 1.0
             last = k == K
@@ -499,7 +513,7 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
                           y_scale=pair.feed_fwd_iu, acc_in=i0 if k == 1 else acc_i,
                           acc_out=acc_i, acc_scale=FI.out_scale, gamma=g,
                           row_mask=mi if last else None, acc_mask=mi, acc_map=am_i,
-                          src_input=io is not None and k == 1)
+                          src_input=io is not None and k == 1, **(il if last else {}))
             yield
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
@@ -543,7 +557,8 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                    order: str = ORDER_GS, out_u: torch.Tensor | None = None,
                    out_i: torch.Tensor | None = None, ws: dict | None = None,
                    grad_i0_dense: bool = True, reduce=None, grad_support=None,
-                   adam_u=None, before_last=None, adam_i=None, src_bits=None):
+                   adam_u=None, before_last=None, adam_i=None, src_bits=None,
+                   frontier_list=None):
     """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final); a
     generator yielding after each item-row product, like forward_steps.
     `adam_u` (optim.AdamRows) fuses the user-table Adam step into the last
@@ -560,7 +575,11 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     are bitwise identical to the dense chain (the skipped terms are +0.0).
     `src_bits`: the item-CSR slot bitmap of the flagged users' edges
     (graph.user_item_slots + bbgr_mark_slots): the first item product then
-    tests liveness on it instead of scanning every index of its rows."""
+    tests liveness on it instead of scanning every index of its rows.
+    `frontier_list=(rows, count)`: GS, no `reduce` — the flagged items as a
+    row list of capacity rows.numel() whose length is the device int64 count
+    (bbgr_mark_list): the first item product then visits those rows only
+    instead of testing every row's mask byte."""
     U, I = pair.num_users, pair.num_items
     d = gU.shape[1]
     _check_table("user grad", gU, U, d)
@@ -593,6 +612,9 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     inp = io is not None
     if order == ORDER_GS:
         bufU, bufI = new("u0", U), new("i0", I)
+        fl = {}
+        if frontier_list is not None and reduce is None and si_int is not None:
+            fl = dict(row_list=frontier_list[0], row_count=frontier_list[1])
         for k in range(K, 0, -1):
             first = k == K
             # first product: Gi_K is zero off the item support (batch items and
@@ -603,7 +625,8 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                           add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
                           src_mask=su if first else None,
                           row_mask=si_int if first else None, add_map=im,
-                          src_input=inp and first, src_bits=src_bits if first else None)
+                          src_input=inp and first, src_bits=src_bits if first else None,
+                          **(fl if first else {}))
             yield
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
@@ -671,11 +694,12 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
              order: str = ORDER_GS, out_u: torch.Tensor | None = None,
              out_i: torch.Tensor | None = None, ws: dict | None = None,
              grad_i0_dense: bool = True, reduce=None, grad_support=None,
-             adam_u=None, before_last=None, adam_i=None, src_bits=None):
+             adam_u=None, before_last=None, adam_i=None, src_bits=None,
+             frontier_list=None):
     """backward_steps run to completion: (grad u0, grad i0)."""
     return drain(backward_steps(pair, gU, gI, num_layers, order, out_u, out_i, ws,
                                 grad_i0_dense, reduce, grad_support, adam_u, before_last,
-                                adam_i, src_bits))
+                                adam_i, src_bits, frontier_list))
 
 
 def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,

@@ -128,7 +128,8 @@ class FusedTrainer:
         # and updates are bitwise identical to the dense step (tested).
         self.frontier = resolve_frontier(frontier, graph.item_csr.nnz)
         self.mask_u = torch.zeros(self.U, dtype=torch.uint8, device=dev)
-        self.mask_i = torch.zeros(self.I, dtype=torch.uint8, device=dev)
+        # (whole 4-byte words: bbgr_mark_list sets the item bytes by word atomics)
+        self.mask_i = torch.zeros((self.I + 3) // 4 * 4, dtype=torch.uint8, device=dev)[: self.I]
         # The first backward item product reads only the batch users' rows of
         # gU (81k of 50M edges at C4) but would scan every index of its
         # frontier rows (20.6M) to find them: a bitmap over the item-CSR slots
@@ -141,6 +142,14 @@ class FusedTrainer:
             self.slot_map = graph.user_item_slots()
             self.slot_bits = torch.zeros(graph.item_csr.nnz // 32 + 4, dtype=torch.int32,
                                          device=dev)
+        # GS: the item frontier also as a row list, built by the marking itself
+        # (bbgr_mark_list; length on the device, so a captured step keeps it):
+        # the first backward item product then visits the frontier's rows
+        # (63k at C4) instead of testing the mask byte of every item row.
+        self.item_list = self.item_count = None
+        if self.frontier and order == ORDER_GS:
+            self.item_list = torch.empty(max(self.I, 1), dtype=torch.int64, device=dev)
+            self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
         # Fused optimizer (GS order): the user Adam runs inside the last backward
         # product's epilogue and the item Adam reads gI/(K+1) straight from the
         # sparse BPR gradient table (grad_scale), so neither weight-gradient
@@ -203,7 +212,7 @@ class FusedTrainer:
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
                 out_i=self.itf, ws=self.ws,
                 final_rows=None if masks is None else
-                (masks[0], masks[1], users if listed else None))
+                (masks[0], masks[1], users if listed else None, self._flist(masks)))
         # (a caller's batch may repeat a user: its last user layer then runs on
         # the de-duplicated mask instead of a row list, whose repeated rows
         # would update the in-place accumulator twice)
@@ -220,7 +229,7 @@ class FusedTrainer:
         else:
             backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                      out_i=self.g_i0, ws=self.ws, grad_support=masks,
-                     src_bits=self._bits(masks))
+                     src_bits=self._bits(masks), frontier_list=self._flist(masks))
             # ego L2 term goes straight to the weight grads (Version-2:503-507):
             # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
             call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
@@ -271,7 +280,7 @@ class FusedTrainer:
 
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
-                 src_bits=self._bits(masks),
+                 src_bits=self._bits(masks), frontier_list=self._flist(masks),
                  before_last=before_last, reduce=reduce)
         if item_adam:
             self._item_adam(item_rows, self.g_if, a_gl, gl)
@@ -315,12 +324,21 @@ class FusedTrainer:
         st = stream_handle()
         B = users.numel()
         call("bbgr_mark_rows", B, ptr(users), value, ptr(self.mask_u), self.U, st)
-        call("bbgr_mark_rows", B, ptr(pos), value, ptr(self.mask_i), self.I, st)
-        call("bbgr_mark_rows", B, ptr(neg), value, ptr(self.mask_i), self.I, st)
         uc = self.graph.user_csr
-        if self.order == ORDER_GS:
-            call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), value,
-                 ptr(self.mask_i), st)
+        lst = getattr(self, "item_list", None)
+        if value and lst is not None:   # flag + list the frontier (GS)
+            li = (ptr(self.mask_i), self.I, ptr(lst), ptr(self.item_count), st)
+            call("bbgr_mark_list", B, ptr(pos), None, None, *li)
+            call("bbgr_mark_list", B, ptr(neg), None, None, *li)
+            call("bbgr_mark_list", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), *li)
+        else:
+            call("bbgr_mark_rows", B, ptr(pos), value, ptr(self.mask_i), self.I, st)
+            call("bbgr_mark_rows", B, ptr(neg), value, ptr(self.mask_i), self.I, st)
+            if self.order == ORDER_GS:
+                call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices),
+                     value, ptr(self.mask_i), st)
+            if lst is not None:
+                self.item_count.zero_()
         if getattr(self, "slot_bits", None) is not None:   # set / clear the batch's bits
             call("bbgr_mark_slots", B, ptr(users), ptr(uc.indptr), ptr(self.slot_map),
                  ptr(self.slot_bits), value, st)
@@ -329,6 +347,11 @@ class FusedTrainer:
     def _bits(self, masks):
         """The slot bitmap for backward(src_bits=...) when the masks are on."""
         return getattr(self, "slot_bits", None) if masks is not None else None
+
+    def _flist(self, masks):
+        """(item row list, device count) for backward(frontier_list=...)."""
+        lst = getattr(self, "item_list", None)
+        return None if masks is None or lst is None else (lst, self.item_count)
 
     def forward(self):
         """Final (layer-mean) tables, rows by input id."""

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 4
+#define BBGR_ABI_VERSION 5
 
 typedef enum {
   BBGR_OK = 0,
@@ -246,7 +246,14 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   edges per test) and loads only live edges' indices: a first backward      */
 /*   product over a few batch rows' edges stops scanning every index of the  */
 /*   row. Results are bitwise those of src_mask alone (same edges, same      */
-/*   order); bits of padding: 3 words beyond nnz/32, readable.                 */
+/*   order); bits of padding: 3 words beyond nnz/32, readable. With src_bits  */
+/*   the rows of one chunk (long_threshold < deg <= chunk_edges) are summed by */
+/*   the row's lane group in the chunk workgroup's order (bitwise the same):  */
+/*   a listed launch must then list them (row_mask alone no longer sums them) */
+/* row_count (nullable, DEVICE int64, with row_list): the list holds           */
+/*   min(n_row_list, *row_count) rows; n_row_list is its capacity. For a list  */
+/*   built on the stream (a captured step): a fixed grid of short-row          */
+/*   workgroups walks it, so the host never reads the length.                  */
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
@@ -304,6 +311,7 @@ typedef struct {
   const int32_t *acc_map;
   const int32_t *add_map;
   const uint32_t *src_bits;
+  const int64_t *row_count;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -482,6 +490,16 @@ int bbgr_mark_rows(int64_t n, const int64_t *idx, uint8_t value, uint8_t *mask,
 int bbgr_mark_neighbors(int64_t n, const int64_t *rows, const int32_t *indptr,
                         const int32_t *indices, uint8_t value, uint8_t *mask,
                         bbgr_stream_t stream);
+/* Flag rows in mask and list each newly flagged row once: indptr == NULL —
+ * the rows rows[k] (k < n; negative / >= n_rows skipped); else every column
+ * indices[e] of every edge e of row rows[k]. A row whose byte was 0 is set to
+ * 1 and appended at list[(*count)++] (count: DEVICE int64, list order
+ * unspecified; rows already flagged are not listed again). mask: 4-byte
+ * aligned, its allocation a whole number of 4-byte words. The frontier of a
+ * step as a row list without a scan of the mask (bbgr_spmm_args.row_count). */
+int bbgr_mark_list(int64_t n, const int64_t *rows, const int32_t *indptr,
+                   const int32_t *indices, uint8_t *mask, int64_t n_rows, int64_t *list,
+                   int64_t *count, bbgr_stream_t stream);
 /* Slot bitmaps (bbgr_spmm_args.src_bits). tmap = bbgr_transpose_slots of the  */
 /* CSR whose rows are listed: for every edge e of row rows[k] (k < n), bit     */
 /* tmap[e] of bits is set (set != 0), or its whole 32-bit word cleared          */

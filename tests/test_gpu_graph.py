@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 from bbgr.graph import BipartiteGraph  # noqa: E402
 from bbgr.synthetic import synthetic_credibility, synthetic_edges  # noqa: E402
+from bbgr.propagate import ORDER_GS  # noqa: E402
 from bbgr.trainer import FusedTrainer, GraphedStep  # noqa: E402
 
 DEV = "cuda"
@@ -140,13 +141,19 @@ def test_transpose_slots_map_every_edge_once():
     assert torch.equal(ic_idx[t], urow) and torch.equal(irow[t], uc_idx)
 
 
-@pytest.mark.parametrize("variant", ["v2_pop", "cu_fair"])
-def test_slot_bitmap_first_item_product_is_bitwise_the_mask(variant):
+@pytest.mark.parametrize("variant,bits,listed", [("v2_pop", True, True),
+                                                 ("cu_fair", True, True),
+                                                 ("v2_pop", True, False),
+                                                 ("v2_pop", False, True)])
+def test_slot_bitmap_first_item_product_is_bitwise_the_mask(variant, bits, listed):
     """The first backward item product tests liveness on the batch users' slot
-    bitmap (bbgr_spmm_args.src_bits) instead of scanning indices: weights,
-    moments and losses over three steps equal the mask-only trainer bit for
-    bit (hub items: chunked and split rows), and the bitmap is all zero again
-    after every step."""
+    bitmap (bbgr_spmm_args.src_bits; single-chunk hub rows then summed by one
+    lane group in the chunk workgroup's order) instead of scanning indices,
+    and visits the frontier through the row list the masking built
+    (bbgr_mark_list, device length): weights, moments and losses over three
+    steps equal the mask-only trainer bit for bit (hub items: chunked and
+    split rows), and the bitmap and list count are zero again after every
+    step."""
     U, I = 20000, 3000
     e = synthetic_edges(U, I, 300000, 8, items="zipf")
     g = BipartiteGraph(e, U, I, "cuda", vertex_order="degree")
@@ -154,9 +161,19 @@ def test_slot_bitmap_first_item_product_is_bitwise_the_mask(variant):
               frontier=True, seed=5)
     a, b = FusedTrainer(g, variant, **kw), FusedTrainer(g, variant, **kw)
     assert a.slot_bits is not None
+    assert (a.item_list is not None) == (a.order == ORDER_GS)   # the list: GS only
+    listed = listed and a.item_list is not None
+    if not bits:
+        a.slot_bits = a.slot_map = None
+    if not listed:
+        a.item_list = None
     b.slot_bits = b.slot_map = None          # the mask-only path
+    b.item_list = None
     for _ in range(3):
         assert float(a.step()) == float(b.step())
-        assert int(a.slot_bits.abs().sum()) == 0
+        if bits:
+            assert int(a.slot_bits.abs().sum()) == 0
+        if listed:
+            assert int(a.item_count.item()) == 0
     for x, y in ((a.user_w, b.user_w), (a.item_w, b.item_w), (a.m_u, b.m_u), (a.v_i, b.v_i)):
         assert torch.equal(x, y)
