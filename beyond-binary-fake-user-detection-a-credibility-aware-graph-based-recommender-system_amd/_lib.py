@@ -88,6 +88,7 @@ class SpmmArgs(ctypes.Structure):
         ("y_map", c_void_p), ("acc_map", c_void_p), ("add_map", c_void_p),
         ("src_bits", c_void_p),
         ("row_count", c_void_p),
+        ("acc_in_map", c_void_p),
     ]
 
 

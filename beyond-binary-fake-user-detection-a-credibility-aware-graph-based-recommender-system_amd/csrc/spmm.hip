@@ -79,6 +79,7 @@ struct SpmmParams {
   // CSR row r reads / writes row map[r] of y (and the fused Adam's rows), of
   // acc_in / acc_out, of add; the masks of those tables index the same rows
   const int *y_map, *acc_map, *add_map;
+  const int *acc_in_map;       // acc_in's own row map (args.acc_in_map; NULL: acc_map's)
   const unsigned *src_bits;    // slot bitmap of live edges (args.src_bits; d >= 64)
   const long *row_count;       // device length of row_list (args.row_count; nullable)
 };
@@ -578,16 +579,21 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
   const long rc = P.acc_map ? (long)P.acc_map[row] : (long)row;
   if (P.acc_out && (!P.acc_mask || P.acc_mask[rc])) {
     const float cs = (P.acc_scale ? P.acc_scale[row] : 1.f) * P.acc_scale_s;
+    // the layer-mean accumulator is streamed (read once, written once per
+    // layer, never gathered): non-temporal, so a dense pass (1.28 GB in and
+    // out for the C4 user table) does not evict the gathered rows from the
+    // Infinity Cache
     float4 *dst = reinterpret_cast<float4 *>(P.acc_out + rc * P.ldacc_out) + lane;
     if (P.acc_in) {
+      const long ri = P.acc_in_map ? (long)P.acc_in_map[row] : rc;
       const float4 *ai =
-          reinterpret_cast<const float4 *>(P.acc_in + rc * P.ldacc_in) + lane;
+          reinterpret_cast<const float4 *>(P.acc_in + ri * P.ldacc_in) + lane;
 #pragma unroll
       for (int k = 0; k < V; ++k)
-        dst[16 * k] = f4_mul(P.gamma, f4_fma(cs, T[k], ai[16 * k]));
+        st_nt(dst + 16 * k, f4_mul(P.gamma, f4_fma(cs, T[k], ld_nt(ai + 16 * k))));
     } else {
 #pragma unroll
-      for (int k = 0; k < V; ++k) dst[16 * k] = f4_mul(P.gamma, f4_mul(cs, T[k]));
+      for (int k = 0; k < V; ++k) st_nt(dst + 16 * k, f4_mul(P.gamma, f4_mul(cs, T[k])));
     }
   }
 }
@@ -1061,6 +1067,7 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.y_map = a->y_map;
   P.acc_map = a->acc_map;
   P.add_map = a->add_map;
+  P.acc_in_map = a->acc_in_map;
   P.src_bits = a->src_bits;
 }
 

@@ -155,6 +155,7 @@ struct Opts {
   float gamma = 1.f;
   const uint8_t *src_mask = nullptr, *row_mask = nullptr, *add_mask = nullptr;
   const int32_t *y_map = nullptr, *acc_map = nullptr, *add_map = nullptr;
+  const int32_t *acc_in_map = nullptr;
   bool src_input = false;
 };
 
@@ -196,6 +197,7 @@ static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) 
   a.y_map = o.y_map;
   a.acc_map = o.acc_map;
   a.add_map = o.add_map;
+  a.acc_in_map = o.acc_in_map;
   // input-order source rows carry no hot prefix; mapped output rows neither
   a.stream_from = o.src_input ? 0 : pr.stream_from(d);
   a.stream_out_from = o.y_map ? 0 : pr.stream_out_from(d);
@@ -211,6 +213,44 @@ static at::TensorOptions u8(const Tensor &like) {
 }
 
 // -- K-layer chains (propagate.forward_steps / backward_steps, no sharding) ----
+// The layer-mean accumulators of an input-order pair (K >= 2) stay in the
+// graph's order between layers: layer 1 reads the caller's u0 / i0 through
+// the map (acc_in_map) into an internal table, the middle layers update it in
+// place with no map, and layer K writes the caller's rows (acc_map) from it
+// (acc_in_map = identity). Same arithmetic per row, so the same bits; at C4
+// the mapped (random-row) accumulator passes cost ~0.45 ms per user product.
+struct AccPlan {
+  Tensor in, out;
+  const int32_t *in_map = nullptr, *out_map = nullptr;
+};
+
+static Tensor iota32(int64_t n, const Tensor &like) {
+  return at::arange(n, at::TensorOptions().dtype(at::kInt).device(like.device()));
+}
+
+static AccPlan acc_plan(int64_t k, int64_t K, const Tensor &x0, const Tensor &caller,
+                        Tensor &internal, const int32_t *map, const Tensor &iota) {
+  AccPlan a;
+  if (!map || K < 2) {   // one table throughout (mapped or not)
+    a.in = k == 1 ? x0 : caller;
+    a.out = caller;
+    a.in_map = a.out_map = map;
+    return a;
+  }
+  a.in = k == 1 ? x0 : internal;
+  a.out = k == K ? caller : internal;
+  a.in_map = k == 1 ? map : (k == K ? iota.data_ptr<int32_t>() : nullptr);
+  a.out_map = k == K ? map : nullptr;
+  return a;
+}
+
+static void set_acc(Opts &o, const AccPlan &a) {
+  o.acc_in = a.in;
+  o.acc_out = a.out;
+  o.acc_map = a.out_map;
+  o.acc_in_map = a.in_map;
+}
+
 static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0, const Tensor &i0,
                                                 int64_t K, bool gs, Tensor acc_u = Tensor(),
                                                 Tensor acc_i = Tensor()) {
@@ -227,6 +267,13 @@ static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0,
   const float gl = (float)(1.0 / (double)(K + 1));   // as the Python float
   const int32_t *am_u = P.io ? P.user_map.data_ptr<int32_t>() : nullptr;
   const int32_t *am_i = P.io ? P.item_map.data_ptr<int32_t>() : nullptr;
+  Tensor int_u, int_i, iota_u, iota_i;   // internal-order accumulators (input-order pair)
+  if (P.io && K >= 2) {
+    int_u = at::empty({U, d}, f32(u0));
+    int_i = at::empty({I, d}, f32(u0));
+    iota_u = iota32(U, u0);
+    iota_i = iota32(I, u0);
+  }
   if (gs) {   // Version-2:482-487: i_k = M_iu u_{k-1}; u_k = M_ui i_k
     Tensor bufU = at::empty({U, d}, f32(u0)), bufI = at::empty({I, d}, f32(u0));
     for (int64_t k = 1; k <= K; ++k) {
@@ -234,21 +281,17 @@ static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0,
       Opts oi;
       oi.y = bufI;
       oi.y_scale = P.feed_fwd_iu;
-      oi.acc_in = k == 1 ? i0 : acc_i;
-      oi.acc_out = acc_i;
+      set_acc(oi, acc_plan(k, K, i0, acc_i, int_i, am_i, iota_i));
       oi.acc_scale = P.fi.out_scale;
       oi.gamma = g;
-      oi.acc_map = am_i;
       oi.src_input = P.io && k == 1;
       spmm(P.fi, k == 1 ? u0 : bufU, k == 1, oi);
       Opts ou;
       if (k < K) ou.y = bufU;
       ou.y_scale = P.feed_fwd_ui;
-      ou.acc_in = k == 1 ? u0 : acc_u;
-      ou.acc_out = acc_u;
+      set_acc(ou, acc_plan(k, K, u0, acc_u, int_u, am_u, iota_u));
       ou.acc_scale = P.fu.out_scale;
       ou.gamma = g;
-      ou.acc_map = am_u;
       spmm(P.fu, bufI, false, ou);
     }
   } else {    // lightgcn_cu.py:429-447: both sides from layer k-1
@@ -261,21 +304,17 @@ static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0,
       Opts oi;
       if (k < K) oi.y = bufI[nxt];
       oi.y_scale = P.feed_fwd_iu;
-      oi.acc_in = k == 1 ? i0 : acc_i;
-      oi.acc_out = acc_i;
+      set_acc(oi, acc_plan(k, K, i0, acc_i, int_i, am_i, iota_i));
       oi.acc_scale = P.fi.out_scale;
       oi.gamma = g;
-      oi.acc_map = am_i;
       oi.src_input = P.io && k == 1;
       spmm(P.fi, k == 1 ? u0 : bufU[cur], k == 1, oi);
       Opts ou;
       if (k < K) ou.y = bufU[nxt];
       ou.y_scale = P.feed_fwd_ui;
-      ou.acc_in = k == 1 ? u0 : acc_u;
-      ou.acc_out = acc_u;
+      set_acc(ou, acc_plan(k, K, u0, acc_u, int_u, am_u, iota_u));
       ou.acc_scale = P.fu.out_scale;
       ou.gamma = g;
-      ou.acc_map = am_u;
       ou.src_input = P.io && k == 1;
       spmm(P.fu, k == 1 ? i0 : bufI[cur], k == 1, ou);
       cur = nxt;

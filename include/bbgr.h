@@ -250,6 +250,12 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   the rows of one chunk (long_threshold < deg <= chunk_edges) are summed by */
 /*   the row's lane group in the chunk workgroup's order (bitwise the same):  */
 /*   a listed launch must then list them (row_mask alone no longer sums them) */
+/* acc_in_map (nullable, int32 [n_rows]): acc_in's own row map — row r reads */
+/*   acc_in row acc_in_map[r] while acc_out is placed by acc_map. Lets a chain */
+/*   keep its layer-mean accumulator in the graph's (degree) order between    */
+/*   layers: the first layer reads the caller's table through its map, the   */
+/*   last writes the caller's order, the middle ones touch no map (random    */
+/*   256-byte rows cost ~30 % of a user-side product at C4).                  */
 /* row_count (nullable, DEVICE int64, with row_list): the list holds           */
 /*   min(n_row_list, *row_count) rows; n_row_list is its capacity. For a list  */
 /*   built on the stream (a captured step): a fixed grid of short-row          */
@@ -312,6 +318,7 @@ typedef struct {
   const int32_t *add_map;
   const uint32_t *src_bits;
   const int64_t *row_count;
+  const int32_t *acc_in_map;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
