@@ -94,6 +94,22 @@ inline bool supported_width(int d) {
   return d == 8 || d == 16 || d == 32 || d == 64 || d == 128 || d == 256;
 }
 
+// Streaming (non-temporal) 16-byte loads / stores: data touched once per
+// pass that should not displace cached rows.
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_nt(const float4 *p) {
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float4 *p, float4 v) {
+  f4v w;
+  w.x = v.x;
+  w.y = v.y;
+  w.z = v.z;
+  w.w = v.w;
+  __builtin_nontemporal_store(w, reinterpret_cast<f4v *>(p));
+}
+
 // ---------------------------------------------------------------------------
 // torch.optim.Adam on one element (amsgrad=False, maximize=False). Shared by
 // adam_kernel and the SpMM epilogue's fused step with every rounding spelled

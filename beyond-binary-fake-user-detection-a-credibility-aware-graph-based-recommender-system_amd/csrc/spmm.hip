@@ -88,19 +88,6 @@ __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
   return make_float4(fmaf(a, x.x, y.x), fmaf(a, x.y, y.y), fmaf(a, x.z, y.z),
                      fmaf(a, x.w, y.w));
 }
-typedef float f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld_nt(const float4 *p) {   // streaming (nt) load
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void st_nt(float4 *p, float4 v) {   // streaming (nt) store
-  f4v w;
-  w.x = v.x;
-  w.y = v.y;
-  w.z = v.z;
-  w.w = v.w;
-  __builtin_nontemporal_store(w, reinterpret_cast<f4v *>(p));
-}
 __device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
