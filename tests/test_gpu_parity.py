@@ -1019,3 +1019,109 @@ def test_mark_rows_skips_out_of_range_indices():
     torch.cuda.synchronize()
     assert mask.cpu().tolist() == [0, 0, 0, 1, 0, 0, 0, 0, 0, 1]
     assert not guard.any()
+
+
+def test_mark_list_flags_and_lists_each_row_once():
+    """bbgr_mark_list: the rows a call flags first are listed once each (rows
+    already flagged, repeats, negatives and out-of-range ids are not), the
+    neighbour form lists N(rows) the same way; list order is free."""
+    from bbgr._lib import call, ptr, stream_handle
+    rng = np.random.default_rng(3)
+    n = 1001                                   # not a multiple of 4: the last word
+    mask = torch.zeros((n + 3) // 4 * 4, dtype=torch.uint8, device=DEV)[:n]
+    mask[7] = 1                                # already flagged: never listed
+    lst = torch.full((n,), -9, dtype=torch.int64, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    ids = np.concatenate([rng.integers(0, n, 3000), [-1, n, n + 5, 7, 7, n - 1]])
+    call("bbgr_mark_list", ids.size, ptr(t(ids, torch.int64)), None, None, ptr(mask), n,
+         ptr(lst), ptr(cnt), stream_handle())
+    want = np.setdiff1d(np.unique(ids[(ids >= 0) & (ids < n)]), [7])
+    k = int(cnt.item())
+    assert k == want.size
+    np.testing.assert_array_equal(np.sort(lst[:k].cpu().numpy()), want)
+    m = mask.cpu().numpy()
+    assert set(np.flatnonzero(m)) == set(want) | {7}
+    # neighbours of some users in a CSR (many shared columns)
+    U, I = 300, n
+    e = synthetic_edges(U, I, 6000, 5, items="zipf")
+    c = Csr(e[0], e[1], U, I, DEV)
+    users = rng.choice(U, 64, replace=False)
+    mask2 = torch.zeros((I + 3) // 4 * 4, dtype=torch.uint8, device=DEV)[:I]
+    cnt.zero_()
+    call("bbgr_mark_list", users.size, ptr(t(users, torch.int64)), ptr(c.indptr),
+         ptr(c.indices), ptr(mask2), I, ptr(lst), ptr(cnt), stream_handle())
+    ip, ix = c.indptr.cpu().numpy(), c.indices[: c.nnz].cpu().numpy()
+    want = np.unique(np.concatenate([ix[ip[u]:ip[u + 1]] for u in users]))
+    k = int(cnt.item())
+    np.testing.assert_array_equal(np.sort(lst[:k].cpu().numpy()), want)
+    np.testing.assert_array_equal(np.flatnonzero(mask2.cpu().numpy()), want)
+
+
+@pytest.mark.parametrize("bits", [False, True])
+def test_row_list_with_device_length(bits):
+    """A row list whose length is in device memory (bbgr_spmm_args.row_count,
+    capacity = numel): entries past the count are never read, the listed rows
+    are bitwise the mask launch's, other rows untouched; with a slot bitmap
+    (spmm_bits_kernel) single- and multi-chunk hub rows too."""
+    from bbgr._lib import call, ptr, stream_handle
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(5)
+    U, I, d = 6000, 400, 64
+    e = synthetic_edges(U, I, 150000, 6, items="zipf")   # item rows up to ~5k edges
+    g = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
+    ic = g.item_csr
+    prod = Product(ic, None, None, None, {})
+    x = torch.zeros(U, d, device=DEV)
+    users = rng.choice(U, 200, replace=False)
+    x[t(users, torch.int64).long()] = t(rng.standard_normal((200, d)).astype(np.float32))
+    su = torch.zeros(U, dtype=torch.uint8, device=DEV)
+    su[t(users, torch.int64).long()] = 1
+    ri = np.sort(rng.choice(I, 150, replace=False))
+    rm = torch.zeros(I, dtype=torch.uint8, device=DEV)
+    rm[t(ri, torch.int64).long()] = 1
+    kw = dict(src_mask=su, row_mask=rm)
+    if bits:
+        slots = g.user_item_slots()
+        sb = torch.zeros(ic.nnz // 32 + 4, dtype=torch.int32, device=DEV)
+        call("bbgr_mark_slots", users.size, ptr(t(users, torch.int64)), ptr(g.user_csr.indptr),
+             ptr(slots), ptr(sb), 1, stream_handle())
+        kw["src_bits"] = sb
+    ref = torch.full((I, d), 3.0, device=DEV)
+    spmm(prod, x, False, y=ref, src_mask=su, row_mask=rm)          # mask launch, no bitmap
+    lst = torch.full((I,), -5, dtype=torch.int64, device=DEV)      # junk past the count
+    lst[: ri.size] = t(rng.permutation(ri), torch.int64).long()
+    cnt = torch.tensor([ri.size], dtype=torch.int64, device=DEV)
+    y = torch.full((I, d), 3.0, device=DEV)
+    spmm(prod, x, False, y=y, row_list=lst, row_count=cnt, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert ic.n_chunks > 0 and int((ic.degrees() > ic.chunk_edges).sum()) > 0   # both hub kinds
+
+
+def test_acc_in_map_reads_acc_in_through_its_own_map():
+    """bbgr_spmm_args.acc_in_map: acc_out row acc_map[r] = gamma * (cs*T +
+    acc_in[acc_in_map[r]]) — the drop-in chain's first / last layer."""
+    import ctypes
+    from bbgr._lib import SpmmArgs, call, ld, ptr, stream_handle
+    rng = np.random.default_rng(9)
+    R_, C_, d = 300, 200, 64
+    e = synthetic_edges(C_, R_, 4000, 7)
+    c = Csr(e[1], e[0], R_, C_, DEV)
+    x = rng.standard_normal((C_, d)).astype(np.float32)
+    acc_in = rng.standard_normal((R_, d)).astype(np.float32)
+    pin, pout = rng.permutation(R_).astype(np.int32), rng.permutation(R_).astype(np.int32)
+    a = SpmmArgs()
+    a.d = d
+    xt, ai = t(x), t(acc_in)
+    ao = torch.zeros(R_, d, device=DEV)
+    a.x, a.ldx = ptr(xt), ld(xt)
+    a.acc_in, a.ldacc_in = ptr(ai), ld(ai)
+    a.acc_out, a.ldacc_out = ptr(ao), ld(ao)
+    a.acc_scale_s, a.gamma, a.y_scale_s, a.add_scale_s, a.col_scale_s = 0.5, 0.25, 1.0, 1.0, 1.0
+    mi, mo = t(pin, torch.int32), t(pout, torch.int32)
+    a.acc_in_map, a.acc_map = ptr(mi), ptr(mo)
+    call("bbgr_spmm", ctypes.byref(c._struct), ctypes.byref(a), stream_handle())
+    T_ = R.csr64(e[1], e[0], np.ones(e.shape[1]), (R_, C_)) @ x.astype(np.float64)
+    want = np.zeros((R_, d))
+    want[pout] = 0.25 * (0.5 * T_ + acc_in[pin].astype(np.float64))
+    assert_parity(ao, want, "acc_in_map")
