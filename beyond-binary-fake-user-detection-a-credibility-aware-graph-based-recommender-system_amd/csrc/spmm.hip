@@ -120,6 +120,21 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 #ifndef BBGR_PAIR_WAVES_MASKED
 #define BBGR_PAIR_WAVES_MASKED 0
 #endif
+// the unweighted (WMODE 0) masked two-row kernel: 64 VGPRs either way, 7 waves
+// by the compiler's choice, 8 with the target (no spill). The src-masked
+// backward user product at C4 (20.6M gathers from the item frontier, dense
+// output) 0.984 -> 0.886 ms (tools/ab_spmm.sh, round 3); the weighted forms
+// spill at 8 and keep the default
+#ifndef BBGR_PAIR_WAVES_MASKED0
+#define BBGR_PAIR_WAVES_MASKED0 8
+#endif
+// ... and the unweighted full two-row kernel (62 -> 63 VGPRs, 7 -> 8 waves, no
+// spill): C4 full user products 1.484 -> 1.451 ms per launch (round 3 A/B;
+// the weighted forms spill at 8; an 8-wave target on the one-row kernels
+// measured slower, item products 1.816 -> 1.829 ms)
+#ifndef BBGR_PAIR_WAVES0
+#define BBGR_PAIR_WAVES0 8
+#endif
 // d = 128
 #ifndef BBGR_ROW_U128
 #define BBGR_ROW_U128 8
@@ -171,25 +186,30 @@ template <int D> struct Tune {   // narrow rows (8, 16, 32): one-row kernels onl
   static constexpr int masked_waves =
       D == 32 ? BBGR_NARROW_MASKED_WAVES32 : D == 16 ? BBGR_NARROW_MASKED_WAVES16 : 0;
   static constexpr int pair_u = 0, pair_u_masked = 0;
-  static constexpr int pair_waves = 0, pair_waves_masked = 0;
+  static constexpr int pair_waves = 0, pair_waves_masked = 0, pair_waves_masked0 = 0;
+  static constexpr int pair_waves0 = 0;
 };
 template <> struct Tune<64> {
   static constexpr int row_u = BBGR_ROW_U, row_waves = BBGR_ROW_WAVES;
   static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U, pair_u_masked = BBGR_PAIR_U_MASKED;
   static constexpr int pair_waves = BBGR_PAIR_WAVES, pair_waves_masked = BBGR_PAIR_WAVES_MASKED;
+  static constexpr int pair_waves_masked0 = BBGR_PAIR_WAVES_MASKED0;
+  static constexpr int pair_waves0 = BBGR_PAIR_WAVES0;
 };
 template <> struct Tune<128> {
   static constexpr int row_u = BBGR_ROW_U128, row_waves = BBGR_ROW_WAVES128;
   static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U128, pair_u_masked = BBGR_PAIR_U128;
   static constexpr int pair_waves = BBGR_PAIR_WAVES128, pair_waves_masked = BBGR_PAIR_WAVES128;
+  static constexpr int pair_waves_masked0 = pair_waves_masked, pair_waves0 = pair_waves;
 };
 template <> struct Tune<256> {
   static constexpr int row_u = BBGR_ROW_U256, row_waves = BBGR_ROW_WAVES256;
   static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U256, pair_u_masked = BBGR_PAIR_U256;
   static constexpr int pair_waves = BBGR_PAIR_WAVES256, pair_waves_masked = BBGR_PAIR_WAVES256;
+  static constexpr int pair_waves_masked0 = pair_waves_masked, pair_waves0 = pair_waves;
 };
 #define BBGR_WAVES(n) __attribute__((amdgpu_waves_per_eu((n) ? (n) : 1, (n) ? (n) : 10)))
 
@@ -894,7 +914,8 @@ __global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::row_waves) void spmm_kerne
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves) void spmm_pair_kernel(
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::pair_waves0
+                                                     : Tune<D>::pair_waves) void spmm_pair_kernel(
     SpmmParams P) {
   spmm_body<D, WMODE, false, true>(P);
 }
@@ -906,7 +927,8 @@ spmm_masked_kernel(SpmmParams P) {
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::pair_waves_masked) void
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::pair_waves_masked0
+                                                     : Tune<D>::pair_waves_masked) void
 spmm_masked_pair_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true, true>(P);
 }
@@ -914,9 +936,11 @@ spmm_masked_pair_kernel(SpmmParams P) {
 // Slot-bitmap launches (args.src_bits, d >= 64, one row per group): liveness
 // from the bitmap, single-chunk long rows summed by their row's group
 // (chunk_row_serial). A symbol of its own so the plain masked kernels keep
-// their register budget.
+// their register budget. Unweighted at d = 64: an 8-wave target (63 VGPRs, no
+// spill), C4 0.108 -> 0.103 ms (round 3 A/B).
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::masked_waves) void spmm_bits_kernel(
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 && D == 64 ? 8 : Tune<D>::masked_waves) void
+spmm_bits_kernel(
     SpmmParams P) {
   spmm_body<D, WMODE, true, false, true>(P);
 }
