@@ -30,6 +30,7 @@
 #include <torch/library.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -109,6 +110,7 @@ struct Pair {
   bool io = false;   // input-order tables over a degree-ordered graph
   Tensor user_map, item_map, user_rank64, item_rank64, item_map64;
   std::vector<Tensor> keep;   // every registered tensor, alive while registered
+  mutable Tensor u2i_slots;   // user-CSR slot -> item-CSR slot (built at first use)
 };
 
 static std::mutex g_mu;
@@ -157,6 +159,9 @@ struct Opts {
   const int32_t *y_map = nullptr, *acc_map = nullptr, *add_map = nullptr;
   const int32_t *acc_in_map = nullptr;
   bool src_input = false;
+  const int64_t *row_list = nullptr, *row_count = nullptr;   // device-length row list
+  int64_t n_row_list = 0;
+  const uint32_t *src_bits = nullptr;                         // slot bitmap of src_mask
 };
 
 static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) {
@@ -198,6 +203,10 @@ static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) 
   a.acc_map = o.acc_map;
   a.add_map = o.add_map;
   a.acc_in_map = o.acc_in_map;
+  a.row_list = o.row_list;
+  a.n_row_list = o.n_row_list;
+  a.row_count = o.row_count;
+  a.src_bits = o.src_bits;
   // input-order source rows carry no hot prefix; mapped output rows neither
   a.stream_from = o.src_input ? 0 : pr.stream_from(d);
   a.stream_out_from = o.y_map ? 0 : pr.stream_out_from(d);
@@ -328,7 +337,84 @@ static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0,
 // item product's output support). Undefined = no masks.
 struct Support {
   Tensor su, si, si_int;
+  // GS rows backward (d >= 64): the item frontier as a device-length row list
+  // and the slot bitmap of the listed users' edges in item-CSR order, for the
+  // first item product (bbgr_spmm_args.row_list / row_count / src_bits)
+  Tensor flist, fcount, bits;
 };
+
+// user-CSR slot -> item-CSR slot holding the same edge, the k-th copy of a
+// duplicate pair mapped to the k-th copy: stable sorts of both CSRs' edge
+// keys (user * I + item, internal ids). Unlike bbgr_transpose_slots (a binary
+// search per edge) it needs no column order inside the rows: an input-order
+// pair's rows keep their columns in the caller's id order. One-time per pair.
+static const Tensor &u2i_slots(const Pair &P, const at::Device &dev) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (!P.u2i_slots.defined()) {
+    const bbgr_csr &uc = P.fu.csr, &ic = P.bi.csr;
+    const int64_t nnz = uc.nnz;
+    const auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
+    Tensor out = at::empty({std::max<int64_t>(nnz, 1)}, i32);
+    if (nnz > 0) {
+      auto rows_of = [&](const int32_t *indptr, int64_t n) {
+        Tensor ptr = at::from_blob(const_cast<int32_t *>(indptr), {n + 1}, i32);
+        Tensor cnt = (ptr.narrow(0, 1, n) - ptr.narrow(0, 0, n)).to(at::kLong);
+        return at::repeat_interleave(cnt);
+      };
+      Tensor uidx = at::from_blob(const_cast<int32_t *>(uc.indices), {nnz}, i32).to(at::kLong);
+      Tensor iidx = at::from_blob(const_cast<int32_t *>(ic.indices), {nnz}, i32).to(at::kLong);
+      Tensor ka = rows_of(uc.indptr, P.U) * P.I + uidx;
+      Tensor kb = iidx * P.I + rows_of(ic.indptr, P.I);
+      Tensor sa = std::get<1>(at::sort(ka, /*stable=*/true, /*dim=*/0, /*descending=*/false));
+      Tensor sb = std::get<1>(at::sort(kb, /*stable=*/true, /*dim=*/0, /*descending=*/false));
+      out.index_put_({sa}, sb.to(at::kInt));
+    }
+    P.u2i_slots = out;
+  }
+  return P.u2i_slots;
+}
+
+// the flagged rows of mask [n] as an ascending device list + device count
+static std::pair<Tensor, Tensor> mask_list(const Tensor &mask) {
+  const int64_t n = mask.numel();
+  const auto i64 = at::TensorOptions().dtype(at::kLong).device(mask.device());
+  size_t need = 0;
+  check(bbgr_mask_to_list(n, mask.data_ptr<uint8_t>(), nullptr, nullptr, nullptr, &need,
+                          cur_stream()),
+        "bbgr_mask_to_list (size)");
+  Tensor ws = at::empty({(int64_t)std::max<size_t>(need, 1)}, u8(mask));
+  Tensor list = at::empty({std::max<int64_t>(n, 1)}, i64), cnt = at::empty({1}, i64);
+  size_t have = (size_t)ws.numel();
+  check(bbgr_mask_to_list(n, mask.data_ptr<uint8_t>(), list.data_ptr<int64_t>(),
+                          cnt.data_ptr<int64_t>(), ws.data_ptr(), &have, cur_stream()),
+        "bbgr_mask_to_list");
+  return {list, cnt};
+}
+
+// BBGR_DROPIN_BITS=0 keeps the mask-only first item product (A/B, tests)
+static bool dropin_bits_enabled() {
+  const char *e = std::getenv("BBGR_DROPIN_BITS");
+  return !(e && e[0] == '0');
+}
+
+// Support.flist / fcount / bits for the listed users ui (internal ids): the
+// first backward item product then visits the frontier's rows only and tests
+// edge liveness 64 slots per load, bitwise the mask-only product (the same
+// live edges in the same order; DESIGN §3 "Frontier products")
+static void frontier_bits(const Pair &P, Support &s, const Tensor &ui, int64_t d) {
+  if (d < 64 || !dropin_bits_enabled() || P.fu.csr.nnz == 0) return;
+  const Tensor &slots = u2i_slots(P, ui.device());
+  auto fl = mask_list(s.si_int.defined() ? s.si_int : s.si);
+  s.flist = fl.first;
+  s.fcount = fl.second;
+  s.bits = at::zeros({P.bi.csr.nnz / 32 + 4},
+                     at::TensorOptions().dtype(at::kInt).device(ui.device()));
+  check(bbgr_mark_slots(ui.numel(), ui.data_ptr<int64_t>(), P.fu.csr.indptr,
+                        slots.data_ptr<int32_t>(),
+                        reinterpret_cast<uint32_t *>(s.bits.data_ptr<int32_t>()), 1,
+                        cur_stream()),
+        "bbgr_mark_slots");
+}
 
 static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU, const Tensor &gI,
                                                  int64_t K, bool gs, const Support &s,
@@ -364,6 +450,12 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       oi.row_mask = first ? si_int : nullptr;
       oi.add_map = im;
       oi.src_input = P.io && first;
+      if (first && s.bits.defined()) {
+        oi.row_list = s.flist.data_ptr<int64_t>();
+        oi.n_row_list = I;
+        oi.row_count = s.fcount.data_ptr<int64_t>();
+        oi.src_bits = reinterpret_cast<const uint32_t *>(s.bits.data_ptr<int32_t>());
+      }
       spmm(P.bi, first ? gU : bufU, first, oi);
       Opts ou;
       ou.add = gU;
@@ -562,6 +654,8 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
     }
     s = Support{mu.narrow(0, 0, U), mi.narrow(0, 0, I), Tensor()};
   }
+  if (gs && K >= 1 && iu.numel() > 0)
+    frontier_bits(*P, s, P->io ? P->user_rank64.index_select(0, iu).contiguous() : iu, d);
   return backward_chain(*P, gU, gI, K, gs, s);
 }
 

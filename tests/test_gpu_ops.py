@@ -273,3 +273,42 @@ def test_sparse_ego_not_chosen_without_dense_path():
     assert "sparse" not in loss.grad_fn.name().lower()
     loss.backward()
     assert m.user_emb.weight.grad.layout == torch.strided
+
+
+@pytest.mark.parametrize("order", ["degree", "input"])
+@pytest.mark.parametrize("d", [64, 128])
+def test_dropin_first_item_product_bitmap_is_bitwise_the_mask(order, d, monkeypatch):
+    """GS rows backward (bbgr::propagate_backward_rows): the first backward
+    item product visits the item frontier as a device-length row list and
+    tests edge liveness on the slot bitmap of the batch users' edges in
+    item-CSR order (frontier_bits / u2i_slots in csrc/torch_ops.cpp). The loss
+    and both weight gradients equal the mask-only product's
+    (BBGR_DROPIN_BITS=0) bit for bit, on a Zipf graph whose hub items are cut
+    into one chunk and into several, with duplicate edges, in both drop-in
+    vertex orders."""
+    from bbgr import operators, ops
+    U_, I_, E_, B_ = 20000, 1500, 400_000, 1024
+    e = synthetic_edges(U_, I_, E_, seed=7, items="zipf", duplicates=50)
+    deg_i = np.bincount(np.asarray(e)[1], minlength=I_)
+    assert (deg_i > 2048).sum() >= 3 and ((deg_i > 256) & (deg_i <= 2048)).sum() >= 10
+    cred = torch.as_tensor(synthetic_credibility(U_, 5))
+    g = torch.Generator().manual_seed(3)
+    users = torch.randint(0, U_, (B_,), generator=g).to(DEV)
+    pos = torch.randint(0, I_, (B_,), generator=g).to(DEV)
+    neg = torch.randint(0, I_, (B_,), generator=g).to(DEV)
+    monkeypatch.setattr(operators, "DROPIN_VERTEX_ORDER", order)
+    M_ui, M_iu = V2.build_message_passing_mats(e, U_, I_, cred, DEV)
+    out = {}
+    for bits in ("1", "0"):
+        monkeypatch.setenv("BBGR_DROPIN_BITS", bits)
+        torch.manual_seed(0)
+        m = V2.LightGCN(U_, I_, d, K, M_ui, M_iu).to(DEV)
+        uf, itf = m.propagate()
+        loss = m.bpr_loss(users, pos, neg, uf, itf, 1e-4)
+        n0 = ops.counters()
+        loss.backward()
+        assert ops.counters()["rows"] - n0["rows"] == 1
+        out[bits] = (float(loss), [p.grad.clone() for p in m.parameters()])
+    assert out["1"][0] == out["0"][0]
+    for a, b in zip(out["1"][1], out["0"][1]):
+        assert torch.equal(a, b)
