@@ -341,6 +341,11 @@ struct Support {
   // and the slot bitmap of the listed users' edges in item-CSR order, for the
   // first item product (bbgr_spmm_args.row_list / row_count / src_bits)
   Tensor flist, fcount, bits;
+  // gU (and su) in the graph's own row order instead of the caller's: the
+  // rows backward builds its gU table itself, so every user product adds it
+  // without the row map (add_mask read at the row, not at user_map[row]) and
+  // the first products gather it through the internal column indices
+  bool gu_internal = false;
 };
 
 // user-CSR slot -> item-CSR slot holding the same edge, the k-th copy of a
@@ -434,6 +439,8 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
   const uint8_t *si_int = s.si_int.defined() ? p<uint8_t>(s.si_int) : si;
   const int32_t *um = P.io ? P.user_map.data_ptr<int32_t>() : nullptr;
   const int32_t *im = P.io ? P.item_map.data_ptr<int32_t>() : nullptr;
+  const int32_t *um_add = s.gu_internal ? nullptr : um;   // gU's row map
+  const bool gu_in = P.io && !s.gu_internal;              // gU in input order
   if (gs) {   // Gi_k = gI' + M_ui^T Gu_k ; Gu_{k-1} = gU' + M_iu^T Gi_k ; Gu_K = gU'
     Tensor bufU = at::empty({U, d}, f32(gU)), bufI = at::empty({I, d}, f32(gU));
     for (int64_t k = K; k >= 1; --k) {
@@ -449,7 +456,7 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       oi.src_mask = first ? su : nullptr;
       oi.row_mask = first ? si_int : nullptr;
       oi.add_map = im;
-      oi.src_input = P.io && first;
+      oi.src_input = gu_in && first;
       if (first && s.bits.defined()) {
         oi.row_list = s.flist.data_ptr<int64_t>();
         oi.n_row_list = I;
@@ -460,7 +467,7 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       Opts ou;
       ou.add = gU;
       ou.add_mask = su;
-      ou.add_map = um;
+      ou.add_map = um_add;
       ou.src_mask = first ? si_int : nullptr;
       ou.add_scale_s = gl;
       if (k > 1) {
@@ -474,7 +481,10 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       }
       spmm(P.bu, bufI, false, ou);
     }
-    at::mul_out(gi0, gI, gl);   // GS: i0 only feeds the layer mean
+    // GS: i0 only feeds the layer mean. The Tensor overload with a CPU 0-dim
+    // float: the Scalar overload of mul.out computes into a temporary and
+    // copies it (a second 256 MB pass at C4); the same float product either way
+    at::mul_out(gi0, gI, at::scalar_tensor(gl, at::TensorOptions().dtype(at::kFloat)));
   } else {    // Jacobi: Gu_{k-1} = gU' + M_iu^T Gi_k ; Gi_{k-1} = gI' + M_ui^T Gu_k
     Tensor bufU[2] = {at::empty({U, d}, f32(gU)), at::empty({U, d}, f32(gU))};
     Tensor bufI[2] = {at::empty({I, d}, f32(gU)), at::empty({I, d}, f32(gU))};
@@ -489,7 +499,7 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       ou.y_scale_s = oi.y_scale_s = ys;
       ou.add = gU;
       ou.add_mask = su;
-      ou.add_map = um;
+      ou.add_map = um_add;
       ou.add_scale_s = gl;
       ou.src_mask = first ? si : nullptr;
       ou.src_input = P.io && first;
@@ -498,7 +508,7 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       oi.add_map = im;
       oi.add_scale_s = gl;
       oi.src_mask = first ? su : nullptr;
-      oi.src_input = P.io && first;
+      oi.src_input = gu_in && first;
       if (k > 1) {
         ou.y = bufU[nxt];
         ou.y_scale = P.feed_bwd_ui;
@@ -625,17 +635,22 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
   const int64_t U = P->U, I = P->I, d = vu.size(1);
   Tensor iu = iu_.to(at::kLong).contiguous();
   Tensor gI = gI_.contiguous();
+  // input-order pair, K >= 1: gU never leaves this op, so it is formed in the
+  // graph's row order (row user_rank[iu[k]]) and the chain reads it unmapped
+  // (Support.gu_internal); the same values at the same rows of the products
+  const bool gu_int = P->io && K >= 1;
+  Tensor ru = gu_int ? P->user_rank64.index_select(0, iu).contiguous() : iu;
   Tensor gU;
   if (K == 0) {
     gU = at::zeros({std::max<int64_t>(U, 1), d}, f32(vu)).narrow(0, 0, U);
   } else {
     gU = at::empty({std::max<int64_t>(U, 1), d}, f32(vu)).narrow(0, 0, U);
-    gU.index_fill_(0, iu, 0.0);
+    gU.index_fill_(0, ru, 0.0);
   }
-  index_add_rows(gU, iu, vu.contiguous());
+  index_add_rows(gU, ru, vu.contiguous());
   Tensor mu = at::zeros({std::max<int64_t>(U, 1)}, u8(vu));
   Tensor mi = at::empty({std::max<int64_t>(I, 1)}, u8(vu));
-  check(bbgr_mark_rows(iu.numel(), iu.data_ptr<int64_t>(), 1, mu.data_ptr<uint8_t>(), U,
+  check(bbgr_mark_rows(ru.numel(), ru.data_ptr<int64_t>(), 1, mu.data_ptr<uint8_t>(), U,
                        cur_stream()),
         "bbgr_mark_rows");
   check(bbgr_row_support(I, (int32_t)d, gI.data_ptr<float>(), ld(gI), mi.data_ptr<uint8_t>(),
@@ -645,6 +660,7 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
   Support s;
   if (P->io) {
     s = io_support(*P, mu.narrow(0, 0, U), mi.narrow(0, 0, I), gs, iu);
+    s.gu_internal = gu_int;
   } else {
     if (gs) {   // the first item product's output support: N(listed users)
       const bbgr_csr &uc = P->fu.csr;
@@ -655,7 +671,7 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
     s = Support{mu.narrow(0, 0, U), mi.narrow(0, 0, I), Tensor()};
   }
   if (gs && K >= 1 && iu.numel() > 0)
-    frontier_bits(*P, s, P->io ? P->user_rank64.index_select(0, iu).contiguous() : iu, d);
+    frontier_bits(*P, s, ru, d);
   return backward_chain(*P, gU, gI, K, gs, s);
 }
 
