@@ -86,13 +86,10 @@ def _receives_dense_grad(final: torch.Tensor, weight: torch.Tensor) -> bool:
 
 def _first_slot(ids: torch.Tensor) -> torch.Tensor:
     """slot[b] = position of the first occurrence of ids[b] (device-only, fixed
-    shape: stable sort, segment starts by cummax)."""
-    n = ids.numel()
+    shape: stable sort, each sorted value's first sorted position by a lower-
+    bound search)."""
     srt, perm = torch.sort(ids, stable=True)
-    pos = torch.arange(n, dtype=torch.int64, device=ids.device)
-    start = torch.ones(n, dtype=torch.bool, device=ids.device)
-    start[1:] = srt[1:] != srt[:-1]
-    head = torch.cummax(torch.where(start, pos, 0), 0).values   # sorted position of the group head
+    head = torch.searchsorted(srt, srt)   # first sorted position of each value
     slot = torch.empty_like(perm)
     slot[perm] = perm[head]
     return slot
