@@ -8,7 +8,8 @@
 //
 //   bbgr::propagate(u0, i0, pair_key, num_layers, order) -> (u_final, i_final)
 //   bbgr::propagate_backward(gU, gI, pair_key, num_layers, order) -> (grad_u0, grad_i0)
-//   bbgr::propagate_backward_rows(iu, vu, gI, num_users, pair_key, num_layers, order)
+//   bbgr::propagate_backward_rows(iu, vu, gI, num_users, pair_key, num_layers, order,
+//                                 ii=None, vi=None)
 //   bbgr::jacobi_layer(u, i, pair_key) -> (new_i, new_u)          (+ _backward)
 //   bbgr::propagate_sym(x0, pair_key, num_layers) -> x_final       (+ _backward)
 //   bbgr::bpr_loss(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair) -> loss
@@ -346,6 +347,10 @@ struct Support {
   // without the row map (add_mask read at the row, not at user_map[row]) and
   // the first products gather it through the internal column indices
   bool gu_internal = false;
+  // gI given as rows (the rows backward with ii / vi): gI is zero off the
+  // listed rows, so the GS weight gradient gI/(K+1) is formed on those rows
+  // of a zeroed table instead of a pass over the whole of gI
+  Tensor gi_rows;
 };
 
 // user-CSR slot -> item-CSR slot holding the same edge, the k-th copy of a
@@ -484,7 +489,13 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
     // GS: i0 only feeds the layer mean. The Tensor overload with a CPU 0-dim
     // float: the Scalar overload of mul.out computes into a temporary and
     // copies it (a second 256 MB pass at C4); the same float product either way
-    at::mul_out(gi0, gI, at::scalar_tensor(gl, at::TensorOptions().dtype(at::kFloat)));
+    const Tensor glt = at::scalar_tensor(gl, at::TensorOptions().dtype(at::kFloat));
+    if (s.gi_rows.defined()) {   // gI holds values on its listed rows only
+      gi0.zero_();
+      gi0.index_copy_(0, s.gi_rows, at::mul(gI.index_select(0, s.gi_rows), glt));
+    } else {
+      at::mul_out(gi0, gI, glt);
+    }
   } else {    // Jacobi: Gu_{k-1} = gU' + M_iu^T Gi_k ; Gi_{k-1} = gI' + M_ui^T Gu_k
     Tensor bufU[2] = {at::empty({U, d}, f32(gU)), at::empty({U, d}, f32(gU))};
     Tensor bufI[2] = {at::empty({I, d}, f32(gU)), at::empty({I, d}, f32(gU))};
@@ -628,13 +639,32 @@ static std::tuple<Tensor, Tensor> propagate_backward_cuda(const Tensor &gU_, con
 // those rows, so the rest is never touched (K = 0 copies gU whole: zeroed).
 static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
     const Tensor &iu_, const Tensor &vu, const Tensor &gI_, int64_t num_users, int64_t key,
-    int64_t K, c10::string_view order) {
+    int64_t K, c10::string_view order, const c10::optional<Tensor> &ii_,
+    const c10::optional<Tensor> &vi_) {
   auto P = pair_of(key);
   const bool gs = is_gs(order);
   TORCH_CHECK(num_users == P->U, "propagate_backward_rows: num_users does not match the pair");
   const int64_t U = P->U, I = P->I, d = vu.size(1);
   Tensor iu = iu_.to(at::kLong).contiguous();
-  Tensor gI = gI_.contiguous();
+  // dL/d(i_final) as rows too (vi[k] adds to item ii[k]; gI_ is then only a
+  // [I, d] placeholder): gI is summed on those rows of a zeroed table (the GS
+  // item product's addend is read on its whole output support, N(users)
+  // included) and its support is the list itself instead of a 256 MB
+  // bbgr_row_support scan; the GS weight gradient gI/(K+1) is formed on the
+  // listed rows only (Support.gi_rows)
+  const bool gi_rows = ii_.has_value() && ii_->defined();
+  TORCH_CHECK(gi_rows == (vi_.has_value() && vi_->defined()),
+              "propagate_backward_rows: ii and vi go together");
+  Tensor ii, gI;
+  if (gi_rows) {
+    ii = ii_->to(at::kLong).contiguous();
+    TORCH_CHECK(vi_->dim() == 2 && vi_->size(0) == ii.numel() && vi_->size(1) == d,
+                "propagate_backward_rows: vi must be [len(ii), d]");
+    gI = at::zeros({std::max<int64_t>(I, 1), d}, f32(vu)).narrow(0, 0, I);
+    index_add_rows(gI, ii, vi_->contiguous());
+  } else {
+    gI = gI_.contiguous();
+  }
   // input-order pair, K >= 1: gU never leaves this op, so it is formed in the
   // graph's row order (row user_rank[iu[k]]) and the chain reads it unmapped
   // (Support.gu_internal); the same values at the same rows of the products
@@ -653,9 +683,16 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
   check(bbgr_mark_rows(ru.numel(), ru.data_ptr<int64_t>(), 1, mu.data_ptr<uint8_t>(), U,
                        cur_stream()),
         "bbgr_mark_rows");
-  check(bbgr_row_support(I, (int32_t)d, gI.data_ptr<float>(), ld(gI), mi.data_ptr<uint8_t>(),
-                         nullptr, nullptr, nullptr, cur_stream()),
-        "bbgr_row_support");
+  if (gi_rows) {
+    mi.zero_();
+    check(bbgr_mark_rows(ii.numel(), ii.data_ptr<int64_t>(), 1, mi.data_ptr<uint8_t>(), I,
+                         cur_stream()),
+          "bbgr_mark_rows");
+  } else {
+    check(bbgr_row_support(I, (int32_t)d, gI.data_ptr<float>(), ld(gI),
+                           mi.data_ptr<uint8_t>(), nullptr, nullptr, nullptr, cur_stream()),
+          "bbgr_row_support");
+  }
   g_rows_backward++;
   Support s;
   if (P->io) {
@@ -670,6 +707,7 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
     }
     s = Support{mu.narrow(0, 0, U), mi.narrow(0, 0, I), Tensor()};
   }
+  if (gi_rows && K >= 1) s.gi_rows = ii;
   if (gs && K >= 1 && iu.numel() > 0)
     frontier_bits(*P, s, ru, d);
   return backward_chain(*P, gU, gI, K, gs, s);
@@ -865,10 +903,9 @@ static std::tuple<Tensor, Tensor> propagate_meta(const Tensor &u0, const Tensor 
                                                  int64_t, c10::string_view) {
   return {at::empty_like(u0), at::empty_like(i0)};
 }
-static std::tuple<Tensor, Tensor> propagate_backward_rows_meta(const Tensor &, const Tensor &vu,
-                                                               const Tensor &gI, int64_t num_users,
-                                                               int64_t, int64_t,
-                                                               c10::string_view) {
+static std::tuple<Tensor, Tensor> propagate_backward_rows_meta(
+    const Tensor &, const Tensor &vu, const Tensor &gI, int64_t num_users, int64_t, int64_t,
+    c10::string_view, const c10::optional<Tensor> &, const c10::optional<Tensor> &) {
   return {at::empty({num_users, vu.size(1)}, vu.options()), at::empty_like(gI)};
 }
 static std::tuple<Tensor, Tensor> jacobi_layer_meta(const Tensor &u, const Tensor &i, int64_t) {
@@ -911,7 +948,9 @@ static c10::TypedOperatorHandle<Sig> op(const char *name) {
 using PropSig = std::tuple<Tensor, Tensor>(const Tensor &, const Tensor &, int64_t, int64_t,
                                            c10::string_view);
 using RowsSig = std::tuple<Tensor, Tensor>(const Tensor &, const Tensor &, const Tensor &, int64_t,
-                                           int64_t, int64_t, c10::string_view);
+                                           int64_t, int64_t, c10::string_view,
+                                           const c10::optional<Tensor> &,
+                                           const c10::optional<Tensor> &);
 using LayerSig = std::tuple<Tensor, Tensor>(const Tensor &, const Tensor &, int64_t);
 using SymSig = Tensor(const Tensor &, int64_t, int64_t);
 using BprSig = Tensor(const Tensor &, const Tensor &, const Tensor &, const Tensor &,
@@ -943,12 +982,20 @@ struct PropagateFn : public torch::autograd::Function<PropagateFn> {
     const std::string order = ctx->saved_data["order"].toStringRef();
     const auto su = ctx->saved_data["su"].toIntVector(), si = ctx->saved_data["si"].toIntVector();
     Tensor gU = go[0], gI = go[1];
-    if (gU.defined() && gU.layout() == at::kSparse && !(gI.defined() && gI.is_sparse())) {
-      // a BPR-shaped gradient handed over as rows (bbgr::bpr_loss_sparse_ego)
+    if (gU.defined() && gU.layout() == at::kSparse) {
+      // a BPR-shaped gradient handed over as rows (bbgr::bpr_loss_sparse_ego):
+      // dL/d(u_final) always, dL/d(i_final) too when it arrives sparse
       Tensor vals = gU._values();
-      if (!gI.defined()) gI = at::zeros(si, vals.options());
       static auto h = op<RowsSig>("bbgr::propagate_backward_rows");
-      auto r = h.call(gU._indices().select(0, 0), vals, gI, su[0], key, K, order);
+      c10::optional<Tensor> ii, vi;
+      if (gI.defined() && gI.is_sparse()) {
+        ii = gI._indices().select(0, 0);
+        vi = gI._values();
+        gI = at::empty(si, vals.options());   // shape only: never read
+      } else if (!gI.defined()) {
+        gI = at::zeros(si, vals.options());
+      }
+      auto r = h.call(gU._indices().select(0, 0), vals, gI, su[0], key, K, order, ii, vi);
       return {std::get<0>(r), std::get<1>(r), Tensor(), Tensor(), Tensor()};
     }
     if (gU.defined() && gU.is_sparse()) gU = gU.to_dense();
@@ -1064,18 +1111,21 @@ struct BprSparseEgoFn : public torch::autograd::Function<BprSparseEgoFn> {
     a.contrib = contrib.data_ptr<float>();
     a.ldcontrib = ld(contrib);
     check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr");
-    Tensor g_if = at::zeros_like(itf);
-    index_add_rows(g_if, at::cat({pos, neg}), contrib.narrow(0, B, 2 * B));
     auto eg = ego_grad_rows(dl, users, pos, neg, ue, ie, reg);
     const Tensor &ru = std::get<0>(eg), &ri = std::get<1>(eg), &iu = std::get<2>(eg),
                  &ii = std::get<3>(eg);
-    Tensor g_uf;
+    Tensor g_uf, g_if;
     if (ctx->saved_data["sparse_uf"].toBool()) {
-      // a dropped triple's row is +0.0 (the kernel zeroes it): clamped ids add nothing
+      // dL/d(u_final) and dL/d(i_final) as rows, summed by propagate's rows
+      // backward (bitwise the dense tables on their rows). A dropped triple's
+      // rows are +0.0 (the kernel zeroes them): clamped ids add nothing
       g_uf = at::sparse_coo_tensor(iu.unsqueeze(0), contrib.narrow(0, 0, B), uf.sizes());
+      g_if = at::sparse_coo_tensor(ii.unsqueeze(0), contrib.narrow(0, B, 2 * B), itf.sizes());
     } else {
       g_uf = at::zeros_like(uf);
       index_add_rows(g_uf, users, contrib.narrow(0, 0, B));
+      g_if = at::zeros_like(itf);
+      index_add_rows(g_if, at::cat({pos, neg}), contrib.narrow(0, B, 2 * B));
     }
     Tensor g_ue = at::sparse_coo_tensor(iu.unsqueeze(0), ru, ue.sizes());
     Tensor g_ie = at::sparse_coo_tensor(ii.unsqueeze(0), ri, ie.sizes());
@@ -1215,7 +1265,7 @@ TORCH_LIBRARY(bbgr, m) {
   m.def("propagate(Tensor u0, Tensor i0, int pair_key, int num_layers, str order) -> (Tensor, Tensor)");
   m.def("propagate_backward(Tensor gU, Tensor gI, int pair_key, int num_layers, str order) -> (Tensor, Tensor)");
   m.def("propagate_backward_rows(Tensor iu, Tensor vu, Tensor gI, int num_users, int pair_key, "
-        "int num_layers, str order) -> (Tensor, Tensor)");
+        "int num_layers, str order, Tensor? ii=None, Tensor? vi=None) -> (Tensor, Tensor)");
   m.def("jacobi_layer(Tensor u, Tensor i, int pair_key) -> (Tensor, Tensor)");
   m.def("jacobi_layer_backward(Tensor g_i, Tensor g_u, int pair_key) -> (Tensor, Tensor)");
   m.def("propagate_sym(Tensor x0, int pair_key, int num_layers) -> Tensor");

@@ -13,7 +13,8 @@ libtorch / TorchScript caller reaches the same operators as torch.ops.bbgr.*:
   bbgr::propagate(u0, i0, pair_key, num_layers, order) -> (u_final, i_final)
   bbgr::propagate_backward(gU, gI, pair_key, num_layers, order) -> (grad_u0, grad_i0)
   bbgr::propagate_backward_rows(iu, vu, gI, num_users, pair_key, num_layers,
-                                order) -> (grad_u0, grad_i0)   (gU given as rows)
+                                order, ii=None, vi=None) -> (grad_u0, grad_i0)
+                                (gU given as rows; gI too with ii / vi)
   bbgr::jacobi_layer(u, i, pair_key) -> (new_i, new_u)   (+ _backward)
   bbgr::propagate_sym(x0, pair_key, num_layers) -> x_final   (+ _backward)
   bbgr::bpr_loss(uf, itf, ue, ie, users, pos, neg, reg, pop, lambda_fair) -> loss

@@ -15,8 +15,8 @@ SCHEMAS = {
     "propagate": "bbgr::propagate(Tensor u0, Tensor i0, int pair_key, int num_layers, str order)"
                  " -> (Tensor, Tensor)",
     "propagate_backward_rows": "bbgr::propagate_backward_rows(Tensor iu, Tensor vu, Tensor gI, "
-                               "int num_users, int pair_key, int num_layers, str order) -> "
-                               "(Tensor, Tensor)",
+                               "int num_users, int pair_key, int num_layers, str order, "
+                               "Tensor? ii=None, Tensor? vi=None) -> (Tensor, Tensor)",
     "bpr_loss": "bbgr::bpr_loss(Tensor uf, Tensor itf, Tensor ue, Tensor ie, Tensor users, "
                 "Tensor pos, Tensor neg, float reg, Tensor? pop, float lambda_fair) -> Tensor",
 }
