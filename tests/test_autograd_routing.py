@@ -69,3 +69,17 @@ def test_not_while_compiling():
 
     torch.compile(probe, backend="eager")(torch.ones(2))
     assert seen and not any(seen)
+
+
+@pytest.mark.parametrize("n,hi", [(1, 5), (2, 1), (7, 3), (1000, 50), (16384, 1_000_000)])
+def test_first_slot_is_the_first_occurrence(n, hi):
+    """bpr._first_slot (the ego rows' slot of each triple; the C++ first_slot
+    in csrc/torch_ops.cpp is the same sort + lower-bound search): slot[b] is
+    the smallest b' with ids[b'] == ids[b]."""
+    g = torch.Generator().manual_seed(n + hi)
+    ids = torch.randint(0, hi, (n,), generator=g)
+    first = {}
+    for b, v in enumerate(ids.tolist()):
+        first.setdefault(v, b)
+    want = torch.tensor([first[v] for v in ids.tolist()])
+    assert torch.equal(bpr._first_slot(ids), want)
