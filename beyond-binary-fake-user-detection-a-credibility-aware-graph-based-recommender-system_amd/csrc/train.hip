@@ -497,7 +497,12 @@ __global__ void scatter_keys_kernel(long n, const long *idx, long n_dst, unsigne
 
 // One 16-lane group per sorted position; the group at the start of a run of
 // equal keys sums the run's source rows in (stable) ascending-k order and adds
-// the total to the destination row once.
+// the total to the destination row once. The run is read 16 positions at a
+// time (lane j loads key / source index t0 + j; the run's part of the window
+// is a prefix, its length a ballot), then up to 8 of its rows are gathered
+// before they are added in order: a hot destination (a popular item drawn
+// many times as a negative) no longer costs one dependent load chain per
+// element. The additions are the same, in the same order (bitwise).
 template <int D>
 __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const unsigned *keys,
                                                                const int *vals,
@@ -505,22 +510,46 @@ __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const uns
                                                                float *dst, long ldd,
                                                                unsigned skip) {
   constexpr int V = RowShape<D>::V;
+  constexpr int G = 8;   // rows in flight
   const long s = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
-  if (s >= n || lane >= RowShape<D>::LANES) return;
+  if (s >= n) return;   // group-uniform
   const unsigned key = keys[s];
-  if (key == skip || (s > 0 && keys[s - 1] == key)) return;
+  if (key == skip || (s > 0 && keys[s - 1] == key)) return;   // group-uniform
+  const bool cols = lane < RowShape<D>::LANES;
   float4 acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (long t = s; t < n && keys[t] == key; ++t) {
-    const float4 *row = reinterpret_cast<const float4 *>(src + (long)vals[t] * lds) + lane;
+  for (long t0 = s;; t0 += 16) {
+    const long tj = t0 + lane;
+    const bool in = tj < n && keys[tj] == key;
+    const int vj = in ? vals[tj] : 0;
+    const unsigned m = (unsigned)((__ballot(in) >> (threadIdx.x & 48)) & 0xffffull);
+    const int cnt = __popc(m);   // keys are sorted: the run's lanes are a prefix
+    for (int j0 = 0; j0 < cnt; j0 += G) {
+      float4 x[G][V];
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      const float4 x = row[16 * k];
-      acc[k] = make_float4(acc[k].x + x.x, acc[k].y + x.y, acc[k].z + x.z, acc[k].w + x.w);
+      for (int g = 0; g < G; ++g) {
+        const int v = __shfl(vj, j0 + g, 16);
+        if (cols && j0 + g < cnt) {
+          const float4 *row = reinterpret_cast<const float4 *>(src + (long)v * lds) + lane;
+#pragma unroll
+          for (int k = 0; k < V; ++k) x[g][k] = row[16 * k];
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (j0 + g < cnt) {
+#pragma unroll
+          for (int k = 0; k < V; ++k)
+            acc[k] = make_float4(acc[k].x + x[g][k].x, acc[k].y + x[g][k].y,
+                                 acc[k].z + x[g][k].z, acc[k].w + x[g][k].w);
+        }
+      }
     }
+    if (cnt < 16) break;
   }
+  if (!cols) return;
   float4 *out = reinterpret_cast<float4 *>(dst + (long)key * ldd) + lane;
 #pragma unroll
   for (int k = 0; k < V; ++k) {

@@ -794,7 +794,7 @@ def test_graph_from_memmaps_matches_array(tmp_path):
         assert torch.equal(g.item_csr.indices, g1.item_csr.indices)
 
 
-@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("d", [8, 16, 32, 64, 128, 256])
 def test_scatter_add_rows_matches_index_add(d):
     """bbgr_scatter_add_rows == numpy add.at (sequential ascending order) bit
     for bit on a zero destination; invalid indices skipped; repeatable."""
