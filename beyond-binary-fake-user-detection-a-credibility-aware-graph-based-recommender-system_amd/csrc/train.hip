@@ -244,10 +244,13 @@ __device__ __forceinline__ AdamConsts device_step_consts(AdamConsts c, float lr,
 // Each workgroup owns contiguous tiles of 256 x ADAM_TILE float4 per stream
 // (thread t on float4 t, t + 256, ...), all loads of a tile issued before the
 // math, every stream read and written non-temporally (each byte is touched
-// once). Measured on the C4 tables (tools/adam_variants.hip, 28 B/param):
-// 5M x 64 1.643 -> 1.439 ms (5.45 -> 6.23 TB/s), 1M x 64 0.375 -> 0.323 ms
-// against the grid-stride one-float4 form; the same bits.
-#define ADAM_TILE 4
+// once), one tile per workgroup (no grid cap). Measured on the C4 tables
+// (tools/adam_variants.hip, 28 B/param): 5M x 64 1.643 -> 1.439 ms (5.45 ->
+// 6.23 TB/s) for 4-float4 tiles and a 4096-workgroup cap against the
+// grid-stride one-float4 form; on a second box the uncapped grid took another
+// 6-8 % (users 1.702 -> 1.568 / 1.595 ms with 4 / 2 float4 per stream, items
+// 0.317 -> 0.309 / 0.297 ms); the same bits.
+#define ADAM_TILE 2
 __global__ __launch_bounds__(256) void adam_kernel(long n4, float4 *p, const float4 *g,
                                                    float4 *m, float4 *v, AdamConsts c0,
                                                    float gs, float lr, const float *bc,
@@ -698,7 +701,7 @@ static int adam_launch(int64_t n, float *param, const float *grad, float *exp_av
   const long n4 = vec ? n / 4 : 0;
   if (n4 > 0) {
     long blocks = (n4 + 256 * ADAM_TILE - 1) / (256 * ADAM_TILE);
-    if (blocks > 256 * 16) blocks = 256 * 16;
+    if (blocks > (1L << 30)) blocks = 1L << 30;   // the kernel strides past it
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n4,
                        (float4 *)param, (const float4 *)grad, (float4 *)exp_avg,
                        (float4 *)exp_avg_sq, c, grad_scale, lr, bc, state);

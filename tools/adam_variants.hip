@@ -208,7 +208,11 @@ int main(int argc, char **argv) {
               {"u2_cap2048", 1, 2048},      {"u2nt_cap4096", 3, 4096},
               {"u4nt_cap2048", 4, 2048},    {"tile4_cap4096", 5, 4096},
               {"tile8_cap2048", 6, 2048},   {"tile4nt_cap4096", 7, 4096},
-              {"tile4_full", 5, (n4 + 1023) / 1024}, {"copy", 8, 4096},
+              {"tile4_full", 5, (n4 + 1023) / 1024}, {"tile4nt_full", 7, (n4 + 1023) / 1024},
+              {"tile4nt_cap8192", 7, 8192}, {"tile4nt_cap2048", 7, 2048},
+              {"tile2nt_cap4096", 10, 4096}, {"tile2nt_full", 10, (n4 + 511) / 512},
+              {"tile8nt_cap2048", 11, 2048}, {"tile8nt_full", 11, (n4 + 2047) / 2048},
+              {"copy", 8, 4096},
               {"rw43", 9, 4096}};
     for (const V &vv : vs) {
       fill(b, n4, h, (float4 *)hm, (float4 *)hv);
@@ -223,6 +227,8 @@ int main(int argc, char **argv) {
           case 5: hipLaunchKernelGGL((adam_tile<4, false>), gd, bd, 0, 0, n4, b.p, b.g, b.m, b.v, c); break;
           case 6: hipLaunchKernelGGL((adam_tile<8, false>), gd, bd, 0, 0, n4, b.p, b.g, b.m, b.v, c); break;
           case 7: hipLaunchKernelGGL((adam_tile<4, true>), gd, bd, 0, 0, n4, b.p, b.g, b.m, b.v, c); break;
+          case 10: hipLaunchKernelGGL((adam_tile<2, true>), gd, bd, 0, 0, n4, b.p, b.g, b.m, b.v, c); break;
+          case 11: hipLaunchKernelGGL((adam_tile<8, true>), gd, bd, 0, 0, n4, b.p, b.g, b.m, b.v, c); break;
           case 8: hipLaunchKernelGGL(copy_k, gd, bd, 0, 0, n4, b.g, b.m); break;
           default: hipLaunchKernelGGL(rw43_k, gd, bd, 0, 0, n4, b.p, b.g, b.m, b.v); break;
         }
@@ -231,7 +237,7 @@ int main(int argc, char **argv) {
       launch();
       CK(hipDeviceSynchronize());
       bool same = true;
-      if (vv.kind <= 7) {
+      if (vv.kind <= 7 || vv.kind >= 10) {
         CK(hipMemcpy(out, b.p, n * 4, hipMemcpyDeviceToHost));
         if (vv.kind == 0 && vv.grid == 4096) memcpy(ref, out, n * 4);
         else same = memcmp(ref, out, n * 4) == 0;
@@ -244,7 +250,7 @@ int main(int argc, char **argv) {
       float ms = 0.f;
       CK(hipEventElapsedTime(&ms, e0, e1));
       ms /= reps;
-      const double bytes = vv.kind == 8 ? 8.0 * n : 28.0 * n;
+      const double bytes = vv.kind == 8 ? 8.0 * n : 28.0 * n;  // copy: 1 read + 1 write
       printf("%s{\"rows\": %ld, \"variant\": \"%s\", \"grid\": %ld, \"ms\": %.4f, \"TBps\": %.3f, "
              "\"bitwise_v0\": %s}\n",
              first ? "" : ",", rows_list[ri], vv.name, vv.grid, ms, bytes / (ms * 1e-3) / 1e12,
