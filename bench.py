@@ -7,11 +7,22 @@ one batch: pop-mix sampling -> K-layer GS propagation (2K fused SpMMs) ->
 fused BPR -> backward (2K transposed SpMMs) -> Adam on every parameter.
 Inputs (graph, operators, tables) are resident in HBM before timing starts.
 
-value = SpMM edges/s of the whole job = 4*K*E edges traversed per step
-        * steps / wall time (max over ranks). BPR steps/s is reported beside.
-roofline = the fused SpMM kernel (dominant kernel): algorithmic bytes per launch
-        B = E*(4 + 4 + 4d) + R*(4 + 4d) / average launch time,
-        measured with events around every SpMM launch inside the timed region.
+value = SpMM edges actually gathered per second, whole job: every launch's
+        gathered edges (source row read and multiply-added; frontier-masked
+        launches count only their live edges) counted on the device over
+        --count-steps steps after the timed region, x steps / wall time of the
+        timed steps (max over ranks). BPR steps/s and the reference-equivalent
+        4*K*E edges per step are reported beside it.
+roofline = the dominant kernel (full-CSR item<-user spmm_kernel): gather-model
+        bytes per launch B = E*(4 + 4 + 4d) + R*(4 + 4d) / its
+        average launch time from HIP events on the launching stream (inside the
+        timed steps on one GPU; over --roofline-steps eager steps after them for
+        sharded / graph-replayed runs). `cache_assisted` flags a gather-model
+        rate above the guide's measured ceiling for random whole-row gathers
+        from HBM (5.8 TB/s): such a rate is served partly by L2 / the Infinity
+        Cache. Step level: the PMC bytes of one whole step (profiles/
+        step_traffic.json, rocprofv3 2*FETCH_SIZE+WRITE_SIZE summed over the
+        step's kernels) / ms_per_step, beside the summed gather-model bytes.
 cpu_baseline = the reference's CPU path (oracle/ref_torch.py: the same torch
         calls) timed on this host on a bounded sample (see "sample").
 """
@@ -42,6 +53,11 @@ from bbgr.synthetic import (CONFIGS, CONFIG_SEED, config_edges, shard_edges_stro
                             shard_edges_weak, synthetic_credibility)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+# MI355X_MICROARCH.md (Infinity Cache section): random whole rows of a buffer far
+# larger than the Infinity Cache, each fetched once, read at 5.5-5.8 TB/s
+# chip-wide (6.3 TB/s for an in-order stream). A gather-model rate above this is
+# cache-assisted: part of the modelled bytes come from L2 / the Infinity Cache.
+HBM_GATHER_CEILING_GBS = 5800.0
 
 
 def log(*a):
@@ -128,60 +144,39 @@ def _cpu_list_text(cpus) -> str:
     return ",".join(out)
 
 
-def numa_local_cpus(n: int) -> list[int]:
-    """Up to n CPUs of this process's affinity set that share one NUMA node
-    (the node holding most of them), so a pinned CPU baseline's threads and
-    first-touch memory stay on one socket."""
-    allowed = os.sched_getaffinity(0)
-    best: list[int] = []
-    base = "/sys/devices/system/node"
-    try:
-        nodes = sorted(x for x in os.listdir(base) if x.startswith("node") and x[4:].isdigit())
-    except OSError:
-        nodes = []
-    for nd in nodes:
-        cpus = []
-        try:
-            text = open(os.path.join(base, nd, "cpulist")).read().strip()
-        except OSError:
-            continue
-        for part in filter(None, text.split(",")):
-            lo, _, hi = part.partition("-")
-            cpus.extend(range(int(lo), int(hi or lo) + 1))
-        mine = [c for c in cpus if c in allowed]
-        if len(mine) > len(best):
-            best = mine
-    return (best or sorted(allowed))[:n]
+def cpu_threads() -> int:
+    """Threads for the CPU baseline: every CPU this process may run on (its
+    affinity set; BASELINE.md §2: torch.set_num_threads(os.cpu_count()), which
+    on a box that restricts affinity is the affinity set)."""
+    return max(1, len(os.sched_getaffinity(0)))
 
 
-def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop", every: int = 16,
-                 reps: int = 5, whole_steps=("C2", "C1"), whole_reps: int = 11,
-                 small_edges: int = 4_000_000):
+def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop",
+                 whole_steps=("C2", "C1"), whole_reps: int = 11,
+                 small_edges: int = 4_000_000, seed: int = 42):
     """The reference's CPU path (oracle/ref_torch.py: the same torch calls as
     Version-2/lighgcn_cu_pop.py:441-450, 482-489, 858-863, lightgcn_cu.py:
-    420-448, 632-652, lightgcn.py:318-349) timed on this host, SURVEY §8(d),
-    for the bench's own variant.
+    420-448, 632-652, lightgcn.py:318-349) timed on this host with every CPU
+    of the process's affinity set, for the bench's variant.
 
     C1 / C2 (small graphs): whole reference steps end to end (sampler loop,
     propagate, loss, backward, Adam), median of `whole_reps` after one warm-up,
     with the run-to-run spread.
 
-    C3 / C4 (50M edges): ONE full forward propagate() over the whole graph
-    (2K torch.sparse.mm, every row; one run: 25-60 s on 16 host cores), plus
-    the backward's products timed on the rows of every `every`-th output
-    vertex (all their edges, the FULL source table gathered) and scaled by
-    edges, torch Adam over all (U+I) x d parameters and the variant's sampler
-    loop on B/`every` users (scaled). Whole reference steps of the same
-    variant at C2 and C1 are timed beside."""
+    C3 / C4 (50M edges): ONE whole reference training step, measured: the
+    variant's per-user sampler loop over the full batch of B users
+    (Version-2:835-849), then loss = bpr(propagate()) (2K torch.sparse.mm over
+    every edge), loss.backward() (autograd's 2K transposed products) and
+    torch.optim.Adam.step() over all (U+I) x d parameters (V2:858-863), each
+    part timed. One run, no warm-up (a step takes minutes of host time); whole
+    reference steps of the same variant at C2 and C1 are timed beside."""
     from oracle import ref_numpy as R
     from oracle import ref_torch as T
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    cores = max(1, min(cores, len(os.sched_getaffinity(0))))
+    cores = cpu_threads()
     torch.set_num_threads(cores)
     U, I, d, K, B = (cfg["num_users"], cfg["num_items"], cfg["emb_dim"], cfg["num_layers"],
                      cfg["batch"])
     E = edges.shape[1]
-    popmix = variant == "v2_pop"
     if E <= small_edges:   # C1 / C2: the whole step, end to end
         med, ts, work = _reference_step_s(cfg_name, variant, whole_reps)
         return {"value": work / med, "unit": "edges/s", "cores": cores, "kind": "port",
@@ -192,86 +187,57 @@ def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop", every: int
                 "whole_step_s": {cfg_name: {"median": med, "runs": ts, "edges_per_s": work / med,
                                             **_spread(ts)}}}
     t_setup = time.perf_counter()
-    torch.manual_seed(42)
-    model, _ = T.reference_model(variant, edges, U, I, d, K, cred)
-    t_setup = time.perf_counter() - t_setup
-    # one full forward propagate() ("one forward for C3/C4")
-    with torch.no_grad():
-        t0 = time.perf_counter()
-        model.finals()
-        t_fwd = time.perf_counter() - t0
-    del model
-    # the backward's products on sampled rows
-    kind = {"cu_fair": "j", "plain": "j"}.get(variant, "gs")
-    if kind == "gs":
-        u, i, w_ui, w_iu = R.gs_values(edges, U, I, cred, method_a=variant == "method_a")
-    else:
-        u, i, w_ui, w_iu, _ = R.j_values(edges, U, I, cred)
-    g = torch.Generator().manual_seed(0)
-    x_u = torch.rand(U, d, generator=g) - 0.5
-    x_i = torch.rand(I, d, generator=g) - 0.5
-    su, si = (u % every) == 0, (i % every) == 0
-    Us, Is = (U + every - 1) // every, (I + every - 1) // every
-    A_b_u = T.coo(i[su], u[su] // every, w_iu[su], (I, Us))       # grad-u rows sampled
-    A_b_i = T.coo(u[si], i[si] // every, w_ui[si], (U, Is))       # grad-i rows sampled
-    e_iu, e_ui = int(si.sum()), int(su.sum())
-    del u, i, w_ui, w_iu, su, si
-
-    def bwd(A, x_s, gy):
-        xs = x_s.clone().requires_grad_()
-        y = torch.sparse.mm(A, xs)
-        t0 = time.perf_counter()
-        y.backward(gy)
-        return time.perf_counter() - t0
-
-    pr = reps + 2   # short (~0.3 s) runs: 2 more steady their medians
-    gi, gu = torch.rand(I, d, generator=g), torch.rand(U, d, generator=g)
-    t_b_u, _ = _median_s(lambda: bwd(A_b_u, x_u[::every].contiguous(), gi), pr)
-    t_b_i, _ = _median_s(lambda: bwd(A_b_i, x_i[::every].contiguous(), gu), pr)
-    del A_b_u, A_b_i, gi, gu
-    s_iu, s_ui = E / max(e_iu, 1), E / max(e_ui, 1)
-    t_bwd = K * (t_b_u * s_ui + t_b_i * s_iu)
-    # torch Adam over every parameter row (the reference's dense gradients)
-    pu, pi = torch.nn.Parameter(x_u), torch.nn.Parameter(x_i)
-    opt = torch.optim.Adam([pu, pi], lr=1e-3)
-    pu.grad, pi.grad = torch.full_like(x_u, 1e-3), torch.full_like(x_i, 1e-3)
-    t_adam, _ = _median_s(opt.step, reps)
-    del opt, pu, pi, x_u, x_i
-    # the variant's per-user sampler loop on B/every users
+    torch.manual_seed(seed)
+    model, popmix = T.reference_model(variant, edges, U, I, d, K, cred)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     indptr, indices = R.edges_to_user_csr(edges, U)
-    pp = R.pop_prob(edges, I)
-    rng = np.random.default_rng(42)
-    nonempty = np.flatnonzero(np.diff(indptr) > 0)
-    n_s = max(1, B // every)
+    pp = R.pop_prob(edges, I) if popmix else None
+    rng = np.random.default_rng(seed)
+    users = rng.permutation(np.flatnonzero(np.diff(indptr) > 0))[:B]
+    t_setup = time.perf_counter() - t_setup
+    # the variant's per-user sampler loop over the whole batch (single thread)
+    t0 = time.perf_counter()
     if popmix:
-        samp = lambda: R.sample_batch_reference_style(  # noqa: E731
-            indptr, indices, rng.choice(nonempty, n_s, replace=False), I, rng, pp)
+        us, ps, ns = R.sample_batch_reference_style(indptr, indices, users, I, rng, pp)
     else:
-        samp = lambda: R.sample_batch_uniform_reference_style(  # noqa: E731
-            indptr, indices, rng.choice(nonempty, n_s, replace=False), I, rng)
-    t_samp, _ = _median_s(samp, reps)
-    t_samp *= B / n_s
-    t_step = t_fwd + t_bwd + t_adam + t_samp
+        us, ps, ns = R.sample_batch_uniform_reference_style(indptr, indices, users, I, rng)
+    t_samp = time.perf_counter() - t0
+    del indptr, indices
+    us, ps, ns = (torch.as_tensor(x) for x in (us, ps, ns))
+    # propagate + BPR loss, backward, Adam: T.train_step split at its parts
+    t0 = time.perf_counter()
+    loss = model.loss(us, ps, ns, 1e-4)
+    t1 = time.perf_counter()
+    opt.zero_grad()
+    loss.backward()
+    t2 = time.perf_counter()
+    opt.step()
+    t3 = time.perf_counter()
+    loss_v = float(loss.item())
+    del loss, opt, model
+    t_fwd, t_bwd, t_adam = t1 - t0, t2 - t1, t3 - t2
+    t_step = t_samp + t_fwd + t_bwd + t_adam
     whole = {n: _reference_step_s(n, variant, whole_reps) for n in whole_steps}
     return {
         "value": 4 * K * E / t_step, "unit": "edges/s", "cores": cores, "kind": "port",
         "bpr_steps_per_s": 1.0 / t_step,
-        "sample": (f"{cfg_name} {variant} step: ONE full forward propagate() {t_fwd:.1f}s "
-                   f"(2K={2 * K} torch.sparse.mm over all {E} edges); backward products from "
-                   f"the rows of every {every}th output vertex, scaled by edges (median of "
-                   f"{pr} after 1 warm-up): grad-u {t_b_u * s_ui:.2f}s, grad-i "
-                   f"{t_b_i * s_iu:.2f}s per layer (x K={K}); torch Adam on {U + I} rows "
-                   f"{t_adam:.2f}s; reference {'pop-mix' if popmix else 'uniform'} sampler "
-                   f"loop {t_samp:.2f}s for B={B} (timed on {n_s} users); est. "
-                   f"{t_step:.1f}s/step. Whole reference steps, median of {whole_reps}: "
+        "sample": (f"ONE whole {cfg_name} {variant} reference step, measured (one run, no "
+                   f"warm-up): {'pop-mix' if popmix else 'uniform'} sampler loop over B={B} "
+                   f"users {t_samp:.1f}s (1 thread), propagate + BPR {t_fwd:.1f}s (2K={2 * K} "
+                   f"torch.sparse.mm over all {E} edges), loss.backward() {t_bwd:.1f}s, torch "
+                   f"Adam over {U + I} rows {t_adam:.2f}s: {t_step:.1f}s/step on {cores} "
+                   f"threads. Whole reference steps, median of {whole_reps}: "
                    + ", ".join(f"{n} {w[0]:.3f}s ({w[2] / w[0] / 1e6:.1f} M edges/s)"
                                for n, w in whole.items())),
         "step_s": t_step,
-        "components_s": {"forward_full": t_fwd, "bwd_grad_u": t_b_u * s_ui * K,
-                         "bwd_grad_i": t_b_i * s_iu * K, "adam": t_adam, "sampler": t_samp},
+        "step_measured": True,
+        "loss": loss_v,
+        "components_s": {"sampler": t_samp, "forward_bpr": t_fwd, "backward": t_bwd,
+                         "adam": t_adam},
         "whole_step_s": {n: {"median": w[0], "runs": w[1], "edges_per_s": w[2] / w[0],
                              **_spread(w[1])} for n, w in whole.items()},
         "setup_s": t_setup,
+        "os_cpu_count": os.cpu_count(),
     }
 
 
@@ -339,13 +305,22 @@ def roofline_groups(timer, counts, steps: int, count_steps: int, n_items: int):
         e["gather_model_bytes"] = gather
         e["gather_model_GBps"] = gather / (e["avg_ms"] * 1e6)
         e["gather_model_frac"] = e["gather_model_GBps"] / HBM_PEAK_GBS
-        e["cache_assisted"] = e["gather_model_frac"] > 1.0
+        e["cache_assisted"] = e["gather_model_GBps"] > HBM_GATHER_CEILING_GBS
         if compulsory is not None:
             e["compulsory_bytes"] = compulsory
             e["compulsory_GBps"] = compulsory / (e["avg_ms"] * 1e6)
             e["compulsory_frac"] = e["compulsory_GBps"] / HBM_PEAK_GBS
         out.append(e)
     return out
+
+
+def step_traffic():
+    """PMC bytes of one whole C4 training step (profiles/step_traffic.json,
+    tools/summarize_profile.py over a tools/profile_box.sh run)."""
+    p = os.path.join(ROOT, "profiles", "step_traffic.json")
+    if not os.path.exists(p):
+        return None
+    return json.load(open(p))
 
 
 def pmc_traffic():
@@ -486,14 +461,6 @@ def main():
     cfg = CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    pinned = None
-    if world == 1 and not args.no_cpu_baseline and not args.sharded:
-        # the CPU baseline's threads on one NUMA node (before any thread pool
-        # exists): on the box's 2-socket host, free-floating threads measured
-        # 83-92 s/step across runs, pinned 78-85 (tools/cpu_baseline_probe.py)
-        want = int(os.environ.get("OMP_NUM_THREADS", "16"))
-        pinned = numa_local_cpus(max(1, want))
-        os.sched_setaffinity(0, pinned)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -753,6 +720,10 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e6) if dom_ms > 0 else 0.0   # GB/s
     spmm_ms_step = sum(g["avg_ms"] * g["launches_per_step"] for g in groups)
     pmc = pmc_traffic() if (args.config == "C4" and world == 1 and not dist_mode) else None
+    stp = step_traffic() if (args.config == "C4" and world == 1 and not dist_mode) else None
+    # every timed launch's gather-model bytes per step (SpMMs incl. the fused
+    # Adam product; the separate item Adam is not an SpMM launch and is left out)
+    step_gather = sum(g["gather_model_bytes"] * g["launches_per_step"] for g in groups)
     steps_per_s = args.steps / elapsed
     if rank != 0:
         if dist_mode:
@@ -763,8 +734,7 @@ def main():
         log("[bench] timing the reference CPU path (bounded sample) ...")
         t_cpu = time.perf_counter()
         cpu = cpu_baseline(edges, cfg, args.config, cred, args.variant)
-        if pinned is not None:
-            cpu["cpus"] = _cpu_list_text(pinned)
+        cpu["cpus"] = _cpu_list_text(os.sched_getaffinity(0))
         log(f"[bench] cpu baseline took {time.perf_counter() - t_cpu:.1f}s")
     torch_ref = None
     if not args.no_torch_reference and not dist_mode and not sharded_gen and not emulate:
@@ -883,7 +853,26 @@ def main():
                                      "PMC, gfx950 correction); counts Infinity-Cache hits",
                      "traffic_source": None if pmc is None else
                      {k: pmc.get(k) for k in ("tag", "commit", "kernel", "avg_us", "dispatches")},
-                     "cache_assisted": achieved > HBM_PEAK_GBS,
+                     "cache_assisted": achieved > HBM_GATHER_CEILING_GBS,
+                     "cache_assisted_rule": "gather-model GB/s above 5800, the guide's "
+                                            "measured rate for random whole-row gathers "
+                                            "from HBM (MI355X_MICROARCH.md)",
+                     "step_gather_model_GBps": step_gather / (1e6 * 1000.0 * elapsed
+                                                              / args.steps),
+                     "step_gather_model_note": "the SpMM launches' gather-model bytes per "
+                                               "step / ms_per_step (zero-reuse model: can "
+                                               "exceed the HBM peak where rows are re-read "
+                                               "from caches)",
+                     "step_traffic_bytes": None if stp is None else
+                     stp["hbm_bytes_per_step_corrected"],
+                     "step_traffic_GBps": None if stp is None else
+                     stp["hbm_bytes_per_step_corrected"] / (1e6 * 1000.0 * elapsed / args.steps),
+                     "step_traffic_frac": None if stp is None else
+                     stp["hbm_bytes_per_step_corrected"] / (1e6 * 1000.0 * elapsed / args.steps)
+                     / HBM_PEAK_GBS,
+                     "step_traffic_source": None if stp is None else
+                     {k: stp.get(k) for k in ("tag", "commit", "steps", "kernel_us_per_step_pmc",
+                                              "source")},
                      "per_kernel": groups},
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},
     }

@@ -269,6 +269,22 @@ def ld(t: torch.Tensor | None) -> int:
     return t.stride(0)
 
 
+def byte_mask(n: int, device) -> torch.Tensor:
+    """A zeroed 1-byte-per-row mask of n rows whose storage covers whole 4-byte
+    words: bbgr_mark_list flags rows with 32-bit atomics on the word holding
+    the byte, so the last row may touch up to 3 bytes past n."""
+    return torch.zeros((int(n) + 3) // 4 * 4, dtype=torch.uint8, device=device)[: int(n)]
+
+
+def check_word_padded(mask: torch.Tensor, n: int, what: str = "mask") -> None:
+    """Refuse a mask for bbgr_mark_list whose storage ends inside the last word."""
+    have = mask.untyped_storage().nbytes() - mask.storage_offset() * mask.element_size()
+    need = (int(n) + 3) // 4 * 4
+    if mask.dtype != torch.uint8 or have < need or mask.data_ptr() % 4:
+        raise ValueError(f"{what}: bbgr_mark_list needs a 4-byte aligned uint8 mask whose "
+                         f"storage covers {need} bytes (have {have}); use _lib.byte_mask")
+
+
 def workspace_query(fn_name: str, *args_before_ws, args_after=()) -> int:
     """Run an entry point in size-query mode (workspace=NULL)."""
     n = c_size_t(0)

@@ -112,6 +112,14 @@ struct Pair {
   Tensor user_map, item_map, user_rank64, item_rank64, item_map64;
   std::vector<Tensor> keep;   // every registered tensor, alive while registered
   mutable Tensor u2i_slots;   // user-CSR slot -> item-CSR slot (built at first use)
+  mutable std::once_flag u2i_once;
+  // the rows backward's frontier buffers, one set per stream (reused: the slot
+  // bitmap is cleared again after each use; frontier_bits / release_bits)
+  struct FrontierBufs {
+    Tensor bits, list, count, ws;
+  };
+  mutable std::mutex fb_mu;
+  mutable std::map<int64_t, FrontierBufs> fb;
 };
 
 static std::mutex g_mu;
@@ -359,8 +367,10 @@ struct Support {
 // search per edge) it needs no column order inside the rows: an input-order
 // pair's rows keep their columns in the caller's id order. One-time per pair.
 static const Tensor &u2i_slots(const Pair &P, const at::Device &dev) {
-  std::lock_guard<std::mutex> g(g_mu);
-  if (!P.u2i_slots.defined()) {
+  // built once per pair under the pair's own flag (not the registry mutex, so
+  // pair_of / workspace lookups on other threads never wait for the sorts);
+  // repeat_interleave is told its output size, so nothing syncs with the host
+  std::call_once(P.u2i_once, [&] {
     const bbgr_csr &uc = P.fu.csr, &ic = P.bi.csr;
     const int64_t nnz = uc.nnz;
     const auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
@@ -369,7 +379,7 @@ static const Tensor &u2i_slots(const Pair &P, const at::Device &dev) {
       auto rows_of = [&](const int32_t *indptr, int64_t n) {
         Tensor ptr = at::from_blob(const_cast<int32_t *>(indptr), {n + 1}, i32);
         Tensor cnt = (ptr.narrow(0, 1, n) - ptr.narrow(0, 0, n)).to(at::kLong);
-        return at::repeat_interleave(cnt);
+        return at::repeat_interleave(cnt, /*output_size=*/nnz);
       };
       Tensor uidx = at::from_blob(const_cast<int32_t *>(uc.indices), {nnz}, i32).to(at::kLong);
       Tensor iidx = at::from_blob(const_cast<int32_t *>(ic.indices), {nnz}, i32).to(at::kLong);
@@ -380,25 +390,28 @@ static const Tensor &u2i_slots(const Pair &P, const at::Device &dev) {
       out.index_put_({sa}, sb.to(at::kInt));
     }
     P.u2i_slots = out;
-  }
+  });
   return P.u2i_slots;
 }
 
-// the flagged rows of mask [n] as an ascending device list + device count
-static std::pair<Tensor, Tensor> mask_list(const Tensor &mask) {
+// the flagged rows of mask [n] as an ascending device list + device count,
+// into the caller's buffers (list >= n rows, count 1, ws grown as needed)
+static void mask_list(const Tensor &mask, Tensor &list, Tensor &cnt, Tensor &ws) {
   const int64_t n = mask.numel();
   const auto i64 = at::TensorOptions().dtype(at::kLong).device(mask.device());
   size_t need = 0;
   check(bbgr_mask_to_list(n, mask.data_ptr<uint8_t>(), nullptr, nullptr, nullptr, &need,
                           cur_stream()),
         "bbgr_mask_to_list (size)");
-  Tensor ws = at::empty({(int64_t)std::max<size_t>(need, 1)}, u8(mask));
-  Tensor list = at::empty({std::max<int64_t>(n, 1)}, i64), cnt = at::empty({1}, i64);
+  if (!ws.defined() || (size_t)ws.numel() < need)
+    ws = at::empty({(int64_t)std::max<size_t>(need, 1)}, u8(mask));
+  if (!list.defined() || list.numel() < std::max<int64_t>(n, 1))
+    list = at::empty({std::max<int64_t>(n, 1)}, i64);
+  if (!cnt.defined()) cnt = at::empty({1}, i64);
   size_t have = (size_t)ws.numel();
   check(bbgr_mask_to_list(n, mask.data_ptr<uint8_t>(), list.data_ptr<int64_t>(),
                           cnt.data_ptr<int64_t>(), ws.data_ptr(), &have, cur_stream()),
         "bbgr_mask_to_list");
-  return {list, cnt};
 }
 
 // BBGR_DROPIN_BITS=0 keeps the mask-only first item product (A/B, tests)
@@ -411,19 +424,41 @@ static bool dropin_bits_enabled() {
 // first backward item product then visits the frontier's rows only and tests
 // edge liveness 64 slots per load, bitwise the mask-only product (the same
 // live edges in the same order; DESIGN §3 "Frontier products")
+// Buffers are per pair and stream and reused: the bitmap is all-zero between
+// uses (release_bits clears the listed users' bits after the chain, as
+// FusedTrainer does), the list / count / hipcub workspace are overwritten. A
+// graph capture gets fresh ones (their zero fill is then part of the graph).
 static void frontier_bits(const Pair &P, Support &s, const Tensor &ui, int64_t d) {
   if (d < 64 || !dropin_bits_enabled() || P.fu.csr.nnz == 0) return;
   const Tensor &slots = u2i_slots(P, ui.device());
-  auto fl = mask_list(s.si_int.defined() ? s.si_int : s.si);
-  s.flist = fl.first;
-  s.fcount = fl.second;
-  s.bits = at::zeros({P.bi.csr.nnz / 32 + 4},
-                     at::TensorOptions().dtype(at::kInt).device(ui.device()));
+  const int64_t nbits = P.bi.csr.nnz / 32 + 4;
+  const auto i32 = at::TensorOptions().dtype(at::kInt).device(ui.device());
+  Pair::FrontierBufs fresh, *b = &fresh;
+  std::unique_lock<std::mutex> g(P.fb_mu, std::defer_lock);
+  if (!capturing()) {
+    g.lock();   // held while this call fills its stream's set (host-side only)
+    b = &P.fb[(int64_t)(intptr_t)cur_stream()];
+  }
+  if (!b->bits.defined()) b->bits = at::zeros({nbits}, i32);
+  mask_list(s.si_int.defined() ? s.si_int : s.si, b->list, b->count, b->ws);
+  s.flist = b->list;
+  s.fcount = b->count;
+  s.bits = b->bits;
   check(bbgr_mark_slots(ui.numel(), ui.data_ptr<int64_t>(), P.fu.csr.indptr,
                         slots.data_ptr<int32_t>(),
                         reinterpret_cast<uint32_t *>(s.bits.data_ptr<int32_t>()), 1,
                         cur_stream()),
         "bbgr_mark_slots");
+}
+
+// clear the listed users' bits again once the chain has read them (stream order)
+static void release_bits(const Pair &P, const Support &s, const Tensor &ui) {
+  if (!s.bits.defined()) return;
+  check(bbgr_mark_slots(ui.numel(), ui.data_ptr<int64_t>(), P.fu.csr.indptr,
+                        P.u2i_slots.data_ptr<int32_t>(),
+                        reinterpret_cast<uint32_t *>(s.bits.data_ptr<int32_t>()), 0,
+                        cur_stream()),
+        "bbgr_mark_slots (clear)");
 }
 
 static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU, const Tensor &gI,
@@ -710,7 +745,9 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
   if (gi_rows && K >= 1) s.gi_rows = ii;
   if (gs && K >= 1 && iu.numel() > 0)
     frontier_bits(*P, s, ru, d);
-  return backward_chain(*P, gU, gI, K, gs, s);
+  auto out = backward_chain(*P, gU, gI, K, gs, s);
+  release_bits(*P, s, ru);
+  return out;
 }
 
 static std::tuple<Tensor, Tensor> jacobi_layer_cuda(const Tensor &u_, const Tensor &i_, int64_t key) {

@@ -588,6 +588,7 @@ class ShardedTrainer(FusedTrainer):
         users = self.next_users()
         B = users.numel()
         f.users = users
+        f.frontier = bool(self.frontier)
         self.sampler.sample(users, f.posneg[:B], f.posneg[B:])
         _all_gather(f.all_items, f.posneg, self.group)
         if not self.frontier:
@@ -644,14 +645,45 @@ class ShardedTrainer(FusedTrainer):
         done.record(side)
         return done
 
-    def step(self) -> torch.Tensor:
+    def pending(self):
+        """The batch already prepared for the next step (users as internal
+        ids), or None. With prefetch on, after a step the sampler counter,
+        epoch and cursor are one batch ahead of step_count: that batch is
+        here, and the next step() trains on it as prepared (a caller that
+        changes batch or frontier settings between steps should drop it
+        with discard_pending() first)."""
+        return None if self._next is None else self._next.users
+
+    def discard_pending(self) -> None:
+        """Forget the prepared batch and clear its masks; the next step()
+        prepares its own (the sampler and the epoch cursor stay where the
+        prepared one left them)."""
         f = self._next
-        if f is None:   # first step: nothing was prepared
+        self._next = None
+        if f is None:
+            return
+        if f.frontier and f.users is not None:   # masks are all-zero between uses
+            call("bbgr_mark_rows", f.users.numel(), ptr(f.users), 0, ptr(f.mask_u), self.U,
+                 stream_handle())
+            f.mask_i.zero_()
+        f.rows = None
+
+    def step(self, prefetch: bool = True) -> torch.Tensor:
+        """One training step. prefetch=False: do not prepare the next step's
+        batch (a caller's last step; no batch is sampled and exchanged that
+        no step trains on)."""
+        if self._next is not None and self._next.frontier != bool(self.frontier):
+            self.discard_pending()   # prepared under the other frontier setting
+        f = self._next
+        if f is None:   # first step (or after discard_pending): nothing prepared
             f = self._fronts[0]
             self._prepare(f)
         nxt = self._fronts[1] if f is self._fronts[0] else self._fronts[0]
-        self._prepare(nxt)   # the next step's batch and frontier (see __init__)
-        self._next = nxt
+        if prefetch:
+            self._prepare(nxt)   # the next step's batch and frontier (see __init__)
+            self._next = nxt
+        else:
+            self._next = None
         self._use(f)
         users, pos, neg = f.users, self.pos, self.neg
         self._last_users = users
@@ -805,14 +837,15 @@ class _Front:
         self.users = None
         self.posneg = torch.empty(2 * B, **i64)
         self.all_items = torch.empty(2 * B_global, **i64)
-        self.mask_u = torch.zeros(U, dtype=torch.uint8, device=dev)
-        self.mask_i = torch.zeros(I, dtype=torch.uint8, device=dev)
+        self.mask_u = _lib.byte_mask(U, dev)
+        self.mask_i = _lib.byte_mask(I, dev)
         self.item_list = torch.empty(max(I, 1), **i64)
         self.item_count = torch.zeros(1, **i64)
         self.positions = torch.zeros(max(I, 1), dtype=torch.int32, device=dev)
         self.offs = torch.zeros(n_bounds, **i64)
         self.offs_host = torch.zeros(n_bounds, dtype=torch.int64).pin_memory()
         self.rows = None   # ItemExchange.list_rows() of the frontier
+        self.frontier = False   # prepared with the frontier masks set
 
 
 class _GlobalItemCsr:

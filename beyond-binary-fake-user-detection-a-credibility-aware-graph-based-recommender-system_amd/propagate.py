@@ -412,9 +412,11 @@ def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw
     if reduce is None:
         spmm(prod, x, first, **kw)
         return
-    for key in ("y_map", "acc_map", "add_map", "src_input"):   # input-order pairs only
-        if kw.pop(key, None):
+    for key in ("y_map", "acc_map", "add_map"):   # input-order pairs only
+        if kw.pop(key, None) is not None:
             raise ValueError("sharded item products take no input-order maps")
+    if kw.pop("src_input", False):
+        raise ValueError("sharded item products take no input-order maps")
     kw.pop("src_bits", None)   # an index-scan shortcut only: the mask alone is exact
     if hasattr(reduce, "item_product"):   # chunked / overlapped exchange
         reduce.item_product(prod, x, first, new, kw)

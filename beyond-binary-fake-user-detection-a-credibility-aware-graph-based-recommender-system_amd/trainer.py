@@ -127,9 +127,9 @@ class FusedTrainer:
         # first backward products skip exact-zero source rows. Loss, gradients
         # and updates are bitwise identical to the dense step (tested).
         self.frontier = resolve_frontier(frontier, graph.item_csr.nnz)
-        self.mask_u = torch.zeros(self.U, dtype=torch.uint8, device=dev)
+        self.mask_u = _lib.byte_mask(self.U, dev)
         # (whole 4-byte words: bbgr_mark_list sets the item bytes by word atomics)
-        self.mask_i = torch.zeros((self.I + 3) // 4 * 4, dtype=torch.uint8, device=dev)[: self.I]
+        self.mask_i = _lib.byte_mask(self.I, dev)
         # The first backward item product reads only the batch users' rows of
         # gU (81k of 50M edges at C4) but would scan every index of its
         # frontier rows (20.6M) to find them: a bitmap over the item-CSR slots
@@ -327,6 +327,7 @@ class FusedTrainer:
         uc = self.graph.user_csr
         lst = getattr(self, "item_list", None)
         if value and lst is not None:   # flag + list the frontier (GS)
+            _lib.check_word_padded(self.mask_i, self.I, "item mask")
             li = (ptr(self.mask_i), self.I, ptr(lst), ptr(self.item_count), st)
             call("bbgr_mark_list", B, ptr(pos), None, None, *li)
             call("bbgr_mark_list", B, ptr(neg), None, None, *li)

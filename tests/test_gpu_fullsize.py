@@ -14,16 +14,23 @@ No assertion compares the GPU with its own intermediates. Checked per config:
   * the drop-in module's final tables (LightGCN.propagate() /
     CredLightGCN.final_embeddings(), i.e. the bbgr::propagate op);
   * the fused training path's forward (degree-ordered graph, the bench layout);
-  * C4: the first fused training step's loss (float64 BPR of the step's batch
-    on the float64 final tables) and grad(u0) / grad(i0) (float64 adjoint chain
-    of that BPR gradient, Version-2:862 autograd).
+  * C3 / C4 / C5: the first fused training step's loss (float64 BPR of the
+    step's batch on the float64 final tables; C3 with the lambda_fair term of
+    lightgcn_cu.py:637-648) and grad(u0) / grad(i0) (float64 adjoint chain of
+    that BPR gradient plus the ego-L2 rows: Version-2:862 / lightgcn_cu.py:650
+    autograd), Jacobi order for C3, Gauss-Seidel for C4 / C5.
 
 Compared rows: random rows of each side, the heaviest rows up to an edge
-budget (the chunked, fixed-order long-row path) and (C4 gradients) the batch
+budget (the chunked, fixed-order long-row path) and (gradients) the batch
 rows. Tolerance: normwise relative <= 1e-5 and max-abs <= 1e-5*max|ref| over
 the compared rows. C5 (500M edges, d=256) runs its float64 chain on 16 of the
-256 columns (propagation acts on each column alone, so those columns are the
-whole chain's; all 256 columns at 500M edges would take ~10 min of host time).
+256 columns (all 256 columns at 500M edges would take ~10 min of host time):
+its u0 / i0 are drawn at full width and then zeroed outside those 16 random
+columns. Propagation acts on each column alone, so the checked columns are
+exactly the full-width chain's; and the BPR dot products then involve only
+those columns, so the float64 loss and gradient of the 16-column chain ARE
+the full-width step's (the other 240 columns of every gradient are 0, also
+checked). The d=256 kernels run unchanged over all 256 columns.
 
   C1  lightgcn.py symmetric path, 943 x 1682, 100K edges, d=64, K=3:
       whole tables against tests/golden/golden_c1.npz (every layer, final,
@@ -191,6 +198,11 @@ def run_full(name, check_grads=False):
     sel_u = sample_rows(chain.deg_u.astype(np.int64), rng, N_SAMPLE, budget)
     sel_i = sample_rows(chain.deg_i.astype(np.int64), rng, N_SAMPLE, budget)
     u0, i0 = device_tables(U, I, d)
+    if cols is not None:   # tables supported on the chain's columns (docstring)
+        off = torch.ones(d, dtype=torch.bool, device=DEV)
+        off[torch.from_numpy(cols).to(DEV)] = False
+        u0[:, off] = 0.0
+        i0[:, off] = 0.0
     u0h, i0h = host_cols(u0, cols), host_cols(i0, cols)
     ruf, ritf, lay_u, lay_i = chain.forward(u0h, i0h, K, order, keep_u=sel_u, keep_i=sel_i)
     _progress(t0, f"{name}: float64 chain done ({'all' if cols is None else len(cols)} columns)")
@@ -227,7 +239,8 @@ def run_full(name, check_grads=False):
     from bbgr.trainer import FusedTrainer
     graph = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
     tr = FusedTrainer(graph, variant, cred=cred, emb_dim=d, num_layers=K,
-                      batch_size=c["batch"], u0=u0, i0=i0, fuse_adam=not check_grads)
+                      batch_size=c["batch"], u0=u0, i0=i0, fuse_adam=not check_grads,
+                      lambda_fair=FAIR.get(name, 0.0))
     del u0, i0
     uf, itf = tr.forward()
     assert_parity(gpu_rows(uf, sel_u, cols), ruf[sel_u], f"{tag} fused forward u_final")
@@ -237,26 +250,35 @@ def run_full(name, check_grads=False):
     if not check_grads:
         return None
     return dict(e=e, U=U, I=I, d=d, K=K, tr=tr, chain=chain, ruf=ruf, ritf=ritf,
-                u0h=u0h, i0h=i0h, rng=rng, budget=budget)
+                u0h=u0h, i0h=i0h, rng=rng, budget=budget, cols=cols, order=order)
 
 
-@pytest.mark.parametrize("name", ["C3", "C5"])
-def test_full_chain_every_layer_and_finals(name):
-    run_full(name)
-    torch.cuda.empty_cache()
+# lambda_fair of the first-step check: lightgcn_cu.py:61 ("set e.g. 1e-2 to
+# enable Eq (3.27)"); the Jacobi family is the only one with the term
+FAIR = {"C3": 1e-2}
 
 
-def test_c4_full_chain_and_first_training_step():
-    """C4 forward as above, then the first fused training step (frontier masks,
-    degree order, B=8192 pop-mix batch): its loss against the float64 BPR
-    (Version-2:495-508) of the step's batch on the float64 final tables, and
-    grad(u0) / grad(i0) on sampled + batch rows against the float64 adjoint
-    chain of that BPR gradient plus the ego-L2 rows."""
+def first_step_grads(name: str):
+    """The config's forward as in run_full, then the first fused training step
+    (frontier masks, degree order, B=8192 batch of the variant's sampler,
+    separate Adam so the weight gradients are kept): its loss against the
+    float64 BPR (Version-2:495-508; + lambda_fair * mean(pop[pos] * s+) with
+    pop = deg_i / max deg_i, lightgcn_cu.py:583-584, 637-648) of the step's
+    batch on the float64 final tables, and grad(u0) / grad(i0) on sampled +
+    batch rows against the float64 adjoint chain of that BPR gradient (the
+    family's own order) plus the ego-L2 rows."""
     from bbgr.trainer import _input_rows
-    w = run_full("C4", check_grads=True)
+    t0 = time.perf_counter()
+    w = run_full(name, check_grads=True)
     tr, chain, U, I, d, K = (w[k] for k in ("tr", "chain", "U", "I", "d", "K"))
-    ruf, ritf, u0h, i0h = w["ruf"], w["ritf"], w["u0h"], w["i0h"]
+    ruf, ritf, u0h, i0h, cols = w["ruf"], w["ritf"], w["u0h"], w["i0h"], w["cols"]
+    lam = FAIR.get(name, 0.0)
+    pop = None
+    if lam:
+        assert tr.pop is not None and tr.lambda_fair == lam
+        pop = chain.deg_i / max(float(chain.deg_i.max()), 1.0)
     loss = float(tr.step())
+    _progress(t0, f"{name}: first fused step done")
     users, pos, neg = (x.cpu().numpy() for x in tr.batch())
     g_u0 = _input_rows(tr.graph.user_order, tr.g_u0)
     g_i0 = _input_rows(tr.graph.item_order, tr.g_i0)
@@ -264,22 +286,41 @@ def test_c4_full_chain_and_first_training_step():
     bi, inv_i = np.unique(np.concatenate([pos, neg]), return_inverse=True)
     B = users.size
     want_loss, g = R.bpr_loss(ruf[bu], ritf[bi], u0h[bu], i0h[bi], inv_u, inv_i[:B],
-                              inv_i[B:], tr.reg)
+                              inv_i[B:], tr.reg, None if pop is None else pop[bi], lam)
     assert abs(loss - want_loss) <= TOL * abs(want_loss), (loss, want_loss)
-    gU = np.zeros((U, d))
-    gI = np.zeros((I, d))
+    dc = u0h.shape[1]
+    gU = np.zeros((U, dc))
+    gI = np.zeros((I, dc))
     gU[bu] = g["g_uf"]
     gI[bi] = g["g_if"]
-    Gu, Gi = chain.backward(gU, gI, K, "gs")
+    Gu, Gi = chain.backward(gU, gI, K, w["order"])
     del gU, gI
     Gu[bu] += g["g_ue"]
     Gi[bi] += g["g_ie"]
+    _progress(t0, f"{name}: float64 adjoint chain done")
     sel_u = sample_rows(chain.deg_u.astype(np.int64), w["rng"], N_SAMPLE, w["budget"],
                         extra=bu[:2000])
     sel_i = sample_rows(chain.deg_i.astype(np.int64), w["rng"], N_SAMPLE, w["budget"],
                         extra=bi[:2000])
-    assert_parity(gpu_rows(g_u0, sel_u), Gu[sel_u], "C4 grad u0")
-    assert_parity(gpu_rows(g_i0, sel_i), Gi[sel_i], "C4 grad i0")
+    assert_parity(gpu_rows(g_u0, sel_u, cols), Gu[sel_u], f"{name} grad u0")
+    assert_parity(gpu_rows(g_i0, sel_i, cols), Gi[sel_i], f"{name} grad i0")
+    if cols is not None:   # the columns off the tables' support carry no gradient
+        off = np.setdiff1d(np.arange(d), cols)
+        for t_, sel, what in ((g_u0, sel_u, "u0"), (g_i0, sel_i, "i0")):
+            assert not np.any(gpu_rows(t_, sel, off)), f"{name} grad {what} off-support columns"
+
+
+@pytest.mark.parametrize("name", ["C3", "C5"])
+def test_full_chain_every_layer_finals_and_first_step_grads(name):
+    first_step_grads(name)
+    torch.cuda.empty_cache()
+
+
+def test_c4_full_chain_and_first_training_step():
+    """C4 forward as in run_full, then the first fused training step (B=8192
+    pop-mix batch): loss and grad(u0) / grad(i0) against the float64 chain."""
+    first_step_grads("C4")
+    torch.cuda.empty_cache()
 
 
 # ---------------------------------------------------------------------------

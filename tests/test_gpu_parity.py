@@ -645,6 +645,11 @@ def test_c2_forward_parity_and_adjoint():
     gU = rng.normal(size=(U, d)).astype(np.float32)
     gI = rng.normal(size=(I, d)).astype(np.float32)
     gu0, gi0 = backward(pair, t(gU), t(gI), K, ORDER_GS)
+    # the backward against the float64 autograd adjoint of the reference chain
+    # (oracle backward_gs: Version-2:482-489 differentiated, V2:862)
+    rgu0, rgi0 = R.backward_gs(M_ui, M_iu, gU, gI, K)
+    assert_parity(gu0, rgu0, "C2 grad u0")
+    assert_parity(gi0, rgi0, "C2 grad i0")
     lhs = (uf.double() * t(gU).double()).sum() + (itf.double() * t(gI).double()).sum()
     rhs = (t(u0).double() * gu0.double()).sum() + (t(i0).double() * gi0.double()).sum()
     assert abs(float(lhs - rhs)) <= 1e-5 * abs(float(lhs))
