@@ -150,4 +150,12 @@ __device__ __forceinline__ long clamp_step(const long *state) {
   return t < 1 ? 1 : (t > n ? n : t);
 }
 
+// The load-balance plan's chunk count of a row of `deg` edges (plan_counts_kernel):
+// 0 for a short row (deg <= thr), else ceil(deg / chunk). Every reader of the
+// plan derives a row's chunking from this one rule (split_row_arrive's chunk
+// index, the slot-bitmap kernel's single-chunk rows).
+__host__ __device__ __forceinline__ int plan_chunks(long deg, int thr, int chunk) {
+  return deg > thr ? (int)((deg + chunk - 1) / chunk) : 0;
+}
+
 }  // namespace bbgr

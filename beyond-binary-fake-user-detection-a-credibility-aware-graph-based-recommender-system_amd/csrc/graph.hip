@@ -76,7 +76,7 @@ __global__ void plan_counts_kernel(int n_rows, const int *indptr, int thr,
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rows) return;
   const int deg = indptr[r + 1] - indptr[r];
-  const int c = deg > thr ? (deg + chunk - 1) / chunk : 0;
+  const int c = plan_chunks(deg, thr, chunk);
   nch[r] = c;
   sflag[r] = c > 1 ? 1 : 0;
 }

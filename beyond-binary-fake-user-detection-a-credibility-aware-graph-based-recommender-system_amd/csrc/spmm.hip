@@ -606,7 +606,10 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
 }
 
 // Fixed-order reduction of the 16 group partials held in LDS; result lands in
-// red[0][*]. Called by all 256 threads.
+// red[0][*]. Called by all 256 threads. It MUST stay a strict left-to-right
+// sum from group 0 (no tree): chunk_row_serial reproduces a single-chunk row
+// bit for bit by adding the live groups' sums in this order and dropping the
+// dead groups' +0.0 terms, which is exact only for a sequential sum.
 template <int D>
 __device__ __forceinline__ void block_reduce16(float4 *red, int g, int lane,
                                                const float4 (&acc)[RowShape<D>::V]) {
@@ -685,7 +688,7 @@ __device__ __forceinline__ void split_row_arrive(const SpmmParams &P, int4 ch, f
   // slot = base + j
   const int eb = P.indptr[ch.x];
   const long len = (long)P.indptr[ch.x + 1] - eb;
-  const int c = (int)((len + P.chunk_edges - 1) / P.chunk_edges);
+  const int c = plan_chunks(len, P.long_threshold, P.chunk_edges);
   const int j = (int)(((long)(ch.y - eb) * c + len - 1) / len);
   const int base = ch.w - j;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -755,10 +758,13 @@ __device__ __forceinline__ void chunk_row_serial(const SpmmParams &P, int eb, in
 }
 
 // Long rows a slot-bitmap launch sums in its short-row groups (chunk_row_serial)
-// instead of chunk workgroups: the rows with a single chunk.
+// instead of chunk workgroups: the rows the plan gives a single chunk (the
+// planner's own rule, plan_chunks), i.e. exactly the rows whose chunk
+// workgroup sums them as one range split 16 ways (tested at deg = thr, thr+1,
+// chunk_edges, chunk_edges+1: test_slot_bitmap_single_chunk_boundary_rows_bitwise).
 template <int D, bool BITS>
 __device__ __forceinline__ bool serial_long(const SpmmParams &P, int len) {
-  if constexpr (BITS && D >= 64) return len <= P.chunk_edges;
+  if constexpr (BITS && D >= 64) return plan_chunks(len, P.long_threshold, P.chunk_edges) == 1;
   return false;
 }
 

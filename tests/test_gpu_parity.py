@@ -1103,6 +1103,47 @@ def test_row_list_with_device_length(bits):
     assert ic.n_chunks > 0 and int((ic.degrees() > ic.chunk_edges).sum()) > 0   # both hub kinds
 
 
+def test_slot_bitmap_single_chunk_boundary_rows_bitwise():
+    """spmm_bits_kernel sums single-chunk hub rows (long_threshold < deg <=
+    chunk_edges) in one lane group (chunk_row_serial) and longer ones in chunk
+    workgroups: rows at both edges of that rule (deg = long_threshold,
+    long_threshold + 1, chunk_edges, chunk_edges + 1, 2 * chunk_edges + 1)
+    must be bitwise the mask-only launch."""
+    from bbgr._lib import call, ptr, stream_handle
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(11)
+    U, d = 9000, 64
+    degs = [64, 65, 2048, 2049, 4097, 40, 3]   # small-graph plan: thr 64, chunk 2048
+    rows = np.concatenate([np.full(k, r) for r, k in enumerate(degs)])
+    cols = np.concatenate([rng.choice(U, k, replace=False) for k in degs])
+    I = len(degs)
+    e = np.stack([cols, rows]).astype(np.int32)   # [users; items]
+    g = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
+    ic = g.item_csr
+    assert ic.long_threshold == 64 and ic.chunk_edges == 2048
+    prod = Product(ic, None, None, None, {})
+    x = torch.zeros(U, d, device=DEV)
+    users = rng.choice(U, 3000, replace=False)
+    x[t(users, torch.int64).long()] = t(rng.standard_normal((3000, d)).astype(np.float32))
+    su = torch.zeros(U, dtype=torch.uint8, device=DEV)
+    su[t(users, torch.int64).long()] = 1
+    rm = torch.ones(I, dtype=torch.uint8, device=DEV)
+    slots = g.user_item_slots()
+    sb = torch.zeros(ic.nnz // 32 + 4, dtype=torch.int32, device=DEV)
+    call("bbgr_mark_slots", users.size, ptr(t(users, torch.int64)), ptr(g.user_csr.indptr),
+         ptr(slots), ptr(sb), 1, stream_handle())
+    ref = torch.full((I, d), 3.0, device=DEV)
+    spmm(prod, x, False, y=ref, src_mask=su, row_mask=rm)
+    lst = torch.arange(I, dtype=torch.int64, device=DEV)
+    cnt = torch.tensor([I], dtype=torch.int64, device=DEV)
+    y = torch.full((I, d), 3.0, device=DEV)
+    spmm(prod, x, False, y=y, row_list=lst, row_count=cnt, src_mask=su, row_mask=rm,
+         src_bits=sb)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert sorted(ic.degrees().cpu().tolist(), reverse=True) == sorted(degs, reverse=True)
+
+
 def test_acc_in_map_reads_acc_in_through_its_own_map():
     """bbgr_spmm_args.acc_in_map: acc_out row acc_map[r] = gamma * (cs*T +
     acc_in[acc_in_map[r]]) — the drop-in chain's first / last layer."""

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of SpMM builds on the GPU box: bench.py with the in-tree libbbgr.so
 # (base) and with each extra library given as an argument (BBGR_LIB).
-# Usage: tools/ab_spmm.sh [path/to/variant/libbbgr.so ...]
+# Usage: tools/probes/ab_spmm.sh [path/to/variant/libbbgr.so ...]
 set -o pipefail
 mkdir -p gpurun_out/ab
 [ -n "$SKIP_TESTS" ] || timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q > gpurun_out/ab/tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/ab/tests.log; exit 1; }

@@ -2,7 +2,7 @@
 user table (5M x 64), HIP-event timed, with the HBM rate of its 28 B/param
 (param, grad, exp_avg, exp_avg_sq in; param, exp_avg, exp_avg_sq out).
 
-    python tools/adam_probe.py [--reps 50]
+    python tools/probes/adam_probe.py [--reps 50]
 """
 from __future__ import annotations
 
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr.optim import adam_step  # noqa: E402

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Build an A/B variant of libbbgr.so with extra -D flags (tools/ab_spmm.sh runs
+# Build an A/B variant of libbbgr.so with extra -D flags (tools/probes/ab_spmm.sh runs
 # bench.py against it through BBGR_LIB). Only spmm.hip is rebuilt; the other
 # objects come from the in-tree build (run build() first).
-# Usage: tools/build_variant.sh <tag> -DFLAG=VALUE ...
+# Usage: tools/probes/build_variant.sh <tag> -DFLAG=VALUE ...
 set -euo pipefail
 TAG=$1; shift
-ROOT=$(cd "$(dirname "$0")/.." && pwd)
+ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 PKG=$(ls -d "$ROOT"/beyond-binary-*_amd)
 OUT=$PKG/lib/ab/$TAG
 mkdir -p "$OUT"

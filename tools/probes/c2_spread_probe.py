@@ -1,7 +1,7 @@
 """Probe: run-to-run spread of the whole C2 reference step (bench.py
 cpu_baseline) under different host-thread settings, pinned to one NUMA node.
 
-    python tools/c2_spread_probe.py [--reps 11]
+    python tools/probes/c2_spread_probe.py [--reps 11]
 
 One JSON line per setting: median, IQR / median, (max - min) / median."""
 from __future__ import annotations
@@ -14,7 +14,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 argv, sys.argv = sys.argv, ["bench.py"]
 import bench  # noqa: E402

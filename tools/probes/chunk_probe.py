@@ -5,7 +5,7 @@ one workgroup each; a chunk's 16 lane groups walk its edges in 16-edge
 batches, so a big chunk is a long dependent chain. On a small graph the few
 hot rows' chunks are the kernel's critical path.
 
-    python tools/chunk_probe.py [--config C2] [--chunks 2048,1024,512,256]
+    python tools/probes/chunk_probe.py [--config C2] [--chunks 2048,1024,512,256]
 """
 from __future__ import annotations
 
@@ -17,7 +17,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr.graph import BipartiteGraph  # noqa: E402

@@ -5,7 +5,7 @@ row's columns (a) in ascending internal (degree-rank) id — the trainer's CSR
 the input-order graph's edge order. Also the middle item product. HIP events
 over repeated launches.
 
-    python tools/colorder_probe.py [--reps 20]
+    python tools/probes/colorder_probe.py [--reps 20]
 """
 from __future__ import annotations
 
@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr._lib import OP_GS  # noqa: E402

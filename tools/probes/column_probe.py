@@ -2,7 +2,7 @@
 alone on one GPU: the per-rank work of an N-GPU column-sharded step) on a
 BASELINE config, across long-row thresholds of the shared graph.
 
-    python tools/column_probe.py [--config C4] [--parts 2,4,8] [--thresholds 256,64,32]
+    python tools/probes/column_probe.py [--config C4] [--parts 2,4,8] [--thresholds 256,64,32]
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr.columns import ColumnShardedTrainer  # noqa: E402

@@ -2,7 +2,7 @@
 host, with the process free to run on any CPU (the default) or pinned to the
 first N CPUs of one NUMA node (--pin).
 
-    python tools/cpu_baseline_probe.py [--runs 3] [--pin 0|16]
+    python tools/probes/cpu_baseline_probe.py [--runs 3] [--pin 0|16]
 """
 from __future__ import annotations
 
@@ -12,7 +12,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from bbgr.synthetic import CONFIGS, CONFIG_SEED, config_edges, synthetic_credibility  # noqa: E402

@@ -4,7 +4,7 @@ launch copies or elementwise kernels besides the bbgr operators. One step on
 a mid-size Zipf graph under torch.profiler; prints the aten ops with their
 parent chain and input shapes.
 
-    python tools/dropin_ops_probe.py
+    python tools/probes/dropin_ops_probe.py
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ import sys
 import torch
 from torch.profiler import ProfilerActivity, profile
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr import lightgcn_cu_pop as V2  # noqa: E402

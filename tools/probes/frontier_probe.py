@@ -10,7 +10,7 @@ HIP events over repeated launches, in forms that give the same rows:
 
 Each form's frontier rows are checked bitwise against mask_nobits.
 
-    python tools/frontier_probe.py [--reps 50]
+    python tools/probes/frontier_probe.py [--reps 50]
 """
 from __future__ import annotations
 
@@ -22,7 +22,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr._lib import call, ptr, stream_handle  # noqa: E402

@@ -7,7 +7,7 @@ over RCCL with a few exchange_parts values):
   step_ms   wall time per step over a synced loop.
 If issue_ms approaches step_ms the GPU starves between launches.
 
-    python tools/host_probe.py [--parts 8,2]
+    python tools/probes/host_probe.py [--parts 8,2]
 """
 from __future__ import annotations
 
@@ -19,7 +19,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 import bbgr  # noqa: E402,F401

@@ -2,7 +2,7 @@
 degree order (graph.HOT_BYTES and the rows/8 cap), on one C4 trainer. The
 rule is swapped between runs on the same trainer (it is evaluated per launch).
 
-    python tools/hot_probe.py [--steps 15]
+    python tools/probes/hot_probe.py [--steps 15]
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr import graph as G  # noqa: E402

@@ -8,7 +8,7 @@ range c's all-reduce overlaps range c+1's SpMM. This times one item product:
            async collective puts on the compute stream)
   rccl     + an async all-reduce of the range (world size 1 over RCCL)
 
-    python tools/range_probe.py [--parts 8]
+    python tools/probes/range_probe.py [--parts 8]
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ import time
 import torch
 import torch.distributed as dist
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 import bbgr  # noqa: E402,F401

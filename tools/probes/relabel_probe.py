@@ -7,7 +7,7 @@ each table into one address range. The step is permutation-equivariant, so
 only the time changes. (The streamed-cold-row A/B of DESIGN §3 ran an earlier
 form of this probe with the stream threshold set per run.)
 
-    python tools/relabel_probe.py [--steps 10] [--modes none,items,users,both]
+    python tools/probes/relabel_probe.py [--steps 10] [--modes none,items,users,both]
 """
 from __future__ import annotations
 
@@ -20,7 +20,7 @@ import time
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 import bbgr  # noqa: E402,F401

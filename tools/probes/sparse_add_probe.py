@@ -2,7 +2,7 @@
 (how the drop-in's sparse ego-L2 rows reach .grad), uncoalesced vs marked
 coalesced, at the C4 table sizes, with the kernels each launches.
 
-    python tools/sparse_add_probe.py
+    python tools/probes/sparse_add_probe.py
 """
 import torch
 from torch.profiler import ProfilerActivity, profile

@@ -2,7 +2,7 @@
 (single-GPU trainer, and the sharded trainer at world 1 over RCCL), to tell
 steady per-step cost from occasional stalls.
 
-    python tools/step_times.py [--steps 30]
+    python tools/probes/step_times.py [--steps 30]
 """
 from __future__ import annotations
 
@@ -16,7 +16,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import torch  # noqa: E402
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr.graph import BipartiteGraph  # noqa: E402
