@@ -171,6 +171,7 @@ _SIGNATURES = {
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
     "bbgr_mark_slots": ([c_int64, _P, _P, _P, _P, c_int32, _P], c_int32),
     "bbgr_mark_list": ([c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P], c_int32),
+    "bbgr_slots_from_perms": ([c_int64, _P, _P, _P, _P, _P], c_int32),
     "bbgr_transpose_slots": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(CsrStruct), _P, _P],
                              c_int32),
     "bbgr_mark_neighbors_of_mask": ([c_int64, _P, _P, _P, _P, ctypes.c_uint8, _P, _P],

@@ -326,10 +326,24 @@ __global__ void degree_count_kernel(long n, const int *ids, int *deg) {
 // of one XCD and a power-law id (one item holds ~1 % of a Zipf graph's edges)
 // sees 1/8 of the same-address traffic; a second pass sums the copies.
 constexpr int DEG_COPIES = 8;
+// One atomic per RUN of equal ids in a wave instead of one per id: edge lists
+// grouped by one endpoint (a user's edges together, as ingested) made a wave's
+// 64 atomics hit a handful of counters, serialised at L2. A lane opens a run
+// where its id differs from the previous lane's; the run's first lane adds the
+// run length (integers: the counts are exact in any order).
 __global__ void degree_count_copies_kernel(long n, const int *ids, int n_bins, int *copies) {
   int *mine = copies + (long)(blockIdx.x % DEG_COPIES) * n_bins;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < n) atomicAdd(mine + ids[e], 1);
+  const int lane = threadIdx.x & 63;
+  const int id = e < n ? ids[e] : -1;
+  const int prev = __shfl(id, lane > 0 ? lane - 1 : 0);
+  const bool start = lane == 0 || id != prev;
+  const unsigned long long starts = __ballot(start);
+  if (start && id >= 0) {
+    const unsigned long long later = lane < 63 ? starts >> (lane + 1) : 0ull;
+    const int end = later ? lane + __ffsll((long long)later) : 64;   // next run's first lane
+    atomicAdd(mine + id, end - lane);
+  }
 }
 
 __global__ void degree_sum_copies_kernel(int n_bins, const int *copies, int *deg) {
@@ -693,6 +707,32 @@ extern "C" int bbgr_transpose_slots(const bbgr_csr *a, const bbgr_csr *b, int32_
                      0, as_stream(stream), (int)a->n_rows, a->indptr, a->indices, b->indptr,
                      b->indices, out);
   BBGR_LAUNCHED("transpose_slots_kernel");
+  return BBGR_OK;
+}
+
+__global__ void invert_slots_kernel(long n, const int *perm, int *inv) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) inv[perm[t]] = (int)t;
+}
+
+__global__ void compose_slots_kernel(long n, const int *perm_a, const int *inv_b, int *out) {
+  const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) out[s] = inv_b[perm_a[s]];
+}
+
+extern "C" int bbgr_slots_from_perms(int64_t nnz, const int32_t *perm_a, const int32_t *perm_b,
+                                     int32_t *out, int32_t *scratch, bbgr_stream_t stream) {
+  BBGR_REQUIRE(nnz >= 0 && nnz < 2147483647LL, "bbgr_slots_from_perms: nnz out of range");
+  if (nnz == 0) return BBGR_OK;
+  BBGR_REQUIRE(perm_a && perm_b && out && scratch, "bbgr_slots_from_perms: null arrays");
+  BBGR_REQUIRE(out != scratch, "bbgr_slots_from_perms: out and scratch alias");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(invert_slots_kernel, dim3(blocks_for(nnz)), dim3(256), 0, st, (long)nnz,
+                     perm_b, scratch);
+  BBGR_LAUNCHED("invert_slots_kernel");
+  hipLaunchKernelGGL(compose_slots_kernel, dim3(blocks_for(nnz)), dim3(256), 0, st, (long)nnz,
+                     perm_a, scratch, out);
+  BBGR_LAUNCHED("compose_slots_kernel");
   return BBGR_OK;
 }
 

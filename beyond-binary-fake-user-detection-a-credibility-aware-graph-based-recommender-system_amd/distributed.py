@@ -24,6 +24,16 @@ SURVEY §8(e). The reference is single-device; this is the build's scale-out:
     only the frontier rows (compacted), not the whole item table.
   * the user Adam runs fused in the last (purely local) backward product and
     the item Adam reads the sparse item gradient, exactly as on one GPU.
+  * item ownership (GS, fused Adam): every rank holds the whole item weight
+    table but OWNS an equal contiguous range of item rows (internal order): it
+    keeps the Adam moments of those rows only and runs the item Adam on them
+    (1/N of the replicated pass). A GS step reads the item weights at the
+    global batch items only (the layer-mean start and the ego-L2 term; the
+    first item product reads user rows), so after the Adam each rank's rows
+    of the NEXT step's batch items (prepared one step ahead) are refreshed
+    from their owners: one all-gather of 2*B_global rows, each row copied
+    from its owner's slot (bit-exact). sync_items() makes the whole table
+    current (eval, state_dict).
 
 Two ways to build the shards:
   ShardedTrainer.from_global_edges(edges, U, I, ...)   strong scaling: one
@@ -356,7 +366,8 @@ class ShardedTrainer(FusedTrainer):
                  frontier="auto", exchange_parts: int = 4, fuse_adam: bool = True,
                  sparse_exchange: bool = True, vertex_order: str = "input",
                  frontier_parts: int = 2, native_comm: bool = False,
-                 overlap_item_adam: bool | None = None, column_chains: int = 1):
+                 overlap_item_adam: bool | None = None, column_chains: int = 1,
+                 own_items: bool = True):
         """local_edges: int32 [2, E_local] with LOCAL user ids; cred / u0: rows of
         this rank's users; i0: the full (replicated) item table; batch_size:
         users per step on THIS rank. vertex_order="degree": local users by
@@ -364,7 +375,8 @@ class ShardedTrainer(FusedTrainer):
         column_chains=C > 1: the propagation runs as C independent chains over
         d/C-column slices of the tables, each on its own stream, their issue
         interleaved one exchange at a time (_interleave), so one chain's SpMMs
-        overlap the other's item all-reduces."""
+        overlap the other's item all-reduces. own_items: item rows owned by
+        ranks (module docstring; GS fused only)."""
         _lib.require_gpu()
         if variant not in VARIANTS:
             raise ValueError(f"unknown variant {variant!r}")
@@ -432,7 +444,17 @@ class ShardedTrainer(FusedTrainer):
         self.B_global = self.B_local * self.world
         z = lambda n: torch.zeros(n, emb_dim, **f32)  # noqa: E731
         self.m_u, self.v_u = z(num_local_users), z(num_local_users)
-        self.m_i, self.v_i = z(num_items), z(num_items)
+        self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
+        # item ownership (module docstring): GS with the fused Adam only (the
+        # Jacobi order reads the whole item weight table in its first user
+        # product, and the unfused path keeps whole gradient tables)
+        self.own_items = self.fuse_adam and bool(own_items)
+        self.item_bounds = [num_items * r // self.world for r in range(self.world + 1)]
+        self.ia, self.ib = ((self.item_bounds[self.rank], self.item_bounds[self.rank + 1])
+                            if self.own_items else (0, num_items))
+        self.m_i, self.v_i = z(self.ib - self.ia), z(self.ib - self.ia)
+        self._bounds_t = torch.tensor(self.item_bounds[1:-1], dtype=torch.int64, device=dev)
+        self._items_stale = False   # some rows of item_w lag their owner's
         self.uf, self.itf = z(num_local_users), z(num_items)
         self.g_uf, self.g_if = z(num_local_users), z(num_items)   # all-zero between steps
         self.g_u0, self.g_i0 = z(num_local_users), z(num_items)
@@ -456,7 +478,6 @@ class ShardedTrainer(FusedTrainer):
         self.perm = None
         # one decision for every rank: the size rule on the GLOBAL edge count
         self.frontier = resolve_frontier(frontier, int(indptr_i[-1]))
-        self.fuse_adam = bool(fuse_adam) and order == ORDER_GS and num_layers >= 1
         self.dev_state = None   # host step scalars (the sharded step is not graph-captured)
         # GS item Adam on a side stream beside the backward chain: its gradient
         # (gI/(K+1) + ego rows) is final once the all-gathered BPR rows are
@@ -575,7 +596,7 @@ class ShardedTrainer(FusedTrainer):
         self.posneg, self.all_items = f.posneg, f.all_items
         B = f.posneg.numel() // 2
         self.pos, self.neg = f.posneg[:B], f.posneg[B:]
-        self.mask_u, self.mask_i = f.mask_u, f.mask_i
+        self.mask_u, self.mask_i, self.mask_b = f.mask_u, f.mask_i, f.mask_b
         self.item_list, self.item_count = f.item_list, f.item_count
 
     def _prepare(self, f: "_Front") -> None:
@@ -591,11 +612,14 @@ class ShardedTrainer(FusedTrainer):
         f.frontier = bool(self.frontier)
         self.sampler.sample(users, f.posneg[:B], f.posneg[B:])
         _all_gather(f.all_items, f.posneg, self.group)
+        f.items_fresh = False
         if not self.frontier:
             return
         st = stream_handle()
         call("bbgr_mark_rows", B, ptr(users), 1, ptr(f.mask_u), self.U, st)
         call("bbgr_mark_rows", 2 * B, ptr(f.posneg), 1, ptr(f.mask_i), self.I, st)
+        call("bbgr_mark_rows", f.all_items.numel(), ptr(f.all_items), 1, ptr(f.mask_b),
+             self.I, st)
         if self.order == ORDER_GS:
             uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), 1,
@@ -645,6 +669,78 @@ class ShardedTrainer(FusedTrainer):
         done.record(side)
         return done
 
+    def _item_adam(self, item_rows, g, a_gl: float, gl: float) -> None:
+        """GS item Adam (FusedTrainer._item_adam) on this rank's OWNED item rows
+        (all rows without item ownership); the rows of the other ranks go stale
+        here until refreshed (_refresh_items / sync_items)."""
+        if not self.own_items:
+            super()._item_adam(item_rows, g, a_gl, gl)
+            return
+        st = stream_handle()
+        call("bbgr_rows_axpy", item_rows.numel(), ptr(item_rows), a_gl, ptr(self.item_w),
+             ld(self.item_w), ptr(g), ld(g), self.d, st)
+        a, b = self.ia, self.ib
+        if b > a:
+            adam_step(self.item_w[a:b], g[a:b], self.m_i, self.v_i, self.step_count, self.lr,
+                      grad_scale=gl)
+        self._items_stale = self.world > 1
+
+    def _owner_rows(self, rows: torch.Tensor) -> torch.Tensor:
+        """The owning rank of each item row (internal id)."""
+        return torch.searchsorted(self._bounds_t, rows, right=True)
+
+    def _refresh_items(self, rows: torch.Tensor) -> None:
+        """item_w[rows] <- the owners' current values (item ownership): one
+        all-gather of every rank's item_w[rows], then each row copied from its
+        owner's slot (exact copies; duplicate rows write the same value)."""
+        if not self._items_stale or rows.numel() == 0:
+            return
+        n, W = rows.numel(), self.world
+        mine = self.item_w.index_select(0, rows)
+        got = torch.empty(W * n, self.d, dtype=torch.float32, device=self.device)
+        _all_gather(got, mine, self.group)
+        pick = self._owner_rows(rows) * n + torch.arange(n, device=self.device)
+        self.item_w.index_copy_(0, rows, got.index_select(0, pick))
+
+    def _gather_owned(self, t: torch.Tensor) -> torch.Tensor:
+        """The whole [I, d] table from every rank's owned slice t ([ib-ia, d])."""
+        W, d = self.world, self.d
+        m = max(self.item_bounds[r + 1] - self.item_bounds[r] for r in range(W))
+        pad = torch.zeros(m, d, dtype=torch.float32, device=self.device)
+        pad[: t.shape[0]] = t
+        got = torch.empty(W * m, d, dtype=torch.float32, device=self.device)
+        _all_gather(got, pad, self.group)
+        return torch.cat([got[r * m: r * m + self.item_bounds[r + 1] - self.item_bounds[r]]
+                          for r in range(W)])
+
+    def sync_items(self) -> dict:
+        """Collective (every rank calls it): make the whole item weight table
+        current on this rank and return the item tables by internal row:
+        {"item_w", "m_i", "v_i"} (the Adam moments gathered from their owners).
+        Without item ownership the local tables are returned as they are."""
+        if not self.own_items or self.world == 1:
+            return {"item_w": self.item_w, "m_i": self.m_i, "v_i": self.v_i}
+        a, b = self.ia, self.ib
+        self.item_w.copy_(self._gather_owned(self.item_w[a:b].contiguous()))
+        self._items_stale = False
+        return {"item_w": self.item_w, "m_i": self._gather_owned(self.m_i),
+                "v_i": self._gather_owned(self.v_i)}
+
+    def forward(self):
+        """Final (layer-mean) tables of the rank's users and of every item,
+        rows by input id (collective: the item sums are exchanged)."""
+        self.sync_items()
+        uf, itf = forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
+                          out_i=self.itf, ws=self.ws, reduce=self.exchange)
+        from .trainer import _input_rows
+        return _input_rows(self.graph.user_order, uf), _input_rows(self.graph.item_order, itf)
+
+    def state_dict(self) -> dict:
+        """Reference keys (Version-2:903) of this rank's user rows and every
+        item row, by input id (collective)."""
+        self.sync_items()
+        return super().state_dict()
+
     def pending(self):
         """The batch already prepared for the next step (users as internal
         ids), or None. With prefetch on, after a step the sampler counter,
@@ -665,6 +761,8 @@ class ShardedTrainer(FusedTrainer):
         if f.frontier and f.users is not None:   # masks are all-zero between uses
             call("bbgr_mark_rows", f.users.numel(), ptr(f.users), 0, ptr(f.mask_u), self.U,
                  stream_handle())
+            call("bbgr_mark_rows", f.all_items.numel(), ptr(f.all_items), 0, ptr(f.mask_b),
+                 self.I, stream_handle())
             f.mask_i.zero_()
         f.rows = None
 
@@ -685,6 +783,9 @@ class ShardedTrainer(FusedTrainer):
         else:
             self._next = None
         self._use(f)
+        if not f.items_fresh:   # (prepared now, or the last step had no prefetch)
+            self._refresh_items(f.all_items)
+            f.items_fresh = True
         users, pos, neg = f.users, self.pos, self.neg
         self._last_users = users
         B = users.numel()
@@ -693,7 +794,8 @@ class ShardedTrainer(FusedTrainer):
         if f.rows is not None:
             for ex in self._exchanges():
                 ex.use_rows(f.rows)
-        final_rows = None if masks is None else (masks[0], masks[1], users)
+        final_rows = None if masks is None else (masks[0], masks[1], users, None,
+                                                 self.mask_b)
         if self.chains:
             self._forward_chains(final_rows)
         else:
@@ -736,7 +838,12 @@ class ShardedTrainer(FusedTrainer):
              ld(self.g_if), self.d, st)
         if masks is not None:
             call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), self.U, st)
+            call("bbgr_mark_rows", self.all_items.numel(), ptr(self.all_items), 0,
+                 ptr(self.mask_b), self.I, st)
             self.mask_i.zero_()
+        if self._next is not None:   # owners' rows of the next step's batch items
+            self._refresh_items(self._next.all_items)
+            self._next.items_fresh = True
         f.rows = None
         for ex in self._exchanges():
             ex.clear_rows()
@@ -846,6 +953,10 @@ class _Front:
         self.offs_host = torch.zeros(n_bounds, dtype=torch.int64).pin_memory()
         self.rows = None   # ItemExchange.list_rows() of the frontier
         self.frontier = False   # prepared with the frontier masks set
+        # every rank's batch items: the item rows whose final value is read
+        # (the item layer-mean accumulator is formed there only)
+        self.mask_b = _lib.byte_mask(I, dev)
+        self.items_fresh = False   # item_w current at all_items (item ownership)
 
 
 class _GlobalItemCsr:

@@ -359,11 +359,23 @@ class BipartiteGraph:
                     call("bbgr_relabel", c.nnz, ptr(c._input_indices), ptr(order.rank),
                          ptr(c.indices), stream_handle())
             u, i = u_int, i_int
+        self._u2i_slots = None
         if not (vertex_order == "degree" and input_col_order):
             self.user_csr = Csr(u, i, num_users, num_items, device,
-                                long_threshold=long_threshold, chunk_edges=chunk_edges)
+                                long_threshold=long_threshold, chunk_edges=chunk_edges,
+                                keep_perm=True)
             self.item_csr = Csr(i, u, num_items, num_users, device,
-                                long_threshold=long_threshold, chunk_edges=chunk_edges)
+                                long_threshold=long_threshold, chunk_edges=chunk_edges,
+                                keep_perm=True)
+            # the user-CSR slot -> item-CSR slot map from the two builds' sort
+            # permutations over the same edge list (user_item_slots); the
+            # permutations themselves are dropped
+            self._u2i_slots = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=device)
+            scratch = torch.empty_like(self._u2i_slots)
+            call("bbgr_slots_from_perms", self.nnz, ptr(self.user_csr.perm),
+                 ptr(self.item_csr.perm), ptr(self._u2i_slots), ptr(scratch), stream_handle())
+            del scratch
+            self.user_csr.perm = self.item_csr.perm = None
         if vertex_order == "degree":
             users_ordered = items_ordered = True
         else:
@@ -398,10 +410,11 @@ class BipartiteGraph:
 
     def user_item_slots(self) -> torch.Tensor:
         """int32 [nnz]: for every user-CSR slot, the item-CSR slot of the same
-        edge (bbgr_transpose_slots; built once). Feeds the slot bitmap of a
-        batch's user edges (bbgr_mark_slots -> bbgr_spmm_args.src_bits)."""
-        t = self.__dict__.get("_u2i_slots")
-        if t is None:
+        edge (bbgr_slots_from_perms at the CSR build; bbgr_transpose_slots for
+        other builds). Feeds the slot bitmap of a batch's user edges
+        (bbgr_mark_slots -> bbgr_spmm_args.src_bits)."""
+        t = self._u2i_slots   # (built with the CSRs; the input-column-order build
+        if t is None:          # falls back to a binary search per edge)
             if not (self.user_csr.cols_sorted and self.item_csr.cols_sorted):
                 raise ValueError("user_item_slots needs column-sorted CSR rows")
             t = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=self.device)

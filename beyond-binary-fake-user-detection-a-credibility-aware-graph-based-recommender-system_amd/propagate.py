@@ -471,15 +471,18 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
     each exchange point), so the caller can interleave the issue of several
     chains (ShardedTrainer column chains); `drain()` / `forward()` run it whole.
     `reduce(t)`: in-place sum over ranks of item-row partial sums (sharded mode).
-    `final_rows=(user_mask, item_mask[, user_list[, (item_list, item_count)]])`:
-    only the flagged rows of the final
+    `final_rows=(user_mask, item_mask[, user_list[, (item_list, item_count)[,
+    item_acc_mask]]])`: only the flagged rows of the final
     tables are needed (a training step reads batch rows only). The last layer
     then computes only those rows; the item mask must cover every item the
     flagged users' last-layer rows read (GS: N(batch users) and the batch
     items; Jacobi: the batch items). Flagged rows are bitwise identical to a
     full pass; the others are left stale. The item list (GS, no `reduce`):
     item_mask's rows with their count in device memory (bbgr_mark_list) — the
-    last item product visits them instead of testing every row's mask byte."""
+    last item product visits them instead of testing every row's mask byte.
+    `item_acc_mask`: the item rows whose FINAL value is read (the batch items;
+    default item_mask): the item layer-mean accumulator is formed on those
+    rows only (item_mask must cover them)."""
     U, I = pair.num_users, pair.num_items
     d = u0.shape[1]
     _check_table("user table", u0, U, d)
@@ -494,8 +497,10 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
     gl = 1.0 / (K + 1)
     FI, FU = pair.fwd_item, pair.fwd_user
     new = _buffers(ws, u0.device, d)
-    mu, mi, ulist, ilist = ((tuple(final_rows) + (None, None))[:4] if final_rows is not None
-                            else (None,) * 4)
+    mu, mi, ulist, ilist, ami = ((tuple(final_rows) + (None, None, None))[:5]
+                                 if final_rows is not None else (None,) * 5)
+    if ami is None:
+        ami = mi
     io = pair.io   # input-order tables over a degree-ordered graph (set_input_order)
     if io is not None and (reduce is not None or final_rows is not None):
         raise ValueError("an input-order pair takes neither a reduce hook nor final_rows")
@@ -514,7 +519,7 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
             _item_product(FI, u0 if k == 1 else bufU, k == 1, reduce, new, y=bufI,
                           y_scale=pair.feed_fwd_iu, acc_in=i0 if k == 1 else acc_i,
                           acc_out=acc_i, acc_scale=FI.out_scale, gamma=g,
-                          row_mask=mi if last else None, acc_mask=mi, acc_map=am_i,
+                          row_mask=mi if last else None, acc_mask=ami, acc_map=am_i,
                           src_input=io is not None and k == 1, **(il if last else {}))
             yield
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
@@ -532,7 +537,7 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
                           y=bufI[nxt] if k < K else None, y_scale=pair.feed_fwd_iu,
                           acc_in=i0 if k == 1 else acc_i, acc_out=acc_i,
                           acc_scale=FI.out_scale, gamma=g, row_mask=mi if last else None,
-                          acc_mask=mi, acc_map=am_i, src_input=io is not None and k == 1)
+                          acc_mask=ami, acc_map=am_i, src_input=io is not None and k == 1)
             yield
             spmm(FU, i0 if k == 1 else bufI[cur], k == 1,
                  y=bufU[nxt] if k < K else None, y_scale=pair.feed_fwd_ui,

@@ -104,6 +104,14 @@ int bbgr_csr_plan_build(const bbgr_csr *csr, int32_t *chunks, int32_t *split,
 /* to the k-th copy). One-time; feeds bbgr_mark_slots.                         */
 int bbgr_transpose_slots(const bbgr_csr *a, const bbgr_csr *b, int32_t *out,
                          bbgr_stream_t stream);
+/* The same map from the two CSR builds' permutations (bbgr_csr_build's      */
+/* perm_out of a and of b over ONE edge list: slot -> edge id): out[s] =      */
+/* inv(perm_b)[perm_a[s]]. Two O(nnz) passes instead of a binary search per   */
+/* edge; equal to bbgr_transpose_slots (the builds' sorts are stable, so the  */
+/* k-th copy of a duplicate pair is the k-th in edge order on both sides).    */
+/* scratch: nnz int32, distinct from out.                                     */
+int bbgr_slots_from_perms(int64_t nnz, const int32_t *perm_a, const int32_t *perm_b,
+                          int32_t *out, int32_t *scratch, bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Vertex order (a one-time relabelling before the CSR build)                 */

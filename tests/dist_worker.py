@@ -53,6 +53,7 @@ def main():
                             user_offset=rank * WEAK_U, frontier=frontier, exchange_parts=2,
                             fuse_adam=False, vertex_order=order)
     loss = float(tr.step())
+    tr.sync_items()                        # item rows owned elsewhere made current
     users, pos, neg = tr.batch()           # input (local) ids
     go, gi = tr.graph.user_order, tr.graph.item_order
 
@@ -87,9 +88,10 @@ def fused_vs_separate(out_dir, variant):
                                 sparse_exchange=sparse)
             losses = [float(tr.step()) for _ in range(3)]
             tag = f"{'fused' if fuse else 'sep'}_{'sparse' if sparse else 'dense'}"
+            items = tr.sync_items()   # (item ownership: rows and moments from the owners)
             out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
-            out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
-            out[f"{tag}_m_i"] = tr.m_i.cpu().numpy()
+            out[f"{tag}_item_w"] = items["item_w"].cpu().numpy()
+            out[f"{tag}_m_i"] = items["m_i"].cpu().numpy()
             out[f"{tag}_loss"] = np.array(losses)
             out[f"{tag}_fused"] = np.array(tr.fuse_adam)
     # the item Adam in the chain instead of on the side stream (world 2
@@ -98,10 +100,21 @@ def fused_vs_separate(out_dir, variant):
                         device="cuda:0", u0=u0, i0=i0, user_offset=rank * WEAK_U,
                         exchange_parts=2, fuse_adam=True, frontier=True, overlap_item_adam=False)
     losses = [float(tr.step()) for _ in range(3)]
+    items = tr.sync_items()
     out["inchain_user_w"] = tr.user_w.cpu().numpy()
-    out["inchain_item_w"] = tr.item_w.cpu().numpy()
-    out["inchain_m_i"] = tr.m_i.cpu().numpy()
+    out["inchain_item_w"] = items["item_w"].cpu().numpy()
+    out["inchain_m_i"] = items["m_i"].cpu().numpy()
     out["inchain_loss"] = np.array(losses)
+    # the replicated item Adam (own_items=False): every rank updates every item
+    # row; bitwise the owned-rows step after the owners' rows are gathered
+    tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3, batch_size=32,
+                        device="cuda:0", u0=u0, i0=i0, user_offset=rank * WEAK_U,
+                        exchange_parts=2, fuse_adam=True, frontier=True, own_items=False)
+    losses = [float(tr.step()) for _ in range(3)]
+    out["replicated_user_w"] = tr.user_w.cpu().numpy()
+    out["replicated_item_w"] = tr.item_w.cpu().numpy()
+    out["replicated_m_i"] = tr.m_i.cpu().numpy()
+    out["replicated_loss"] = np.array(losses)
     # two column chains (32 columns each, own streams and exchange groups)
     for fuse in (False, True):
         tr = ShardedTrainer(e, WEAK_U, WEAK_I, variant, emb_dim=64, num_layers=3,
@@ -111,7 +124,7 @@ def fused_vs_separate(out_dir, variant):
         losses = [float(tr.step()) for _ in range(3)]
         tag = f"chains_{'fused' if fuse else 'sep'}"
         out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
-        out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
+        out[f"{tag}_item_w"] = tr.sync_items()["item_w"].cpu().numpy()
         out[f"{tag}_loss"] = np.array(losses)
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"fused{rank}.npz"), **out)

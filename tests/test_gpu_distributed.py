@@ -129,6 +129,12 @@ def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
     for rk in ranks:   # item Adam beside the chain (default at N > 1) == in the chain
         for key in ("user_w", "item_w", "m_i", "loss"):
             np.testing.assert_array_equal(rk[f"fused_sparse_{key}"], rk[f"inchain_{key}"])
+            # item rows owned by ranks (the fused default) == every rank updating
+            # every item row, bit for bit (the next batch's rows refreshed from
+            # their owners between steps)
+            if variant == "v2_pop":
+                np.testing.assert_array_equal(rk[f"fused_sparse_{key}"],
+                                              rk[f"replicated_{key}"])
     # two column chains (column_chains=2): the same step over two 32-column
     # slices on their own streams and groups; narrow rows sum in slot order,
     # so equal to rounding, and replicas still bitwise identical

@@ -139,6 +139,14 @@ def test_transpose_slots_map_every_edge_once():
     urow = torch.repeat_interleave(torch.arange(U), uc_ptr[1:] - uc_ptr[:-1])
     irow = torch.repeat_interleave(torch.arange(I), ic_ptr[1:] - ic_ptr[:-1])
     assert torch.equal(ic_idx[t], urow) and torch.equal(irow[t], uc_idx)
+    # the map built from the CSR builds' permutations (user_item_slots) is
+    # bitwise the per-edge binary search's (bbgr_transpose_slots)
+    import ctypes
+    from bbgr._lib import call, ptr, stream_handle
+    ts = torch.empty(max(E, 1), dtype=torch.int32, device="cuda")
+    call("bbgr_transpose_slots", ctypes.byref(g.user_csr._struct),
+         ctypes.byref(g.item_csr._struct), ptr(ts), stream_handle())
+    assert torch.equal(ts[:E].long().cpu(), t[:E])
 
 
 @pytest.mark.parametrize("variant,bits,listed", [("v2_pop", True, True),

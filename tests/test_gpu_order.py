@@ -46,6 +46,10 @@ def test_degree_count_and_order_match_numpy(n):
     np.testing.assert_array_equal(_relabel(t(ids, torch.int32), o).cpu().numpy(), rank[ids])
     x = t(rng.normal(size=(n, 3)))
     assert torch.equal(o.rows_to_input(o.rows_to_internal(x)), x)
+    # ids grouped by value (an edge list ingested one user at a time): one
+    # atomic per run of equal ids in a wave, the same exact counts
+    grouped = np.sort(ids, kind="stable")
+    np.testing.assert_array_equal(_degree_count(t(grouped, torch.int32), n).cpu().numpy(), want)
 
 
 def test_ordered_graph_csrs_are_the_relabelled_graph():
