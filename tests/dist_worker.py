@@ -161,6 +161,8 @@ def rccl_single_rank(out_dir, variant, order="input"):
         out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
         out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
         out[f"{tag}_m_u"] = tr.m_u.cpu().numpy()
+        uf, itf = tr.forward()   # sharded: collective, item sums exchanged
+        out[f"{tag}_uf"], out[f"{tag}_itf"] = uf.cpu().numpy(), itf.cpu().numpy()
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, "rccl1.npz"), **out)
     nat.close()   # bbgr_comm_destroy

@@ -165,7 +165,7 @@ def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, 
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     z = dict(np.load(tmp_path / "rccl1.npz"))
     np.testing.assert_allclose(z["sharded_loss"], z["single_loss"], rtol=1e-6)
-    for key in ("user_w", "item_w", "m_u"):
+    for key in ("user_w", "item_w", "m_u", "uf", "itf"):
         a, b = z[f"sharded_{key}"], z[f"single_{key}"]
         err = np.linalg.norm(a - b) / np.linalg.norm(b)
         assert err < 1e-6, (key, err)

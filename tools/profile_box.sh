@@ -11,10 +11,9 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run \
   -- python3 bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace_bench.log
+# every kernel (no include filter): profiles/step_traffic.json sums a whole step
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/fetch -o run \
-  --kernel-include-regex "spmm|adam|bpr|epilogue|sample" \
   -- python3 bench.py $ARGS > $OUT/fetch_bench.json 2> $OUT/fetch_bench.log
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/write -o run \
-  --kernel-include-regex "spmm|adam|bpr|epilogue|sample" \
   -- python3 bench.py $ARGS > $OUT/write_bench.json 2> $OUT/write_bench.log
 find $OUT -name "*.csv" | head -50

@@ -36,6 +36,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--column-chains", default="1")
     ap.add_argument("--frontier-parts", default="2")
+    ap.add_argument("--own-items-of", type=int, default=None,
+                    help="item rows owned per rank as at world size N (default: --parts-of): "
+                         "the probe's rank runs the item Adam on I/N rows, as an N-rank step "
+                         "does (at world size 1 it would own every row)")
     ap.add_argument("--profile", default="",
                     help="cProfile the timed steps into <this>.c<chains>x<parts>f<fparts>")
     a = ap.parse_args()
@@ -60,6 +64,11 @@ def main():
                             vertex_order="degree", exchange_parts=xp,
                             overlap_item_adam=True, column_chains=chains,
                             frontier_parts=fparts)
+        own = a.parts_of if a.own_items_of is None else a.own_items_of
+        if own > 1 and tr.own_items:   # an N-rank step's item Adam share (rows [0, I/N))
+            n = I // own
+            tr.ia, tr.ib = 0, n
+            tr.m_i, tr.v_i = tr.m_i[:n].clone(), tr.v_i[:n].clone()
         for _ in range(3):
             tr.step()
         torch.cuda.synchronize()
@@ -82,6 +91,7 @@ def main():
         print(json.dumps({"config": a.config, "rank_of": a.parts_of, "users": hi - lo,
                           "edges": int(local.shape[1]), "exchange_parts": xp,
                           "column_chains": chains, "frontier_parts": fparts,
+                          "item_rows_owned": tr.ib - tr.ia,
                           "ms_per_step": ms, "host_issue_ms": 1000.0 * issue / a.steps}),
               flush=True)
         tr.close()
