@@ -20,11 +20,16 @@ def edges_to_user_csr(edges_2xE: np.ndarray, num_users: int):
     (user, item) == mergesort by user then per-row np.sort)."""
     u = edges_2xE[0].astype(np.int64)
     it = edges_2xE[1].astype(np.int64)
-    order = np.lexsort((it, u))
     counts = np.bincount(u, minlength=num_users)
     indptr = np.zeros(num_users + 1, dtype=np.int64)
     indptr[1:] = np.cumsum(counts)
-    return indptr, it[order].copy()
+    if it.size == 0:
+        return indptr, it.copy()
+    # rows by user, items ascending inside a row: the sorted (user, item) keys
+    # (equal keys are equal pairs, so a plain sort is the stable one)
+    m = int(it.max()) + 1
+    keys = np.sort(u * m + it)
+    return indptr, keys % m
 
 
 def user_has_item(indptr, indices, user: int, item: int) -> bool:
