@@ -146,9 +146,15 @@ def _cpu_list_text(cpus) -> str:
 
 def cpu_threads() -> int:
     """Threads for the CPU baseline: every CPU this process may run on (its
-    affinity set; BASELINE.md §2: torch.set_num_threads(os.cpu_count()), which
-    on a box that restricts affinity is the affinity set)."""
-    return max(1, len(os.sched_getaffinity(0)))
+    affinity set; BASELINE.md §2: torch.set_num_threads(os.cpu_count())),
+    capped by the host's CPU share for this job when the environment states
+    one (OMP_NUM_THREADS: the GPU box sets it to its per-GPU share, 16, while
+    os.cpu_count() and the affinity set show the whole shared machine)."""
+    n = max(1, len(os.sched_getaffinity(0)))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return n
 
 
 def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop",
@@ -238,6 +244,9 @@ def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop",
                              **_spread(w[1])} for n, w in whole.items()},
         "setup_s": t_setup,
         "os_cpu_count": os.cpu_count(),
+        "affinity_cpus": len(os.sched_getaffinity(0)),
+        "threads_note": "threads = the affinity set, capped by the job's CPU share "
+                        "(OMP_NUM_THREADS on the GPU box: 16 per GPU of a shared host)",
     }
 
 
@@ -734,7 +743,7 @@ def main():
         log("[bench] timing the reference CPU path (bounded sample) ...")
         t_cpu = time.perf_counter()
         cpu = cpu_baseline(edges, cfg, args.config, cred, args.variant)
-        cpu["cpus"] = _cpu_list_text(os.sched_getaffinity(0))
+        cpu["affinity"] = _cpu_list_text(os.sched_getaffinity(0))
         log(f"[bench] cpu baseline took {time.perf_counter() - t_cpu:.1f}s")
     torch_ref = None
     if not args.no_torch_reference and not dist_mode and not sharded_gen and not emulate:

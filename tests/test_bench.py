@@ -84,7 +84,8 @@ def test_cpu_baseline_large_path_on_small_graph(bench, variant):
     r = bench.cpu_baseline(e, cfg, "X", synthetic_credibility(U, 3), variant,
                            whole_steps=("C1",), whole_reps=3, small_edges=0)
     assert r["kind"] == "port" and r["unit"] == "edges/s"
-    assert r["cores"] == len(os.sched_getaffinity(0)) and r["step_measured"]
+    assert r["cores"] == bench.cpu_threads() and r["step_measured"]
+    assert r["cores"] <= r["affinity_cpus"] == len(os.sched_getaffinity(0))
     comp = r["components_s"]
     assert set(comp) == {"sampler", "forward_bpr", "backward", "adam"}
     assert all(v > 0 for v in comp.values())
@@ -129,10 +130,17 @@ def test_column_shard_widths_and_partition_rule():
     assert can_shard_columns(256, 8, MIN_AUTO_WIDTH)
 
 
-def test_cpu_list_text_and_threads(bench):
-    """The CPU baseline runs on every CPU of the affinity set, printed as ranges."""
+def test_cpu_list_text_and_threads(bench, monkeypatch):
+    """The CPU baseline runs on every CPU of the affinity set, capped by the
+    job's stated CPU share (OMP_NUM_THREADS); lists print as ranges."""
     import os
-    assert bench.cpu_threads() == len(os.sched_getaffinity(0))
+    n = len(os.sched_getaffinity(0))
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    assert bench.cpu_threads() == n
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    assert bench.cpu_threads() == 1
+    monkeypatch.setenv("OMP_NUM_THREADS", str(n + 100))
+    assert bench.cpu_threads() == n
     assert bench._cpu_list_text([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
     assert bench._cpu_list_text([5]) == "5"
 
