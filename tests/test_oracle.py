@@ -237,6 +237,31 @@ def test_edges_to_user_csr_sorted_rows():
     assert indices.tolist() == [0, 1, 2, 0, 3]
 
 
+def test_edges_to_user_csr_equals_the_reference_loop():
+    """The oracle's CSR (sorted (user, item) keys) is the array the reference's
+    own loop builds (Version-2/lighgcn_cu_pop.py:309-327: mergesort by user,
+    then np.sort of each row), written out literally here; with duplicates,
+    empty rows and an unsorted input order."""
+    rng = np.random.default_rng(7)
+    U, I = 60, 25
+    e = np.stack([rng.integers(0, U - 5, 900), rng.integers(0, I, 900)]).astype(np.int32)
+    e = np.concatenate([e, e[:, :40]], 1)[:, rng.permutation(940)]
+    u, it = e[0].astype(np.int64), e[1].astype(np.int64)
+    order = np.argsort(u, kind="mergesort")
+    u, it = u[order], it[order]
+    indptr = np.zeros(U + 1, dtype=np.int64)
+    indptr[1:] = np.cumsum(np.bincount(u, minlength=U))
+    indices = it.copy()
+    for user in range(U):
+        a, b = indptr[user], indptr[user + 1]
+        if b - a > 1:
+            indices[a:b] = np.sort(indices[a:b])
+    got_ptr, got_idx = R.edges_to_user_csr(e, U)
+    np.testing.assert_array_equal(got_ptr, indptr)
+    np.testing.assert_array_equal(got_idx, indices)
+    assert got_idx.dtype == np.int64 and got_ptr.dtype == np.int64
+
+
 def test_metrics_at_k_known_answers():
     import math
     p, r, n = R.metrics_at_k([5, 3, 9, 1], {3}, 2)
