@@ -100,6 +100,42 @@ def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
     out.copy_(torch.cat(parts))
 
 
+def owner_bounds(num_items: int, world: int) -> list[int]:
+    """Item ownership: N equal contiguous row ranges, bounds[world+1]."""
+    return [num_items * r // world for r in range(world + 1)]
+
+
+def refresh_from_owners(table: torch.Tensor, rows: torch.Tensor, bounds: list[int],
+                        group=None) -> None:
+    """table[rows] <- the owning ranks' rows (rank r owns [bounds[r], bounds[r+1])):
+    one all-gather of every rank's table[rows], then each row copied from its
+    owner's slot (exact copies; duplicate rows write the same value)."""
+    n, d = rows.numel(), table.shape[1]
+    world = len(bounds) - 1
+    if n == 0 or world == 1:
+        return
+    inner = torch.tensor(bounds[1:-1], dtype=torch.int64, device=rows.device)
+    mine = table.index_select(0, rows)
+    got = torch.empty(world * n, d, dtype=table.dtype, device=table.device)
+    _all_gather(got, mine, group)
+    owner = torch.searchsorted(inner, rows, right=True)
+    pick = owner * n + torch.arange(n, device=rows.device)
+    table.index_copy_(0, rows, got.index_select(0, pick))
+
+
+def gather_owned(owned: torch.Tensor, bounds: list[int], group=None) -> torch.Tensor:
+    """The whole [bounds[-1], d] table from every rank's owned slice (rank r's
+    `owned` holds rows [bounds[r], bounds[r+1]))."""
+    world = len(bounds) - 1
+    sizes = [bounds[r + 1] - bounds[r] for r in range(world)]
+    m, d = max(sizes), owned.shape[1]
+    pad = torch.zeros(m, d, dtype=owned.dtype, device=owned.device)
+    pad[: owned.shape[0]] = owned
+    got = torch.empty(world * m, d, dtype=owned.dtype, device=owned.device)
+    _all_gather(got, pad, group)
+    return torch.cat([got[r * m: r * m + sizes[r]] for r in range(world)])
+
+
 class RcclItemComm:
     """The item exchange through the C ABI's own RCCL communicator
     (bbgr_comm_init / bbgr_allreduce_items) instead of torch.distributed's
@@ -449,11 +485,10 @@ class ShardedTrainer(FusedTrainer):
         # Jacobi order reads the whole item weight table in its first user
         # product, and the unfused path keeps whole gradient tables)
         self.own_items = self.fuse_adam and bool(own_items)
-        self.item_bounds = [num_items * r // self.world for r in range(self.world + 1)]
+        self.item_bounds = owner_bounds(num_items, self.world)
         self.ia, self.ib = ((self.item_bounds[self.rank], self.item_bounds[self.rank + 1])
                             if self.own_items else (0, num_items))
         self.m_i, self.v_i = z(self.ib - self.ia), z(self.ib - self.ia)
-        self._bounds_t = torch.tensor(self.item_bounds[1:-1], dtype=torch.int64, device=dev)
         self._items_stale = False   # some rows of item_w lag their owner's
         self.uf, self.itf = z(num_local_users), z(num_items)
         self.g_uf, self.g_if = z(num_local_users), z(num_items)   # all-zero between steps
@@ -685,33 +720,10 @@ class ShardedTrainer(FusedTrainer):
                       grad_scale=gl)
         self._items_stale = self.world > 1
 
-    def _owner_rows(self, rows: torch.Tensor) -> torch.Tensor:
-        """The owning rank of each item row (internal id)."""
-        return torch.searchsorted(self._bounds_t, rows, right=True)
-
     def _refresh_items(self, rows: torch.Tensor) -> None:
-        """item_w[rows] <- the owners' current values (item ownership): one
-        all-gather of every rank's item_w[rows], then each row copied from its
-        owner's slot (exact copies; duplicate rows write the same value)."""
-        if not self._items_stale or rows.numel() == 0:
-            return
-        n, W = rows.numel(), self.world
-        mine = self.item_w.index_select(0, rows)
-        got = torch.empty(W * n, self.d, dtype=torch.float32, device=self.device)
-        _all_gather(got, mine, self.group)
-        pick = self._owner_rows(rows) * n + torch.arange(n, device=self.device)
-        self.item_w.index_copy_(0, rows, got.index_select(0, pick))
-
-    def _gather_owned(self, t: torch.Tensor) -> torch.Tensor:
-        """The whole [I, d] table from every rank's owned slice t ([ib-ia, d])."""
-        W, d = self.world, self.d
-        m = max(self.item_bounds[r + 1] - self.item_bounds[r] for r in range(W))
-        pad = torch.zeros(m, d, dtype=torch.float32, device=self.device)
-        pad[: t.shape[0]] = t
-        got = torch.empty(W * m, d, dtype=torch.float32, device=self.device)
-        _all_gather(got, pad, self.group)
-        return torch.cat([got[r * m: r * m + self.item_bounds[r + 1] - self.item_bounds[r]]
-                          for r in range(W)])
+        """item_w[rows] <- the owners' current values (refresh_from_owners)."""
+        if self._items_stale:
+            refresh_from_owners(self.item_w, rows, self.item_bounds, self.group)
 
     def sync_items(self) -> dict:
         """Collective (every rank calls it): make the whole item weight table
@@ -720,11 +732,11 @@ class ShardedTrainer(FusedTrainer):
         Without item ownership the local tables are returned as they are."""
         if not self.own_items or self.world == 1:
             return {"item_w": self.item_w, "m_i": self.m_i, "v_i": self.v_i}
-        a, b = self.ia, self.ib
-        self.item_w.copy_(self._gather_owned(self.item_w[a:b].contiguous()))
+        a, b, g = self.ia, self.ib, self.group
+        self.item_w.copy_(gather_owned(self.item_w[a:b].contiguous(), self.item_bounds, g))
         self._items_stale = False
-        return {"item_w": self.item_w, "m_i": self._gather_owned(self.m_i),
-                "v_i": self._gather_owned(self.v_i)}
+        return {"item_w": self.item_w, "m_i": gather_owned(self.m_i, self.item_bounds, g),
+                "v_i": gather_owned(self.v_i, self.item_bounds, g)}
 
     def forward(self):
         """Final (layer-mean) tables of the rank's users and of every item,

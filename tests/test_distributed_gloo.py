@@ -121,3 +121,43 @@ def test_shard_edges_strong_partitions_a_config_graph():
         tops.append(set(np.argsort(-np.bincount(e[1], minlength=c["num_items"]))[:20]))
     assert total == c["num_edges"]
     assert len(tops[0] & tops[1] & tops[2]) >= 10   # one popularity order
+
+
+def _owner_worker(rank, world, port, out):
+    """Item ownership's exchanges (bbgr.distributed.refresh_from_owners /
+    gather_owned, the product functions ShardedTrainer calls): every rank holds
+    a whole table whose rows it owns are current and the rest stale."""
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bbgr  # noqa: F401
+    from bbgr.distributed import gather_owned, owner_bounds, refresh_from_owners
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    I, d = 23, 5
+    bounds = owner_bounds(I, world)
+    g = torch.Generator().manual_seed(0)
+    truth = torch.randn(I, d, generator=g)
+    truth[3] = -0.0   # signed zeros and exact bit patterns travel as copies
+    stale = truth + 100.0 * (rank + 1)   # every rank's view: stale everywhere ...
+    a, b = bounds[rank], bounds[rank + 1]
+    stale[a:b] = truth[a:b]               # ... but at the rows it owns
+    rows = torch.tensor([0, 3, 3, I - 1, bounds[1], 7, 0, 11], dtype=torch.int64)
+    t = stale.clone()
+    refresh_from_owners(t, rows, bounds)
+    whole = gather_owned(truth[a:b].contiguous(), bounds)
+    np.savez(os.path.join(out, f"own{rank}.npz"), t=t.numpy(), stale=stale.numpy(),
+             truth=truth.numpy(), rows=rows.numpy(), whole=whole.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_item_ownership_refresh_and_gather_are_exact(tmp_path, world):
+    mp.spawn(_owner_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for k in range(world):
+        z = np.load(tmp_path / f"own{k}.npz")
+        rows = np.unique(z["rows"])
+        got, want = z["t"], z["stale"].copy()
+        want[rows] = z["truth"][rows]          # refreshed rows = the owners' bits
+        assert got.tobytes() == want.tobytes()
+        assert np.signbit(got[3]).all()        # -0.0 copied, not summed
+        assert z["whole"].tobytes() == z["truth"].tobytes()
