@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--threads", default="16,15,12,8")
     ap.add_argument("--config", default="C2")
     a = ap.parse_args()
-    cpus = bench.numa_local_cpus(16)
+    cpus = sorted(os.sched_getaffinity(0))[:16]
     os.sched_setaffinity(0, cpus)
     for n in (int(x) for x in a.threads.split(",")):
         torch.set_num_threads(n)

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--pin", type=int, default=0)
     a = ap.parse_args()
     if a.pin:
-        os.sched_setaffinity(0, set(bench.numa_local_cpus(a.pin)))
+        os.sched_setaffinity(0, set(sorted(os.sched_getaffinity(0))[:a.pin]))
     cfg = CONFIGS["C4"]
     edges = config_edges("C4")
     cred = synthetic_credibility(cfg["num_users"], CONFIG_SEED["C4"])
