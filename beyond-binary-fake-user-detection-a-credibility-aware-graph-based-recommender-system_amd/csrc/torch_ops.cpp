@@ -379,7 +379,9 @@ static const Tensor &u2i_slots(const Pair &P, const at::Device &dev) {
       auto rows_of = [&](const int32_t *indptr, int64_t n) {
         Tensor ptr = at::from_blob(const_cast<int32_t *>(indptr), {n + 1}, i32);
         Tensor cnt = (ptr.narrow(0, 1, n) - ptr.narrow(0, 0, n)).to(at::kLong);
-        return at::repeat_interleave(cnt, /*output_size=*/nnz);
+        // (the optional output size selects the repeats-only overload; a plain
+        // int64 would bind to repeat_interleave(self, repeats) instead)
+        return at::repeat_interleave(cnt, std::optional<int64_t>(nnz));
       };
       Tensor uidx = at::from_blob(const_cast<int32_t *>(uc.indices), {nnz}, i32).to(at::kLong);
       Tensor iidx = at::from_blob(const_cast<int32_t *>(ic.indices), {nnz}, i32).to(at::kLong);
