@@ -291,6 +291,9 @@ class ItemExchange:
     def item_product(self, prod, x, first, new, kw) -> None:
         src_mask = kw.pop("src_mask", None)
         row_mask = kw.pop("row_mask", None)
+        # the slot bitmap of src_mask's live edges: used by the frontier
+        # (row-list) launches, where most listed rows' edges are dead
+        src_bits = kw.pop("src_bits", None)
         fr = self.rows() if row_mask is not None else None
         works = []
         if fr is not None:
@@ -306,10 +309,10 @@ class ItemExchange:
                 part = lst[a:b]
                 if positions is not None:   # listed row lst[j] -> row j of c
                     spmm(prod, x, first, y=c, y_map=positions, src_mask=src_mask,
-                         row_mask=row_mask, row_list=part, rng=rg)
+                         row_mask=row_mask, row_list=part, rng=rg, src_bits=src_bits)
                 else:
                     spmm(prod, x, first, y=t, src_mask=src_mask, row_mask=row_mask,
-                         row_list=part, rng=rg)
+                         row_list=part, rng=rg, src_bits=src_bits)
                     call("bbgr_rows_gather", b - a, ptr(part), ptr(t), ld(t), ptr(c[a:b]),
                          ld(c), d, stream_handle())
                 self._allreduce_async(c[a:b], works)
@@ -535,8 +538,15 @@ class ShardedTrainer(FusedTrainer):
         # them copied a step ago instead of waiting for the GPU to get there
         # (at N = 8 that wait serialised host issue and GPU work).
         n_bounds = max(exchange_parts, frontier_parts) + 2
-        self._fronts = [_Front(B, self.B_global, num_local_users, num_items, n_bounds, dev)
-                        for _ in range(2)]
+        # the first backward item product's slot bitmap (FusedTrainer): the
+        # rank's batch users' edges in its item-CSR order, per front; full-width
+        # tables only (column chains run narrow kernels, which keep the mask)
+        self.slot_map = None
+        if self.frontier and emb_dim >= 64 and not self.chains:
+            self.slot_map = self.graph.user_item_slots()
+        n_bits = self.graph.item_csr.nnz // 32 + 4 if self.slot_map is not None else 0
+        self._fronts = [_Front(B, self.B_global, num_local_users, num_items, n_bounds, dev,
+                               n_bits) for _ in range(2)]
         self._next = None
         self._list_ws = None
         self._list_need = None
@@ -632,6 +642,7 @@ class ShardedTrainer(FusedTrainer):
         B = f.posneg.numel() // 2
         self.pos, self.neg = f.posneg[:B], f.posneg[B:]
         self.mask_u, self.mask_i, self.mask_b = f.mask_u, f.mask_i, f.mask_b
+        self.slot_bits = f.slot_bits
         self.item_list, self.item_count = f.item_list, f.item_count
 
     def _prepare(self, f: "_Front") -> None:
@@ -655,6 +666,7 @@ class ShardedTrainer(FusedTrainer):
         call("bbgr_mark_rows", 2 * B, ptr(f.posneg), 1, ptr(f.mask_i), self.I, st)
         call("bbgr_mark_rows", f.all_items.numel(), ptr(f.all_items), 1, ptr(f.mask_b),
              self.I, st)
+        self._mark_slots(f, 1)
         if self.order == ORDER_GS:
             uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), 1,
@@ -662,6 +674,13 @@ class ShardedTrainer(FusedTrainer):
         dist.all_reduce(f.mask_i, op=dist.ReduceOp.SUM, group=self.group)  # <= world: no wrap
         if self.sparse_exchange:
             self._list_rows(f)
+
+    def _mark_slots(self, f: "_Front", value: int) -> None:
+        """Set / clear the slot bits of f's users' edges (bbgr_mark_slots)."""
+        if f.slot_bits is not None and f.users is not None:
+            uc = self.graph.user_csr
+            call("bbgr_mark_slots", f.users.numel(), ptr(f.users), ptr(uc.indptr),
+                 ptr(self.slot_map), ptr(f.slot_bits), value, stream_handle())
 
     def _list_rows(self, f: "_Front") -> None:
         st = stream_handle()
@@ -775,6 +794,7 @@ class ShardedTrainer(FusedTrainer):
                  stream_handle())
             call("bbgr_mark_rows", f.all_items.numel(), ptr(f.all_items), 0, ptr(f.mask_b),
                  self.I, stream_handle())
+            self._mark_slots(f, 0)
             f.mask_i.zero_()
         f.rows = None
 
@@ -852,6 +872,7 @@ class ShardedTrainer(FusedTrainer):
             call("bbgr_mark_rows", B, ptr(users), 0, ptr(self.mask_u), self.U, st)
             call("bbgr_mark_rows", self.all_items.numel(), ptr(self.all_items), 0,
                  ptr(self.mask_b), self.I, st)
+            self._mark_slots(f, 0)
             self.mask_i.zero_()
         if self._next is not None:   # owners' rows of the next step's batch items
             self._refresh_items(self._next.all_items)
@@ -951,7 +972,8 @@ class _Front:
     """One step's batch and frontier (ShardedTrainer keeps two: the running
     step's and the next one's). Masks are all-zero between uses."""
 
-    def __init__(self, B: int, B_global: int, U: int, I: int, n_bounds: int, dev):
+    def __init__(self, B: int, B_global: int, U: int, I: int, n_bounds: int, dev,
+                 n_bits: int = 0):
         i64 = dict(dtype=torch.int64, device=dev)
         self.users = None
         self.posneg = torch.empty(2 * B, **i64)
@@ -969,6 +991,9 @@ class _Front:
         # (the item layer-mean accumulator is formed there only)
         self.mask_b = _lib.byte_mask(I, dev)
         self.items_fresh = False   # item_w current at all_items (item ownership)
+        # slot bitmap of the batch users' edges (all-zero between uses)
+        self.slot_bits = (torch.zeros(n_bits, dtype=torch.int32, device=dev) if n_bits
+                          else None)
 
 
 class _GlobalItemCsr:

@@ -417,10 +417,10 @@ def _item_product(prod: Product, x: torch.Tensor, first: bool, reduce, new, **kw
             raise ValueError("sharded item products take no input-order maps")
     if kw.pop("src_input", False):
         raise ValueError("sharded item products take no input-order maps")
-    kw.pop("src_bits", None)   # an index-scan shortcut only: the mask alone is exact
-    if hasattr(reduce, "item_product"):   # chunked / overlapped exchange
+    if hasattr(reduce, "item_product"):   # chunked / overlapped exchange (takes src_bits)
         reduce.item_product(prod, x, first, new, kw)
         return
+    kw.pop("src_bits", None)   # an index-scan shortcut only: the mask alone is exact
     src_mask = kw.pop("src_mask", None)
     row_mask = kw.pop("row_mask", None)
     t = new("partial", prod.csr.n_rows)

@@ -4,6 +4,7 @@
 #   profile  rocprofv3 kernel trace + FETCH_SIZE + WRITE_SIZE passes of the C4 bench
 #   shard    the N=8 user-row rank probe (1 and 2 column chains)
 #   dropin   the drop-in module step (FusedAdam / foreach Adam)
+#   rehearsal the driver's N=4 / N=8 bench commands over gloo on one GPU
 # Usage: tools/gpu_r4_measure.sh <tag> <pass>...   outputs under gpurun_out/<tag>/
 set -o pipefail
 T=${1:-r4m}; shift
@@ -30,6 +31,10 @@ shard)
 dropin)
   timeout -k 10 300 python tools/dropin_probe.py --adam bbgr > $O/dropin_bbgr.json 2> $O/dropin_bbgr.log || fail dropin $O/dropin_bbgr.log
   timeout -k 10 300 python tools/dropin_probe.py --adam foreach > $O/dropin_foreach.json 2> $O/dropin_foreach.log || fail dropin_foreach $O/dropin_foreach.log
+  ;;
+rehearsal)   # the driver's N=4 / N=8 bench commands over gloo on this one GPU
+  timeout -k 10 1000 bash tools/probes/gpu_rehearsal_n48.sh ${T}/rehearsal > $O/rehearsal.log 2>&1 || fail rehearsal $O/rehearsal.log
+  cat $O/rehearsal.log
   ;;
 *) echo "unknown pass $WHAT"; exit 2 ;;
 esac
