@@ -6,7 +6,7 @@ O=gpurun_out/r4b
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 hard() { case $1 in 124|134|137|139) echo "HARD FAIL ($1) in $2"; tail -30 "$3"; exit 1;; esac; }
-timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_order.py tests/test_gpu_parity.py -m gpu -v --durations=10 --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_order.py tests/test_gpu_parity.py tests/test_gpu_distributed.py tests/test_gpu_graph.py -m gpu -v --durations=10 --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; hard $rc tests $O/gpu_tests.log
 echo "TESTS rc=$rc"; grep -E "passed|failed" $O/gpu_tests.log | tail -2; grep FAILED $O/gpu_tests.log | head
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.log
