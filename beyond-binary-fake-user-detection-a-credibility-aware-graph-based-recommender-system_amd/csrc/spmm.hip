@@ -132,6 +132,10 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
 // spill): C4 full user products 1.484 -> 1.451 ms per launch (round 3 A/B;
 // the weighted forms spill at 8; an 8-wave target on the one-row kernels
 // measured slower, item products 1.816 -> 1.829 ms)
+// the unweighted d = 64 slot-bitmap kernel (spmm_bits_kernel)
+#ifndef BBGR_BITS_WAVES0
+#define BBGR_BITS_WAVES0 8
+#endif
 #ifndef BBGR_PAIR_WAVES0
 #define BBGR_PAIR_WAVES0 8
 #endif
@@ -221,6 +225,35 @@ __device__ __forceinline__ unsigned long long slot_bits64(const unsigned *bits, 
   return sh ? (x >> sh) | ((unsigned long long)bits[w + 2] << (64 - sh)) : x;
 }
 
+// Stable compaction of a 16-lane group's live edges (my >= 0) onto its first
+// lanes: afterwards lane j holds the j-th live edge of the batch in CSR order
+// (index and weight), and the live count is returned. A slot-bitmap batch
+// (about 1 live edge in 16 at C4) is then gathered in ceil(live / U) load
+// rounds instead of ceil(16 / U) mostly idle ones: C4 first backward item
+// product 0.111 -> 0.106 ms. The plain src-masked kernels do not use it: there
+// 41 % of the edges are live, and the permute's latency in every batch's
+// dependent chain (index -> mask -> permute -> gather) cost more than the
+// idle slots (masked user product 0.913 -> 0.98-0.99 ms, round 4 A/B).
+// The skipped edges would each add +0.0 to a sum that started at +0.0 and so
+// is never -0.0: s + 0.0 == s, results are unchanged bit for bit.
+// ds_permute (forward permute) sends every lane's pair to its rank among the
+// live (or, after them, the dead) lanes of its group: a permutation, so each
+// lane receives exactly one. Called with the whole wave converged.
+template <int WMODE>
+__device__ __forceinline__ int compact_live(int &my, float &mw) {
+  const unsigned long long b = __ballot(my >= 0);
+  const int base = threadIdx.x & 48;
+  const int l = threadIdx.x & 15;
+  const unsigned lm = (unsigned)((b >> base) & 0xffffull);
+  const unsigned below = (1u << l) - 1u;
+  const int nlive = __popc(lm);
+  const int p = my >= 0 ? __popc(lm & below) : nlive + __popc(~lm & below);
+  const int to = (base + p) << 2;
+  my = __builtin_amdgcn_ds_permute(to, my);
+  if (WMODE != 0) mw = __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(mw)));
+  return nlive;
+}
+
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
 template <int D, int WMODE, bool MASKED, bool BITS = false>
 __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
@@ -228,7 +261,7 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
   constexpr int V = D / 64;
   constexpr int U = Tune<D>::row_u;   // source rows in flight per group per batch
   for (int e0 = eb; e0 < ee; e0 += 16) {
-    const int n = min(16, ee - e0);
+    int n = min(16, ee - e0);
     unsigned live = 0xffffu;   // slot-bitmap mode: this batch's live edges
     if constexpr (MASKED && BITS) {
       // liveness from the bitmap, 64 edges per test: a dead window costs one
@@ -254,9 +287,11 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
       }
     }
-    if (MASKED && !BITS && P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
-      const unsigned long long live = __ballot(my >= 0);
-      if (((live >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
+    if constexpr (MASKED && BITS) {   // live edges first (sparse: ~1 of 16 live)
+      n = compact_live<WMODE>(my, mw);
+    } else if (MASKED && P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
+      const unsigned long long lv = __ballot(my >= 0);
+      if (((lv >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
     }
     for (int j0 = 0; j0 < n; j0 += U) {
       float4 v[U][V];
@@ -945,7 +980,7 @@ spmm_masked_pair_kernel(SpmmParams P) {
 // their register budget. Unweighted at d = 64: an 8-wave target (63 VGPRs, no
 // spill), C4 0.108 -> 0.103 ms (round 3 A/B).
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 && D == 64 ? 8 : Tune<D>::masked_waves) void
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 && D == 64 ? BBGR_BITS_WAVES0 : Tune<D>::masked_waves) void
 spmm_bits_kernel(
     SpmmParams P) {
   spmm_body<D, WMODE, true, false, true>(P);

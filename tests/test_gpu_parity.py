@@ -959,6 +959,43 @@ def test_spmm_pair_rows_match_single_row_path(d, mode, monkeypatch):
         np.testing.assert_array_equal(b, a)
 
 
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_src_masked_launch_is_bitwise_the_dense_product(d, mode, monkeypatch):
+    """A src-masked launch (dead edges skipped) is bitwise the unmasked launch
+    over the source table zeroed off the mask, for live fractions 0 .. 1, one-
+    and two-row kernels, every weight mode, chunked long rows and row ranges.
+    (The slot-bitmap path's live-edge compaction is pinned against the mask by
+    test_row_list_with_device_length / the single-chunk boundary test.)"""
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(300 + d + mode)
+    Rn, Cn = 2500, 900
+    deg = rng.geometric(0.1, Rn) - 1
+    deg[rng.choice(Rn, 5, replace=False)] = [16, 17, 31, 200, 900]
+    rows = np.repeat(np.arange(Rn), deg).astype(np.int32)
+    cols = rng.integers(0, Cn, rows.size).astype(np.int32)
+    vals = rng.uniform(0.1, 1.0, rows.size).astype(np.float32)
+    cs = rng.uniform(0.5, 2.0, Cn).astype(np.float32)
+    c = Csr(rows, cols, Rn, Cn, DEV, edge_values=t(vals) if mode == 1 else None,
+            long_threshold=64, chunk_edges=128)
+    prod = Product(c, c.values if mode == 1 else None, t(cs) if mode == 2 else None, None, {})
+    x = rng.uniform(-1, 1, (Cn, d)).astype(np.float32)
+    for frac in (0.0, 0.05, 0.41, 0.9, 1.0):
+        m = (rng.random(Cn) < frac).astype(np.uint8)
+        xm = t(x * m[:, None])
+        for pair in (0, 1):
+            monkeypatch.setenv("BBGR_SPMM_PAIR", str(pair))
+            for rg in [None] + list(c.row_ranges(2)):
+                kw = {} if rg is None else {"rng": rg}
+                ref = torch.full((Rn, d), 7.0, device=DEV)
+                got = torch.full((Rn, d), 7.0, device=DEV)
+                spmm(prod, xm, True, y=ref, y_scale_s=0.5, **kw)
+                spmm(prod, xm, True, y=got, y_scale_s=0.5, src_mask=t(m, torch.uint8), **kw)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(got.cpu().numpy(), ref.cpu().numpy(),
+                                              err_msg=f"frac={frac} pair={pair} rng={rg}")
+
+
 @pytest.mark.parametrize("variant", ["gs", "method_a", "jacobi"])
 def test_every_layer_vs_oracle(gold, variant):
     """SURVEY §8(d) parity, per layer k and side: the operators' products
