@@ -74,6 +74,13 @@ def spmm_adam_bytes(nnz: int, rows: int, d: int) -> int:
     return spmm_bytes(nnz, rows, d) - rows * 4 * d + 6 * rows * 4 * d
 
 
+def spmm_adam_side_bytes(nnz: int, rows: int, d: int) -> int:
+    """A product that still writes its output and carries another table's Adam
+    (the GS item Adam on the last backward item product): the SpMM bytes plus
+    the gradient row read and param / exp_avg / exp_avg_sq read + write."""
+    return spmm_bytes(nnz, rows, d) + 7 * rows * 4 * d
+
+
 def _median_s(fn, reps: int = 5, warmup: int = 1):
     """Median wall time of fn() over `reps` runs after `warmup` untimed runs.
     fn may return its own measured seconds (a sub-interval); else the call is timed."""
@@ -306,10 +313,10 @@ def roofline_groups(timer, counts, steps: int, count_steps: int, n_items: int):
             compulsory = None
         else:
             rows_l, nnz_l = rows / n, nnz / n
-            gather = spmm_bytes(nnz_l, rows_l, d) if kind == "full" else \
-                spmm_adam_bytes(nnz_l, rows_l, d)
+            gather = (spmm_bytes if kind == "full" else spmm_adam_side_bytes
+                      if kind == "adam_side" else spmm_adam_bytes)(nnz_l, rows_l, d)
             compulsory = _compulsory_bytes(nnz_l, rows_l, nc, d) + \
-                (0 if kind == "full" else 5 * rows_l * 4 * d)
+                {"full": 0, "adam": 5, "adam_side": 7}[kind] * rows_l * 4 * d
             e["rows_per_launch"], e["edges_per_launch"] = rows_l, nnz_l
         e["gather_model_bytes"] = gather
         e["gather_model_GBps"] = gather / (e["avg_ms"] * 1e6)
@@ -836,7 +843,8 @@ def main():
                          for r, z, ms in timer.sequence("full", timer_steps)],
                      "adam_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
-                         for r, z, ms in timer.sequence("adam", timer_steps)],
+                         for r, z, ms in timer.sequence("adam", timer_steps)
+                         + timer.sequence("adam_side", timer_steps)],
                      "masked_sequence_ms": [
                          {"rows": r, "nnz": z, "avg_ms": ms}
                          for r, z, ms in timer.sequence("masked", timer_steps)]},

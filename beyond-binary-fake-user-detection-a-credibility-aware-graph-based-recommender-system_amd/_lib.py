@@ -89,6 +89,7 @@ class SpmmArgs(ctypes.Structure):
         ("src_bits", c_void_p),
         ("row_count", c_void_p),
         ("acc_in_map", c_void_p),
+        ("adam_grad", c_void_p), ("adam_grad_ld", c_int64), ("adam_grad_scale", c_float),
     ]
 
 
@@ -197,6 +198,9 @@ _SIGNATURES = {
     "bbgr_list_offsets": ([c_int32, _P, _P, _P, _P, _P], c_int32),
     "bbgr_list_positions": ([c_int64, _P, _P, _P, _P], c_int32),
     "bbgr_rows_gather": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
+    "bbgr_rows_copy": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
+    "bbgr_rows_add_unique": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P],
+                             c_int32),
     # blueprint names, thin forms of the entry points above
     "bbgr_spmm_f32": ([ctypes.POINTER(CsrStruct), _P, c_int64, _P, c_int64, c_int32, _P, _P,
                        _P, c_float, _P], c_int32),
@@ -230,7 +234,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 5:
+        if handle.bbgr_abi_version() != 6:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

@@ -82,6 +82,9 @@ struct SpmmParams {
   const int *acc_in_map;       // acc_in's own row map (args.acc_in_map; NULL: acc_map's)
   const unsigned *src_bits;    // slot bitmap of live edges (args.src_bits; d >= 64)
   const long *row_count;       // device length of row_list (args.row_count; nullable)
+  const float *adam_g;         // fused Adam's own gradient table (args.adam_grad; nullable)
+  long adam_g_ld;
+  float adam_g_scale;
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -616,7 +619,19 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
         for (int k = 0; k < V; ++k) dst[16 * k] = G[k];
       }
     }
-    if (P.adam_p) adam_row<D>(P, ry, lane, G);
+    if (P.adam_p && P.adam_g) {   // Adam of another table riding on this row write
+      const float4 *gr = reinterpret_cast<const float4 *>(P.adam_g + ry * P.adam_g_ld) + lane;
+      float4 Ga[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) {   // gs * g, as adam_kernel forms it
+        const float4 g4 = ld_nt(gr + 16 * k);
+        Ga[k] = make_float4(P.adam_g_scale * g4.x, P.adam_g_scale * g4.y,
+                            P.adam_g_scale * g4.z, P.adam_g_scale * g4.w);
+      }
+      adam_row<D>(P, ry, lane, Ga);
+    } else if (P.adam_p) {
+      adam_row<D>(P, ry, lane, G);
+    }
   }
   const long rc = P.acc_map ? (long)P.acc_map[row] : (long)row;
   if (P.acc_out && (!P.acc_mask || P.acc_mask[rc])) {
@@ -1121,6 +1136,9 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.add_map = a->add_map;
   P.acc_in_map = a->acc_in_map;
   P.src_bits = a->src_bits;
+  P.adam_g = a->adam_grad;
+  P.adam_g_ld = a->adam_grad_ld;
+  P.adam_g_scale = a->adam_grad_scale;
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {
@@ -1128,6 +1146,7 @@ static bool adam_ok(const bbgr_spmm_args *a, int d) {
   const bool dev = a->adam_state != nullptr;
   return a->adam_exp_avg && a->adam_exp_avg_sq && ld_ok(a->adam_param, a->adam_ld, d) &&
          ld_ok(a->adam_exp_avg, a->adam_ld, d) && ld_ok(a->adam_exp_avg_sq, a->adam_ld, d) &&
+         (!a->adam_grad || ld_ok(a->adam_grad, a->adam_grad_ld, d)) &&
          (dev ? a->adam_bc_table != nullptr
               : (a->adam_bias_correction1 > 0.f && a->adam_bias_correction2_sqrt > 0.f));
 }

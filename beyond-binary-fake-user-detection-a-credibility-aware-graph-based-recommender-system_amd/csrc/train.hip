@@ -470,6 +470,37 @@ __global__ void rows_axpy_kernel(long n, const long *idx, float alpha,
     atomicAdd(dst + r * ldd + c, alpha * src[r * lds + c]);
 }
 
+// dst[idx[k]] = src[idx[k]] (idx < 0 skipped; repeats write the same row).
+__global__ __launch_bounds__(256) void rows_copy_kernel(long n, const long *idx,
+                                                        const float4 *src, long lds4,
+                                                        float4 *dst, long ldd4, int d4) {
+  const long k = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (k >= n) return;
+  const long r = idx[k];
+  if (r < 0) return;
+  for (int c = threadIdx.x & 15; c < d4; c += 16) dst[r * ldd4 + c] = src[r * lds4 + c];
+}
+
+// dst[idx[k]] += (0 + src[k]) for distinct idx: a one-addend segment of
+// scatter_segments_kernel (acc = 0 + x, then dst + acc), bit for bit.
+__global__ __launch_bounds__(256) void rows_add_unique_kernel(long n, const long *idx,
+                                                              const float4 *src, long lds4,
+                                                              float4 *dst, long ldd4, int d4,
+                                                              long n_dst) {
+  const long k = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (k >= n) return;
+  const long r = idx[k];
+  if (r < 0 || r >= n_dst) return;
+  const float4 *in = src + k * lds4;
+  float4 *out = dst + r * ldd4;
+  for (int c = threadIdx.x & 15; c < d4; c += 16) {
+    const float4 x = in[c];
+    const float4 a = make_float4(0.f + x.x, 0.f + x.y, 0.f + x.z, 0.f + x.w);
+    const float4 o = out[c];
+    out[c] = make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w);
+  }
+}
+
 // dst[k, :] = src[idx[k], :] (zero row for idx < 0); float4 per lane, one
 // 16-lane group per row: the compaction of frontier rows for the sparse
 // multi-GPU exchange.
@@ -864,6 +895,40 @@ extern "C" int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha,
                      as_stream(stream), (long)n, (const long *)idx, alpha, src,
                      (long)ldsrc, dst, (long)lddst, d);
   BBGR_LAUNCHED("rows_axpy_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_rows_copy(int64_t n, const int64_t *idx, const float *src,
+                              int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
+                              bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && d > 0 && (d & 3) == 0 && ldsrc >= d && lddst >= d &&
+                   (ldsrc & 3) == 0 && (lddst & 3) == 0,
+               "bbgr_rows_copy: bad sizes (d, ld multiples of 4, ld >= d)");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx && src && dst && aligned16(src) && aligned16(dst),
+               "bbgr_rows_copy: null or unaligned arrays");
+  hipLaunchKernelGGL(rows_copy_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)idx,
+                     reinterpret_cast<const float4 *>(src), (long)ldsrc / 4,
+                     reinterpret_cast<float4 *>(dst), (long)lddst / 4, d / 4);
+  BBGR_LAUNCHED("rows_copy_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_rows_add_unique(int64_t n, const int64_t *idx, const float *src,
+                                    int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
+                                    int64_t n_dst, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n_dst >= 0 && d > 0 && (d & 3) == 0 && ldsrc >= d && lddst >= d &&
+                   (ldsrc & 3) == 0 && (lddst & 3) == 0,
+               "bbgr_rows_add_unique: bad sizes (d, ld multiples of 4, ld >= d)");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx && src && dst && aligned16(src) && aligned16(dst),
+               "bbgr_rows_add_unique: null or unaligned arrays");
+  hipLaunchKernelGGL(rows_add_unique_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)idx,
+                     reinterpret_cast<const float4 *>(src), (long)ldsrc / 4,
+                     reinterpret_cast<float4 *>(dst), (long)lddst / 4, d / 4, (long)n_dst);
+  BBGR_LAUNCHED("rows_add_unique_kernel");
   return BBGR_OK;
 }
 

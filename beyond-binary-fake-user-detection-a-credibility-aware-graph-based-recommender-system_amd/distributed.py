@@ -114,6 +114,9 @@ def refresh_from_owners(table: torch.Tensor, rows: torch.Tensor, bounds: list[in
     world = len(bounds) - 1
     if n == 0 or world == 1:
         return
+    # a -1 "no negative" row (the sampler gave up) refreshes row 0 instead: a
+    # copy of its owner's current value, harmless, and every rank keeps n rows
+    rows = rows.clamp(min=0)
     inner = torch.tensor(bounds[1:-1], dtype=torch.int64, device=rows.device)
     mine = table.index_select(0, rows)
     got = torch.empty(world * n, d, dtype=table.dtype, device=table.device)
@@ -711,8 +714,9 @@ class ShardedTrainer(FusedTrainer):
         gl = 1.0 / (self.K + 1)
         a_gl = (2.0 * self.reg / self.B_global) / gl
         step_count, self.step_count = self.step_count, self.step_count + 1
-        with torch.cuda.stream(side):
-            self.g_adam.index_copy_(0, rows, self.g_if.index_select(0, rows))
+        with torch.cuda.stream(side):   # (a -1 "no negative" row is skipped)
+            call("bbgr_rows_copy", rows.numel(), ptr(rows), ptr(self.g_if), ld(self.g_if),
+                 ptr(self.g_adam), ld(self.g_adam), self.d, stream_handle())
             self._item_adam(rows, self.g_adam, a_gl, gl)
             call("bbgr_rows_zero", rows.numel(), ptr(rows), ptr(self.g_adam),
                  ld(self.g_adam), self.d, stream_handle())
@@ -839,7 +843,8 @@ class ShardedTrainer(FusedTrainer):
         call("bbgr_bpr", ctypes.byref(a), st)
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
-        self.scatter(self.g_uf, users, self.contrib[:B])
+        # (every step's batch holds distinct users: next_users)
+        self.scatter(self.g_uf, users, self.contrib[:B], unique=True)
         # item gradient of the global batch: every rank's (pos, neg) rows
         # (gathered with the batch) and their per-triple gradient rows, summed
         # in rank-major order

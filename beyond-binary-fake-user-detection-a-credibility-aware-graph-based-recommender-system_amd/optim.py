@@ -67,12 +67,18 @@ class AdamRows:
     """Arguments of a fused Adam step applied inside an SpMM epilogue
     (bbgr_spmm_args.adam_*): the row gradient never touches HBM. With
     `dev` (DeviceStepState) the step t and bias corrections are read on the
-    device (graph-captured steps)."""
+    device (graph-captured steps). `grad` (a table like param): the gradient
+    is grad_scale * grad[row] instead of the launch's row value, which is then
+    still written to y (bbgr_spmm_args.adam_grad): another table's Adam riding
+    on a product over the same rows."""
 
     def __init__(self, param, exp_avg, exp_avg_sq, step: int, lr: float, beta1: float = 0.9,
                  beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0,
-                 dev: DeviceStepState | None = None):
+                 dev: DeviceStepState | None = None, grad=None, grad_scale: float = 1.0):
         self.param, self.exp_avg, self.exp_avg_sq = param, exp_avg, exp_avg_sq
+        if grad is not None and (grad.shape != param.shape or grad.dtype != param.dtype):
+            raise ValueError("AdamRows: grad must be a table shaped like param")
+        self.grad, self.grad_scale = grad, grad_scale
         self.lr, self.beta1, self.beta2, self.eps, self.wd = lr, beta1, beta2, eps, weight_decay
         self.bc1 = 1.0 - beta1 ** step
         self.bc2s = math.sqrt(1.0 - beta2 ** step)
@@ -93,6 +99,9 @@ class AdamRows:
         a.adam_bias_correction1, a.adam_bias_correction2_sqrt = self.bc1, self.bc2s
         if self.dev is not None:
             a.adam_bc_table, a.adam_state = ptr(self.dev.bc_table), ptr(self.dev.state)
+        if self.grad is not None:
+            a.adam_grad, a.adam_grad_ld = ptr(self.grad), ld(self.grad)
+            a.adam_grad_scale = self.grad_scale
 
 
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,

@@ -358,7 +358,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
         call("bbgr_spmm", ctypes.byref(cs), ctypes.byref(a), stream_handle())
         return
     masked = src_mask is not None or row_mask is not None or row_list is not None
-    kind = "masked" if masked else ("adam" if adam is not None else "full")
+    kind = "masked" if masked else ("full" if adam is None else
+                                    "adam" if adam.grad is None else "adam_side")
     if row_count is not None:   # the list is row_mask's rows; its length is on the device
         row_list = None
     if _timer.count:
@@ -575,6 +576,10 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     Jacobi order, K >= 2, no `reduce`: `adam_i` fuses the item-table Adam into
     the last item-row product the same way (out_i untouched). Jacobi K == 1
     reads gU / gI as the last products' SOURCE tables: not fusable there.
+    GS order, K >= 2, no `reduce`: `adam_i` carrying its own gradient table
+    (AdamRows(grad=...): the item weights only feed the layer mean, so their
+    gradient is known before the chain) rides on the last item product, a
+    dense launch over every item row that still writes its output.
     `grad_support=(user_mask, item_mask)`: gU is zero outside the flagged users
     and, for GS, the first item product's output is zero outside the flagged
     items (GS: batch items and N(batch users); Jacobi: gI's own support). The
@@ -622,8 +627,12 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
         fl = {}
         if frontier_list is not None and reduce is None and si_int is not None:
             fl = dict(row_list=frontier_list[0], row_count=frontier_list[1])
+        if adam_i is not None and (K < 2 or reduce is not None or adam_i.grad is None):
+            raise ValueError("GS backward: a fused item Adam needs K >= 2, no reduce hook "
+                             "and its own gradient table (AdamRows(grad=...))")
         for k in range(K, 0, -1):
             first = k == K
+            ka = {"adam": adam_i} if (k == 1 and adam_i is not None) else {}
             # first product: Gi_K is zero off the item support (batch items and
             # N(batch users)) and the next product reads only that support, so
             # the other rows are neither computed nor written (row_mask)
@@ -633,7 +642,7 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                           src_mask=su if first else None,
                           row_mask=si_int if first else None, add_map=im,
                           src_input=inp and first, src_bits=src_bits if first else None,
-                          **(fl if first else {}))
+                          **(fl if first else {}), **ka)
             yield
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,

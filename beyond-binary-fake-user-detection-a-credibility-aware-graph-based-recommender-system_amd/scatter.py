@@ -23,7 +23,11 @@ class RowScatter:
     def __init__(self):
         self._ws = None
 
-    def __call__(self, dst: torch.Tensor, index: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    def __call__(self, dst: torch.Tensor, index: torch.Tensor, src: torch.Tensor,
+                 unique: bool = False) -> torch.Tensor:
+        """unique=True: the caller guarantees distinct indices (a batch of
+        distinct users): one launch, bitwise the sorted path
+        (bbgr_rows_add_unique)."""
         _lib.require_gpu(dst)
         n = index.numel()
         if src.shape[0] < n or src.shape[1] != dst.shape[1]:
@@ -32,6 +36,10 @@ class RowScatter:
             if not (t.dtype == torch.float32 and t.stride(1) == 1):
                 raise ValueError("index_add_rows: fp32 row-major tables")
         index = index.to(torch.int64).contiguous()
+        if unique:
+            call("bbgr_rows_add_unique", n, ptr(index), ptr(src), ld(src), ptr(dst), ld(dst),
+                 dst.shape[1], dst.shape[0], stream_handle())
+            return dst
         need = ctypes.c_size_t(0)
         args = (n, ptr(index), ptr(src), ld(src), ptr(dst), ld(dst), dst.shape[1], dst.shape[0])
         call("bbgr_scatter_add_rows", *args, None, ctypes.byref(need), stream_handle())

@@ -217,7 +217,8 @@ class FusedTrainer:
         # the de-duplicated mask instead of a row list, whose repeated rows
         # would update the in-place accumulator twice)
         self._bpr(users, pos, neg, B)
-        self.scatter(self.g_uf, users, self.contrib[:B])
+        # an epoch slice holds distinct users: their rows are added without the sort
+        self.scatter(self.g_uf, users, self.contrib[:B], unique=listed)
         self.scatter(self.g_if, self.posneg[: 2 * B], self.contrib[B: 3 * B])
         call("bbgr_bpr_reduce", B, ptr(self.parts), float(self.reg), float(self.lambda_fair),
              ptr(self.loss), st)
@@ -278,12 +279,38 @@ class FusedTrainer:
             call("bbgr_rows_axpy", B, ptr(users), a_gl, ptr(self.user_w), ld(self.user_w),
                  ptr(self.g_uf), ld(self.g_uf), self.d, st)
 
+        # The item Adam rides on the last backward item product (a dense launch
+        # over every item row, K >= 2): its gradient gI/(K+1) + ego rows is final
+        # before the chain starts, so it is formed in a side table (zero off the
+        # batch items, like g_if) that the product's epilogue reads, and the
+        # 28 B / parameter pass overlaps the product's gathers. Bitwise the
+        # separate _item_adam (same additions, same Adam arithmetic).
+        side = item_adam and reduce is None and self.K >= 2
+        adam_i = None
+        if side:
+            ga = self._item_grad_side()   # (a -1 "no negative" row is skipped)
+            call("bbgr_rows_copy", item_rows.numel(), ptr(item_rows), ptr(self.g_if),
+                 ld(self.g_if), ptr(ga), ld(ga), self.d, st)
+            call("bbgr_rows_axpy", item_rows.numel(), ptr(item_rows), a_gl, ptr(self.item_w),
+                 ld(self.item_w), ptr(ga), ld(ga), self.d, st)
+            adam_i = AdamRows(self.item_w, self.m_i, self.v_i, self.step_count, self.lr,
+                              dev=self.dev_state, grad=ga, grad_scale=gl)
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
                  src_bits=self._bits(masks), frontier_list=self._flist(masks),
-                 before_last=before_last, reduce=reduce)
-        if item_adam:
+                 before_last=before_last, reduce=reduce, adam_i=adam_i)
+        if side:   # the side table is all-zero between steps
+            call("bbgr_rows_zero", item_rows.numel(), ptr(item_rows), ptr(ga), ld(ga), self.d,
+                 st)
+        elif item_adam:
             self._item_adam(item_rows, self.g_if, a_gl, gl)
+
+    def _item_grad_side(self) -> torch.Tensor:
+        """The fused item Adam's gradient table [I, d], all-zero between steps."""
+        ga = getattr(self, "_g_item_side", None)
+        if ga is None:
+            ga = self._g_item_side = torch.zeros_like(self.g_if)
+        return ga
 
     def _item_adam(self, item_rows, g, a_gl: float, gl: float) -> None:
         """GS item Adam: grad_i0 = gl * (gI + a_gl * i0[pos, neg]) (Version-2:

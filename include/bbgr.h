@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 5
+#define BBGR_ABI_VERSION 6
 
 typedef enum {
   BBGR_OK = 0,
@@ -268,6 +268,13 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   min(n_row_list, *row_count) rows; n_row_list is its capacity. For a list  */
 /*   built on the stream (a captured step): a fixed grid of short-row          */
 /*   workgroups walks it, so the host never reads the length.                  */
+/* adam_grad (nullable, with adam_param; ABI 6): the fused Adam's gradient is */
+/*   adam_grad_scale * adam_grad[row] (row stride adam_grad_ld) instead of the */
+/*   row value, and y is written as usual: an item-row product of the GS      */
+/*   backward carries the item table's Adam step, whose gradient (the sparse  */
+/*   BPR rows / (K+1) + ego rows) is final before the product runs, so the   */
+/*   separate pass over the item table (28 B / parameter) overlaps the        */
+/*   product's gathers. Same rounding as bbgr_adam with grad_scale.          */
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
@@ -327,6 +334,9 @@ typedef struct {
   const uint32_t *src_bits;
   const int64_t *row_count;
   const int32_t *acc_in_map;
+  const float *adam_grad;
+  int64_t adam_grad_ld;
+  float adam_grad_scale;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -456,11 +466,25 @@ int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha, const float *src,
                    int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
                    bbgr_stream_t stream);
 
+/* dst[idx[k], :d] = src[idx[k], :d] for k < n (ABI 6; idx[k] < 0 skipped,  */
+/* repeated rows write the same value). d and both ld multiples of 4, tables */
+/* 16-byte aligned. Copies a sparse table's batch rows into another.         */
+int bbgr_rows_copy(int64_t n, const int64_t *idx, const float *src, int64_t ldsrc,
+                   float *dst, int64_t lddst, int32_t d, bbgr_stream_t stream);
+
 /* dst[k, :d] = src[idx[k], :d] for k < n (zero row where idx[k] < 0). d and
  * both ld multiples of 4, tables 16-byte aligned. Compacts frontier rows for
  * the sparse multi-GPU exchange (the inverse is bbgr_epilogue's row_list). */
 int bbgr_rows_gather(int64_t n, const int64_t *idx, const float *src, int64_t ldsrc,
                      float *dst, int64_t lddst, int32_t d, bbgr_stream_t stream);
+
+/* bbgr_scatter_add_rows for DISTINCT indices (ABI 6): dst[idx[k], :d] +=     */
+/* (0 + src[k, :d]), the same additions a one-addend segment makes, in one   */
+/* launch without the sort (a training batch of distinct users). Negative or */
+/* >= n_dst indices are skipped; repeated indices are the caller's error.    */
+int bbgr_rows_add_unique(int64_t n, const int64_t *idx, const float *src, int64_t ldsrc,
+                         float *dst, int64_t lddst, int32_t d, int64_t n_dst,
+                         bbgr_stream_t stream);
 
 /* Deterministic index_add_: dst[idx[k], :d] += src[k, :d] for k < n, with   */
 /* the addends of each destination row summed in ascending k and added once  */

@@ -799,6 +799,26 @@ def test_graph_from_memmaps_matches_array(tmp_path):
         assert torch.equal(g.item_csr.indices, g1.item_csr.indices)
 
 
+@pytest.mark.parametrize("d", [16, 64, 256])
+def test_rows_add_unique_is_bitwise_the_sorted_scatter(d):
+    """bbgr_rows_add_unique (distinct indices, no sort) == bbgr_scatter_add_rows
+    bit for bit, signed zeros included (a one-addend segment adds 0 + x), onto
+    a zero and a non-zero destination; invalid indices skipped."""
+    from bbgr.scatter import RowScatter
+    rng = np.random.default_rng(50 + d)
+    n_dst = 5000
+    idx = rng.permutation(n_dst + 40)[:3000] - 20       # distinct, some out of range
+    src = rng.normal(size=(idx.size, d)).astype(np.float32)
+    src[:7] = -0.0
+    src[7:9] = 0.0
+    for base in (np.zeros((n_dst, d), np.float32), rng.normal(size=(n_dst, d)).astype(np.float32)):
+        base[:3] = -0.0
+        a = RowScatter()(t(base), t(idx, torch.int64), t(src))
+        b = RowScatter()(t(base), t(idx, torch.int64), t(src), unique=True)
+        np.testing.assert_array_equal(b.cpu().numpy().view(np.uint32),
+                                      a.cpu().numpy().view(np.uint32))
+
+
 @pytest.mark.parametrize("d", [8, 16, 32, 64, 128, 256])
 def test_scatter_add_rows_matches_index_add(d):
     """bbgr_scatter_add_rows == numpy add.at (sequential ascending order) bit
