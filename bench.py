@@ -429,9 +429,12 @@ def main():
     ap.add_argument("--vertex-order", default="degree", choices=["degree", "input"],
                     help="number users / items by descending degree inside the graph "
                          "(hot rows cached, cold rows streamed) or keep the input ids")
-    ap.add_argument("--native-comm", action="store_true",
-                    help="N>1: item all-reduces through the C ABI's own RCCL communicator "
-                         "(bbgr_allreduce_items) instead of torch.distributed")
+    ap.add_argument("--native-comm", nargs="?", const="stream", default="off",
+                    choices=["off", "stream", "inline"],
+                    help="N>1 user rows: the item exchange through the C ABI's own RCCL "
+                         "communicator (bbgr_allreduce_items) on a comm stream ('stream', "
+                         "the bare flag), or every collective of the step inline on the "
+                         "compute stream ('inline': one column chain)")
     ap.add_argument("--column-chains", type=int, default=None,
                     help="users partition: run the propagation as this many column chains "
                          "(d/C columns each, own stream, issue interleaved per exchange) so "
@@ -538,6 +541,10 @@ def main():
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} d={d} K={K} B={B} "
         f"scaling={scaling} generated in {time.perf_counter() - t0:.1f}s")
 
+    if args.native_comm == "inline":   # one chain, no ranges: nothing overlaps the wire
+        args.column_chains = 1
+        args.exchange_parts = 1 if args.exchange_parts is None else args.exchange_parts
+        args.frontier_parts = 1 if args.frontier_parts is None else args.frontier_parts
     if args.column_chains is None:
         # small per-rank shards only: there the exchange outlasts the rank's
         # item products; a big shard's item product hides it by itself (C5)
@@ -550,8 +557,8 @@ def main():
         args.frontier_parts = 1 if args.column_chains > 1 else 2
     xp = dict(exchange_parts=args.exchange_parts, frontier_parts=args.frontier_parts,
               vertex_order=args.vertex_order)
-    if args.native_comm:
-        xp["native_comm"] = True
+    if args.native_comm != "off":
+        xp["native_comm"] = True if args.native_comm == "stream" else "inline"
     if args.column_chains > 1:
         xp["column_chains"] = args.column_chains
     frontier = {"auto": "auto", "on": True, "off": False}[args.frontier]

@@ -164,6 +164,8 @@ _SIGNATURES = {
     "bbgr_comm_init": ([_P, c_int32, c_int32, _P], c_int32),
     "bbgr_comm_destroy": ([_P], c_int32),
     "bbgr_allreduce_items": ([_P, _P, c_int64, _P], c_int32),
+    "bbgr_comm_allreduce": ([_P, _P, c_int64, c_int32, c_int32, _P], c_int32),
+    "bbgr_comm_allgather": ([_P, _P, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_ewa_normalize": ([ctypes.POINTER(CsrStruct), _P, _P, _P, _P, c_int64, c_int32, c_int32,
                             c_float, c_float, c_float, _P, _P, _P, _P,
                             ctypes.POINTER(c_size_t), _P], c_int32),

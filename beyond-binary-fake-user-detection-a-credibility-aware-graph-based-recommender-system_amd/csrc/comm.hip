@@ -21,6 +21,8 @@ struct RcclApi {
   ncclResult_t (*comm_destroy)(ncclComm_t);
   ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t,
                              ncclComm_t, hipStream_t);
+  ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
+                             hipStream_t);
   const char *(*error_string)(ncclResult_t);
   bool ok;
 };
@@ -35,8 +37,10 @@ static RcclApi &rccl() {
     a.comm_init_rank = reinterpret_cast<decltype(a.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
     a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
     a.all_reduce = reinterpret_cast<decltype(a.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(h, "ncclAllGather"));
     a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
-    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_reduce;
+    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_reduce &&
+           a.all_gather;
     return a;
   }();
   return api;
@@ -46,6 +50,25 @@ static int rccl_fail(ncclResult_t r, const char *what) {
   const char *msg = rccl().error_string ? rccl().error_string(r) : "?";
   set_error("%s: RCCL error %d (%s)", what, (int)r, msg);
   return BBGR_ERR_HIP;
+}
+
+static bool nccl_dtype(int32_t dt, ncclDataType_t *t) {
+  switch (dt) {
+    case BBGR_DT_U8: *t = ncclUint8; return true;
+    case BBGR_DT_I32: *t = ncclInt32; return true;
+    case BBGR_DT_I64: *t = ncclInt64; return true;
+    case BBGR_DT_F32: *t = ncclFloat32; return true;
+    default: return false;
+  }
+}
+
+static bool nccl_op(int32_t op, ncclRedOp_t *o) {
+  switch (op) {
+    case BBGR_RED_SUM: *o = ncclSum; return true;
+    case BBGR_RED_MAX: *o = ncclMax; return true;
+    case BBGR_RED_MIN: *o = ncclMin; return true;
+    default: return false;
+  }
 }
 
 #define BBGR_RCCL(call, what)                              \
@@ -95,5 +118,33 @@ extern "C" int bbgr_allreduce_items(void *comm, float *items, int64_t count,
   BBGR_RCCL(rccl().all_reduce(items, items, (size_t)count, ncclFloat32, ncclSum,
                               static_cast<ncclComm_t>(comm), as_stream(stream)),
             "ncclAllReduce");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_comm_allreduce(void *comm, void *buf, int64_t count, int32_t dtype,
+                                   int32_t op, bbgr_stream_t stream) {
+  ncclDataType_t t;
+  ncclRedOp_t o;
+  BBGR_REQUIRE(comm && count >= 0 && (count == 0 || buf) && nccl_dtype(dtype, &t) &&
+                   nccl_op(op, &o),
+               "bbgr_comm_allreduce: bad args");
+  if (count == 0) return BBGR_OK;
+  BBGR_REQUIRE(rccl().ok, "bbgr_comm_allreduce: librccl.so.1 not found");
+  BBGR_RCCL(rccl().all_reduce(buf, buf, (size_t)count, t, o, static_cast<ncclComm_t>(comm),
+                              as_stream(stream)),
+            "ncclAllReduce");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_comm_allgather(void *comm, const void *send, void *recv, int64_t count,
+                                   int32_t dtype, bbgr_stream_t stream) {
+  ncclDataType_t t;
+  BBGR_REQUIRE(comm && count >= 0 && (count == 0 || (send && recv)) && nccl_dtype(dtype, &t),
+               "bbgr_comm_allgather: bad args");
+  if (count == 0) return BBGR_OK;
+  BBGR_REQUIRE(rccl().ok, "bbgr_comm_allgather: librccl.so.1 not found");
+  BBGR_RCCL(rccl().all_gather(send, recv, (size_t)count, t, static_cast<ncclComm_t>(comm),
+                              as_stream(stream)),
+            "ncclAllGather");
   return BBGR_OK;
 }

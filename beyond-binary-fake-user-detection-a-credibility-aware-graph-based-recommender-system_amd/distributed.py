@@ -106,10 +106,11 @@ def owner_bounds(num_items: int, world: int) -> list[int]:
 
 
 def refresh_from_owners(table: torch.Tensor, rows: torch.Tensor, bounds: list[int],
-                        group=None) -> None:
+                        group=None, gather=None) -> None:
     """table[rows] <- the owning ranks' rows (rank r owns [bounds[r], bounds[r+1])):
     one all-gather of every rank's table[rows], then each row copied from its
-    owner's slot (exact copies; duplicate rows write the same value)."""
+    owner's slot (exact copies; duplicate rows write the same value).
+    `gather(out, inp)`: the all-gather to use (default: torch.distributed's)."""
     n, d = rows.numel(), table.shape[1]
     world = len(bounds) - 1
     if n == 0 or world == 1:
@@ -120,7 +121,10 @@ def refresh_from_owners(table: torch.Tensor, rows: torch.Tensor, bounds: list[in
     inner = torch.tensor(bounds[1:-1], dtype=torch.int64, device=rows.device)
     mine = table.index_select(0, rows)
     got = torch.empty(world * n, d, dtype=table.dtype, device=table.device)
-    _all_gather(got, mine, group)
+    if gather is None:
+        _all_gather(got, mine, group)
+    else:
+        gather(got, mine)
     owner = torch.searchsorted(inner, rows, right=True)
     pick = owner * n + torch.arange(n, device=rows.device)
     table.index_copy_(0, rows, got.index_select(0, pick))
@@ -139,15 +143,29 @@ def gather_owned(owned: torch.Tensor, bounds: list[int], group=None) -> torch.Te
     return torch.cat([got[r * m: r * m + sizes[r]] for r in range(world)])
 
 
+_DTYPES = {torch.uint8: 0, torch.int32: 1, torch.int64: 2, torch.float32: 3}
+_REDOPS = {"sum": 0, "max": 1, "min": 2}
+
+
 class RcclItemComm:
     """The item exchange through the C ABI's own RCCL communicator
     (bbgr_comm_init / bbgr_allreduce_items) instead of torch.distributed's
     collective machinery. The unique id travels once over `group`; each
     all-reduce is enqueued on a high-priority comm stream behind the compute
     stream's work so far, and wait() makes the compute stream wait for all of
-    them."""
+    them.
 
-    def __init__(self, group=None, device=None):
+    inline=True: every collective runs ON the caller's current stream, in
+    issue order (bbgr_allreduce_items / bbgr_comm_allreduce /
+    bbgr_comm_allgather): no hop to a comm stream and back (two cross-stream
+    waits, ~26 us per exchange on MI355X) where nothing is to overlap the
+    collective anyway — one column chain, the exchange not cut in ranges.
+    The sharded step then routes ALL its collectives (batch ids, masks, BPR
+    rows, item refresh, loss) through this one communicator, so every rank's
+    collectives run in one order on one stream."""
+
+    def __init__(self, group=None, device=None, inline: bool = False):
+        self.inline = bool(inline)
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         ids = (ctypes.c_uint8 * 128)()
         if rank == 0:
@@ -164,6 +182,9 @@ class RcclItemComm:
         self.pending = False
 
     def allreduce_async(self, t: torch.Tensor) -> None:
+        if self.inline:
+            call("bbgr_allreduce_items", self.comm, ptr(t), t.numel(), stream_handle())
+            return
         self.stream.wait_stream(torch.cuda.current_stream(t.device))
         t.record_stream(self.stream)   # the allocator must not reuse t before the sum lands
         call("bbgr_allreduce_items", self.comm, ptr(t), t.numel(), self.stream.cuda_stream)
@@ -173,6 +194,20 @@ class RcclItemComm:
         if self.pending:
             torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
             self.pending = False
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None:
+        """In-place all-reduce of a contiguous tensor on the current stream."""
+        if not t.is_contiguous():
+            raise ValueError("all_reduce of a non-contiguous tensor")
+        call("bbgr_comm_allreduce", self.comm, ptr(t), t.numel(), _DTYPES[t.dtype], _REDOPS[op],
+             stream_handle())
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """out (world * inp.numel() elements, rank-major) <- every rank's inp."""
+        if not (out.is_contiguous() and inp.is_contiguous()) or out.dtype != inp.dtype:
+            raise ValueError("all_gather: contiguous tensors of one dtype")
+        call("bbgr_comm_allgather", self.comm, ptr(inp), ptr(out), inp.numel(),
+             _DTYPES[inp.dtype], stream_handle())
 
     def close(self) -> None:
         if self.comm:
@@ -231,6 +266,9 @@ class ItemExchange:
     def __call__(self, t: torch.Tensor) -> None:
         if not t.is_contiguous():
             raise ValueError("item exchange: all-reduce of a non-contiguous table")
+        if self.native is not None and self.native.inline:
+            self.native.all_reduce(t)
+            return
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def ranges(self, csr):
@@ -435,8 +473,18 @@ class ShardedTrainer(FusedTrainer):
         self.order, self.lr, self.reg = order, lr, reg
         self.lambda_fair, self.seed = lambda_fair, seed
         self.exchange = ItemExchange(group, exchange_parts, frontier_parts)
-        if native_comm:   # item all-reduces through bbgr_allreduce_items (own RCCL comm)
-            self.exchange.native = RcclItemComm(group, dev)
+        # native_comm: True / "stream" = the item all-reduces through the C ABI's
+        # own RCCL communicator on a comm stream; "inline" = every collective of
+        # the step through it, on the compute stream (RcclItemComm)
+        if native_comm not in (False, True, "stream", "inline", None):
+            raise ValueError("native_comm must be False, True, 'stream' or 'inline'")
+        inline = native_comm == "inline"
+        if inline and int(column_chains) > 1:
+            raise ValueError("native_comm='inline' runs one chain (chains overlap their "
+                             "exchanges on a shared comm stream)")
+        if native_comm:
+            self.exchange.native = RcclItemComm(group, dev, inline=inline)
+        self._inline = self.exchange.native if inline else None
 
         def global_degrees(deg: torch.Tensor) -> torch.Tensor:
             g = deg.to(torch.int64)
@@ -610,6 +658,20 @@ class ShardedTrainer(FusedTrainer):
                 prod.first_layer_values()
         return chains
 
+    def _gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """All-gather of the step (batch ids, BPR rows, item refresh)."""
+        if self._inline is not None:
+            self._inline.all_gather(out, inp)
+        else:
+            _all_gather(out, inp, self.group)
+
+    def _reduce(self, t: torch.Tensor) -> None:
+        """In-place sum over the ranks (item mask bytes, loss)."""
+        if self._inline is not None:
+            self._inline.all_reduce(t)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
     def _exchanges(self) -> list:
         return [ch.exchange for ch in self.chains] if self.chains else [self.exchange]
 
@@ -660,7 +722,7 @@ class ShardedTrainer(FusedTrainer):
         f.users = users
         f.frontier = bool(self.frontier)
         self.sampler.sample(users, f.posneg[:B], f.posneg[B:])
-        _all_gather(f.all_items, f.posneg, self.group)
+        self._gather(f.all_items, f.posneg)
         f.items_fresh = False
         if not self.frontier:
             return
@@ -674,7 +736,7 @@ class ShardedTrainer(FusedTrainer):
             uc = self.graph.user_csr
             call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), 1,
                  ptr(f.mask_i), st)
-        dist.all_reduce(f.mask_i, op=dist.ReduceOp.SUM, group=self.group)  # <= world: no wrap
+        self._reduce(f.mask_i)   # byte sum <= world: no wrap
         if self.sparse_exchange:
             self._list_rows(f)
 
@@ -746,7 +808,8 @@ class ShardedTrainer(FusedTrainer):
     def _refresh_items(self, rows: torch.Tensor) -> None:
         """item_w[rows] <- the owners' current values (refresh_from_owners)."""
         if self._items_stale:
-            refresh_from_owners(self.item_w, rows, self.item_bounds, self.group)
+            refresh_from_owners(self.item_w, rows, self.item_bounds, self.group,
+                                gather=self._gather)
 
     def sync_items(self) -> dict:
         """Collective (every rank calls it): make the whole item weight table
@@ -848,7 +911,7 @@ class ShardedTrainer(FusedTrainer):
         # item gradient of the global batch: every rank's (pos, neg) rows
         # (gathered with the batch) and their per-triple gradient rows, summed
         # in rank-major order
-        _all_gather(self.all_contrib, self.contrib[B: 3 * B], self.group)
+        self._gather(self.all_contrib, self.contrib[B: 3 * B])
         self.scatter(self.g_if, self.all_items, self.all_contrib)
         alpha = 2.0 * self.reg / self.B_global            # ego L2 (Version-2:503-507)
         if self.chains:
@@ -885,7 +948,7 @@ class ShardedTrainer(FusedTrainer):
         f.rows = None
         for ex in self._exchanges():
             ex.clear_rows()
-        dist.all_reduce(self.loss, op=dist.ReduceOp.SUM, group=self.group)
+        self._reduce(self.loss)
         self.loss.mul_(1.0 / self.world)
         return self.loss
 

@@ -246,8 +246,8 @@ class FusedTrainer:
                       dev=self.dev_state)
         # restore the all-zero invariant of the sparse gradient tables
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
-        call("bbgr_rows_zero", B, ptr(pos), ptr(self.g_if), ld(self.g_if), self.d, st)
-        call("bbgr_rows_zero", B, ptr(neg), ptr(self.g_if), ld(self.g_if), self.d, st)
+        call("bbgr_rows_zero", 2 * B, ptr(self.posneg), ptr(self.g_if), ld(self.g_if), self.d,
+             st)   # (pos and neg: posneg[:B], posneg[B:2B])
         if masks is not None:
             self._set_masks(users, pos, neg, 0)
         return self.loss
@@ -353,15 +353,20 @@ class FusedTrainer:
         call("bbgr_mark_rows", B, ptr(users), value, ptr(self.mask_u), self.U, st)
         uc = self.graph.user_csr
         lst = getattr(self, "item_list", None)
+        # pos and neg are one contiguous vector when they are the trainer's own
+        # posneg halves (both marked by one launch)
+        pn = (pos.data_ptr() == self.posneg.data_ptr()
+              and neg.data_ptr() == self.posneg.data_ptr() + 8 * B)
+        items = [(2 * B, ptr(self.posneg))] if pn else [(B, ptr(pos)), (B, ptr(neg))]
         if value and lst is not None:   # flag + list the frontier (GS)
             _lib.check_word_padded(self.mask_i, self.I, "item mask")
             li = (ptr(self.mask_i), self.I, ptr(lst), ptr(self.item_count), st)
-            call("bbgr_mark_list", B, ptr(pos), None, None, *li)
-            call("bbgr_mark_list", B, ptr(neg), None, None, *li)
+            for n, p in items:
+                call("bbgr_mark_list", n, p, None, None, *li)
             call("bbgr_mark_list", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), *li)
         else:
-            call("bbgr_mark_rows", B, ptr(pos), value, ptr(self.mask_i), self.I, st)
-            call("bbgr_mark_rows", B, ptr(neg), value, ptr(self.mask_i), self.I, st)
+            for n, p in items:
+                call("bbgr_mark_rows", n, p, value, ptr(self.mask_i), self.I, st)
             if self.order == ORDER_GS:
                 call("bbgr_mark_neighbors", B, ptr(users), ptr(uc.indptr), ptr(uc.indices),
                      value, ptr(self.mask_i), st)

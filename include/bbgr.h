@@ -125,9 +125,11 @@ int bbgr_slots_from_perms(int64_t nnz, const int32_t *perm_a, const int32_t *per
 /* degree[j] = number of e < n_ids with ids[e] == j, j < n (exact).           */
 int bbgr_degree_count(int64_t n_ids, const int32_t *ids, int32_t n, int32_t *degree,
                       bbgr_stream_t stream);
-/* The same with 8 replicated counter arrays (one per XCD's workgroups) summed */
-/* at the end: power-law ids contend 8x less (workspace: 32*n bytes; query     */
-/* with workspace == NULL).                                                    */
+/* The same with a workspace (query with workspace == NULL): below 4M ids, 8  */
+/* replicated counter arrays (one per XCD's workgroups) summed at the end     */
+/* (power-law ids contend 8x less; 32*n bytes); from 4M ids on, a radix sort */
+/* of the ids, a run-length encode and one scatter of the run lengths (no    */
+/* atomics; ~4*n_ids + 8*n bytes + sort scratch). Ids must lie in [0, n).    */
 int bbgr_degree_count_ws(int64_t n_ids, const int32_t *ids, int32_t n, int32_t *degree,
                          void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
 /* perm[new] = old id, rank[old] = new id, by descending degree; equal degrees */
@@ -578,6 +580,17 @@ int bbgr_comm_init(void **comm_out, int32_t nranks, int32_t rank, const uint8_t 
 int bbgr_comm_destroy(void *comm);
 /* In-place sum over the ranks of items[count] (fp32), stream-ordered.       */
 int bbgr_allreduce_items(void *comm, float *items, int64_t count, bbgr_stream_t stream);
+/* The sharded step's other collectives on the same communicator (ABI 6), so */
+/* a caller can keep EVERY collective of a step on its compute stream, in    */
+/* issue order (no hop to a comm stream and back): in-place all-reduce of    */
+/* buf[count] and all-gather of count elements per rank into recv[nranks *   */
+/* count] (rank-major). dtype: bbgr_dtype; op: bbgr_redop.                   */
+typedef enum { BBGR_DT_U8 = 0, BBGR_DT_I32 = 1, BBGR_DT_I64 = 2, BBGR_DT_F32 = 3 } bbgr_dtype;
+typedef enum { BBGR_RED_SUM = 0, BBGR_RED_MAX = 1, BBGR_RED_MIN = 2 } bbgr_redop;
+int bbgr_comm_allreduce(void *comm, void *buf, int64_t count, int32_t dtype, int32_t op,
+                        bbgr_stream_t stream);
+int bbgr_comm_allgather(void *comm, const void *send, void *recv, int64_t count,
+                        int32_t dtype, bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Negative / positive sampling                                               */

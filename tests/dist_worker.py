@@ -154,9 +154,13 @@ def rccl_single_rank(out_dir, variant, order="input"):
                             vertex_order=order, column_chains=2, **kw)   # interleaved chains
     chains_nat = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=1,
                                 vertex_order=order, column_chains=2, native_comm=True, **kw)
+    # every collective of the step on the compute stream (bbgr_comm_allreduce /
+    # _allgather / bbgr_allreduce_items inline)
+    inl = ShardedTrainer(e, U, I, variant, device="cuda:0", exchange_parts=3,
+                         vertex_order=order, native_comm="inline", **kw)
     out = {}
     for tag, tr in (("sharded", sh), ("single", one), ("native", nat), ("chains", chains),
-                    ("chains_native", chains_nat)):
+                    ("chains_native", chains_nat), ("inline", inl)):
         out[f"{tag}_loss"] = np.array([float(tr.step()) for _ in range(3)])
         out[f"{tag}_user_w"] = tr.user_w.cpu().numpy()
         out[f"{tag}_item_w"] = tr.item_w.cpu().numpy()
@@ -167,6 +171,7 @@ def rccl_single_rank(out_dir, variant, order="input"):
     np.savez(os.path.join(out_dir, "rccl1.npz"), **out)
     nat.close()   # bbgr_comm_destroy
     chains_nat.close()
+    inl.close()
     dist.destroy_process_group()
 
 

@@ -169,8 +169,10 @@ def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, 
         a, b = z[f"sharded_{key}"], z[f"single_{key}"]
         err = np.linalg.norm(a - b) / np.linalg.norm(b)
         assert err < 1e-6, (key, err)
-        # the C ABI's own RCCL communicator (bbgr_allreduce_items) == torch's
+        # the C ABI's own RCCL communicator (bbgr_allreduce_items) == torch's,
+        # on its comm stream and with every collective inline on the compute stream
         np.testing.assert_array_equal(z[f"native_{key}"], z[f"sharded_{key}"])
+        np.testing.assert_array_equal(z[f"inline_{key}"], z[f"sharded_{key}"])
         # two interleaved column chains on their own streams, through torch's
         # collectives and through the C ABI's communicator (shared by the chains)
         for tag in ("chains", "chains_native"):
@@ -179,6 +181,7 @@ def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, 
     np.testing.assert_allclose(z["chains_loss"], z["single_loss"], rtol=1e-6)
     np.testing.assert_allclose(z["chains_native_loss"], z["single_loss"], rtol=1e-6)
     np.testing.assert_array_equal(z["native_loss"], z["sharded_loss"])
+    np.testing.assert_array_equal(z["inline_loss"], z["sharded_loss"])
 
 
 @pytest.mark.parametrize("variant,frontier,order,world", [

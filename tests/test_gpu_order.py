@@ -28,8 +28,9 @@ def rel(got, ref):
     return np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)
 
 
-@pytest.mark.parametrize("n", [1, 7, 1000, 300_000])
+@pytest.mark.parametrize("n", [1, 7, 1000, 300_000, 2_000_000])
 def test_degree_count_and_order_match_numpy(n):
+    """(n = 2M: 6M ids, the sort / run-length path of bbgr_degree_count_ws)"""
     from bbgr.graph import _degree_count, _relabel
     rng = np.random.default_rng(n)
     ids = rng.zipf(1.3, size=3 * n + 5).astype(np.int64) % n      # many ties, some zeros

@@ -40,6 +40,9 @@ def main():
                     help="item rows owned per rank as at world size N (default: --parts-of): "
                          "the probe's rank runs the item Adam on I/N rows, as an N-rank step "
                          "does (at world size 1 it would own every row)")
+    ap.add_argument("--native-comm", default="off", choices=["off", "stream", "inline"],
+                    help="the exchange through the C ABI's RCCL communicator: on a comm "
+                         "stream, or every collective inline on the compute stream")
     ap.add_argument("--profile", default="",
                     help="cProfile the timed steps into <this>.c<chains>x<parts>f<fparts>")
     a = ap.parse_args()
@@ -63,7 +66,9 @@ def main():
                             batch_size=max(1, B // a.parts_of), device="cuda",
                             vertex_order="degree", exchange_parts=xp,
                             overlap_item_adam=True, column_chains=chains,
-                            frontier_parts=fparts)
+                            frontier_parts=fparts,
+                            native_comm={"off": False, "stream": True,
+                                         "inline": "inline"}[a.native_comm])
         own = a.parts_of if a.own_items_of is None else a.own_items_of
         if own > 1 and tr.own_items:   # an N-rank step's item Adam share (rows [0, I/N))
             n = I // own
@@ -91,6 +96,7 @@ def main():
         print(json.dumps({"config": a.config, "rank_of": a.parts_of, "users": hi - lo,
                           "edges": int(local.shape[1]), "exchange_parts": xp,
                           "column_chains": chains, "frontier_parts": fparts,
+                          "native_comm": a.native_comm,
                           "item_rows_owned": tr.ib - tr.ia,
                           "ms_per_step": ms, "host_issue_ms": 1000.0 * issue / a.steps}),
               flush=True)
