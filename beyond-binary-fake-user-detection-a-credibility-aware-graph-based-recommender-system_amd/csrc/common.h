@@ -101,6 +101,8 @@ __device__ __forceinline__ float4 ld_nt(const float4 *p) {
   const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
   return make_float4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ int ld_nt(const int *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float ld_nt(const float *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_nt(float4 *p, float4 v) {
   f4v w;
   w.x = v.x;

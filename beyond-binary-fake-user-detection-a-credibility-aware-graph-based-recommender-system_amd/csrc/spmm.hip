@@ -98,6 +98,21 @@ __device__ __forceinline__ float4 f4_mul(float a, float4 x) {
   return make_float4(a * x.x, a * x.y, a * x.z, a * x.w);
 }
 
+// Column indices and per-edge values are read once per launch (200 MB each at
+// C4). Streaming (non-temporal) loads for them, so they would not displace
+// gathered rows from L2 / the Infinity Cache, measured slower (round 4 A/B,
+// tools/probes/gpu_ab_nt_index.sh: C4 step 16.72 -> 16.84 ms, masked user
+// product 1.115 -> 1.136 ms on one box): default-policy loads
+// (BBGR_NT_INDEX=1 builds the streamed form).
+#ifndef BBGR_NT_INDEX
+#define BBGR_NT_INDEX 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_edge(const T *p) {
+  if constexpr (BBGR_NT_INDEX != 0) return ld_nt(p);
+  return *p;
+}
+
 // Per-width tuning (measured with tools/ab_spmm.sh A/B builds; every value
 // can be overridden with -D for such builds):
 //   row_u        source rows in flight per 16-lane group, one-row kernels
@@ -283,10 +298,10 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     int my = -1;
     float mw = 0.f;
     if (lane < n && ((live >> lane) & 1u)) {
-      my = P.indices[e0 + lane];
+      my = ld_edge(P.indices + e0 + lane);
       if (MASKED && !BITS && P.src_mask && !P.src_mask[my]) my = -1;   // exact-zero source row
       if (my >= 0) {
-        if (WMODE == 1) mw = P.edge_val[e0 + lane];
+        if (WMODE == 1) mw = ld_edge(P.edge_val + e0 + lane);
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
       }
     }
@@ -470,18 +485,18 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     int myA = -1, myB = -1;
     float mwA = 0.f, mwB = 0.f;
     if (lane < na) {
-      myA = P.indices[ebA + o + lane];
+      myA = ld_edge(P.indices + ebA + o + lane);
       if (MASKED && P.src_mask && !P.src_mask[myA]) myA = -1;
       if (myA >= 0) {
-        if (WMODE == 1) mwA = P.edge_val[ebA + o + lane];
+        if (WMODE == 1) mwA = ld_edge(P.edge_val + ebA + o + lane);
         if (WMODE == 2) mwA = P.col_scale[myA] * P.col_scale_s;
       }
     }
     if (lane < nb) {
-      myB = P.indices[ebB + o + lane];
+      myB = ld_edge(P.indices + ebB + o + lane);
       if (MASKED && P.src_mask && !P.src_mask[myB]) myB = -1;
       if (myB >= 0) {
-        if (WMODE == 1) mwB = P.edge_val[ebB + o + lane];
+        if (WMODE == 1) mwB = ld_edge(P.edge_val + ebB + o + lane);
         if (WMODE == 2) mwB = P.col_scale[myB] * P.col_scale_s;
       }
     }
