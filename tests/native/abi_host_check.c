@@ -108,6 +108,27 @@ int main(void) {
   expect_error("adam_f32 negative n", bbgr_adam_f32(-1, f4, f4, f4, f4, 1e-3f, 0.9f, 0.999f,
                                                     1e-8f, 0.f, 1.f, 1.f, 1.f, NULL));
   expect_error("allreduce null comm", bbgr_allreduce_items(NULL, f4, 4, NULL));
+  expect_error("comm_allreduce null comm", bbgr_comm_allreduce(NULL, f4, 4, BBGR_DT_F32,
+                                                               BBGR_RED_SUM, NULL));
+  expect_error("comm_allreduce bad dtype", bbgr_comm_allreduce((void *)f4, f4, 4, 9,
+                                                               BBGR_RED_SUM, NULL));
+  expect_error("comm_allgather null comm", bbgr_comm_allgather(NULL, f4, f4, 4, BBGR_DT_F32,
+                                                               NULL));
+  expect_error("rows_copy bad d", bbgr_rows_copy(4, NULL, f4, 64, f4, 64, 6, NULL));
+  expect_ok("rows_copy empty", bbgr_rows_copy(0, NULL, NULL, 64, NULL, 64, 64, NULL));
+  expect_error("rows_add_unique bad ld", bbgr_rows_add_unique(4, NULL, f4, 32, f4, 64, 64, 8,
+                                                              NULL));
+  expect_ok("rows_add_unique empty", bbgr_rows_add_unique(0, NULL, NULL, 64, NULL, 64, 64, 8,
+                                                          NULL));
+  {
+    size_t need = 0;   /* sort path from 4M ids: a workspace query only */
+    expect_ok("degree_count_ws sort query",
+              bbgr_degree_count_ws((int64_t)1 << 23, NULL, 1000, NULL, NULL, &need, NULL));
+    if (need < ((size_t)1 << 25)) {
+      fprintf(stderr, "degree_count_ws sort workspace too small: %zu\n", need);
+      ++failures;
+    }
+  }
   expect_error("eval sampled null", bbgr_eval_sampled(NULL, NULL, NULL, NULL));
   expect_error("eval full null", bbgr_eval_full(NULL, NULL, NULL, NULL));
 
