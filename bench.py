@@ -784,8 +784,10 @@ def main():
         from dropin_probe import run as dropin_run
         dropin = dropin_run(args.config, edges, cred, device=dev)
         dropin["note"] = ("Version-2 LightGCN drop-in (bbgr ops: propagate, bpr_loss and "
-                          "their registered backward) + torch.optim.Adam(foreach), input "
-                          "vertex order, uniform batches (tools/dropin_probe.py)")
+                          "their registered backward; get_user_item_emb() tables deferred, "
+                          "so bpr_loss computes the batch rows only, bbgr::propagate_rows) + "
+                          "torch.optim.Adam(foreach), input vertex order, uniform batches "
+                          "(tools/dropin_probe.py)")
         if torch_ref is not None:
             dropin["speedup_vs_torch"] = torch_ref["step_ms"] / dropin["step_ms"]
     dense_equiv = 4 * K * E

@@ -98,7 +98,8 @@ def _first_slot(ids: torch.Tensor) -> torch.Tensor:
 # autograd nodes whose backward returns dense gradients for their leaf inputs
 # and takes a sparse dL/d(u_final) (bbgr::propagate_backward_rows): the C++
 # bbgr::propagate node (ops.PROPAGATE_NODE)
-PROPAGATE_NODES = {"torch::autograd::CppNode<bbgr_torch::PropagateFn>"}
+PROPAGATE_NODES = {"torch::autograd::CppNode<bbgr_torch::PropagateFn>",
+                   "torch::autograd::CppNode<bbgr_torch::PropagateRowsFn>"}
 
 
 def _from_propagate_op(final: torch.Tensor) -> bool:

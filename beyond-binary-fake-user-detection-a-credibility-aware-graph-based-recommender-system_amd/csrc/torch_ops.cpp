@@ -165,6 +165,7 @@ struct Opts {
   float acc_scale_s = 1.f;
   float gamma = 1.f;
   const uint8_t *src_mask = nullptr, *row_mask = nullptr, *add_mask = nullptr;
+  const uint8_t *acc_mask = nullptr;
   const int32_t *y_map = nullptr, *acc_map = nullptr, *add_map = nullptr;
   const int32_t *acc_in_map = nullptr;
   bool src_input = false;
@@ -208,6 +209,7 @@ static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) 
   a.src_mask = o.src_mask;
   a.row_mask = o.row_mask;
   a.add_mask = o.add_mask;
+  a.acc_mask = o.acc_mask;
   a.y_map = o.y_map;
   a.acc_map = o.acc_map;
   a.add_map = o.add_map;
@@ -337,6 +339,127 @@ static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0,
       spmm(P.fu, k == 1 ? i0 : bufI[cur], k == 1, ou);
       cur = nxt;
     }
+  }
+  return {acc_u, acc_i};
+}
+
+// A zeroed byte mask of n rows in whole 4-byte words (bbgr_mark_list sets its
+// bytes with word atomics).
+static Tensor byte_mask(int64_t n, const Tensor &like) {
+  return at::zeros({(std::max<int64_t>(n, 1) + 3) / 4 * 4}, u8(like)).narrow(0, 0, n);
+}
+
+// ids in [0, n) -> rank[ids] (graph order), anything else -> -1 (skipped by
+// the marking kernels)
+static Tensor to_graph_rows(const Tensor &ids, int64_t n, const Tensor &rank64) {
+  if (n == 0) return at::full_like(ids, -1);
+  Tensor ok = (ids >= 0).logical_and(ids < n);
+  if (!rank64.defined()) return at::where(ok, ids, at::full_like(ids, -1));
+  return at::where(ok, rank64.index_select(0, ids.clamp(0, n - 1)), at::full_like(ids, -1));
+}
+
+// The GS finals at the listed rows only (bbgr::propagate_rows): u_final at
+// `users`, i_final at `items` (the caller's rows: input ids of an input-order
+// pair); every other row of the two returned tables is left unwritten. The
+// dense layers 1..K-1 run as in forward_chain, with their layer-mean
+// accumulators touched at the listed rows only (acc_mask); layer K computes
+// the item frontier (listed items and N(listed users)) as a device-length row
+// list and the listed users only. The same per-row arithmetic as the dense
+// chain, so the listed rows hold the dense chain's bits. A training step that
+// reads the finals only at its batch rows (the reference's get_user_item_emb
+// -> bpr_loss, Version-2:858-859) skips the two last-layer full products and
+// the full-table accumulator passes. Jacobi order: the dense chain.
+static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, const Tensor &i0,
+                                               int64_t K, bool gs, const Tensor &users_,
+                                               const Tensor &items_) {
+  if (!gs || K == 0) return forward_chain(P, u0, i0, K, gs);
+  const int64_t U = P.U, I = P.I, d = u0.size(1);
+  check_table("user table", u0, U, d);
+  check_table("item table", i0, I, d);
+  Tensor users = users_.to(at::kLong).contiguous().view({-1});
+  Tensor items = items_.to(at::kLong).contiguous().view({-1});
+  Tensor acc_u = at::empty({U, d}, f32(u0)), acc_i = at::empty({I, d}, f32(u0));
+  const hipStream_t st = cur_stream();
+  // graph-order rows; masks in the caller's order (mu_in / mi_in) and in the
+  // graph's (mu / mi); non-io pairs: one order
+  Tensor ui = to_graph_rows(users, U, P.io ? P.user_rank64 : Tensor());
+  Tensor ii = to_graph_rows(items, I, P.io ? P.item_rank64 : Tensor());
+  Tensor mu = byte_mask(U, u0), mi = byte_mask(I, u0), fr = byte_mask(I, u0);
+  Tensor ulist = at::empty({std::max<int64_t>(users.numel(), 1)}, users.options());
+  Tensor flist = at::empty({std::max<int64_t>(I, 1)}, users.options());
+  Tensor ucount = at::zeros({1}, users.options()), fcount = at::zeros({1}, users.options());
+  // the distinct listed users (a list of distinct rows for the last user product)
+  check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), nullptr, nullptr,
+                       mu.data_ptr<uint8_t>(), U, ulist.data_ptr<int64_t>(),
+                       ucount.data_ptr<int64_t>(), st),
+        "bbgr_mark_list");
+  check(bbgr_mark_rows(ii.numel(), ii.data_ptr<int64_t>(), 1, mi.data_ptr<uint8_t>(), I, st),
+        "bbgr_mark_rows");
+  // the last item product's rows: listed items and every neighbour of a listed user
+  const bbgr_csr &uc = P.fu.csr;
+  check(bbgr_mark_list(ii.numel(), ii.data_ptr<int64_t>(), nullptr, nullptr,
+                       fr.data_ptr<uint8_t>(), I, flist.data_ptr<int64_t>(),
+                       fcount.data_ptr<int64_t>(), st),
+        "bbgr_mark_list");
+  check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), uc.indptr, uc.indices,
+                       fr.data_ptr<uint8_t>(), I, flist.data_ptr<int64_t>(),
+                       fcount.data_ptr<int64_t>(), st),
+        "bbgr_mark_list");
+  Tensor mu_in = mu, mi_in = mi;
+  if (P.io) {
+    mu_in = byte_mask(U, u0);
+    mi_in = byte_mask(I, u0);
+    check(bbgr_mark_rows(users.numel(), users.data_ptr<int64_t>(), 1, mu_in.data_ptr<uint8_t>(),
+                         U, st),
+          "bbgr_mark_rows");
+    check(bbgr_mark_rows(items.numel(), items.data_ptr<int64_t>(), 1, mi_in.data_ptr<uint8_t>(),
+                         I, st),
+          "bbgr_mark_rows");
+  }
+  const float gl = (float)(1.0 / (double)(K + 1));
+  const int32_t *am_u = P.io ? P.user_map.data_ptr<int32_t>() : nullptr;
+  const int32_t *am_i = P.io ? P.item_map.data_ptr<int32_t>() : nullptr;
+  Tensor int_u, int_i, iota_u, iota_i;
+  if (P.io && K >= 2) {
+    int_u = at::empty({U, d}, f32(u0));
+    int_i = at::empty({I, d}, f32(u0));
+    iota_u = iota32(U, u0);
+    iota_i = iota32(I, u0);
+  }
+  Tensor bufU = at::empty({U, d}, f32(u0)), bufI = at::empty({I, d}, f32(u0));
+  for (int64_t k = 1; k <= K; ++k) {
+    const float g = k == K ? gl : 1.f;
+    Opts oi;
+    oi.y = bufI;
+    oi.y_scale = P.feed_fwd_iu;
+    const AccPlan ai = acc_plan(k, K, i0, acc_i, int_i, am_i, iota_i);
+    set_acc(oi, ai);
+    oi.acc_mask = (ai.out_map ? mi_in : mi).data_ptr<uint8_t>();
+    oi.acc_scale = P.fi.out_scale;
+    oi.gamma = g;
+    oi.src_input = P.io && k == 1;
+    if (k == K) {   // the item frontier, listed on the device
+      oi.row_mask = fr.data_ptr<uint8_t>();
+      oi.row_list = flist.data_ptr<int64_t>();
+      oi.n_row_list = I;
+      oi.row_count = fcount.data_ptr<int64_t>();
+    }
+    spmm(P.fi, k == 1 ? u0 : bufU, k == 1, oi);
+    Opts ou;
+    if (k < K) ou.y = bufU;
+    ou.y_scale = P.feed_fwd_ui;
+    const AccPlan au = acc_plan(k, K, u0, acc_u, int_u, am_u, iota_u);
+    set_acc(ou, au);
+    ou.acc_mask = (au.out_map ? mu_in : mu).data_ptr<uint8_t>();
+    ou.acc_scale = P.fu.out_scale;
+    ou.gamma = g;
+    if (k == K) {   // the listed users only
+      ou.row_mask = mu.data_ptr<uint8_t>();
+      ou.row_list = ulist.data_ptr<int64_t>();
+      ou.n_row_list = users.numel();
+      ou.row_count = ucount.data_ptr<int64_t>();
+    }
+    spmm(P.fu, bufI, false, ou);
   }
   return {acc_u, acc_i};
 }
@@ -660,6 +783,14 @@ static std::tuple<Tensor, Tensor> propagate_cuda(const Tensor &u0, const Tensor 
   return forward_chain(*P, u0.contiguous(), i0.contiguous(), K, is_gs(order));
 }
 
+static std::tuple<Tensor, Tensor> propagate_rows_cuda(const Tensor &u0, const Tensor &i0,
+                                                      const Tensor &users, const Tensor &items,
+                                                      int64_t key, int64_t K,
+                                                      c10::string_view order) {
+  auto P = pair_of(key);
+  return forward_rows(*P, u0.contiguous(), i0.contiguous(), K, is_gs(order), users, items);
+}
+
 static std::tuple<Tensor, Tensor> propagate_backward_cuda(const Tensor &gU_, const Tensor &gI_,
                                                           int64_t key, int64_t K,
                                                           c10::string_view order) {
@@ -942,6 +1073,11 @@ static std::tuple<Tensor, Tensor> propagate_meta(const Tensor &u0, const Tensor 
                                                  int64_t, c10::string_view) {
   return {at::empty_like(u0), at::empty_like(i0)};
 }
+static std::tuple<Tensor, Tensor> propagate_rows_meta(const Tensor &u0, const Tensor &i0,
+                                                      const Tensor &, const Tensor &, int64_t,
+                                                      int64_t, c10::string_view) {
+  return {at::empty_like(u0), at::empty_like(i0)};
+}
 static std::tuple<Tensor, Tensor> propagate_backward_rows_meta(
     const Tensor &, const Tensor &vu, const Tensor &gI, int64_t num_users, int64_t, int64_t,
     c10::string_view, const c10::optional<Tensor> &, const c10::optional<Tensor> &) {
@@ -1017,6 +1153,13 @@ struct PropagateFn : public torch::autograd::Function<PropagateFn> {
     return {std::get<0>(r), std::get<1>(r)};
   }
   static variable_list backward(AutogradContext *ctx, variable_list go) {
+    auto r = propagate_grads(ctx, go);
+    return {r.first, r.second, Tensor(), Tensor(), Tensor()};
+  }
+
+  // (grad u0, grad i0) of the linear K-layer chain: a function of dL/d(finals)
+  // alone, so the rows forward (PropagateRowsFn) shares it
+  static std::pair<Tensor, Tensor> propagate_grads(AutogradContext *ctx, variable_list go) {
     const int64_t key = ctx->saved_data["key"].toInt(), K = ctx->saved_data["K"].toInt();
     const std::string order = ctx->saved_data["order"].toStringRef();
     const auto su = ctx->saved_data["su"].toIntVector(), si = ctx->saved_data["si"].toIntVector();
@@ -1035,7 +1178,7 @@ struct PropagateFn : public torch::autograd::Function<PropagateFn> {
         gI = at::zeros(si, vals.options());
       }
       auto r = h.call(gU._indices().select(0, 0), vals, gI, su[0], key, K, order, ii, vi);
-      return {std::get<0>(r), std::get<1>(r), Tensor(), Tensor(), Tensor()};
+      return {std::get<0>(r), std::get<1>(r)};
     }
     if (gU.defined() && gU.is_sparse()) gU = gU.to_dense();
     if (gI.defined() && gI.is_sparse()) gI = gI.to_dense();
@@ -1044,7 +1187,35 @@ struct PropagateFn : public torch::autograd::Function<PropagateFn> {
     if (!gI.defined()) gI = at::zeros(si, ref.options());
     static auto h = op<PropSig>("bbgr::propagate_backward");
     auto r = h.call(gU, gI, key, K, order);
-    return {std::get<0>(r), std::get<1>(r), Tensor(), Tensor(), Tensor()};
+    return {std::get<0>(r), std::get<1>(r)};
+  }
+};
+
+using PropRowsSig = std::tuple<Tensor, Tensor>(const Tensor &, const Tensor &, const Tensor &,
+                                               const Tensor &, int64_t, int64_t,
+                                               c10::string_view);
+
+// bbgr::propagate_rows: the finals valid at the listed rows only; the backward
+// is propagate's (the chain is linear: its gradient does not read the forward
+// values), so a BPR gradient over those rows flows exactly as through
+// bbgr::propagate
+struct PropagateRowsFn : public torch::autograd::Function<PropagateRowsFn> {
+  static variable_list forward(AutogradContext *ctx, const Tensor &u0, const Tensor &i0,
+                               const Tensor &users, const Tensor &items, int64_t key, int64_t K,
+                               c10::string_view order) {
+    ctx->saved_data["key"] = key;
+    ctx->saved_data["K"] = K;
+    ctx->saved_data["order"] = std::string(order);
+    ctx->saved_data["su"] = u0.sizes().vec();
+    ctx->saved_data["si"] = i0.sizes().vec();
+    at::AutoDispatchBelowADInplaceOrView g;
+    static auto h = op<PropRowsSig>("bbgr::propagate_rows");
+    auto r = h.call(u0, i0, users, items, key, K, order);
+    return {std::get<0>(r), std::get<1>(r)};
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list go) {
+    auto r = PropagateFn::propagate_grads(ctx, go);
+    return {r.first, r.second, Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
   }
 };
 
@@ -1179,6 +1350,13 @@ static std::tuple<Tensor, Tensor> propagate_autograd(const Tensor &u0, const Ten
   auto r = PropagateFn::apply(u0, i0, key, K, order);
   return {r[0], r[1]};
 }
+static std::tuple<Tensor, Tensor> propagate_rows_autograd(const Tensor &u0, const Tensor &i0,
+                                                          const Tensor &users,
+                                                          const Tensor &items, int64_t key,
+                                                          int64_t K, c10::string_view order) {
+  auto r = PropagateRowsFn::apply(u0, i0, users, items, key, K, order);
+  return {r[0], r[1]};
+}
 static std::tuple<Tensor, Tensor> jacobi_layer_autograd(const Tensor &u, const Tensor &i,
                                                         int64_t key) {
   auto r = JacobiLayerFn::apply(u, i, key);
@@ -1303,6 +1481,8 @@ static std::vector<int64_t> counters() { return {g_rows_backward.load(), g_dense
 TORCH_LIBRARY(bbgr, m) {
   m.def("propagate(Tensor u0, Tensor i0, int pair_key, int num_layers, str order) -> (Tensor, Tensor)");
   m.def("propagate_backward(Tensor gU, Tensor gI, int pair_key, int num_layers, str order) -> (Tensor, Tensor)");
+  m.def("propagate_rows(Tensor u0, Tensor i0, Tensor users, Tensor items, int pair_key, "
+        "int num_layers, str order) -> (Tensor, Tensor)");
   m.def("propagate_backward_rows(Tensor iu, Tensor vu, Tensor gI, int num_users, int pair_key, "
         "int num_layers, str order, Tensor? ii=None, Tensor? vi=None) -> (Tensor, Tensor)");
   m.def("jacobi_layer(Tensor u, Tensor i, int pair_key) -> (Tensor, Tensor)");
@@ -1325,6 +1505,7 @@ TORCH_LIBRARY(bbgr, m) {
 
 TORCH_LIBRARY_IMPL(bbgr, CUDA, m) {
   m.impl("propagate", &bbgr_torch::propagate_cuda);
+  m.impl("propagate_rows", &bbgr_torch::propagate_rows_cuda);
   m.impl("propagate_backward", &bbgr_torch::propagate_backward_cuda);
   m.impl("propagate_backward_rows", &bbgr_torch::propagate_backward_rows_cuda);
   m.impl("jacobi_layer", &bbgr_torch::jacobi_layer_cuda);
@@ -1338,6 +1519,7 @@ TORCH_LIBRARY_IMPL(bbgr, CUDA, m) {
 
 TORCH_LIBRARY_IMPL(bbgr, Meta, m) {
   m.impl("propagate", &bbgr_torch::propagate_meta);
+  m.impl("propagate_rows", &bbgr_torch::propagate_rows_meta);
   m.impl("propagate_backward", &bbgr_torch::propagate_meta);
   m.impl("propagate_backward_rows", &bbgr_torch::propagate_backward_rows_meta);
   m.impl("jacobi_layer", &bbgr_torch::jacobi_layer_meta);
@@ -1351,6 +1533,7 @@ TORCH_LIBRARY_IMPL(bbgr, Meta, m) {
 
 TORCH_LIBRARY_IMPL(bbgr, Autograd, m) {
   m.impl("propagate", &bbgr_torch::propagate_autograd);
+  m.impl("propagate_rows", &bbgr_torch::propagate_rows_autograd);
   m.impl("jacobi_layer", &bbgr_torch::jacobi_layer_autograd);
   m.impl("propagate_sym", &bbgr_torch::propagate_sym_autograd);
   m.impl("bpr_loss", &bbgr_torch::bpr_loss_autograd);

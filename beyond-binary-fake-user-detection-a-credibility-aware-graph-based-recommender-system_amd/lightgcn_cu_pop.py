@@ -23,10 +23,12 @@ from __future__ import annotations
 import torch
 
 from . import bpr as _bpr
+from . import lazy as _lazy
 from ._lib import OP_GS
 from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator, build_pair,
                         resolve_pair)
 from .propagate import ORDER_GS, OperatorPair, propagate as _propagate
+from .propagate import propagate_rows as _propagate_rows
 
 
 def _build(train_edges_2xE, num_users, num_items, cred_u, device, kind):
@@ -44,6 +46,10 @@ def build_message_passing_mats(train_edges_2xE, num_users: int, num_items: int,
 
 
 class LightGCN(torch.nn.Module):
+    # propagate() returns deferred tables (bbgr.lazy): bpr_loss over one call's
+    # pair computes the batch rows only; any other use computes them whole
+    lazy_finals = True
+
     def __init__(self, num_users, num_items, emb_dim, num_layers, M_ui, M_iu):
         super().__init__()
         self.num_users = num_users
@@ -65,12 +71,20 @@ class LightGCN(torch.nn.Module):
         return self._pair
 
     def propagate(self):
-        return _propagate(self._operator_pair(), self.user_emb.weight, self.item_emb.weight,
-                          self.num_layers, ORDER_GS)
+        pair, K = self._operator_pair(), self.num_layers
+        u0, i0 = self.user_emb.weight, self.item_emb.weight
+        if self.lazy_finals and _lazy.supported(u0, i0):
+            return _lazy.deferred_pair(
+                lambda: _propagate(pair, u0, i0, K, ORDER_GS),
+                lambda users, items: _propagate_rows(pair, u0, i0, K, ORDER_GS, users, items),
+                u0, i0)
+        return _propagate(pair, u0, i0, K, ORDER_GS)
 
     def get_user_item_emb(self):
         return self.propagate()
 
     def bpr_loss(self, users, pos_items, neg_items, user_emb, item_emb, reg_weight: float):
+        user_emb, item_emb, users, pos_items, neg_items = _lazy.batch_finals(
+            user_emb, item_emb, users, pos_items, neg_items)
         return _bpr.bpr_loss(users, pos_items, neg_items, user_emb, item_emb,
                              self.user_emb.weight, self.item_emb.weight, reg_weight)

@@ -11,6 +11,9 @@ bpr_loss, backward, Adam) survives torch.compile and CUDA-graph capture, and a
 libtorch / TorchScript caller reaches the same operators as torch.ops.bbgr.*:
 
   bbgr::propagate(u0, i0, pair_key, num_layers, order) -> (u_final, i_final)
+  bbgr::propagate_rows(u0, i0, users, items, pair_key, num_layers, order)
+                                -> (u_final, i_final) valid at the listed rows only
+                                (GS; backward: propagate's)
   bbgr::propagate_backward(gU, gI, pair_key, num_layers, order) -> (grad_u0, grad_i0)
   bbgr::propagate_backward_rows(iu, vu, gI, num_users, pair_key, num_layers,
                                 order, ii=None, vi=None) -> (grad_u0, grad_i0)
@@ -57,6 +60,7 @@ def load() -> None:
 load()
 
 propagate = torch.ops.bbgr.propagate
+propagate_rows = torch.ops.bbgr.propagate_rows
 propagate_backward = torch.ops.bbgr.propagate_backward
 propagate_backward_rows = torch.ops.bbgr.propagate_backward_rows
 jacobi_layer = torch.ops.bbgr.jacobi_layer
@@ -69,6 +73,7 @@ bpr_loss_sparse_ego = torch.ops.bbgr.bpr_loss_sparse_ego
 
 # autograd node name of bbgr::propagate (bpr.py reads the graph)
 PROPAGATE_NODE = "torch::autograd::CppNode<bbgr_torch::PropagateFn>"
+PROPAGATE_ROWS_NODE = "torch::autograd::CppNode<bbgr_torch::PropagateRowsFn>"
 
 _keys = itertools.count(1)
 

@@ -728,6 +728,16 @@ def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers
     return ops.propagate(u0, i0, ops.pair_key(pair), int(num_layers), order)
 
 
+def propagate_rows(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
+                   order: str, users: torch.Tensor, items: torch.Tensor):
+    """propagate() with the final tables valid at the listed rows only (users,
+    items: the caller's row ids; GS order — Jacobi computes every row):
+    bbgr::propagate_rows. Its backward is propagate's, so a loss over those
+    rows gets the same gradients; the listed rows hold the same bits."""
+    from . import ops
+    return ops.propagate_rows(u0, i0, users, items, ops.pair_key(pair), int(num_layers), order)
+
+
 # ---------------------------------------------------------------------------
 # Square generic operator (lightgcn.py fed an arbitrary N x N sparse tensor)
 # ---------------------------------------------------------------------------

@@ -1,0 +1,127 @@
+"""GPU: the drop-in's deferred final tables (bbgr.lazy, bbgr::propagate_rows).
+
+The reference's step reads the propagated tables only through bpr_loss at the
+batch rows (Version-2/lighgcn_cu_pop.py:858-863). The drop-in's propagate()
+defers them: bpr_loss over one call's pair computes the batch rows only, any
+other use computes the whole tables. Both must give the dense path's values
+bit for bit: the loss, every gradient, the Adam-updated weights, and the
+tables a caller reads.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from bbgr import lazy  # noqa: E402
+from bbgr import lightgcn_cu_pop as V2  # noqa: E402
+from bbgr import lightgcn_cu_pop_long_tail_exposure as MA  # noqa: E402
+from bbgr import operators  # noqa: E402
+from bbgr.synthetic import synthetic_credibility, synthetic_edges  # noqa: E402
+
+DEV = "cuda"
+U, I, E, D, B = 1500, 700, 20000, 64, 512
+
+
+def _model(K, module=V2, lazy_on=True, seed=0):
+    e = synthetic_edges(U, I, E, seed=4, items="zipf")
+    torch.manual_seed(seed)
+    cred = torch.as_tensor(synthetic_credibility(U, 4))
+    M_ui, M_iu = module.build_message_passing_mats(e, U, I, cred, DEV)
+    m = module.LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    m.lazy_finals = lazy_on
+    return m
+
+
+def _batch(seed):
+    g = torch.Generator().manual_seed(seed)
+    users = torch.randperm(U, generator=g)[:B].to(DEV)          # the reference's slices
+    pos = torch.randint(0, I, (B,), generator=g).to(DEV)
+    neg = torch.randint(0, I, (B,), generator=g).to(DEV)
+    return users, pos, neg
+
+
+def _steps(m, batches, opt_cls=torch.optim.Adam):
+    """The reference's loop body (Version-2:858-863) over the batches."""
+    opt = opt_cls(m.parameters(), lr=1e-3)
+    losses = []
+    for users, pos, neg in batches:
+        user_emb, item_emb = m.get_user_item_emb()
+        loss = m.bpr_loss(users, pos, neg, user_emb, item_emb, 1e-4)
+        opt.zero_grad()
+        loss.backward()
+        grads = [p.grad.clone() for p in m.parameters()]
+        opt.step()
+        losses.append((float(loss), grads))
+    return losses
+
+
+@pytest.mark.parametrize("K", [3, 2, 1, 0])
+@pytest.mark.parametrize("order", ["degree", "input"])
+def test_deferred_step_is_bitwise_the_dense_step(K, order, monkeypatch):
+    """Three reference steps, deferred (rows only) vs dense: losses, gradients
+    and weights equal bit for bit — the drop-in graph in degree order with the
+    caller's tables in input order (maps), and a graph kept in input order."""
+    monkeypatch.setattr(operators, "DROPIN_VERTEX_ORDER", order)
+    batches = [_batch(s) for s in range(3)]
+    # a repeated user and a negative outside the table (a sampler giving up)
+    batches[1][0][5] = batches[1][0][6]
+    batches[2][2][3] = -1
+    a, b = _model(K, lazy_on=True), _model(K, lazy_on=False)
+    ra, rb = _steps(a, batches), _steps(b, batches)
+    for (la, ga), (lb, gb) in zip(ra, rb):
+        assert la == lb
+        for x, y in zip(ga, gb):
+            assert torch.equal(x, y)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)
+
+
+def test_deferred_tables_compute_on_use_and_equal_the_dense_tables():
+    a, b = _model(3, lazy_on=True), _model(3, lazy_on=False)
+    uf, itf = a.propagate()
+    assert isinstance(uf, lazy.DeferredFinal) and isinstance(itf, lazy.DeferredFinal)
+    # metadata answers without computing
+    assert uf.shape == (U, D) and itf.size(0) == I and uf.dtype == torch.float32
+    assert uf.device.type == "cuda" and uf.dim() == 2 and len(itf) == I and uf.requires_grad
+    assert uf._pending.out is None
+    ru, ri = b.propagate()
+    assert torch.equal(uf[torch.arange(U, device=DEV)], ru)    # indexing computes
+    assert uf._pending.out is not None
+    assert torch.equal(itf.clone(), ri)
+    assert type(uf + 0) is torch.Tensor                        # results are plain
+    # the computed tables carry the autograd graph of the call
+    (uf.sum() + 2 * itf.sum()).backward()
+    (ru.sum() + 2 * ri.sum()).backward()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa.grad, pb.grad)
+    # no_grad evaluation (the reference's evaluate_*): tables without a graph
+    with torch.no_grad():
+        ue, ie = a.get_user_item_emb()
+        s = ue[:10] @ ie.T
+    assert not s.requires_grad
+    assert torch.equal(s, (ru[:10] @ ri.T).detach())
+
+
+def test_deferred_tables_read_after_a_weight_update_raise():
+    m = _model(3)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    users, pos, neg = _batch(0)
+    uf, itf = m.get_user_item_emb()
+    m.bpr_loss(users, pos, neg, uf, itf, 1e-4).backward()
+    opt.step()                                   # the weights change in place
+    with pytest.raises(RuntimeError, match="weights changed"):
+        uf[0]
+    uf2, itf2 = m.get_user_item_emb()            # a new call is current
+    assert np.isfinite(float(m.bpr_loss(users, pos, neg, uf2, itf2, 1e-4)))
+
+
+def test_method_a_module_defers_too():
+    """lightgcn_cu_pop_long_tail_exposure (Method-A operators) inherits the
+    deferred tables: its step equals its dense step bit for bit."""
+    batches = [_batch(s) for s in range(2)]
+    a, b = _model(3, MA, lazy_on=True), _model(3, MA, lazy_on=False)
+    for (la, ga), (lb, gb) in zip(_steps(a, batches), _steps(b, batches)):
+        assert la == lb
+        for x, y in zip(ga, gb):
+            assert torch.equal(x, y)

@@ -38,7 +38,7 @@ def timed(fn, steps: int) -> float:
 
 def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
         adam: str = "foreach", device=None, pre_ordered: bool = False,
-        items_ordered: bool = False) -> dict:
+        items_ordered: bool = False, dense_finals: bool = False) -> dict:
     c = CONFIGS[cfg_name]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
     e = config_edges(cfg_name) if edges is None else edges
@@ -58,6 +58,8 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
     torch.cuda.synchronize()
     build_s = time.perf_counter() - t0      # the drop-in builder (device graph + scales)
     model = V2.LightGCN(U, I, d, K, M_ui, M_iu).to(dev)   # the reference's module init
+    if dense_finals:   # propagate() computes both whole tables at the call
+        model.lazy_finals = False
     if pre_ordered:
         assert M_ui.graph.user_csr.cols_by_degree and M_ui.graph.item_csr.cols_by_degree
     torch.cuda.synchronize()
@@ -91,9 +93,18 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
         fwd_bwd()
         opt.step()
 
-    def fwd():
+    def fwd():   # the step's forward as the reference's loop runs it: tables -> loss
+        k = next(it) % n_b
         with torch.no_grad():
-            model.propagate()
+            uf, itf = model.propagate()
+            model.bpr_loss(users[k], pos[k], neg[k], uf, itf, 1e-4)
+
+    def full_tables():   # every row of both final tables (evaluation's use)
+        from bbgr.lazy import resolve
+        with torch.no_grad():
+            uf, itf = model.propagate()
+            resolve(uf)
+            resolve(itf)
 
     for _ in range(warmup):
         step()
@@ -101,7 +112,9 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
            "items_ordered": items_ordered,
            "setup_s": setup_s, "build_s": build_s, "model_init_s": setup_s - build_s,
            "first_call_s": first_call_s, "steps": steps,
+           "lazy_finals": bool(model.lazy_finals),
            "step_ms": timed(step, steps), "forward_ms": timed(fwd, steps),
+           "full_tables_ms": timed(full_tables, steps),
            "forward_backward_ms": timed(fwd_bwd, steps)}
     fwd_bwd()
     out["adam_ms"] = timed(opt.step, steps)
@@ -120,9 +133,12 @@ def main():
                     help="hand the model an edge list already in descending-degree order")
     ap.add_argument("--items-ordered", action="store_true",
                     help="only the item ids handed over in descending-degree order")
+    ap.add_argument("--dense-finals", action="store_true",
+                    help="LightGCN.lazy_finals = False: whole final tables at every call")
     a = ap.parse_args()
     print(json.dumps(run(a.config, steps=a.steps, warmup=a.warmup, adam=a.adam,
-                         pre_ordered=a.pre_ordered, items_ordered=a.items_ordered)),
+                         pre_ordered=a.pre_ordered, items_ordered=a.items_ordered,
+                         dense_finals=a.dense_finals)),
           flush=True)
 
 
