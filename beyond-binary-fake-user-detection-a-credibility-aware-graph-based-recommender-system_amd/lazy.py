@@ -82,8 +82,8 @@ def _resolve(x):
 
 class DeferredFinal(torch.Tensor):
     """One final table of a propagate() call (side 0: users, 1: items),
-    computed on first use (module docstring). Its own storage is an
-    uninitialised table of the right shape: nothing reads it."""
+    computed on first use (module docstring). Its own storage is a shared
+    uninitialised table of the right shape (_placeholder): nothing reads it."""
 
     @staticmethod
     def __new__(cls, pending: _Pending, side: int, like: torch.Tensor, requires_grad: bool):
@@ -114,15 +114,28 @@ def supported(u0: torch.Tensor, i0: torch.Tensor) -> bool:
     return not torch.cuda.is_current_stream_capturing()
 
 
+# One placeholder table per (shape, dtype, device), shared by every deferred
+# table of that shape: nothing reads or writes it (every use resolves first),
+# it only gives the tensor its metadata and in-bounds storage.
+_placeholders: dict = {}
+
+
+def _placeholder(like: torch.Tensor) -> torch.Tensor:
+    key = (tuple(like.shape), like.dtype, like.device)
+    t = _placeholders.get(key)
+    if t is None:
+        if len(_placeholders) >= 4:   # a few model shapes alive at once, at most
+            _placeholders.pop(next(iter(_placeholders)))
+        t = _placeholders[key] = torch.empty(like.shape, dtype=like.dtype, device=like.device)
+    return t
+
+
 def deferred_pair(full_fn, rows_fn, u0: torch.Tensor, i0: torch.Tensor):
     """(u_final, i_final) as DeferredFinal tensors of one call."""
     p = _Pending(full_fn, rows_fn, u0, i0)
     rg = p.grad and (u0.requires_grad or i0.requires_grad)
-    d = u0.shape[1]
-    return (DeferredFinal(p, 0, torch.empty(u0.shape[0], d, dtype=u0.dtype, device=u0.device),
-                          rg),
-            DeferredFinal(p, 1, torch.empty(i0.shape[0], d, dtype=i0.dtype, device=i0.device),
-                          rg))
+    return (DeferredFinal(p, 0, _placeholder(u0.detach()), rg),
+            DeferredFinal(p, 1, _placeholder(i0.detach()), rg))
 
 
 def batch_finals(user_final, item_final, users, pos, neg):

@@ -141,7 +141,8 @@ def _owner_worker(rank, world, port, out):
     stale = truth + 100.0 * (rank + 1)   # every rank's view: stale everywhere ...
     a, b = bounds[rank], bounds[rank + 1]
     stale[a:b] = truth[a:b]               # ... but at the rows it owns
-    rows = torch.tensor([0, 3, 3, I - 1, bounds[1], 7, 0, 11], dtype=torch.int64)
+    # (-1: a sampler's "no negative" row, refreshed as row 0)
+    rows = torch.tensor([0, 3, 3, I - 1, bounds[1], 7, -1, 11], dtype=torch.int64)
     t = stale.clone()
     refresh_from_owners(t, rows, bounds)
     whole = gather_owned(truth[a:b].contiguous(), bounds)
@@ -155,7 +156,7 @@ def test_item_ownership_refresh_and_gather_are_exact(tmp_path, world):
     mp.spawn(_owner_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for k in range(world):
         z = np.load(tmp_path / f"own{k}.npz")
-        rows = np.unique(z["rows"])
+        rows = np.unique(np.clip(z["rows"], 0, None))
         got, want = z["t"], z["stale"].copy()
         want[rows] = z["truth"][rows]          # refreshed rows = the owners' bits
         assert got.tobytes() == want.tobytes()
