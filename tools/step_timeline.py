@@ -52,12 +52,16 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--marker", default="sample_kernel")
     ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--index", type=int, default=None,
+                    help="print this segment (counted from the first marker) instead of "
+                         "the median of the last --steps")
     a = ap.parse_args()
     rows = load(a.trace)
     marks = [i for i, r in enumerate(rows) if a.marker in r[2]]
     if len(marks) < 2:
         raise SystemExit(f"fewer than 2 '{a.marker}' launches in the trace")
-    steps = [(marks[k], marks[k + 1]) for k in range(len(marks) - 1)][-a.steps:]
+    steps = [(marks[k], marks[k + 1]) for k in range(len(marks) - 1)]
+    steps = steps[a.index:a.index + 1] if a.index is not None else steps[-a.steps:]
     stats = []
     for i0, i1 in steps:
         seg = rows[i0:i1]
