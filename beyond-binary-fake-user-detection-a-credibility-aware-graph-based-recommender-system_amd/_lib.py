@@ -201,6 +201,7 @@ _SIGNATURES = {
     "bbgr_list_positions": ([c_int64, _P, _P, _P, _P], c_int32),
     "bbgr_rows_gather": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_rows_copy": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
+    "bbgr_first_slot": ([c_int64, _P, c_int64, _P, _P, _P], c_int32),
     "bbgr_rows_add_unique": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P],
                              c_int32),
     # blueprint names, thin forms of the entry points above

@@ -1030,13 +1030,32 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_cuda(
 // slot[b] = position of the first occurrence of ids[b] (device-only): stable
 // sort, then each sorted value's first sorted position by a binary search
 // (a lower bound; one launch instead of a cummax scan and its masks)
-static Tensor first_slot(const Tensor &ids) {
-  auto sorted = at::sort(ids, /*stable=*/true, /*dim=*/0, /*descending=*/false);
-  const Tensor &srt = std::get<0>(sorted);
-  const Tensor &perm = std::get<1>(sorted);
-  Tensor head = at::searchsorted(srt, srt, /*out_int32=*/false, /*right=*/false);
-  Tensor slot = at::empty_like(perm);
-  slot.index_put_({perm}, perm.index_select(0, head));
+// slot[b] = first b' with ids[b'] == ids[b] (ids in [0, n_rows)): bbgr_first_slot
+// over a per-(device, n_rows) scratch of INT32_MAX rows, kept between calls
+// (each call leaves it all INT32_MAX); one per stream, like the workspaces
+static Tensor first_slot(const Tensor &ids_, int64_t n_rows) {
+  Tensor ids = ids_.to(at::kLong).contiguous();
+  Tensor slot = at::empty_like(ids);
+  static std::mutex mu;
+  static std::map<std::tuple<int64_t, int64_t, int64_t>, Tensor> scratch;
+  Tensor first;
+  const auto fresh = [&] {
+    return at::full({std::max<int64_t>(n_rows, 1)}, 0x7fffffff,
+                    at::TensorOptions().dtype(at::kInt).device(ids.device()));
+  };
+  if (capturing()) {   // a captured step fills its own (the fill replays with it)
+    first = fresh();
+  } else {
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple((int64_t)ids.device().index(), n_rows,
+                                     (int64_t)(intptr_t)cur_stream());
+    auto it = scratch.find(key);
+    if (it == scratch.end()) it = scratch.emplace(key, fresh()).first;
+    first = it->second;
+  }
+  check(bbgr_first_slot(ids.numel(), ids.data_ptr<int64_t>(), n_rows, first.data_ptr<int32_t>(),
+                        slot.data_ptr<int64_t>(), cur_stream()),
+        "bbgr_first_slot");
   return slot;
 }
 
@@ -1053,7 +1072,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
   Tensor valid = (users >= 0) & (users < U) & (pos >= 0) & (pos < I) & (neg >= 0) & (neg < I);
   Tensor iu = users.clamp(0, U - 1);
   Tensor ii = at::cat({pos, neg}).clamp(0, I - 1);
-  Tensor su = first_slot(iu), si = first_slot(ii);
+  Tensor su = first_slot(iu, U), si = first_slot(ii, I);
   Tensor ue_c = ue.index_select(0, iu).contiguous(), ie_c = ie.index_select(0, ii).contiguous();
   Tensor cu = at::where(valid, su, at::full_like(su, -1)).contiguous();
   Tensor gu = at::zeros({B, d}, f32(ue)), gi = at::zeros({2 * B, d}, f32(ue));

@@ -470,6 +470,28 @@ __global__ void rows_axpy_kernel(long n, const long *idx, float alpha,
     atomicAdd(dst + r * ldd + c, alpha * src[r * lds + c]);
 }
 
+// bbgr_first_slot: first[ids[k]] = min k (atomic minimum: order-free), then
+// slot[k] = first[ids[k]], then first[ids[k]] = INT32_MAX again.
+__global__ void first_slot_min_kernel(long n, const long *ids, long n_rows, int *first) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const long r = ids[k];
+  if (r >= 0 && r < n_rows) atomicMin(first + r, (int)k);
+}
+__global__ void first_slot_read_kernel(long n, const long *ids, long n_rows, const int *first,
+                                       long *slot) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const long r = ids[k];
+  slot[k] = (r >= 0 && r < n_rows) ? (long)first[r] : k;
+}
+__global__ void first_slot_reset_kernel(long n, const long *ids, long n_rows, int *first) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const long r = ids[k];
+  if (r >= 0 && r < n_rows) first[r] = 0x7fffffff;
+}
+
 // dst[idx[k]] = src[idx[k]] (idx < 0 skipped; repeats write the same row).
 __global__ __launch_bounds__(256) void rows_copy_kernel(long n, const long *idx,
                                                         const float4 *src, long lds4,
@@ -895,6 +917,25 @@ extern "C" int bbgr_rows_axpy(int64_t n, const int64_t *idx, float alpha,
                      as_stream(stream), (long)n, (const long *)idx, alpha, src,
                      (long)ldsrc, dst, (long)lddst, d);
   BBGR_LAUNCHED("rows_axpy_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_first_slot(int64_t n, const int64_t *ids, int64_t n_rows, int32_t *first,
+                               int64_t *slot, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n < (1LL << 31) && n_rows >= 0, "bbgr_first_slot: bad sizes");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(ids && first && slot, "bbgr_first_slot: null arrays");
+  hipStream_t st = as_stream(stream);
+  const unsigned g = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(first_slot_min_kernel, dim3(g), dim3(256), 0, st, (long)n,
+                     (const long *)ids, (long)n_rows, first);
+  BBGR_LAUNCHED("first_slot_min_kernel");
+  hipLaunchKernelGGL(first_slot_read_kernel, dim3(g), dim3(256), 0, st, (long)n,
+                     (const long *)ids, (long)n_rows, (const int *)first, (long *)slot);
+  BBGR_LAUNCHED("first_slot_read_kernel");
+  hipLaunchKernelGGL(first_slot_reset_kernel, dim3(g), dim3(256), 0, st, (long)n,
+                     (const long *)ids, (long)n_rows, first);
+  BBGR_LAUNCHED("first_slot_reset_kernel");
   return BBGR_OK;
 }
 

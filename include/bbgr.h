@@ -488,6 +488,14 @@ int bbgr_rows_add_unique(int64_t n, const int64_t *idx, const float *src, int64_
                          float *dst, int64_t lddst, int32_t d, int64_t n_dst,
                          bbgr_stream_t stream);
 
+/* slot[k] = the first k' <= k with ids[k'] == ids[k], for k < n (ABI 6; ids */
+/* in [0, n_rows)). first: int32 [n_rows] scratch holding INT32_MAX at every */
+/* row (left so on return). The BPR ego rows' "add into the row of the first */
+/* occurrence" without a sort: an atomic minimum per row (order-free, so    */
+/* deterministic), a gather, and a reset of the touched rows.              */
+int bbgr_first_slot(int64_t n, const int64_t *ids, int64_t n_rows, int32_t *first,
+                    int64_t *slot, bbgr_stream_t stream);
+
 /* Deterministic index_add_: dst[idx[k], :d] += src[k, :d] for k < n, with   */
 /* the addends of each destination row summed in ascending k and added once  */
 /* (stable radix sort of idx, then one segment sum per row). Negative or     */

@@ -73,9 +73,10 @@ def test_not_while_compiling():
 
 @pytest.mark.parametrize("n,hi", [(1, 5), (2, 1), (7, 3), (1000, 50), (16384, 1_000_000)])
 def test_first_slot_is_the_first_occurrence(n, hi):
-    """bpr._first_slot (the ego rows' slot of each triple; the C++ first_slot
-    in csrc/torch_ops.cpp is the same sort + lower-bound search): slot[b] is
-    the smallest b' with ids[b'] == ids[b]."""
+    """bpr._first_slot (the ego rows' slot of each triple, by a sort +
+    lower-bound search; the C++ operators use bbgr_first_slot, an atomic
+    minimum per row, checked against this in tests/test_gpu_parity.py): slot[b]
+    is the smallest b' with ids[b'] == ids[b]."""
     g = torch.Generator().manual_seed(n + hi)
     ids = torch.randint(0, hi, (n,), generator=g)
     first = {}

@@ -799,6 +799,38 @@ def test_graph_from_memmaps_matches_array(tmp_path):
         assert torch.equal(g.item_csr.indices, g1.item_csr.indices)
 
 
+@pytest.mark.parametrize("n,hi", [(1, 5), (7, 3), (16384, 1_000_000), (16384, 40), (300, 300)])
+def test_first_slot_kernel_is_the_first_occurrence(n, hi):
+    """bbgr_first_slot (the C++ operators' ego-row slots): slot[b] is the
+    smallest b' with ids[b'] == ids[b], as bpr._first_slot's sort computes
+    it; ids outside [0, hi) keep their own slot; the scratch is left all
+    INT32_MAX for the next call."""
+    import ctypes
+    from bbgr import _lib, bpr
+    g = torch.Generator().manual_seed(n + hi)
+    ids = torch.randint(-1, hi + 1, (n,), generator=g)
+    valid = (ids >= 0) & (ids < hi)
+    first_of = {}
+    for b, v in enumerate(ids.tolist()):
+        if 0 <= v < hi:
+            first_of.setdefault(v, b)
+    want = torch.tensor([first_of.get(v, b) for b, v in enumerate(ids.tolist())])
+    # (bpr._first_slot's sort gives the same on the valid entries)
+    vb = valid.nonzero().flatten()
+    assert torch.equal(vb[bpr._first_slot(ids[valid])], want[valid])
+    first = torch.full((hi,), 0x7fffffff, dtype=torch.int32, device=DEV)
+    slot = torch.empty(n, dtype=torch.int64, device=DEV)
+    idd = ids.to(DEV)
+    for _ in range(2):   # reusable scratch
+        _lib.call("bbgr_first_slot", n, _lib.ptr(idd), hi, _lib.ptr(first), _lib.ptr(slot),
+                  _lib.stream_handle())
+        torch.cuda.synchronize()
+        got = slot.cpu()
+        assert torch.equal(got[valid], want[valid])
+        assert torch.equal(got[~valid], torch.arange(n)[~valid])
+        assert bool((first == 0x7fffffff).all())
+
+
 @pytest.mark.parametrize("d", [16, 64, 256])
 def test_rows_add_unique_is_bitwise_the_sorted_scatter(d):
     """bbgr_rows_add_unique (distinct indices, no sort) == bbgr_scatter_add_rows
