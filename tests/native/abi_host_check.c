@@ -114,6 +114,9 @@ int main(void) {
                                                                BBGR_RED_SUM, NULL));
   expect_error("comm_allgather null comm", bbgr_comm_allgather(NULL, f4, f4, 4, BBGR_DT_F32,
                                                                NULL));
+  expect_error("first_slot bad n", bbgr_first_slot(-1, NULL, 4, NULL, NULL, NULL));
+  expect_error("first_slot null", bbgr_first_slot(4, NULL, 4, NULL, NULL, NULL));
+  expect_ok("first_slot empty", bbgr_first_slot(0, NULL, 4, NULL, NULL, NULL));
   expect_error("rows_copy bad d", bbgr_rows_copy(4, NULL, f4, 64, f4, 64, 6, NULL));
   expect_ok("rows_copy empty", bbgr_rows_copy(0, NULL, NULL, 64, NULL, 64, 64, NULL));
   expect_error("rows_add_unique bad ld", bbgr_rows_add_unique(4, NULL, f4, 32, f4, 64, 64, 8,
