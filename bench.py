@@ -821,7 +821,11 @@ def main():
                                       if dist_mode and not columns and args.column_chains > 1
                                       else "")
                                    + (f", {args.exchange_parts} item-row ranges per exchange"
-                                      if dist_mode and not columns else ""))},
+                                      if dist_mode and not columns else "")
+                                   + (f", collectives via the C ABI's communicator "
+                                      f"({args.native_comm})"
+                                      if dist_mode and not columns and args.native_comm != "off"
+                                      else ""))},
         "bpr_steps_per_s": steps_per_s,
         "torch_gpu_reference": torch_ref,
         "dropin_module_step": dropin,

@@ -242,6 +242,24 @@ def test_bench_two_ranks_on_c2(tmp_path, partition):
     assert j["partition_beside"] is None
 
 
+def test_bench_sharded_single_rank_with_inline_collectives(tmp_path):
+    """bench.py's user-row step at world size 1 over RCCL (--sharded) with
+    every collective inline on the compute stream (--native-comm inline): one
+    chain, no ranges, a JSON line with the step's value."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--sharded", "--config", "C2",
+           "--steps", "3", "--warmup", "1", "--dense-check", "0", "--frontier", "on",
+           "--native-comm", "inline", "--no-cpu-baseline", "--no-torch-reference"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    j = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert j["value"] > 0 and j["config"]["num_edges"] == 1_000_000
+    assert "1 item-row ranges" in j["config"]["parallelism"]
+    assert "(inline)" in j["config"]["parallelism"]
+
+
 def test_bench_two_ranks_measures_both_partitions(tmp_path):
     """--partition-beside (the N > 1 default): the other partition of the same
     graph is timed the same way in the same run; the faster is the line and the
