@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 import bbgr  # noqa: E402,F401
 from bbgr.graph import BipartiteGraph  # noqa: E402
 from bbgr.synthetic import CONFIGS, CONFIG_SEED, config_edges, synthetic_credibility  # noqa: E402
-from bbgr.trainer import FusedTrainer  # noqa: E402
+from bbgr.trainer import FusedTrainer, GraphedStep  # noqa: E402
 
 
 def main():
@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--thresholds", default="256",
                     help="long-row thresholds (rows above are cut into chunk workgroups)")
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--variant", default="v2_pop")
+    ap.add_argument("--graph", action="store_true", help="replay the step as a HIP graph")
     a = ap.parse_args()
     c = CONFIGS[a.config]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
@@ -41,15 +43,17 @@ def main():
                     for t in a.thresholds.split(",")):
         g = BipartiteGraph(e, U, I, "cuda", vertex_order="degree", chunk_edges=ch,
                            long_threshold=thr)
-        tr = FusedTrainer(g, "v2_pop", cred=cred, emb_dim=d, num_layers=K, batch_size=B)
+        tr = FusedTrainer(g, a.variant, cred=cred, emb_dim=d, num_layers=K, batch_size=B)
+        step = GraphedStep(tr).step if a.graph else tr.step
         for _ in range(5):
-            tr.step()
+            step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            tr.step()
+            step()
         torch.cuda.synchronize()
-        print(json.dumps({"config": a.config, "chunk_edges": ch, "long_threshold": thr,
+        print(json.dumps({"config": a.config, "variant": a.variant, "graph": a.graph,
+                          "chunk_edges": ch, "long_threshold": thr,
                           "item_chunks": g.item_csr.n_chunks, "user_chunks": g.user_csr.n_chunks,
                           "ms_per_step": round(1000 * (time.perf_counter() - t0) / a.steps, 4)}),
               flush=True)
