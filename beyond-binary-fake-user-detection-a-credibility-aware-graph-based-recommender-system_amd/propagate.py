@@ -30,6 +30,7 @@ The transposes are the other CSR with the scale roles swapped.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -296,6 +297,47 @@ def mask_signature(src_mask, row_mask, row_list) -> str:
 _timer: SpmmTimer | None = None
 
 
+class ListLength:
+    """The length of a row list built on the stream (bbgr_mark_list's device
+    count), for spmm(row_count=...). A launch over a device-length list needs
+    a grid for the list's capacity (C4: 62.5k short-row workgroups for the
+    ~60k-row item frontier; most only read the length and exit, ~60 us of the
+    first backward item product). On an eager stream `publish()` copies the
+    count to pinned host memory right after the list is built; a launch then
+    waits for that copy and passes the exact list, so its grid is the list's.
+    The wait comes where the launch is issued — behind the forward's dense
+    products, milliseconds of queued GPU work — so the GPU does not idle.
+    Inside a graph capture (or before publish / after invalidate) the launch
+    keeps the device count. The rows and their arithmetic are the same either
+    way (bitwise). BBGR_LIST_HOST=0 keeps the device count always (A/B runs)."""
+
+    enabled = os.environ.get("BBGR_LIST_HOST", "1") != "0"
+
+    def __init__(self, count: torch.Tensor):
+        self.count = count
+        self._host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+        self._event = None
+
+    def publish(self) -> None:
+        """After the list is built, on the current stream."""
+        self._event = None
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
+            return
+        self._host.copy_(self.count, non_blocking=True)
+        self._event = torch.cuda.Event()
+        self._event.record()
+
+    def invalidate(self) -> None:
+        self._event = None
+
+    def length(self) -> int | None:
+        """The published length (waits for its copy), or None: use the device count."""
+        if self._event is None or torch.cuda.is_current_stream_capturing():
+            return None
+        self._event.synchronize()
+        return int(self._host[0])
+
+
 def set_spmm_timer(t: SpmmTimer | None) -> None:
     global _timer
     _timer = t
@@ -315,7 +357,15 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     bitmap of src_mask's live edges in this CSR (bbgr_spmm_args.src_bits).
     `row_count` (device int64): row_list holds that many rows (its numel() is
     the capacity; bbgr_spmm_args.row_count) — a list built on the stream, the
-    rows row_mask flags."""
+    rows row_mask flags; a ListLength passes the list at its published length
+    instead when there is one."""
+    listed_on_device = row_count is not None
+    if isinstance(row_count, ListLength):
+        n = row_count.length()
+        if n is None:
+            row_count = row_count.count
+        else:
+            row_list, row_count = row_list[:n], None
     d = x.shape[1]
     a = _lib.SpmmArgs()
     a.d = d
@@ -360,7 +410,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     masked = src_mask is not None or row_mask is not None or row_list is not None
     kind = "masked" if masked else ("full" if adam is None else
                                     "adam" if adam.grad is None else "adam_side")
-    if row_count is not None:   # the list is row_mask's rows; its length is on the device
+    if listed_on_device:   # the list is row_mask's rows, built on the stream
         row_list = None
     if _timer.count:
         call("bbgr_spmm", ctypes.byref(cs), ctypes.byref(a), stream_handle())

@@ -24,7 +24,7 @@ from ._lib import OP_GS, OP_J, OP_METHOD_A, OP_SYM, call, ld, ptr, stream_handle
 from .bpr import bpr_args
 from .graph import BipartiteGraph
 from .optim import AdamRows, DeviceStepState, adam_step
-from .propagate import ORDER_GS, ORDER_J, OperatorPair, backward, forward
+from .propagate import ORDER_GS, ORDER_J, ListLength, OperatorPair, backward, forward
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .scatter import RowScatter
 
@@ -146,10 +146,13 @@ class FusedTrainer:
         # (bbgr_mark_list; length on the device, so a captured step keeps it):
         # the first backward item product then visits the frontier's rows
         # (63k at C4) instead of testing the mask byte of every item row.
-        self.item_list = self.item_count = None
+        # Its launches take the list at its length (P.ListLength) when the step
+        # runs eagerly, at its capacity with the device count when captured.
+        self.item_list = self.item_count = self.item_len = None
         if self.frontier and order == ORDER_GS:
             self.item_list = torch.empty(max(self.I, 1), dtype=torch.int64, device=dev)
             self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.item_len = ListLength(self.item_count)
         # Fused optimizer (GS order): the user Adam runs inside the last backward
         # product's epilogue and the item Adam reads gI/(K+1) straight from the
         # sparse BPR gradient table (grad_scale), so neither weight-gradient
@@ -364,6 +367,8 @@ class FusedTrainer:
             for n, p in items:
                 call("bbgr_mark_list", n, p, None, None, *li)
             call("bbgr_mark_list", B, ptr(users), ptr(uc.indptr), ptr(uc.indices), *li)
+            if getattr(self, "item_len", None) is not None:
+                self.item_len.publish()
         else:
             for n, p in items:
                 call("bbgr_mark_rows", n, p, value, ptr(self.mask_i), self.I, st)
@@ -372,6 +377,8 @@ class FusedTrainer:
                      value, ptr(self.mask_i), st)
             if lst is not None:
                 self.item_count.zero_()
+                if getattr(self, "item_len", None) is not None:
+                    self.item_len.invalidate()
         if getattr(self, "slot_bits", None) is not None:   # set / clear the batch's bits
             call("bbgr_mark_slots", B, ptr(users), ptr(uc.indptr), ptr(self.slot_map),
                  ptr(self.slot_bits), value, st)
@@ -384,7 +391,10 @@ class FusedTrainer:
     def _flist(self, masks):
         """(item row list, device count) for backward(frontier_list=...)."""
         lst = getattr(self, "item_list", None)
-        return None if masks is None or lst is None else (lst, self.item_count)
+        if masks is None or lst is None:
+            return None
+        ll = getattr(self, "item_len", None)   # (a subclass may point item_count elsewhere)
+        return lst, ll if ll is not None and ll.count is self.item_count else self.item_count
 
     def forward(self):
         """Final (layer-mean) tables, rows by input id."""

@@ -739,6 +739,40 @@ def test_frontier_step_matches_dense_step(variant):
     assert int(front.mask_u.sum()) == 0 and int(front.mask_i.sum()) == 0
 
 
+def test_host_length_item_list_is_bitwise_the_device_count(monkeypatch):
+    """The trainer's frontier-list launches (last forward item layer, first
+    backward item product) take the list at its published host length
+    (propagate.ListLength: a grid sized to the list) instead of the capacity
+    with the device count: same rows, same arithmetic — losses and weights
+    bitwise equal over steps, the published length the device count."""
+    from bbgr import propagate as PP
+    from bbgr.synthetic import CONFIGS, config_edges
+    from bbgr.trainer import FusedTrainer
+    c = CONFIGS["C2"]
+    U, I = c["num_users"], c["num_items"]
+    g = BipartiteGraph(config_edges("C2"), U, I, DEV, vertex_order="degree")
+    kw = dict(cred=synthetic_credibility(U, 2), emb_dim=64, num_layers=3, batch_size=4096,
+              frontier=True)
+    host = FusedTrainer(g, "v2_pop", **kw)
+    seen = []
+    real = PP.ListLength.length
+
+    def spy(self):
+        n = real(self)
+        seen.append((n, int(self.count.item()) if n is not None else None))
+        return n
+    monkeypatch.setattr(PP.ListLength, "length", spy)
+    lh = [float(host.step()) for _ in range(3)]
+    assert seen and all(n is not None and n == cnt and n > 0 for n, cnt in seen)
+    monkeypatch.setattr(PP.ListLength, "length", lambda self: None)   # device count
+    dev = FusedTrainer(g, "v2_pop", **kw)
+    ld_ = [float(dev.step()) for _ in range(3)]
+    assert lh == ld_
+    for a, b in ((host.user_w, dev.user_w), (host.item_w, dev.item_w),
+                 (host.m_i, dev.m_i), (host.v_u, dev.v_u)):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("variant,K", [("v2_pop", 3), ("method_a", 2), ("v2_pop", 1),
                                        ("cu_fair", 3), ("cu_fair", 2), ("plain", 3)])
 def test_fused_adam_step_matches_unfused(variant, K):
