@@ -793,20 +793,73 @@ __device__ __forceinline__ void chunk_row_serial(const SpmmParams &P, int eb, in
   // once; only live ranges are gathered. A dead range's sum is +0.0 and
   // s + 0.0 == s (s is never -0.0: a sum from +0.0), so skipping it keeps the
   // workgroup's value bit for bit.
-  bool live = false;
+  //
+  // Lane g also counts range g's live edges and keeps the first one's slot.
+  // When no range holds more than one (the common case: ~1 live edge in 600
+  // at C4), every live range's sum is its one term (0 + x, or fma(w, x, 0)),
+  // so the group loads all their column indices in one round and gathers the
+  // rows two at a time, adding the terms in range order: the same operations
+  // as the per-range gathers below, without one dependent chain per range.
+  int cnt = 0, fe = -1;
   {
     const int gb = eb + lane * per, ge = min(ee, gb + per);
 #pragma unroll 1
-    for (int e = gb; e < ge && !live; e += 64) {
+    for (int e = gb; e < ge; e += 64) {
       unsigned long long w = slot_bits64(P.src_bits, e);
       if (ge - e < 64) w &= (1ull << (ge - e)) - 1ull;
-      live = w != 0ull;
+      if (w != 0ull && fe < 0) fe = e + __builtin_ctzll(w);
+      cnt += __popcll(w);
     }
   }
-  unsigned segs = (unsigned)((__ballot(live) >> (threadIdx.x & 48)) & 0xffffull);
+  const int base = threadIdx.x & 48;
+  unsigned segs = (unsigned)((__ballot(cnt != 0) >> base) & 0xffffull);
+  const bool multi = ((__ballot(cnt > 1) >> base) & 0xffffull) != 0ull;
 #pragma unroll
   for (int k = 0; k < V; ++k) s[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   bool first = true;
+  if (!multi) {
+    int my = -1;
+    float mw = 0.f;
+    if (fe >= 0) {
+      my = ld_edge(P.indices + fe);
+      if (WMODE == 1) mw = ld_edge(P.edge_val + fe);
+      if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
+    }
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    while (segs) {
+      int gg[2];
+      float4 v[2][V];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        gg[j] = segs ? __ffs(segs) - 1 : -1;
+        segs &= segs ? segs - 1u : 0u;
+        const int c = __shfl(my, gg[j] < 0 ? 0 : gg[j], 16);
+        if (gg[j] >= 0) {
+          const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + lane;
+          if (c >= P.nt_from) {
+#pragma unroll
+            for (int k = 0; k < V; ++k) v[j][k] = ld_nt(src + 16 * k);
+          } else {
+#pragma unroll
+            for (int k = 0; k < V; ++k) v[j][k] = src[16 * k];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (gg[j] < 0) continue;
+        const float w = __shfl(mw, gg[j], 16);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const float4 p = WMODE == 0 ? f4_add(z, v[j][k]) : f4_fma(w, v[j][k], z);
+          s[k] = first ? p : f4_add(s[k], p);
+        }
+        first = false;
+      }
+    }
+    return;
+  }
 #pragma unroll 1
   while (segs) {
     const int g = __ffs(segs) - 1;

@@ -1267,6 +1267,48 @@ def test_slot_bitmap_single_chunk_boundary_rows_bitwise():
     assert sorted(ic.degrees().cpu().tolist(), reverse=True) == sorted(degs, reverse=True)
 
 
+@pytest.mark.parametrize("n_live", [12, 60, 400])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_slot_bitmap_sparse_live_rows_bitwise(n_live, weighted):
+    """chunk_row_serial's fast path: with few live source rows most of a
+    single-chunk row's 16 ranges hold at most one live edge (their terms are
+    gathered together and added in range order); with more, some range holds
+    two and the row takes the per-range path. Both bitwise the mask-only
+    launch, unweighted and with per-edge values (C4's live density is ~1 edge
+    in 600)."""
+    from bbgr._lib import call, ptr, stream_handle
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(n_live)
+    U, d = 9000, 64
+    degs = [300, 700, 1200, 2048, 2049, 65, 64, 5]
+    rows = np.concatenate([np.full(k, r) for r, k in enumerate(degs)])
+    cols = np.concatenate([rng.choice(U, k, replace=False) for k in degs])
+    I = len(degs)
+    e = np.stack([cols, rows]).astype(np.int32)
+    g = BipartiteGraph(e, U, I, DEV, vertex_order="degree")
+    ic = g.item_csr
+    vals = t(rng.uniform(-1.5, 1.5, ic.nnz).astype(np.float32)) if weighted else None
+    prod = Product(ic, vals, None, None, {})
+    x = torch.zeros(U, d, device=DEV)
+    users = rng.choice(U, n_live, replace=False)
+    x[t(users, torch.int64).long()] = t(rng.standard_normal((n_live, d)).astype(np.float32))
+    su = torch.zeros(U, dtype=torch.uint8, device=DEV)
+    su[t(users, torch.int64).long()] = 1
+    rm = torch.ones(I, dtype=torch.uint8, device=DEV)
+    sb = torch.zeros(ic.nnz // 32 + 4, dtype=torch.int32, device=DEV)
+    call("bbgr_mark_slots", users.size, ptr(t(users, torch.int64)), ptr(g.user_csr.indptr),
+         ptr(g.user_item_slots()), ptr(sb), 1, stream_handle())
+    ref = torch.full((I, d), 3.0, device=DEV)
+    spmm(prod, x, False, y=ref, src_mask=su, row_mask=rm)
+    y = torch.full((I, d), 3.0, device=DEV)
+    spmm(prod, x, False, y=y, row_list=torch.arange(I, dtype=torch.int64, device=DEV),
+         row_count=torch.tensor([I], dtype=torch.int64, device=DEV), src_mask=su, row_mask=rm,
+         src_bits=sb)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert bool((ref != 3.0).any())
+
+
 def test_acc_in_map_reads_acc_in_through_its_own_map():
     """bbgr_spmm_args.acc_in_map: acc_out row acc_map[r] = gamma * (cs*T +
     acc_in[acc_in_map[r]]) — the drop-in chain's first / last layer."""
