@@ -471,6 +471,13 @@ def main():
     ap.add_argument("--partition-beside", type=int, default=1,
                     help="strong N > 1: also time the other partition (columns / users) on "
                          "the same graph and report the faster as the line (0 = off)")
+    ap.add_argument("--chain-beside", type=int, default=1,
+                    help="strong N > 1, user-row partition: also time the step as ONE chain "
+                         "with no item-row ranges and every collective inline on the compute "
+                         "stream (the C ABI's RCCL communicator; over gloo, where RCCL cannot "
+                         "share a GPU, the same one-chain schedule through torch's "
+                         "collectives) beside the default chain setting; the faster is the "
+                         "line, the other is reported as chain_beside (0 = off)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="N>1: strong (default) = the config's one graph cut into N user "
                          "ranges (the metric's |E|); weak = every rank owns a full "
@@ -564,8 +571,10 @@ def main():
     frontier = {"auto": "auto", "on": True, "off": False}[args.frontier]
     if args.dense:
         frontier = False
-    def build(part: str):
-        """The trainer of one partition ("columns" / "users" at N > 1)."""
+    def build(part: str, xpo: dict | None = None):
+        """The trainer of one partition ("columns" / "users" at N > 1); xpo:
+        the user-row exchange settings (default: xp)."""
+        xq = xp if xpo is None else xpo
         if emulate:
             from bbgr.columns import ColumnShardedTrainer
             return ColumnShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
@@ -587,14 +596,14 @@ def main():
         if weak:
             return ShardedTrainer(edges, U, I, args.variant, cred=cred, emb_dim=d,
                                   num_layers=K, batch_size=B, device=dev, user_offset=rank * U,
-                                  frontier=frontier, **xp)
+                                  frontier=frontier, **xq)
         if sharded_gen:
             return ShardedTrainer(edges, hi - lo, I, args.variant, cred=cred, emb_dim=d,
                                   num_layers=K, batch_size=max(1, B // world), device=dev,
-                                  user_offset=lo, frontier=frontier, **xp)
+                                  user_offset=lo, frontier=frontier, **xq)
         return ShardedTrainer.from_global_edges(edges, U, I, args.variant, cred=cred,
                                                 emb_dim=d, num_layers=K, batch_size=B,
-                                                device=dev, frontier=frontier, **xp)
+                                                device=dev, frontier=frontier, **xq)
 
     from bbgr.trainer import FRONTIER_MIN_EDGES
     count_steps = max(1, args.count_steps)
@@ -694,28 +703,87 @@ def main():
                     value=gathered_step * args.steps / elapsed,
                     ms_per_step=1000.0 * elapsed / args.steps)
 
+    backend_nccl = dist_mode and torch.distributed.get_backend() == "nccl"
+    # the user-row step as ONE chain with every collective in issue order on
+    # the compute stream: through the C ABI's RCCL communicator,
+    # or over gloo (ranks sharing a GPU, where RCCL cannot run) the same
+    # one-chain, one-range schedule through torch's collectives
+    inline_xp = None
+    if args.native_comm != "inline":
+        inline_xp = dict(xp, exchange_parts=1, frontier_parts=1)
+        inline_xp.pop("column_chains", None)
+        inline_xp.pop("native_comm", None)
+        if backend_nccl:
+            inline_xp["native_comm"] = "inline"
+
+    def chain_mode(xq: dict) -> str:
+        nc = xq.get("native_comm")
+        c = xq.get("column_chains", 1)
+        if nc == "inline":
+            return "1 chain, every collective inline on the compute stream (C ABI RCCL)"
+        how = ("C ABI RCCL on a comm stream" if nc else "torch collectives")
+        return f"{c} chain{'s' if c > 1 else ''}, {xq['exchange_parts']} item-row range(s), {how}"
+
     trainer = build(partition)
     res = measure(trainer, partition, args.dense_check)
+    res["xp"] = xp
+    runs = [res]
     U_job = U * (world if weak else 1)
-    partition_beside = None
+    strong_multi = dist_mode and world > 1 and not weak
+    todo = []
+    if strong_multi and partition == "users" and args.chain_beside and inline_xp is not None:
+        todo.append(("users", inline_xp))
     other = {"columns": "users", "users": "columns"}.get(partition)
-    if (dist_mode and world > 1 and not weak and not sharded_gen and args.partition_beside
+    if (strong_multi and not sharded_gen and args.partition_beside
             and (other == "users" or can_shard_columns(d, world))):
         # strong N > 1: the other partition, measured the same way right after;
         # the faster one is the line, the other is reported beside it (the
         # per-link exchange model cannot settle N = 2 / 4 without the links)
+        todo.append((other, xp))
+        if other == "users" and args.chain_beside and inline_xp is not None:
+            todo.append(("users", inline_xp))
+    for part, xq in todo:
         trainer.close()
         del trainer
         torch.cuda.empty_cache()
-        trainer = build(other)
-        res_other = measure(trainer, other, args.dense_check)
-        if res_other["elapsed"] < res["elapsed"]:
-            res, res_other = res_other, res
-        partition_beside = {k: res_other[k] for k in ("part", "ms_per_step", "value", "E",
-                                                       "final_loss")}
-        partition_beside["note"] = ("the other strong-scaling partition of the same graph, "
-                                    "timed the same way in the same run; the faster one is "
-                                    "the line")
+        trainer = build(part, xq)
+        r = measure(trainer, part, args.dense_check)
+        r["xp"] = xq
+        runs.append(r)
+    # every rank holds the same max-over-ranks times: the same choice everywhere
+    res = min(runs, key=lambda r: r["elapsed"])
+
+    def beside(r: dict, note: str) -> dict:
+        b = {k: r[k] for k in ("part", "ms_per_step", "value", "E", "final_loss")}
+        if r["part"] == "users":
+            b["chain_mode"] = chain_mode(r["xp"])
+        b["note"] = note
+        return b
+
+    partition_beside = chain_beside = None
+    others = [r for r in runs if r["part"] != res["part"]]
+    if others:
+        partition_beside = beside(min(others, key=lambda r: r["elapsed"]),
+                                  "the other strong-scaling partition of the same graph, timed "
+                                  "the same way in the same run; the faster one is the line")
+    users_runs = sorted((r for r in runs if r["part"] == "users"), key=lambda r: r["elapsed"])
+    if len(users_runs) == 2:
+        chain_beside = beside(users_runs[1],
+                              "the user-row partition's other chain setting, timed the same way "
+                              "in the same run (user-row line: "
+                              + chain_mode(users_runs[0]["xp"]) + ")")
+        chain_beside["faster_users_ms_per_step"] = users_runs[0]["ms_per_step"]
+        chain_beside["faster_chain_mode"] = chain_mode(users_runs[0]["xp"])
+        if not backend_nccl:
+            chain_beside["backend_note"] = ("gloo rehearsal: RCCL cannot run two ranks on one "
+                                            "GPU, so the one-chain setting uses torch's "
+                                            "collectives; on RCCL it runs inline through the "
+                                            "C ABI's communicator")
+    xsel = res.get("xp") or xp
+    sel_chains = xsel.get("column_chains", 1)
+    sel_parts = xsel.get("exchange_parts", args.exchange_parts)
+    sel_native = {True: "stream", "stream": "stream", "inline": "inline"}.get(
+        xsel.get("native_comm"), "off")
     columns = res["columns"]
     E, use_graph, timer, timer_steps = res["E"], res["use_graph"], res["timer"], res["timer_steps"]
     events_in_loop, elapsed, final_loss = res["events_in_loop"], res["elapsed"], res["final_loss"]
@@ -817,20 +885,21 @@ def main():
                                    "single GPU (fused trainer)" if not dist_mode else
                                    f"user-rows x{world}"
                                    + (" (sharded trainer)" if dist_mode and world == 1 else "")
-                                   + (f", {args.column_chains} column chains"
-                                      if dist_mode and not columns and args.column_chains > 1
+                                   + (f", {sel_chains} column chains"
+                                      if dist_mode and not columns and sel_chains > 1
                                       else "")
-                                   + (f", {args.exchange_parts} item-row ranges per exchange"
+                                   + (f", {sel_parts} item-row ranges per exchange"
                                       if dist_mode and not columns else "")
                                    + (f", collectives via the C ABI's communicator "
-                                      f"({args.native_comm})"
-                                      if dist_mode and not columns and args.native_comm != "off"
+                                      f"({sel_native})"
+                                      if dist_mode and not columns and sel_native != "off"
                                       else ""))},
         "bpr_steps_per_s": steps_per_s,
         "torch_gpu_reference": torch_ref,
         "dropin_module_step": dropin,
         "weak_beside": weak_beside,
         "partition_beside": partition_beside,
+        "chain_beside": chain_beside,
         "partition": ("columns" if columns else "users") if dist_mode else
                      (f"one column shard of {emulate}" if emulate else "single GPU"),
         "graph_replay": use_graph,

@@ -126,11 +126,29 @@ __device__ __forceinline__ T ld_edge(const T *p) {
 #ifndef BBGR_ROW_WAVES
 #define BBGR_ROW_WAVES 0
 #endif
+// occupancy target of the UNWEIGHTED (WMODE 0) one-row kernels: without one
+// the compiler takes 106 SGPRs, which admits only 6 workgroups per CU
+// (MI355X_MICROARCH.md, residency), at 7 / 8 waves 94 / 78 SGPRs and no spill;
+// the weighted forms spill at 8 (round 3's slower 8-wave A/B)
+#ifndef BBGR_ROW_WAVES0
+#define BBGR_ROW_WAVES0 0
+#endif
+// Two-row kernels at the 8-wave target hold at most 64 VGPRs: with 4 rows in
+// flight per row they spilled (12 / 24 B per lane in the full / masked form,
+// round 5: every 16-edge batch wrote and re-read its spill slots through L2,
+// 5-12.5M extra 64-B write requests per C4 launch, TCC_WRITE 25.0M / 32.5M
+// against the 20.0M of the output rows, profiles/r5c_*). 2 / 3 rows in flight
+// per row fit without spilling (55 / 59 VGPRs) and the many rows of a user
+// table keep the CU busy anyway: C4 full user products 1.556 -> 1.47-1.48
+// ms, the src-masked backward user product 1.14 -> 0.92 ms, step 17.00 ->
+// 16.51-16.55 ms (profiles/r5e_ab_spills.txt). The sums are unchanged bit for
+// bit (each row still adds its edges in CSR order).
+// tests/test_kernel_resources.py keeps every product kernel spill-free.
 #ifndef BBGR_PAIR_U
-#define BBGR_PAIR_U 4
+#define BBGR_PAIR_U 2
 #endif
 #ifndef BBGR_PAIR_U_MASKED
-#define BBGR_PAIR_U_MASKED 4
+#define BBGR_PAIR_U_MASKED 3
 #endif
 #ifndef BBGR_PAIR_WAVES
 #define BBGR_PAIR_WAVES 0
@@ -138,11 +156,10 @@ __device__ __forceinline__ T ld_edge(const T *p) {
 #ifndef BBGR_PAIR_WAVES_MASKED
 #define BBGR_PAIR_WAVES_MASKED 0
 #endif
-// the unweighted (WMODE 0) masked two-row kernel: 64 VGPRs either way, 7 waves
-// by the compiler's choice, 8 with the target (no spill). The src-masked
-// backward user product at C4 (20.6M gathers from the item frontier, dense
-// output) 0.984 -> 0.886 ms (tools/ab_spmm.sh, round 3); the weighted forms
-// spill at 8 and keep the default
+// the unweighted (WMODE 0) masked two-row kernel at 8 waves (59 VGPRs with 3
+// rows in flight per row, no spill; round 3 measured the 8-wave target 0.984
+// -> 0.886 ms for the src-masked backward user product, tools/ab_spmm.sh);
+// the weighted forms keep the compiler's choice
 #ifndef BBGR_PAIR_WAVES_MASKED0
 #define BBGR_PAIR_WAVES_MASKED0 8
 #endif
@@ -150,9 +167,11 @@ __device__ __forceinline__ T ld_edge(const T *p) {
 // spill): C4 full user products 1.484 -> 1.451 ms per launch (round 3 A/B;
 // the weighted forms spill at 8; an 8-wave target on the one-row kernels
 // measured slower, item products 1.816 -> 1.829 ms)
-// the unweighted d = 64 slot-bitmap kernel (spmm_bits_kernel)
+// the unweighted d = 64 slot-bitmap kernel (spmm_bits_kernel): the 8-wave
+// target spilled 16 B per lane after the single-live-edge path (round 4);
+// the compiler's choice (67 VGPRs, 7 waves) measures the same 0.094-0.097 ms
 #ifndef BBGR_BITS_WAVES0
-#define BBGR_BITS_WAVES0 8
+#define BBGR_BITS_WAVES0 0
 #endif
 #ifndef BBGR_PAIR_WAVES0
 #define BBGR_PAIR_WAVES0 8
@@ -204,6 +223,7 @@ __device__ __forceinline__ T ld_edge(const T *p) {
 
 template <int D> struct Tune {   // narrow rows (8, 16, 32): one-row kernels only
   static constexpr int row_u = 0;
+  static constexpr int row_waves0 = 0;
   static constexpr int row_waves = D == 32 ? BBGR_NARROW_WAVES32 : D == 16 ? BBGR_NARROW_WAVES16 : 0;
   static constexpr int masked_waves =
       D == 32 ? BBGR_NARROW_MASKED_WAVES32 : D == 16 ? BBGR_NARROW_MASKED_WAVES16 : 0;
@@ -213,6 +233,7 @@ template <int D> struct Tune {   // narrow rows (8, 16, 32): one-row kernels onl
 };
 template <> struct Tune<64> {
   static constexpr int row_u = BBGR_ROW_U, row_waves = BBGR_ROW_WAVES;
+  static constexpr int row_waves0 = BBGR_ROW_WAVES0;
   static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U, pair_u_masked = BBGR_PAIR_U_MASKED;
   static constexpr int pair_waves = BBGR_PAIR_WAVES, pair_waves_masked = BBGR_PAIR_WAVES_MASKED;
@@ -221,6 +242,7 @@ template <> struct Tune<64> {
 };
 template <> struct Tune<128> {
   static constexpr int row_u = BBGR_ROW_U128, row_waves = BBGR_ROW_WAVES128;
+  static constexpr int row_waves0 = row_waves;
   static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U128, pair_u_masked = BBGR_PAIR_U128;
   static constexpr int pair_waves = BBGR_PAIR_WAVES128, pair_waves_masked = BBGR_PAIR_WAVES128;
@@ -228,6 +250,7 @@ template <> struct Tune<128> {
 };
 template <> struct Tune<256> {
   static constexpr int row_u = BBGR_ROW_U256, row_waves = BBGR_ROW_WAVES256;
+  static constexpr int row_waves0 = row_waves;
   static constexpr int masked_waves = row_waves;
   static constexpr int pair_u = BBGR_PAIR_U256, pair_u_masked = BBGR_PAIR_U256;
   static constexpr int pair_waves = BBGR_PAIR_WAVES256, pair_waves_masked = BBGR_PAIR_WAVES256;
@@ -1033,7 +1056,9 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
 // (low-degree table) forms are their own symbols too, with their own
 // occupancy target.
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::row_waves) void spmm_kernel(SpmmParams P) {
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::row_waves0
+                                                     : Tune<D>::row_waves) void spmm_kernel(
+    SpmmParams P) {
   spmm_body<D, WMODE, false, false>(P);
 }
 
@@ -1045,7 +1070,9 @@ __global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::pair_waves0
 }
 
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::masked_waves : Tune<D>::row_waves) void
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? (Tune<D>::row_waves0 ? Tune<D>::row_waves0
+                                                                       : Tune<D>::masked_waves)
+                                                     : Tune<D>::row_waves) void
 spmm_masked_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true, false>(P);
 }
@@ -1060,8 +1087,9 @@ spmm_masked_pair_kernel(SpmmParams P) {
 // Slot-bitmap launches (args.src_bits, d >= 64, one row per group): liveness
 // from the bitmap, single-chunk long rows summed by their row's group
 // (chunk_row_serial). A symbol of its own so the plain masked kernels keep
-// their register budget. Unweighted at d = 64: an 8-wave target (63 VGPRs, no
-// spill), C4 0.108 -> 0.103 ms (round 3 A/B).
+// their register budget. Unweighted at d = 64: BBGR_BITS_WAVES0 (the round-3
+// 8-wave target spills since round 4's single-live-edge path; compiler's
+// choice now).
 template <int D, int WMODE>
 __global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 && D == 64 ? BBGR_BITS_WAVES0 : Tune<D>::masked_waves) void
 spmm_bits_kernel(
@@ -1072,7 +1100,9 @@ spmm_bits_kernel(
 // Full-CSR launch whose epilogue applies the fused Adam step (its bytes add the
 // parameter / moment streams): a third symbol so rooflines stay per kind.
 template <int D, int WMODE>
-__global__ __launch_bounds__(256) BBGR_WAVES(Tune<D>::row_waves) void spmm_adam_kernel(SpmmParams P) {
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::row_waves0
+                                                     : Tune<D>::row_waves) void spmm_adam_kernel(
+    SpmmParams P) {
   spmm_body<D, WMODE, false, false>(P);
 }
 

@@ -553,15 +553,21 @@ static bool dropin_bits_enabled() {
 // uses (release_bits clears the listed users' bits after the chain, as
 // FusedTrainer does), the list / count / hipcub workspace are overwritten. A
 // graph capture gets fresh ones (their zero fill is then part of the graph).
-static void frontier_bits(const Pair &P, Support &s, const Tensor &ui, int64_t d) {
-  if (d < 64 || !dropin_bits_enabled() || P.fu.csr.nnz == 0) return;
+// The returned lock (the pair's frontier mutex) is held by the caller until
+// release_bits has been issued: another host thread's backward on the same
+// stream then issues its marking after this one's clear, so stream order keeps
+// each chain's bitmap, list and count its own. Only the host-side issue is
+// serialised; the GPU work of different streams still overlaps.
+static std::unique_lock<std::mutex> frontier_bits(const Pair &P, Support &s, const Tensor &ui,
+                                                  int64_t d) {
+  std::unique_lock<std::mutex> g(P.fb_mu, std::defer_lock);
+  if (d < 64 || !dropin_bits_enabled() || P.fu.csr.nnz == 0) return g;
   const Tensor &slots = u2i_slots(P, ui.device());
   const int64_t nbits = P.bi.csr.nnz / 32 + 4;
   const auto i32 = at::TensorOptions().dtype(at::kInt).device(ui.device());
   Pair::FrontierBufs fresh, *b = &fresh;
-  std::unique_lock<std::mutex> g(P.fb_mu, std::defer_lock);
   if (!capturing()) {
-    g.lock();   // held while this call fills its stream's set (host-side only)
+    g.lock();
     b = &P.fb[(int64_t)(intptr_t)cur_stream()];
   }
   if (!b->bits.defined()) b->bits = at::zeros({nbits}, i32);
@@ -574,6 +580,7 @@ static void frontier_bits(const Pair &P, Support &s, const Tensor &ui, int64_t d
                         reinterpret_cast<uint32_t *>(s.bits.data_ptr<int32_t>()), 1,
                         cur_stream()),
         "bbgr_mark_slots");
+  return g;
 }
 
 // clear the listed users' bits again once the chain has read them (stream order)
@@ -876,9 +883,27 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
     s = Support{mu.narrow(0, 0, U), mi.narrow(0, 0, I), Tensor()};
   }
   if (gi_rows && K >= 1) s.gi_rows = ii;
+  std::unique_lock<std::mutex> fb_lock;
   if (gs && K >= 1 && iu.numel() > 0)
-    frontier_bits(*P, s, ru, d);
+    fb_lock = frontier_bits(*P, s, ru, d);
+  // the bitmap must be all-zero again on every exit: the clear is issued
+  // after the chain, also when the chain throws (then best effort: a clear
+  // that fails too leaves the error of the chain as the one reported)
+  struct Release {
+    const Pair &P;
+    const Support &s;
+    const Tensor &ru;
+    bool armed = true;
+    ~Release() {
+      if (!armed) return;
+      try {
+        release_bits(P, s, ru);
+      } catch (...) {
+      }
+    }
+  } rel{*P, s, ru};
   auto out = backward_chain(*P, gU, gI, K, gs, s);
+  rel.armed = false;
   release_bits(*P, s, ru);
   return out;
 }
@@ -1032,12 +1057,19 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_cuda(
 // (a lower bound; one launch instead of a cummax scan and its masks)
 // slot[b] = first b' with ids[b'] == ids[b] (ids in [0, n_rows)): bbgr_first_slot
 // over a per-(device, n_rows) scratch of INT32_MAX rows, kept between calls
-// (each call leaves it all INT32_MAX); one per stream, like the workspaces
+// (each call leaves it all INT32_MAX, in stream order); one per stream, like
+// the workspaces. At most kFirstSlotScratch tables are kept (the least
+// recently used is dropped): a process cycling through streams or model sizes
+// holds a bounded n_rows int32 each (20 MB for U = 5M). An entry inherited by a
+// new stream at a recycled address is still all INT32_MAX once the old
+// stream's work has drained, which destroying a stream waits for.
+static constexpr size_t kFirstSlotScratch = 8;
 static Tensor first_slot(const Tensor &ids_, int64_t n_rows) {
   Tensor ids = ids_.to(at::kLong).contiguous();
   Tensor slot = at::empty_like(ids);
   static std::mutex mu;
-  static std::map<std::tuple<int64_t, int64_t, int64_t>, Tensor> scratch;
+  static std::map<std::tuple<int64_t, int64_t, int64_t>, std::pair<Tensor, uint64_t>> scratch;
+  static uint64_t tick = 0;
   Tensor first;
   const auto fresh = [&] {
     return at::full({std::max<int64_t>(n_rows, 1)}, 0x7fffffff,
@@ -1050,8 +1082,17 @@ static Tensor first_slot(const Tensor &ids_, int64_t n_rows) {
     const auto key = std::make_tuple((int64_t)ids.device().index(), n_rows,
                                      (int64_t)(intptr_t)cur_stream());
     auto it = scratch.find(key);
-    if (it == scratch.end()) it = scratch.emplace(key, fresh()).first;
-    first = it->second;
+    if (it == scratch.end()) {
+      if (scratch.size() >= kFirstSlotScratch) {
+        auto lru = scratch.begin();
+        for (auto j = scratch.begin(); j != scratch.end(); ++j)
+          if (j->second.second < lru->second.second) lru = j;
+        scratch.erase(lru);
+      }
+      it = scratch.emplace(key, std::make_pair(fresh(), uint64_t(0))).first;
+    }
+    it->second.second = ++tick;
+    first = it->second.first;
   }
   check(bbgr_first_slot(ids.numel(), ids.data_ptr<int64_t>(), n_rows, first.data_ptr<int32_t>(),
                         slot.data_ptr<int64_t>(), cur_stream()),

@@ -424,6 +424,21 @@ class ItemExchange:
         return r, 1.0 / ys_s
 
 
+def _item_table_owner(fn):
+    """Marks a ShardedTrainer method that may read the item table while rows
+    owned by other ranks lag (ShardedTrainer.item_w)."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        self.__dict__["_inside"] = self.__dict__.get("_inside", 0) + 1
+        try:
+            return fn(self, *args, **kwargs)
+        finally:
+            self.__dict__["_inside"] -= 1
+    return wrapper
+
+
 class ShardedTrainer(FusedTrainer):
     """FusedTrainer's step on one user shard (see the module docstring).
 
@@ -628,6 +643,28 @@ class ShardedTrainer(FusedTrainer):
         tr.bounds = bounds
         return tr
 
+    # -- the item weight table ----------------------------------------------
+    @property
+    def item_w(self) -> torch.Tensor:
+        """The item weight table (internal rows). With item ownership at N > 1
+        a step updates only this rank's owned rows and the next batch's item
+        rows are refreshed from their owners, so between steps the other rows
+        lag the owners' values. Reading it then raises instead of returning
+        stale rows: call sync_items() on every rank first (collective), or read
+        sync_items()["item_w"]. The reference's weights are always current
+        (Version-2/lighgcn_cu_pop.py:863); step(), forward(), state_dict() and
+        sync_items() read it internally."""
+        if self.__dict__.get("_items_stale") and not self.__dict__.get("_inside", 0):
+            raise RuntimeError(
+                "ShardedTrainer.item_w: item rows owned by other ranks are stale between "
+                "steps (item ownership, N > 1); call sync_items() on every rank first "
+                "(collective), or read sync_items()['item_w']")
+        return self.__dict__["_item_table"]
+
+    @item_w.setter
+    def item_w(self, t: torch.Tensor) -> None:
+        self.__dict__["_item_table"] = t
+
     def _build_chains(self, n: int, emb_dim: int, group, parts: int, frontier_parts: int,
                       native_comm: bool, indptr_i, dev) -> list:
         if n == 1:
@@ -811,6 +848,7 @@ class ShardedTrainer(FusedTrainer):
             refresh_from_owners(self.item_w, rows, self.item_bounds, self.group,
                                 gather=self._gather)
 
+    @_item_table_owner
     def sync_items(self) -> dict:
         """Collective (every rank calls it): make the whole item weight table
         current on this rank and return the item tables by internal row:
@@ -824,6 +862,7 @@ class ShardedTrainer(FusedTrainer):
         return {"item_w": self.item_w, "m_i": gather_owned(self.m_i, self.item_bounds, g),
                 "v_i": gather_owned(self.v_i, self.item_bounds, g)}
 
+    @_item_table_owner
     def forward(self):
         """Final (layer-mean) tables of the rank's users and of every item,
         rows by input id (collective: the item sums are exchanged)."""
@@ -833,6 +872,7 @@ class ShardedTrainer(FusedTrainer):
         from .trainer import _input_rows
         return _input_rows(self.graph.user_order, uf), _input_rows(self.graph.item_order, itf)
 
+    @_item_table_owner
     def state_dict(self) -> dict:
         """Reference keys (Version-2:903) of this rank's user rows and every
         item row, by input id (collective)."""
@@ -865,6 +905,7 @@ class ShardedTrainer(FusedTrainer):
             f.mask_i.zero_()
         f.rows = None
 
+    @_item_table_owner
     def step(self, prefetch: bool = True) -> torch.Tensor:
         """One training step. prefetch=False: do not prepare the next step's
         batch (a caller's last step; no batch is sampled and exchanged that

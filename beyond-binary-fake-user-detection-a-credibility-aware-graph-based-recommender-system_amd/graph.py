@@ -51,6 +51,11 @@ def long_threshold_for(nnz: int) -> int:
 # the 256 MB Infinity Cache for the streams of the launch; at most 1/8 of the
 # rows (C4: the 625k highest-degree users and 125k items stay cached).
 HOT_BYTES = 192 << 20
+# Output store policy of degree-ordered tables (A/B runs, BBGR_STREAM_OUT):
+# "split" = the hot prefix default-policy, the rest non-temporal (stream_out_from);
+# "nt" = every row non-temporal; "none" = every row default-policy.
+import os as _os  # noqa: E402
+OUT_POLICY = _os.environ.get("BBGR_STREAM_OUT", "split")
 
 
 def _as_device_i32(x, device) -> torch.Tensor:
@@ -199,6 +204,10 @@ class Csr:
             return 0
         hot = self.__dict__.get("hot_bytes", HOT_BYTES)
         if self.n_rows * 4 * d <= hot:
+            return 0
+        if OUT_POLICY == "nt":      # A/B: every output row streamed
+            return 1
+        if OUT_POLICY == "none":    # A/B: every output row default policy
             return 0
         return max(1, min(self.n_rows // 8, hot // (4 * d)))
 

@@ -18,6 +18,10 @@ from __future__ import annotations
 import torch
 
 from . import bpr as _bpr
+# the reference module's host CSR helpers / samplers, bit-exact (numpy stream
+# included) and O(log I) per popularity draw: bbgr.host_sampler
+from .host_sampler import (edges_to_user_csr, sample_neg_item, sample_pos_item,
+                           user_has_item)  # noqa: F401
 from ._lib import OP_SYM
 from .operators import NormAdjOperator, build_pair, square_from_torch_sparse
 from .propagate import (ORDER_J, OperatorPair, _SquareFn, backward as _bwd,

@@ -17,6 +17,10 @@ import numpy as np
 import torch
 
 from . import bpr as _bpr
+# the reference module's host CSR helpers / samplers, bit-exact (numpy stream
+# included) and O(log I) per popularity draw: bbgr.host_sampler
+from .host_sampler import (edges_to_user_csr, sample_neg_item, sample_pos_item,
+                           user_has_item)  # noqa: F401
 from ._lib import OP_J
 from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator, build_pair,
                         input_order_vector, resolve_pair)

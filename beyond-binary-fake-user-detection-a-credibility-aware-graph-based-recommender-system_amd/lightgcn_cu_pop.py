@@ -23,6 +23,10 @@ from __future__ import annotations
 import torch
 
 from . import bpr as _bpr
+# the reference module's host CSR helpers / samplers, bit-exact (numpy stream
+# included) and O(log I) per popularity draw: bbgr.host_sampler
+from .host_sampler import (edges_to_user_csr, sample_neg_item_popmix, sample_pos_item,
+                           user_has_item)  # noqa: F401
 from . import lazy as _lazy
 from ._lib import OP_GS
 from .operators import (ITEM_FROM_USER, USER_FROM_ITEM, BipartiteOperator, build_pair,

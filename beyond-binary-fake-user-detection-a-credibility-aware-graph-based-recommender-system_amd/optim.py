@@ -157,4 +157,8 @@ class FusedAdam(torch.optim.Optimizer):
                 adam_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"],
                           int(st["step"].item()), group["lr"], b1, b2, group["eps"],
                           group["weight_decay"])
+                # the kernel wrote p through a raw pointer: bump its version as an
+                # in-place torch op would, so autograd's saved-tensor checks and
+                # the deferred final tables (bbgr.lazy) see the update
+                torch.autograd.graph.increment_version(p)
         return loss

@@ -309,12 +309,19 @@ class ListLength:
     products, milliseconds of queued GPU work — so the GPU does not idle.
     Inside a graph capture (or before publish / after invalidate) the launch
     keeps the device count. The rows and their arithmetic are the same either
-    way (bitwise). BBGR_LIST_HOST=0 keeps the device count always (A/B runs)."""
+    way (bitwise). BBGR_LIST_HOST=0 keeps the device count always (A/B runs).
+
+    `wait`: whether a consumer may block on the copy. Only where the stream
+    holds queued work between the list and its first consumer (the trainer's
+    K >= 2 dense forward layers) does the wait cost the GPU nothing; with
+    wait=False a consumer takes the published length only if the copy has
+    already landed (event query), else the device count."""
 
     enabled = os.environ.get("BBGR_LIST_HOST", "1") != "0"
 
-    def __init__(self, count: torch.Tensor):
+    def __init__(self, count: torch.Tensor, wait: bool = True):
         self.count = count
+        self.wait = bool(wait)
         self._host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
         self._event = None
 
@@ -331,10 +338,14 @@ class ListLength:
         self._event = None
 
     def length(self) -> int | None:
-        """The published length (waits for its copy), or None: use the device count."""
+        """The published length (waiting for its copy when `wait`), or None:
+        use the device count."""
         if self._event is None or torch.cuda.is_current_stream_capturing():
             return None
-        self._event.synchronize()
+        if not self._event.query():
+            if not self.wait:
+                return None
+            self._event.synchronize()
         return int(self._host[0])
 
 

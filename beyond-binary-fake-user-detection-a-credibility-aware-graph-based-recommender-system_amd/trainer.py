@@ -152,7 +152,9 @@ class FusedTrainer:
         if self.frontier and order == ORDER_GS:
             self.item_list = torch.empty(max(self.I, 1), dtype=torch.int64, device=dev)
             self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
-            self.item_len = ListLength(self.item_count)
+            # a host wait for the list's length is free only behind the dense
+            # forward layers (K >= 2); at K = 1 its consumer is the next launch
+            self.item_len = ListLength(self.item_count, wait=num_layers >= 2)
         # Fused optimizer (GS order): the user Adam runs inside the last backward
         # product's epilogue and the item Adam reads gI/(K+1) straight from the
         # sparse BPR gradient table (grad_scale), so neither weight-gradient

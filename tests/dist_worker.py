@@ -100,7 +100,15 @@ def fused_vs_separate(out_dir, variant):
                         device="cuda:0", u0=u0, i0=i0, user_offset=rank * WEAK_U,
                         exchange_parts=2, fuse_adam=True, frontier=True, overlap_item_adam=False)
     losses = [float(tr.step()) for _ in range(3)]
+    # between steps, rows owned by the other rank lag: reading the table raises
+    # (1) instead of returning them; without ownership it reads (2)
+    try:
+        tr.item_w
+        out["stale_guard"] = np.array(2)
+    except RuntimeError:
+        out["stale_guard"] = np.array(1)
     items = tr.sync_items()
+    out["inchain_item_w_attr"] = tr.item_w.cpu().numpy()   # current after sync_items()
     out["inchain_user_w"] = tr.user_w.cpu().numpy()
     out["inchain_item_w"] = items["item_w"].cpu().numpy()
     out["inchain_m_i"] = items["m_i"].cpu().numpy()

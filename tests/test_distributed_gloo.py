@@ -162,3 +162,28 @@ def test_item_ownership_refresh_and_gather_are_exact(tmp_path, world):
         assert got.tobytes() == want.tobytes()
         assert np.signbit(got[3]).all()        # -0.0 copied, not summed
         assert z["whole"].tobytes() == z["truth"].tobytes()
+
+
+def test_sharded_item_table_guard_raises_on_stale_rows():
+    """ShardedTrainer.item_w: between steps with item
+    ownership at N > 1 the rows owned by other ranks lag, so an outside read
+    raises (never returns stale rows); the trainer's own methods (step,
+    sync_items, forward, state_dict) read it; once current it reads freely."""
+    import torch
+    from bbgr.distributed import ShardedTrainer, _item_table_owner
+    tr = object.__new__(ShardedTrainer)
+    t = torch.arange(6.0).reshape(3, 2)
+    tr.item_w = t
+    tr._items_stale = False
+    assert tr.item_w is t
+    tr._items_stale = True                       # after an owned-rows Adam at N > 1
+    with pytest.raises(RuntimeError, match="sync_items"):
+        tr.item_w
+    inside = _item_table_owner(lambda self: self.item_w)
+    assert inside(tr) is t                       # the trainer's own methods
+    with pytest.raises(RuntimeError):            # ... and only while inside
+        tr.item_w
+    tr._items_stale = False                      # what sync_items() leaves
+    assert tr.item_w is t
+    for name in ("step", "sync_items", "forward", "state_dict"):
+        assert getattr(ShardedTrainer, name).__wrapped__ is not None

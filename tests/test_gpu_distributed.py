@@ -135,6 +135,12 @@ def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
             if variant == "v2_pop":
                 np.testing.assert_array_equal(rk[f"fused_sparse_{key}"],
                                               rk[f"replicated_{key}"])
+    for rk in ranks:   # the stale-row guard
+        own = variant == "v2_pop"   # item ownership: GS with the fused Adam
+        assert int(rk["stale_guard"]) == (1 if own else 2)
+        np.testing.assert_array_equal(rk["inchain_item_w_attr"], rk["inchain_item_w"])
+        if own:
+            np.testing.assert_array_equal(rk["inchain_item_w_attr"], rk["replicated_item_w"])
     # two column chains (column_chains=2): the same step over two 32-column
     # slices on their own streams and groups; narrow rows sum in slot order,
     # so equal to rounding, and replicas still bitwise identical
@@ -225,7 +231,7 @@ def test_bench_two_ranks_on_c2(tmp_path, partition):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "3",
            "--warmup", "1", "--dense-check", "1", "--frontier", "on", "--partition", partition,
-           "--weak-beside", "2", "--partition-beside", "0"] + \
+           "--weak-beside", "2", "--partition-beside", "0", "--chain-beside", "0"] + \
         (["--column-chains", "2"] if chains else [])
     env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
@@ -276,3 +282,14 @@ def test_bench_two_ranks_measures_both_partitions(tmp_path):
     assert {j["partition"], b["part"]} == {"columns", "users"}
     assert j["ms_per_step"] <= b["ms_per_step"] and b["E"] == 1_000_000
     assert j["weak_beside"] is None and j["dense_ms_per_step"] > 0
+    # --chain-beside (default): the user-row step in both chain settings — the
+    # default (1 chain, 4 ranges over gloo at N = 2) and the one-chain inline
+    # schedule — the slower reported beside, the faster named in it
+    c = j["chain_beside"]
+    assert c["part"] == "users" and c["E"] == 1_000_000
+    assert c["chain_mode"] != c["faster_chain_mode"]
+    assert c["faster_users_ms_per_step"] <= c["ms_per_step"]
+    assert "1 item-row range" in c["chain_mode"] + c["faster_chain_mode"]
+    assert "gloo" in c["backend_note"]
+    users_ms = (j["ms_per_step"] if j["partition"] == "users" else b["ms_per_step"])
+    assert users_ms == c["faster_users_ms_per_step"]

@@ -103,9 +103,14 @@ def test_deferred_tables_compute_on_use_and_equal_the_dense_tables():
     assert torch.equal(s, (ru[:10] @ ri.T).detach())
 
 
-def test_deferred_tables_read_after_a_weight_update_raise():
+@pytest.mark.parametrize("opt_name", ["torch", "fused"])
+def test_deferred_tables_read_after_a_weight_update_raise(opt_name):
+    """torch.optim.Adam bumps the weights' versions; bbgr.optim.FusedAdam writes
+    them through a raw pointer and bumps them itself: either way a deferred
+    table read after the step raises instead of using the new weights."""
+    from bbgr.optim import FusedAdam
     m = _model(3)
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    opt = (torch.optim.Adam if opt_name == "torch" else FusedAdam)(m.parameters(), lr=1e-3)
     users, pos, neg = _batch(0)
     uf, itf = m.get_user_item_emb()
     m.bpr_loss(users, pos, neg, uf, itf, 1e-4).backward()

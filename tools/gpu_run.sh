@@ -1,0 +1,115 @@
+#!/bin/bash
+# The one GPU-box runner (gpurun), replacing the per-run scripts of round 4:
+#
+#   gpurun --timeout T -- bash tools/gpu_run.sh <tag> <step> [<step> ...]
+#
+# Output lands in gpurun_out/<tag>/. Every GPU step runs under its own
+# timeout; the first hard failure (fault, abort, segfault, time limit) ends the
+# script, and no step is ever retried.
+#
+# steps:
+#   box        GPU / driver / partition / clock facts of this box (box.txt)
+#   tests      the whole `pytest -m gpu` suite (TESTS=<pytest args> narrows it)
+#   smoke      __graft_entry__.smoke()
+#   bench      the default bench line (BENCH_ARGS appended), bench.json
+#   quick      bench --steps 10 without the CPU / stock-torch / drop-in legs
+#   profile    tools/profile_box.sh <tag> (kernel trace + FETCH_SIZE + WRITE_SIZE)
+#   storeab    output store policy A/B (BBGR_STREAM_OUT = split / nt / none):
+#              a quick bench and a WRITE_SIZE + FETCH_SIZE pass over the SpMM
+#              kernels for each policy
+#   shard      tools/shard_probe.py with SHARD_ARGS (one user-row rank alone)
+#   rehearse   bench.py --gpus $N over gloo, N ranks on this one GPU (N=2 default)
+set -o pipefail
+T=$1; shift
+O=gpurun_out/$T
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+
+hard() {  # rc, step, log: stop on a fault / abort / segfault / time limit
+  case $1 in 124|134|137|139) echo "HARD FAIL ($1) in $2"; tail -30 "$3"; exit 1;; esac
+}
+quick_args="--steps 10 --warmup 2 --no-cpu-baseline --no-torch-reference --dense-check 0"
+
+for step in "$@"; do
+  s0=$(date +%s)
+  case $step in
+    box)
+      { rocm-smi --showproductname --showmemorypartition --showcomputepartition \
+          --showclocks --showdriverversion --showfwinfo 2>&1
+        rocminfo 2>&1 | grep -E "Marketing Name|Compute Unit|Max Clock|Cache Info|L1|L2|L3|Chip ID" | head -40
+        uname -r; grep -m1 "model name" /proc/cpuinfo; nproc; free -g | head -2
+      } > "$O/box.txt" 2>&1
+      grep -E "Memory Partition|Compute Partition|sclk|mclk|fclk" "$O/box.txt" | head -12 ;;
+    tests)
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 500 \
+        --timeout-method thread ${TESTS:-} > "$O/gpu_tests.log" 2>&1
+      rc=$?; hard $rc tests "$O/gpu_tests.log"
+      echo "TESTS rc=$rc"; grep -E "passed|failed" "$O/gpu_tests.log" | tail -1
+      grep FAILED "$O/gpu_tests.log" | head
+      [ $rc -eq 0 ] || exit 1 ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
+      rc=$?; hard $rc smoke "$O/smoke.log"; echo "SMOKE rc=$rc"; tail -1 "$O/smoke.log"
+      [ $rc -eq 0 ] || exit 1 ;;
+    bench)
+      timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > "$O/bench.json" 2> "$O/bench.log"
+      rc=$?; hard $rc bench "$O/bench.log"; echo "BENCH rc=$rc"
+      [ $rc -eq 0 ] || { tail -20 "$O/bench.log"; exit 1; }
+      python tools/bench_brief.py "$O/bench.json" ;;
+    quick)
+      timeout -k 10 400 python -u bench.py $quick_args ${BENCH_ARGS:-} > "$O/quick.json" 2> "$O/quick.log"
+      rc=$?; hard $rc quick "$O/quick.log"; echo "QUICK rc=$rc"
+      [ $rc -eq 0 ] || { tail -20 "$O/quick.log"; exit 1; }
+      python tools/bench_brief.py "$O/quick.json" ;;
+    profile)
+      timeout -k 10 1000 bash tools/profile_box.sh "$T" ${PROFILE_ARGS:-} > "$O/profile.log" 2>&1
+      rc=$?; hard $rc profile "$O/profile.log"; echo "PROFILE rc=$rc"
+      [ $rc -eq 0 ] || { tail -30 "$O/profile.log"; exit 1; } ;;
+    storeab)
+      pargs="--steps 4 --warmup 1 --no-cpu-baseline --no-torch-reference --dense-check 0 --count-steps 1"
+      for pol in ${POLICIES:-split nt none}; do
+        BBGR_STREAM_OUT=$pol timeout -k 10 400 python -u bench.py $quick_args \
+          > "$O/ab_$pol.json" 2> "$O/ab_$pol.log"
+        rc=$?; hard $rc "ab $pol" "$O/ab_$pol.log"; [ $rc -eq 0 ] || { tail -20 "$O/ab_$pol.log"; exit 1; }
+        echo "policy $pol: $(python tools/bench_brief.py "$O/ab_$pol.json" | head -1)"
+        for c in WRITE_SIZE FETCH_SIZE; do
+          BBGR_STREAM_OUT=$pol timeout -k 10 400 rocprofv3 --pmc $c -T --output-format csv \
+            --kernel-include-regex "spmm" -d "$O/pmc_${pol}_$c" -o run \
+            -- python3 bench.py $pargs > "$O/pmc_${pol}_$c.json" 2> "$O/pmc_${pol}_$c.log"
+          rc=$?; hard $rc "pmc $pol $c" "$O/pmc_${pol}_$c.log"
+          [ $rc -eq 0 ] || { tail -20 "$O/pmc_${pol}_$c.log"; exit 1; }
+        done
+      done
+      python tools/pmc_brief.py "$O" ;;
+    counters)  # the PMC counters this box offers
+      timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1
+      echo "COUNTERS rc=$?"; grep -c "TCC" "$O/counters.txt" ;;
+    pmc)       # PMC passes over the SpMM kernels: PMC_SETS = "CTR1,CTR2 CTR3 ..." (one pass per word)
+      pargs="--steps 4 --warmup 1 --no-cpu-baseline --no-torch-reference --dense-check 0 --count-steps 1"
+      k=0
+      for set in ${PMC_SETS:-}; do
+        k=$((k+1))
+        timeout -s KILL 120 rocprofv3 --pmc ${set//,/ } -T --output-format csv \
+          --kernel-include-regex "${PMC_REGEX:-spmm}" -d "$O/pmcset_$k" -o run \
+          -- python3 bench.py $pargs ${BENCH_ARGS:-} > "$O/pmcset_$k.json" 2> "$O/pmcset_$k.log"
+        rc=$?; hard $rc "pmc set $set" "$O/pmcset_$k.log"
+        [ $rc -eq 0 ] || { tail -20 "$O/pmcset_$k.log"; exit 1; }
+        echo "pmc set $k ($set) ok"
+      done ;;
+    shard)
+      timeout -k 10 900 python -u tools/shard_probe.py ${SHARD_ARGS:-} > "$O/shard.jsonl" 2> "$O/shard.log"
+      rc=$?; hard $rc shard "$O/shard.log"; echo "SHARD rc=$rc"; tail -3 "$O/shard.jsonl"
+      [ $rc -eq 0 ] || { tail -20 "$O/shard.log"; exit 1; } ;;
+    rehearse)
+      n=${N:-2}
+      BBGR_DIST_BACKEND=gloo timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus "$n" \
+        --steps 3 --warmup 1 ${REHEARSE_ARGS:-} > "$O/rehearsal_gloo$n.json" 2> "$O/rehearsal_gloo$n.log"
+      rc=$?; hard $rc rehearse "$O/rehearsal_gloo$n.log"; echo "REHEARSE N=$n rc=$rc"
+      [ $rc -eq 0 ] || { tail -20 "$O/rehearsal_gloo$n.log"; exit 1; }
+      python tools/bench_brief.py "$O/rehearsal_gloo$n.json" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  echo "[$step] $(( $(date +%s) - s0 )) s"
+done
+echo ALL_DONE
