@@ -841,7 +841,7 @@ def main():
                              "(sparse_coo_tensor.coalesce, torch.sparse.mm, stack.mean, "
                              "autograd, torch.optim.Adam) on this GPU, uniform batches "
                              "(tools/torch_sparse_step.py); not the oracle, not the product")
-    dropin = None
+    dropin = dropin_fused = dropin_bwd = None
     if (not args.no_torch_reference and not dist_mode and not sharded_gen and not emulate
             and args.variant == "v2_pop"):
         # the same step through the drop-in module API (lightgcn_cu_pop.LightGCN on
@@ -849,15 +849,25 @@ def main():
         log("[bench] timing the drop-in module step ...")
         if os.path.join(ROOT, "tools") not in sys.path:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from dropin_probe import run as dropin_run
-        dropin = dropin_run(args.config, edges, cred, device=dev)
-        dropin["note"] = ("Version-2 LightGCN drop-in (bbgr ops: propagate, bpr_loss and "
-                          "their registered backward; get_user_item_emb() tables deferred, "
-                          "so bpr_loss computes the batch rows only, bbgr::propagate_rows) + "
-                          "torch.optim.Adam(foreach), input vertex order, uniform batches "
-                          "(tools/dropin_probe.py)")
+        from dropin_probe import run_many as dropin_run_many
+        runs = dropin_run_many(args.config, edges, cred, device=dev,
+                               adams=("foreach", "bbgr", "bbgr_bwd"))
+        dropin, dropin_fused, dropin_bwd = runs["foreach"], runs["bbgr"], runs["bbgr_bwd"]
+        common = ("Version-2 LightGCN drop-in (bbgr ops: propagate, bpr_loss and their "
+                  "registered backward; get_user_item_emb() tables deferred, so bpr_loss "
+                  "computes the batch rows only, bbgr::propagate_rows), input vertex order, "
+                  "uniform batches (tools/dropin_probe.py)")
+        dropin["note"] = common + " + torch.optim.Adam(foreach), the reference's optimizer"
+        dropin_fused["note"] = (common + " + bbgr.optim.FusedAdam (same state keys), on the "
+                                "same model right after the foreach timing")
+        dropin_bwd["note"] = (common + " + bbgr.optim.FusedAdam(fuse_backward=True): the "
+                              "optimizer step inside loss.backward(), in the last backward "
+                              "products' epilogues (bbgr::bpr_adam_backward); the loop body "
+                              "unchanged")
         if torch_ref is not None:
             dropin["speedup_vs_torch"] = torch_ref["step_ms"] / dropin["step_ms"]
+            dropin_fused["speedup_vs_torch"] = torch_ref["step_ms"] / dropin_fused["step_ms"]
+            dropin_bwd["speedup_vs_torch"] = torch_ref["step_ms"] / dropin_bwd["step_ms"]
     dense_equiv = 4 * K * E
     out = {
         "metric": "SpMM edges/sec + BPR steps/sec, |E|=50M d=64, 1/2/4/8 MI355X; %HBM roofline",
@@ -897,6 +907,8 @@ def main():
         "bpr_steps_per_s": steps_per_s,
         "torch_gpu_reference": torch_ref,
         "dropin_module_step": dropin,
+        "dropin_fused_adam_step": dropin_fused,
+        "dropin_backward_adam_step": dropin_bwd,
         "weak_beside": weak_beside,
         "partition_beside": partition_beside,
         "chain_beside": chain_beside,

@@ -90,6 +90,7 @@ class SpmmArgs(ctypes.Structure):
         ("row_count", c_void_p),
         ("acc_in_map", c_void_p),
         ("adam_grad", c_void_p), ("adam_grad_ld", c_int64), ("adam_grad_scale", c_float),
+        ("adam_map", c_void_p),
     ]
 
 
@@ -237,7 +238,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 6:
+        if handle.bbgr_abi_version() != 7:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

@@ -51,7 +51,7 @@ def column_range(emb_dim: int, parts: int, index: int) -> tuple[int, int]:
 # Narrowest column shard the bench's auto partition picks: random gathers of
 # rows under 64 B (16 fp32 columns) fetch whole cache lines for a fraction of
 # them. Measured per-rank C4 steps (one shard alone, tools/probes/column_probe.py,
-# profiles/r23_*, r32_*): 32 columns 9.05 ms, 16 columns 7.85 ms, 8 columns 7.76 ms
+# profiles/round1-2/r23_*, r32_*): 32 columns 9.05 ms, 16 columns 7.85 ms, 8 columns 7.76 ms
 # (the 8-column item product fetches ~3.7x its bytes); single GPU 16.7 ms.
 MIN_AUTO_WIDTH = 16
 

@@ -85,6 +85,7 @@ struct SpmmParams {
   const float *adam_g;         // fused Adam's own gradient table (args.adam_grad; nullable)
   long adam_g_ld;
   float adam_g_scale;
+  const int *adam_map;         // the fused Adam's row map (args.adam_map; NULL: y_map's)
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -137,11 +138,11 @@ __device__ __forceinline__ T ld_edge(const T *p) {
 // flight per row they spilled (12 / 24 B per lane in the full / masked form,
 // round 5: every 16-edge batch wrote and re-read its spill slots through L2,
 // 5-12.5M extra 64-B write requests per C4 launch, TCC_WRITE 25.0M / 32.5M
-// against the 20.0M of the output rows, profiles/r5c_*). 2 / 3 rows in flight
+// against the 20.0M of the output rows, profiles/round5/r5c_*). 2 / 3 rows in flight
 // per row fit without spilling (55 / 59 VGPRs) and the many rows of a user
 // table keep the CU busy anyway: C4 full user products 1.556 -> 1.47-1.48
 // ms, the src-masked backward user product 1.14 -> 0.92 ms, step 17.00 ->
-// 16.51-16.55 ms (profiles/r5e_ab_spills.txt). The sums are unchanged bit for
+// 16.51-16.55 ms (profiles/round5/r5e_ab_spills.txt). The sums are unchanged bit for
 // bit (each row still adds its edges in CSR order).
 // tests/test_kernel_resources.py keeps every product kernel spill-free.
 #ifndef BBGR_PAIR_U
@@ -657,8 +658,9 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
         for (int k = 0; k < V; ++k) dst[16 * k] = G[k];
       }
     }
+    const long ra_ = P.adam_map ? (long)P.adam_map[row] : ry;   // the Adam's rows
     if (P.adam_p && P.adam_g) {   // Adam of another table riding on this row write
-      const float4 *gr = reinterpret_cast<const float4 *>(P.adam_g + ry * P.adam_g_ld) + lane;
+      const float4 *gr = reinterpret_cast<const float4 *>(P.adam_g + ra_ * P.adam_g_ld) + lane;
       float4 Ga[V];
 #pragma unroll
       for (int k = 0; k < V; ++k) {   // gs * g, as adam_kernel forms it
@@ -666,9 +668,9 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
         Ga[k] = make_float4(P.adam_g_scale * g4.x, P.adam_g_scale * g4.y,
                             P.adam_g_scale * g4.z, P.adam_g_scale * g4.w);
       }
-      adam_row<D>(P, ry, lane, Ga);
+      adam_row<D>(P, ra_, lane, Ga);
     } else if (P.adam_p) {
-      adam_row<D>(P, ry, lane, G);
+      adam_row<D>(P, ra_, lane, G);
     }
   }
   const long rc = P.acc_map ? (long)P.acc_map[row] : (long)row;
@@ -1237,6 +1239,7 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.adam_g = a->adam_grad;
   P.adam_g_ld = a->adam_grad_ld;
   P.adam_g_scale = a->adam_grad_scale;
+  P.adam_map = a->adam_map;
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {

@@ -153,6 +153,14 @@ static float *workspace(const Product &pr, int d, const at::Device &dev) {
 }
 
 // -- one fused SpMM launch (propagate.spmm) ------------------------------------
+// One parameter table's Adam step (torch.optim.Adam semantics, host bias
+// corrections): bbgr.optim.FusedAdam in backward mode hands these over.
+struct AdamTable {
+  Tensor p, m, v;
+  float lr = 1e-3f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, wd = 0.f;
+  float bc1 = 1.f, bc2s = 1.f;
+};
+
 struct Opts {
   Tensor y;
   const float *y_scale = nullptr;
@@ -172,7 +180,14 @@ struct Opts {
   const int64_t *row_list = nullptr, *row_count = nullptr;   // device-length row list
   int64_t n_row_list = 0;
   const uint32_t *src_bits = nullptr;                         // slot bitmap of src_mask
+  // fused Adam on this launch's rows (bbgr_spmm_args.adam_*; null: none)
+  const AdamTable *adam = nullptr;
+  const float *adam_grad = nullptr;   // its gradient table (nullable: the row value)
+  int64_t adam_grad_ld = 0;
+  float adam_grad_scale = 1.f;
+  const int32_t *adam_map = nullptr;  // its row map (nullable: y_map's)
 };
+
 
 static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) {
   bbgr_spmm_args a;
@@ -218,6 +233,24 @@ static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) 
   a.n_row_list = o.n_row_list;
   a.row_count = o.row_count;
   a.src_bits = o.src_bits;
+  if (o.adam) {
+    const AdamTable &A = *o.adam;
+    a.adam_param = A.p.data_ptr<float>();
+    a.adam_exp_avg = A.m.data_ptr<float>();
+    a.adam_exp_avg_sq = A.v.data_ptr<float>();
+    a.adam_ld = ld(A.p);
+    a.adam_lr = A.lr;
+    a.adam_beta1 = A.beta1;
+    a.adam_beta2 = A.beta2;
+    a.adam_eps = A.eps;
+    a.adam_weight_decay = A.wd;
+    a.adam_bias_correction1 = A.bc1;
+    a.adam_bias_correction2_sqrt = A.bc2s;
+    a.adam_grad = o.adam_grad;
+    a.adam_grad_ld = o.adam_grad_ld;
+    a.adam_grad_scale = o.adam_grad_scale;
+    a.adam_map = o.adam_map;
+  }
   // input-order source rows carry no hot prefix; mapped output rows neither
   a.stream_from = o.src_input ? 0 : pr.stream_from(d);
   a.stream_out_from = o.y_map ? 0 : pr.stream_out_from(d);
@@ -593,14 +626,32 @@ static void release_bits(const Pair &P, const Support &s, const Tensor &ui) {
         "bbgr_mark_slots (clear)");
 }
 
+// The drop-in's in-backward Adam (GS, K >= 2; bbgr_torch::bpr_adam_backward):
+// the user step rides on the last user product, which then writes no gradient
+// table; the item step on the last item product (a dense launch over every
+// item row), reading its gradient gl * item_grad from a caller-order side
+// table (gI + (K+1) * ego rows, formed before the chain); the batch users'
+// ego-L2 rows enter gU just before the last user product (gU[r] += (K+1) *
+// ego[r], so G = out * T + gl * gU carries them), as FusedTrainer does.
+static void index_add_rows(Tensor &dst, const Tensor &index, const Tensor &src);
+
+struct StepAdam {
+  AdamTable user, item;
+  Tensor item_grad;                 // [I, d], caller's row order
+  Tensor ego_u_vals;                // (K+1) * ego rows, aligned with the users' rows
+  Tensor ego_u_rows;                // their gU rows (set by rows_backward)
+};
+
 static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU, const Tensor &gI,
                                                  int64_t K, bool gs, const Support &s,
-                                                 Tensor gu0 = Tensor(), Tensor gi0 = Tensor()) {
+                                                 Tensor gu0 = Tensor(), Tensor gi0 = Tensor(),
+                                                 const StepAdam *sa = nullptr) {
   const int64_t U = P.U, I = P.I, d = gU.size(1);
   check_table("user grad", gU, U, d);
   check_table("item grad", gI, I, d);
-  if (!gu0.defined()) gu0 = at::empty({U, d}, f32(gU));
-  if (!gi0.defined()) gi0 = at::empty({I, d}, f32(gU));
+  TORCH_CHECK(!sa || (gs && K >= 2), "bbgr: the in-backward Adam needs the GS order and K >= 2");
+  if (!sa && !gu0.defined()) gu0 = at::empty({U, d}, f32(gU));
+  if (!sa && !gi0.defined()) gi0 = at::empty({I, d}, f32(gU));
   if (K == 0) {
     gu0.copy_(gU);
     gi0.copy_(gI);
@@ -635,6 +686,13 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
         oi.row_count = s.fcount.data_ptr<int64_t>();
         oi.src_bits = reinterpret_cast<const uint32_t *>(s.bits.data_ptr<int32_t>());
       }
+      if (sa && k == 1) {   // the item Adam rides on the last item product
+        oi.adam = &sa->item;
+        oi.adam_grad = sa->item_grad.data_ptr<float>();
+        oi.adam_grad_ld = ld(sa->item_grad);
+        oi.adam_grad_scale = gl;
+        oi.adam_map = im;   // bufI is in the graph's order, the weights in the caller's
+      }
       spmm(P.bi, first ? gU : bufU, first, oi);
       Opts ou;
       ou.add = gU;
@@ -646,6 +704,12 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
         ou.y = bufU;
         ou.y_scale = P.feed_bwd_ui;
         ou.add_scale = P.bi.in_scale;
+      } else if (sa) {   // the user Adam: no gradient table, ego rows in gU first
+        Tensor g = gU;
+        index_add_rows(g, sa->ego_u_rows, sa->ego_u_vals);
+        ou.y_scale = P.bu.out_scale;
+        ou.y_map = um;   // the Adam's rows: the caller's order
+        ou.adam = &sa->user;
       } else {
         ou.y = gu0;
         ou.y_scale = P.bu.out_scale;
@@ -653,6 +717,7 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       }
       spmm(P.bu, bufI, false, ou);
     }
+    if (sa) return {Tensor(), Tensor()};
     // GS: i0 only feeds the layer mean. The Tensor overload with a CPU 0-dim
     // float: the Scalar overload of mul.out computes into a temporary and
     // copies it (a second 256 MB pass at C4); the same float product either way
@@ -812,13 +877,27 @@ static std::tuple<Tensor, Tensor> propagate_backward_cuda(const Tensor &gU_, con
 // formed on the listed rows only (zeroed, then summed in ascending k) and the
 // masks come from the list: every read of gU in a K >= 1 chain is masked to
 // those rows, so the rest is never touched (K = 0 copies gU whole: zeroed).
+static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, const Tensor &iu_,
+                                                const Tensor &vu, const Tensor &gI_, int64_t K,
+                                                bool gs, const c10::optional<Tensor> &ii_,
+                                                const c10::optional<Tensor> &vi_,
+                                                StepAdam *sa = nullptr);
+
 static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
     const Tensor &iu_, const Tensor &vu, const Tensor &gI_, int64_t num_users, int64_t key,
     int64_t K, c10::string_view order, const c10::optional<Tensor> &ii_,
     const c10::optional<Tensor> &vi_) {
   auto P = pair_of(key);
-  const bool gs = is_gs(order);
   TORCH_CHECK(num_users == P->U, "propagate_backward_rows: num_users does not match the pair");
+  return rows_backward(P, iu_, vu, gI_, K, is_gs(order), ii_, vi_);
+}
+
+// the body of propagate_backward_rows; `sa`: the in-backward Adam (no gradient
+// tables returned)
+static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, const Tensor &iu_,
+                                                const Tensor &vu, const Tensor &gI_, int64_t K,
+                                                bool gs, const c10::optional<Tensor> &ii_,
+                                                const c10::optional<Tensor> &vi_, StepAdam *sa) {
   const int64_t U = P->U, I = P->I, d = vu.size(1);
   Tensor iu = iu_.to(at::kLong).contiguous();
   // dL/d(i_final) as rows too (vi[k] adds to item ii[k]; gI_ is then only a
@@ -845,6 +924,7 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
   // (Support.gu_internal); the same values at the same rows of the products
   const bool gu_int = P->io && K >= 1;
   Tensor ru = gu_int ? P->user_rank64.index_select(0, iu).contiguous() : iu;
+  if (sa) sa->ego_u_rows = ru;   // the ego rows land on the same gU rows as vu
   Tensor gU;
   if (K == 0) {
     gU = at::zeros({std::max<int64_t>(U, 1), d}, f32(vu)).narrow(0, 0, U);
@@ -902,7 +982,7 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
       }
     }
   } rel{*P, s, ru};
-  auto out = backward_chain(*P, gU, gI, K, gs, s);
+  auto out = backward_chain(*P, gU, gI, K, gs, s, Tensor(), Tensor(), sa);
   rel.armed = false;
   release_bits(*P, s, ru);
   return out;
@@ -1126,6 +1206,62 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
   a.ldgie = ld(gi);
   check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr (ego rows)");
   return {gu, gi, iu, ii};
+}
+
+// bbgr::bpr_adam_backward — the drop-in step's backward with the optimizer in
+// it (bbgr.optim.FusedAdam(fuse_backward=True); GS, K >= 2; eager only):
+// dL/d(finals) as the BPR kernel's per-triple rows scaled by dloss (as
+// bpr_loss_sparse_ego's backward), the ego-L2 rows in first-slot form
+// (ego_grad_rows), then propagate_backward_rows' chain with the user Adam on
+// its last user product and the item Adam on its last item product (StepAdam).
+// Updates u0, i0 and their moments in place; no gradient table is written.
+// Versus the separate step (gradients, then bbgr_adam) the ego rows are added
+// before the last products' epilogues instead of after them: the same terms,
+// rounded in another order (FusedTrainer's order).
+static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const Tensor &itf_,
+                                   const Tensor &u0, const Tensor &i0, const Tensor &users_,
+                                   const Tensor &pos_, const Tensor &neg_, double reg,
+                                   int64_t key, int64_t K, const Tensor &m_u, const Tensor &v_u,
+                                   const Tensor &m_i, const Tensor &v_i, double lr, double beta1,
+                                   double beta2, double eps, double wd, double bc1_u,
+                                   double bc2s_u, double bc1_i, double bc2s_i) {
+  auto P = pair_of(key);
+  TORCH_CHECK(K >= 2, "bpr_adam_backward: the in-backward Adam needs num_layers >= 2");
+  const int64_t d = u0.size(1), U = P->U, I = P->I;
+  check_table("user weights", u0, U, d);
+  check_table("item weights", i0, I, d);
+  for (const Tensor *t : {&u0, &i0, &m_u, &v_u, &m_i, &v_i})
+    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kFloat,
+                "bpr_adam_backward: weights and moments must be contiguous fp32");
+  TORCH_CHECK(m_u.sizes() == u0.sizes() && v_u.sizes() == u0.sizes() &&
+                  m_i.sizes() == i0.sizes() && v_i.sizes() == i0.sizes(),
+              "bpr_adam_backward: moment shapes");
+  Tensor users = idx64(users_), pos = idx64(pos_), neg = idx64(neg_);
+  Tensor uf = uf_.contiguous(), itf = itf_.contiguous();
+  const int64_t B = users.numel();
+  Tensor dl = dloss.to(at::kFloat).contiguous().reshape({});
+  Tensor contrib = at::empty({3 * B, d}, f32(uf));
+  bbgr_bpr_args a = bpr_args(users, pos, neg, uf, itf, u0, i0, reg, c10::nullopt, 0.0);
+  a.dloss = dl.data_ptr<float>();
+  a.contrib = contrib.data_ptr<float>();
+  a.ldcontrib = ld(contrib);
+  check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr");
+  auto eg = ego_grad_rows(dl, users, pos, neg, u0, i0, reg);
+  const Tensor &ru = std::get<0>(eg), &ri = std::get<1>(eg), &iu = std::get<2>(eg),
+               &ii = std::get<3>(eg);
+  const Tensor kp1 = at::scalar_tensor((float)(K + 1), at::TensorOptions().dtype(at::kFloat));
+  StepAdam sa;
+  sa.user = AdamTable{u0, m_u, v_u, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
+                      (float)bc1_u, (float)bc2s_u};
+  sa.item = AdamTable{i0, m_i, v_i, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
+                      (float)bc1_i, (float)bc2s_i};
+  sa.ego_u_vals = at::mul(ru, kp1);
+  // the item gradient / gl: the BPR rows, then the ego rows, per item in
+  // ascending source order
+  Tensor vi = contrib.narrow(0, B, 2 * B);
+  sa.item_grad = at::zeros({std::max<int64_t>(I, 1), d}, f32(uf)).narrow(0, 0, I);
+  index_add_rows(sa.item_grad, at::cat({ii, ii}), at::cat({vi, at::mul(ri, kp1)}));
+  rows_backward(P, iu, contrib.narrow(0, 0, B), i0, K, true, ii, vi, &sa);
 }
 
 // -- Meta kernels (shapes only; torch.compile traces through them) ---------------
@@ -1557,6 +1693,11 @@ TORCH_LIBRARY(bbgr, m) {
   m.def("bpr_loss_sparse_ego(Tensor uf, Tensor itf, Tensor ue, Tensor ie, Tensor users, "
         "Tensor pos, Tensor neg, float reg, Tensor? pop, float lambda_fair, bool sparse_uf) "
         "-> Tensor");
+  m.def("bpr_adam_backward(Tensor dloss, Tensor uf, Tensor itf, Tensor(a!) u0, Tensor(b!) i0, "
+        "Tensor users, Tensor pos, Tensor neg, float reg, int pair_key, int num_layers, "
+        "Tensor(c!) m_u, Tensor(d!) v_u, Tensor(e!) m_i, Tensor(f!) v_i, float lr, float beta1, "
+        "float beta2, float eps, float weight_decay, float bc1_u, float bc2s_u, float bc1_i, "
+        "float bc2s_i) -> ()");
   m.def("_register_pair(int key, Tensor?[] tensors, int[] meta) -> ()",
         &bbgr_torch::register_pair);
   m.def("_unregister_pair(int key) -> ()", &bbgr_torch::unregister_pair);
@@ -1575,6 +1716,7 @@ TORCH_LIBRARY_IMPL(bbgr, CUDA, m) {
   m.impl("bpr_loss", &bbgr_torch::bpr_loss_cuda);
   m.impl("bpr_loss_backward", &bbgr_torch::bpr_loss_backward_cuda);
   m.impl("bpr_loss_sparse_ego", &bbgr_torch::bpr_loss_sparse_ego_cuda);
+  m.impl("bpr_adam_backward", &bbgr_torch::bpr_adam_backward_cuda);
 }
 
 TORCH_LIBRARY_IMPL(bbgr, Meta, m) {

@@ -39,7 +39,7 @@ DEFAULT_CHUNK_EDGES = 2048
 # On a small graph the longest short row is the launch's critical path: at C2
 # (1M edges) the step ran 0.887 ms with 256, 0.710 with 128, 0.579 with 64,
 # 0.579 with 32, 0.812 with 16; at C4 (50M) 16.77 / 16.76 / 16.97 ms for
-# 256 / 128 / 64 (tools/probes/chunk_probe.py, profiles/r15_chunk_probe.jsonl).
+# 256 / 128 / 64 (tools/probes/chunk_probe.py, profiles/round1-2/r15_chunk_probe.jsonl).
 SMALL_CSR_EDGES = 8_000_000
 
 

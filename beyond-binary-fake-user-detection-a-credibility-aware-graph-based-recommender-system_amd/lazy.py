@@ -40,9 +40,10 @@ class _Pending:
     """One propagate() call: its weights, their versions, its grad mode, and
     the dense tables once computed."""
 
-    def __init__(self, full_fn, rows_fn, u0: torch.Tensor, i0: torch.Tensor):
+    def __init__(self, full_fn, rows_fn, u0: torch.Tensor, i0: torch.Tensor, step=None):
         self.full_fn, self.rows_fn = full_fn, rows_fn
         self.u0, self.i0 = u0, i0
+        self.step = step   # (pair_key, num_layers) of a GS chain: the in-backward Adam
         self.version = (u0._version, i0._version)
         self.grad = torch.is_grad_enabled()
         self.out = None
@@ -130,9 +131,10 @@ def _placeholder(like: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def deferred_pair(full_fn, rows_fn, u0: torch.Tensor, i0: torch.Tensor):
-    """(u_final, i_final) as DeferredFinal tensors of one call."""
-    p = _Pending(full_fn, rows_fn, u0, i0)
+def deferred_pair(full_fn, rows_fn, u0: torch.Tensor, i0: torch.Tensor, step=None):
+    """(u_final, i_final) as DeferredFinal tensors of one call. `step`:
+    (pair_key, num_layers) when the chain is GS (fused_bpr_step may run it)."""
+    p = _Pending(full_fn, rows_fn, u0, i0, step)
     rg = p.grad and (u0.requires_grad or i0.requires_grad)
     return (DeferredFinal(p, 0, _placeholder(u0.detach()), rg),
             DeferredFinal(p, 1, _placeholder(i0.detach()), rg))
@@ -158,3 +160,64 @@ def batch_finals(user_final, item_final, users, pos, neg):
 def resolve(x):
     """A DeferredFinal's dense table (computed once), any other value as is."""
     return _resolve(x)
+
+
+class _BprAdamStep(torch.autograd.Function):
+    """loss = bpr_loss over one deferred call's batch rows; its backward is the
+    whole chain's with the optimizer step in it (bbgr::bpr_adam_backward):
+    the weights are updated in place and get no gradient."""
+
+    @staticmethod
+    def forward(ctx, u0, i0, users, pos, neg, reg, pending, opt):
+        from . import ops
+        uf, itf = pending.rows_fn(users, torch.cat([pos, neg]))
+        loss = ops.bpr_loss(uf, itf, u0, i0, users, pos, neg, float(reg), None, 0.0)
+        ctx.save_for_backward(uf, itf, u0, i0, users, pos, neg)
+        ctx.reg, ctx.chain, ctx.opt = float(reg), pending.step, opt
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import ops
+        uf, itf, u0, i0, users, pos, neg = ctx.saved_tensors
+        key, K = ctx.chain
+
+        def run(states, group, corr):
+            su, si = states
+            b1, b2 = group["betas"]
+            ops.bpr_adam_backward(g.detach(), uf, itf, u0.detach(), i0.detach(), users, pos,
+                                  neg, ctx.reg, key, K, su["exp_avg"], su["exp_avg_sq"],
+                                  si["exp_avg"], si["exp_avg_sq"], float(group["lr"]),
+                                  float(b1), float(b2), float(group["eps"]),
+                                  float(group["weight_decay"]), corr[0][0], corr[0][1],
+                                  corr[1][0], corr[1][1])
+
+        ctx.opt.step_in_backward([u0, i0], run)
+        return (None,) * 8
+
+
+def fused_bpr_step(user_final, item_final, users, pos, neg, reg_weight: float):
+    """bpr_loss of one deferred propagate() call with bbgr.optim.FusedAdam(
+    fuse_backward=True) owning both weights (GS, num_layers >= 2, eager): the
+    loss, whose backward runs the optimizer step (optim.FusedAdam). None when
+    that does not apply (the caller takes the usual path)."""
+    if not (isinstance(user_final, DeferredFinal) and isinstance(item_final, DeferredFinal)):
+        return None
+    p = user_final._pending
+    if (item_final._pending is not p or user_final._side != 0 or item_final._side != 1
+            or p.out is not None or p.step is None or p.step[1] < 2 or not p.grad
+            or not torch.is_grad_enabled()):
+        return None
+    u0, i0 = p.u0, p.i0
+    if not (u0.requires_grad and i0.requires_grad and u0.is_leaf and i0.is_leaf
+            and u0.is_contiguous() and i0.is_contiguous()):
+        return None
+    from .optim import backward_optimizer
+    opt = backward_optimizer(u0, i0)
+    if opt is None:
+        return None
+    p._check()
+    dev = u0.device
+    users, pos, neg = (torch.as_tensor(t).to(device=dev, dtype=torch.int64).contiguous()
+                       for t in (users, pos, neg))
+    return _BprAdamStep.apply(u0, i0, users, pos, neg, float(reg_weight), p, opt)

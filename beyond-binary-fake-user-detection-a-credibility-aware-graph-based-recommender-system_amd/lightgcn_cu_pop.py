@@ -78,16 +78,23 @@ class LightGCN(torch.nn.Module):
         pair, K = self._operator_pair(), self.num_layers
         u0, i0 = self.user_emb.weight, self.item_emb.weight
         if self.lazy_finals and _lazy.supported(u0, i0):
+            from .ops import pair_key
             return _lazy.deferred_pair(
                 lambda: _propagate(pair, u0, i0, K, ORDER_GS),
                 lambda users, items: _propagate_rows(pair, u0, i0, K, ORDER_GS, users, items),
-                u0, i0)
+                u0, i0, step=(pair_key(pair), K))
         return _propagate(pair, u0, i0, K, ORDER_GS)
 
     def get_user_item_emb(self):
         return self.propagate()
 
     def bpr_loss(self, users, pos_items, neg_items, user_emb, item_emb, reg_weight: float):
+        # bbgr.optim.FusedAdam(fuse_backward=True) on both tables: the backward
+        # of this loss runs the optimizer step (lazy.fused_bpr_step)
+        fused = _lazy.fused_bpr_step(user_emb, item_emb, users, pos_items, neg_items,
+                                     reg_weight)
+        if fused is not None:
+            return fused
         user_emb, item_emb, users, pos_items, neg_items = _lazy.batch_finals(
             user_emb, item_emb, users, pos_items, neg_items)
         return _bpr.bpr_loss(users, pos_items, neg_items, user_emb, item_emb,

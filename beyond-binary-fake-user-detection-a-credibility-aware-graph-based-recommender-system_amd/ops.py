@@ -70,6 +70,7 @@ propagate_sym_backward = torch.ops.bbgr.propagate_sym_backward
 bpr_loss = torch.ops.bbgr.bpr_loss
 bpr_loss_backward = torch.ops.bbgr.bpr_loss_backward
 bpr_loss_sparse_ego = torch.ops.bbgr.bpr_loss_sparse_ego
+bpr_adam_backward = torch.ops.bbgr.bpr_adam_backward
 
 # autograd node name of bbgr::propagate (bpr.py reads the graph)
 PROPAGATE_NODE = "torch::autograd::CppNode<bbgr_torch::PropagateFn>"

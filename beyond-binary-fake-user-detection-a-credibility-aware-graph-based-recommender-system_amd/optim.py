@@ -129,12 +129,93 @@ def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,
          float(grad_scale), float(bc1), float(bc2s), stream_handle())
 
 
+# parameters owned by a FusedAdam in backward mode: id -> (weakref(param), weakref(opt))
+_IN_BACKWARD: dict = {}
+
+
+def backward_optimizer(*params):
+    """The FusedAdam(fuse_backward=True) that owns every one of `params` in one
+    param group, or None."""
+    found = None
+    for p in params:
+        e = _IN_BACKWARD.get(id(p))
+        if e is None or e[0]() is not p:
+            return None
+        o = e[1]()
+        if o is None or (found is not None and o is not found):
+            return None
+        found = o
+    if found is None or found._group_of(params) is None:
+        return None
+    return found
+
+
 class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam on the bbgr_adam kernel (module docstring).
+
+    fuse_backward=True (the drop-in LightGCN of Version-2 / Method A, GS
+    order, num_layers >= 2): the step of the model's two embedding tables runs
+    INSIDE loss.backward(), in the epilogues of the last backward SpMMs
+    (bbgr::bpr_adam_backward): the user step on the last user product, the item
+    step on the last item product, so neither gradient table is written nor
+    re-read. Those parameters then get no .grad, and the following step()
+    leaves them alone (they were stepped already); anything else in the
+    optimizer steps as usual. The reference's loop (zero_grad, backward,
+    step: Version-2/lighgcn_cu_pop.py:861-863) runs unchanged. Each backward
+    through bpr_loss is one optimizer step. The update equals the separate
+    step's up to rounding: the ego-L2 rows join the gradient before the last
+    products' epilogues, not after them (FusedTrainer's order)."""
+
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0):
+                 weight_decay: float = 0.0, fuse_backward: bool = False):
         if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError("invalid Adam hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.fuse_backward = bool(fuse_backward)
+        self._stepped: set = set()   # ids of parameters stepped in the last backward
+        if self.fuse_backward:
+            import weakref
+            me = weakref.ref(self)
+            for g in self.param_groups:
+                for p in g["params"]:
+                    _IN_BACKWARD[id(p)] = (weakref.ref(p), me)
+
+    def _group_of(self, params):
+        for g in self.param_groups:
+            ids = {id(p) for p in g["params"]}
+            if all(id(p) in ids for p in params):
+                return g
+        return None
+
+    def _init_state(self, p):
+        st = self.state[p]
+        if not st:
+            st["step"] = torch.tensor(0.0)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    @torch.no_grad()
+    def step_in_backward(self, params, run) -> None:
+        """One Adam step of `params` (one param group) carried out by `run(states,
+        group, corrections)` inside a backward pass: the step counts advance,
+        corrections = [(1 - beta1^t, sqrt(1 - beta2^t)) per parameter] (host
+        double, as adam_step), and step() then skips these parameters."""
+        g = self._group_of(params)
+        if g is None:
+            raise RuntimeError("FusedAdam.step_in_backward: parameters not in one group")
+        b1, b2 = g["betas"]
+        states, corr = [], []
+        for p in params:
+            st = self._init_state(p)
+            st["step"] += 1
+            t = int(st["step"].item())
+            states.append(st)
+            corr.append((1.0 - b1 ** t, math.sqrt(1.0 - b2 ** t)))
+        run(states, g, corr)
+        for p in params:
+            self._stepped.add(id(p))
+            torch.autograd.graph.increment_version(p)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -145,14 +226,13 @@ class FusedAdam(torch.optim.Optimizer):
         for group in self.param_groups:
             b1, b2 = group["betas"]
             for p in group["params"]:
+                if id(p) in self._stepped:   # stepped inside the backward already
+                    self._stepped.discard(id(p))
+                    continue
                 if p.grad is None:
                     continue
                 _lib.require_gpu(p)
-                st = self.state[p]
-                if not st:
-                    st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st = self._init_state(p)
                 st["step"] += 1
                 adam_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"],
                           int(st["step"].item()), group["lr"], b1, b2, group["eps"],

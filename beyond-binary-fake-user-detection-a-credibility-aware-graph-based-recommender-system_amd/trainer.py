@@ -39,7 +39,7 @@ VARIANTS = {
 
 # frontier="auto": masks pay only on graphs whose full-CSR products take well
 # over the mask build (~0.05 ms of small launches). At C2 (1M edges) the masked
-# step measured 1.092 ms against 1.058 dense (profiles/r08_c2_bench.json); at
+# step measured 1.092 ms against 1.058 dense (profiles/round1-2/r08_c2_bench.json); at
 # C4 (50M) 17.0 against 23.5. Below this many edges the step runs dense.
 FRONTIER_MIN_EDGES = 4_000_000
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 6
+#define BBGR_ABI_VERSION 7
 
 typedef enum {
   BBGR_OK = 0,
@@ -277,6 +277,10 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   BPR rows / (K+1) + ego rows) is final before the product runs, so the   */
 /*   separate pass over the item table (28 B / parameter) overlaps the        */
 /*   product's gathers. Same rounding as bbgr_adam with grad_scale.          */
+/* adam_map (nullable, int32 [n_rows]; ABI 7): the fused Adam's rows (param, */
+/*   exp_avg, exp_avg_sq and adam_grad) of CSR row r are row adam_map[r]      */
+/*   instead of y_map's: a product that writes y in the graph's order while  */
+/*   the weights live in the caller's (the drop-in's in-backward item Adam). */
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
@@ -339,6 +343,7 @@ typedef struct {
   const float *adam_grad;
   int64_t adam_grad_ld;
   float adam_grad_scale;
+  const int32_t *adam_map;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,

@@ -130,3 +130,65 @@ def test_method_a_module_defers_too():
         assert la == lb
         for x, y in zip(ga, gb):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("module", [V2, MA])
+def test_fused_backward_adam_matches_the_separate_step(module):
+    """bbgr.optim.FusedAdam(fuse_backward=True): the reference's loop body
+    (Version-2:858-863) unchanged, the optimizer step carried out inside
+    loss.backward() by bbgr::bpr_adam_backward (Adam in the last backward
+    products' epilogues). Against FusedAdam's separate step on the same
+    batches: the same losses at step 1 (same forward), the moments after step 1
+    within 1e-6 (the gradient, rounded in another order), the weights after
+    three steps normwise, no .grad on the stepped tables, one step per
+    backward, and a deferred table read after the step raises."""
+    from bbgr.optim import FusedAdam
+    batches = [_batch(s) for s in range(3)]
+    batches[1][0][5] = batches[1][0][6]   # a repeated user
+    a, b = _model(3, module), _model(3, module)
+    w0 = [p.detach().clone() for p in b.parameters()]
+    oa = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
+    ob = FusedAdam(b.parameters(), lr=1e-3)
+    for k, (users, pos, neg) in enumerate(batches):
+        ls = []
+        for m, o in ((a, oa), (b, ob)):
+            uf, itf = m.get_user_item_emb()
+            loss = m.bpr_loss(users, pos, neg, uf, itf, 1e-4)
+            o.zero_grad()
+            loss.backward()
+            o.step()
+            ls.append(float(loss))
+        if k == 0:
+            assert ls[0] == ls[1]
+            for pa, pb in zip(a.parameters(), b.parameters()):
+                for key in ("exp_avg", "exp_avg_sq"):
+                    x, y = oa.state[pa][key], ob.state[pb][key]
+                    assert float((x - y).norm() / y.norm()) < 1e-6, key
+        else:
+            assert abs(ls[0] - ls[1]) <= 1e-6 * abs(ls[1])
+    for pa, pb, p0 in zip(a.parameters(), b.parameters(), w0):
+        assert pa.grad is None and int(oa.state[pa]["step"]) == 3
+        da, db = pa.detach() - p0, pb.detach() - p0
+        assert float((da - db).norm() / db.norm()) < 1e-3
+    uf, itf = a.get_user_item_emb()
+    a.bpr_loss(*batches[0], uf, itf, 1e-4).backward()   # a fourth step, in the backward
+    with pytest.raises(RuntimeError, match="weights changed"):
+        uf[0]
+
+
+def test_fused_backward_adam_falls_back_where_it_does_not_apply():
+    """K = 1 (the last products are the first), torch.optim.Adam, or a weight
+    outside the optimizer: the usual path, bit for bit the separate step."""
+    from bbgr.optim import FusedAdam
+    batches = [_batch(s) for s in range(2)]
+    a, b = _model(1), _model(1)
+    ra = _steps(a, batches, lambda ps, lr: FusedAdam(ps, lr=lr, fuse_backward=True))
+    rb = _steps(b, batches, lambda ps, lr: FusedAdam(ps, lr=lr))
+    for (la, ga), (lb, gb) in zip(ra, rb):
+        assert la == lb and all(torch.equal(x, y) for x, y in zip(ga, gb))
+    c = _model(3)
+    oc = FusedAdam([c.user_emb.weight], lr=1e-3, fuse_backward=True)   # item table not in it
+    uf, itf = c.get_user_item_emb()
+    c.bpr_loss(*batches[0], uf, itf, 1e-4).backward()
+    assert c.user_emb.weight.grad is not None and c.item_emb.weight.grad is not None
+    oc.step()

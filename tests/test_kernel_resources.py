@@ -3,8 +3,8 @@
 A spilling kernel writes and re-reads its spill slots through L2 on every
 batch: at C4 the two-row SpMM kernels' 12-24 B per lane of scratch at the
 8-wave target issued 5-12.5M extra 64-B write requests per launch (TCC_WRITE
-25.0M / 32.5M against the 20.0M of the output rows, profiles/r5c_*) and cost
-0.47 ms per step (profiles/r5e_ab_spills.txt). The metadata of the built
+25.0M / 32.5M against the 20.0M of the output rows, profiles/round5/r5c_*) and cost
+0.47 ms per step (profiles/round5/r5e_ab_spills.txt). The metadata of the built
 gfx950 code objects (tools/kernel_resources.py) shows it without a GPU.
 """
 import os

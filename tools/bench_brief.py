@@ -23,7 +23,7 @@ def main(path: str):
     c = j.get("cpu_baseline")
     if c:
         print(f"  cpu {c['value'] / 1e6:.2f} M/s on {c['cores']} threads: {c['sample'][:160]}")
-    for k in ("dropin_module_step", "dropin_fused_adam_step"):
+    for k in ("dropin_module_step", "dropin_fused_adam_step", "dropin_backward_adam_step"):
         d = j.get(k)
         if d:
             print(f"  {k}: " + json.dumps({x: d.get(x) for x in

@@ -39,6 +39,17 @@ def timed(fn, steps: int) -> float:
 def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
         adam: str = "foreach", device=None, pre_ordered: bool = False,
         items_ordered: bool = False, dense_finals: bool = False) -> dict:
+    """One optimizer (module docstring)."""
+    return run_many(cfg_name, edges, cred_np, steps, warmup, (adam,), device, pre_ordered,
+                    items_ordered, dense_finals)[adam]
+
+
+def run_many(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
+             adams=("foreach",), device=None, pre_ordered: bool = False,
+             items_ordered: bool = False, dense_finals: bool = False) -> dict:
+    """{adam: result} for each optimizer in `adams`, on ONE model built once
+    (each optimizer starts fresh on the weights the previous one left: the
+    timings do not depend on the values)."""
     c = CONFIGS[cfg_name]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
     e = config_edges(cfg_name) if edges is None else edges
@@ -69,18 +80,13 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
         model.propagate()   # first call: operator pair registration + first-layer values
     torch.cuda.synchronize()
     first_call_s = time.perf_counter() - t1
-    if adam == "bbgr":   # bbgr.optim.FusedAdam (bbgr_adam per parameter)
-        from bbgr.optim import FusedAdam
-        opt = FusedAdam(model.parameters(), lr=1e-3)
-    else:
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3,
-                               **({"fused": True} if adam == "fused" else {"foreach": True}))
     g = torch.Generator(device=dev).manual_seed(1)
     n_b = warmup + steps
     users = torch.randint(0, U, (n_b, B), device=dev, generator=g)
     pos = torch.randint(0, I, (n_b, B), device=dev, generator=g)
     neg = torch.randint(0, I, (n_b, B), device=dev, generator=g)
     it = iter(range(10**9))
+    opt = None
 
     def fwd_bwd():
         k = next(it) % n_b
@@ -106,21 +112,34 @@ def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 
             resolve(uf)
             resolve(itf)
 
-    for _ in range(warmup):
-        step()
-    out = {"config": cfg_name, "adam": adam, "pre_ordered": pre_ordered,
-           "items_ordered": items_ordered,
-           "setup_s": setup_s, "build_s": build_s, "model_init_s": setup_s - build_s,
-           "first_call_s": first_call_s, "steps": steps,
-           "lazy_finals": bool(model.lazy_finals),
-           "step_ms": timed(step, steps), "forward_ms": timed(fwd, steps),
-           "full_tables_ms": timed(full_tables, steps),
-           "forward_backward_ms": timed(fwd_bwd, steps)}
-    fwd_bwd()
-    out["adam_ms"] = timed(opt.step, steps)
-    del model, opt, M_ui, M_iu, users, pos, neg
+    res = {}
+    for adam in adams:
+        if adam in ("bbgr", "bbgr_bwd"):   # bbgr.optim.FusedAdam (bbgr_adam per parameter,
+            from bbgr.optim import FusedAdam   # or inside the backward's last products)
+            opt = FusedAdam(model.parameters(), lr=1e-3, fuse_backward=adam == "bbgr_bwd")
+        else:
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3,
+                                   **({"fused": True} if adam == "fused" else {"foreach": True}))
+        for _ in range(warmup):
+            step()
+        out = {"config": cfg_name, "adam": adam, "pre_ordered": pre_ordered,
+               "items_ordered": items_ordered,
+               "setup_s": setup_s, "build_s": build_s, "model_init_s": setup_s - build_s,
+               "first_call_s": first_call_s, "steps": steps,
+               "lazy_finals": bool(model.lazy_finals),
+               "step_ms": timed(step, steps), "forward_ms": timed(fwd, steps),
+               "full_tables_ms": timed(full_tables, steps),
+               "forward_backward_ms": timed(fwd_bwd, steps)}
+        fwd_bwd()
+        out["adam_ms"] = timed(opt.step, steps)
+        out["optimizer"] = ("bbgr.optim.FusedAdam" if adam == "bbgr" else
+                            "bbgr.optim.FusedAdam(fuse_backward=True)" if adam == "bbgr_bwd" else
+                            f"torch.optim.Adam({adam})")
+        res[adam] = out
+        opt = None
+    del model, M_ui, M_iu, users, pos, neg
     torch.cuda.empty_cache()
-    return out
+    return res
 
 
 def main():
@@ -128,7 +147,7 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--adam", default="foreach", choices=["foreach", "fused", "bbgr"])
+    ap.add_argument("--adam", default="foreach", choices=["foreach", "fused", "bbgr", "bbgr_bwd"])
     ap.add_argument("--pre-ordered", action="store_true",
                     help="hand the model an edge list already in descending-degree order")
     ap.add_argument("--items-ordered", action="store_true",

@@ -18,7 +18,12 @@
 #              a quick bench and a WRITE_SIZE + FETCH_SIZE pass over the SpMM
 #              kernels for each policy
 #   shard      tools/shard_probe.py with SHARD_ARGS (one user-row rank alone)
+#   shardprof  the same under a rocprofv3 kernel trace, one step's timeline
 #   rehearse   bench.py --gpus $N over gloo, N ranks on this one GPU (N=2 default)
+#   counters   the PMC counters this box offers (rocprofv3 -L)
+#   pmc        PMC passes over the SpMM kernels (PMC_SETS: one pass per word)
+#   dropin     the drop-in module step (FusedAdam / torch foreach Adam) + trace
+#   configs    one bench line per config (CONFIGS="C1 C2 C3 C5")
 set -o pipefail
 T=$1; shift
 O=gpurun_out/$T
@@ -100,6 +105,14 @@ for step in "$@"; do
       timeout -k 10 900 python -u tools/shard_probe.py ${SHARD_ARGS:-} > "$O/shard.jsonl" 2> "$O/shard.log"
       rc=$?; hard $rc shard "$O/shard.log"; echo "SHARD rc=$rc"; tail -3 "$O/shard.jsonl"
       [ $rc -eq 0 ] || { tail -20 "$O/shard.log"; exit 1; } ;;
+    shardprof)  # the same probe under a rocprofv3 kernel trace, one step's timeline
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$O/shardprof" \
+        -o run -- python3 tools/shard_probe.py ${SHARD_ARGS:-} > "$O/shardprof.jsonl" 2> "$O/shardprof.log"
+      rc=$?; hard $rc shardprof "$O/shardprof.log"; echo "SHARDPROF rc=$rc"
+      [ $rc -eq 0 ] || { tail -20 "$O/shardprof.log"; exit 1; }
+      tr=$(find "$O/shardprof" -name "*kernel_trace.csv" | head -1)
+      python tools/step_timeline.py "$tr" --marker "${MARKER:-sample_kernel}" > "$O/shard_timeline.txt"
+      head -3 "$O/shard_timeline.txt" ;;
     rehearse)
       n=${N:-2}
       BBGR_DIST_BACKEND=gloo timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 \
@@ -108,6 +121,32 @@ for step in "$@"; do
       rc=$?; hard $rc rehearse "$O/rehearsal_gloo$n.log"; echo "REHEARSE N=$n rc=$rc"
       [ $rc -eq 0 ] || { tail -20 "$O/rehearsal_gloo$n.log"; exit 1; }
       python tools/bench_brief.py "$O/rehearsal_gloo$n.json" ;;
+    dropin)    # the drop-in module step (FusedAdam, torch foreach Adam) + a kernel trace
+      for a in bbgr foreach; do
+        timeout -k 10 400 python tools/dropin_probe.py --adam $a > "$O/dropin_$a.json" \
+          2> "$O/dropin_$a.log"
+        rc=$?; hard $rc "dropin $a" "$O/dropin_$a.log"
+        [ $rc -eq 0 ] || { tail -20 "$O/dropin_$a.log"; exit 1; }
+        cat "$O/dropin_$a.json"
+      done
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$O/dropin_trace" \
+        -o run -- python3 tools/dropin_probe.py --adam bbgr --steps 5 --warmup 2 \
+        > "$O/dropin_trace.json" 2> "$O/dropin_trace.log"
+      rc=$?; hard $rc dropin_trace "$O/dropin_trace.log"; [ $rc -eq 0 ] || exit 1
+      tr=$(find "$O/dropin_trace" -name "*kernel_trace.csv" | head -1)
+      python tools/step_timeline.py "$tr" --marker bpr_reduce_kernel > "$O/dropin_timeline.txt"
+      head -3 "$O/dropin_timeline.txt" ;;
+    configs)   # one bench line per config (CONFIGS; C1 on lightgcn.py's path, C3 on lightgcn_cu.py's)
+      for c in ${CONFIGS:-C1 C2 C3 C5}; do
+        extra=""
+        case $c in C1) extra="--variant plain";; C3) extra="--variant cu_fair --no-torch-reference";;
+                   C5) extra="--no-torch-reference --steps 5 --warmup 1";; esac
+        timeout -k 10 900 python -u bench.py --config $c $extra > "$O/${c,,}_bench.json" \
+          2> "$O/${c,,}_bench.log"
+        rc=$?; hard $rc "bench $c" "$O/${c,,}_bench.log"
+        [ $rc -eq 0 ] || { tail -20 "$O/${c,,}_bench.log"; exit 1; }
+        echo "$c: $(python tools/bench_brief.py "$O/${c,,}_bench.json" | head -1)"
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "[$step] $(( $(date +%s) - s0 )) s"

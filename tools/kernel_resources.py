@@ -8,7 +8,7 @@ llvm-readobj): .vgpr_count, .sgpr_count, .private_segment_fixed_size (bytes
 of scratch per lane: register spills). A spilling SpMM kernel writes and
 re-reads its spill slots through L2 on every batch; at C4 the two-row kernels'
 spills (12-24 B per lane at the 8-wave target) issued 5-12.5M extra 64-B
-write requests per launch (profiles/r5c_*), so tests/test_kernel_resources.py
+write requests per launch (profiles/round5/r5c_*), so tests/test_kernel_resources.py
 keeps the product kernels spill-free.
 """
 from __future__ import annotations

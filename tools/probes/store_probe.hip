@@ -1,6 +1,6 @@
 // Store-pattern probe (round 5): why the two-rows-per-group SpMM kernels
 // issue more L2 write requests than the one-row kernels for the same dense
-// output table (profiles/r5c_*: TCC_WRITE 32.5M vs 20.0M per 1.28 GB).
+// output table (profiles/round5/r5c_*: TCC_WRITE 32.5M vs 20.0M per 1.28 GB).
 // Writes a 5M x 64 fp32 table with the store shapes of spmm.hip's epilogues:
 //   mode 0  one row per 16-lane group, 16 rows per 256-thread block
 //   mode 1  two rows per group (rows j, j+16), 32 rows per block, stored A then B

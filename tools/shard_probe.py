@@ -1,10 +1,12 @@
-"""Probe: one rank's share of the user-row-sharded C4 step, alone on one GPU.
+"""Probe: one rank's share of the user-row-sharded step, alone on one GPU.
 
 Rank 0 of an N-way strong split of the config's graph (edge-balanced user
 range, global batch / N users per step) runs as a world-size-1 RCCL
 ShardedTrainer: its collectives are local copies, so the time is the rank's
 compute plus the exchange machinery's launch / range overheads without the
-wire time (DESIGN §6 model: compute(N)). Swept over exchange_parts.
+wire time (DESIGN §6 model: compute(N)). Swept over exchange_parts. C5 (500M
+edges) is drawn per user shard (synthetic.shard_edges_strong, bench.py's N > 1
+form), so rank 0's 62.5M-edge share never needs the whole graph.
 
     python tools/shard_probe.py [--config C4] [--parts-of 8] [--exchange-parts 1,2,4,8]
                                 [--column-chains 1,2]
@@ -52,13 +54,20 @@ def main():
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     c = CONFIGS[a.config]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
-    e = config_edges(a.config)
-    deg_u = np.bincount(e[0].astype(np.int64), minlength=U)
-    bounds = partition_users(deg_u, a.parts_of)
-    lo, hi = int(bounds[0]), int(bounds[1])
-    local = shard_edges(e, lo, hi)
-    cred = synthetic_credibility(U, CONFIG_SEED[a.config])[lo:hi]
-    del e
+    if c["num_edges"] > 100_000_000:
+        # C5: drawn per user shard as bench.py does at N > 1 (shard_edges_strong):
+        # rank 0's users and edges only, never the whole 500M-edge graph
+        from bbgr.synthetic import shard_edges_strong
+        local, lo, hi = shard_edges_strong(a.config, 0, a.parts_of)
+        cred = synthetic_credibility(hi - lo, CONFIG_SEED[a.config])
+    else:
+        e = config_edges(a.config)
+        deg_u = np.bincount(e[0].astype(np.int64), minlength=U)
+        bounds = partition_users(deg_u, a.parts_of)
+        lo, hi = int(bounds[0]), int(bounds[1])
+        local = shard_edges(e, lo, hi)
+        cred = synthetic_credibility(U, CONFIG_SEED[a.config])[lo:hi]
+        del e
     runs = [(int(x), int(ch), int(fp)) for ch in a.column_chains.split(",")
             for x in a.exchange_parts.split(",") for fp in a.frontier_parts.split(",")]
     for xp, chains, fparts in runs:

@@ -1,10 +1,10 @@
-"""Summarise a tools/profile_box.sh run into profiles/<tag>_*.
+"""Summarise a tools/profile_box.sh run into profiles/<round>/<tag>_*.
 
     python tools/summarize_profile.py r01
 
 Inputs : gpurun_out/prof_<tag>/{trace,fetch,write}/run_*.csv (rocprofv3)
-Outputs: profiles/<tag>_kernel_stats.csv   (rocprofv3 --stats summary, verbatim)
-         profiles/<tag>_summary.json/.md   (per-kernel avg time, PMC bytes)
+Outputs: profiles/<round>/<tag>_kernel_stats.csv   (rocprofv3 --stats summary, verbatim)
+         profiles/<round>/<tag>_summary.json/.md   (per-kernel avg time, PMC bytes)
          profiles/spmm_traffic.json        (read by bench.py: roofline.traffic)
          profiles/step_traffic.json        (read by bench.py: roofline.step_*; the
                                             PMC bytes of one whole training step)
@@ -29,9 +29,22 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def round_dir(tag: str) -> str:
+    """profiles/ keeps each round's records in its own directory (r5x: round5)."""
+    import re
+    if re.match(r"r5[a-z]", tag):
+        return "round5"
+    if re.match(r"r4[a-z]", tag):
+        return "round4"
+    if re.match(r"r3([a-z]|$)", tag):
+        return "round3"
+    return "round1-2"
+
+
 def main(tag: str):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    dst = os.path.join(ROOT, "profiles")
+    top = os.path.join(ROOT, "profiles")
+    dst = os.path.join(top, round_dir(tag))
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(dst, f"{tag}_kernel_stats.csv"))
@@ -93,8 +106,8 @@ def main(tag: str):
                    "avg_us": avg_us, "dispatches": n,
                    "per_grid": {f'{e["kernel"]}@{e["grid"]}': e["hbm_bytes_corrected"]
                                 for e in dom},
-                   "source": f"profiles/{tag}_summary.json"},
-                  open(os.path.join(dst, "spmm_traffic.json"), "w"), indent=1)
+                   "source": f"profiles/{round_dir(tag)}/{tag}_summary.json"},
+                  open(os.path.join(top, "spmm_traffic.json"), "w"), indent=1)
     # the whole step: every PMC-profiled kernel dispatched at least once per
     # profiled step (one-time setup kernels dispatch fewer times), its bytes x
     # dispatches / steps. BBGR_PROFILE_STEPS = the bench's warmup + timed +
@@ -114,8 +127,8 @@ def main(tag: str):
                    "note": "2*FETCH_SIZE+WRITE_SIZE (gfx950 read correction) summed over the "
                            "PMC-profiled kernels of one step; FETCH_SIZE counts Infinity-Cache "
                            "hits, so this bounds the step's HBM bytes from above",
-                   "source": f"profiles/{tag}_summary.json"},
-                  open(os.path.join(dst, "step_traffic.json"), "w"), indent=1)
+                   "source": f"profiles/{round_dir(tag)}/{tag}_summary.json"},
+                  open(os.path.join(top, "step_traffic.json"), "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
         fh.write(f"# rocprofv3 summary {tag}\n\n| kernel | calls | avg us | % |\n|---|---|---|---|\n")
         for k, v in sorted(summary["stats"].items(), key=lambda kv: -kv[1]["pct"])[:15]:
