@@ -38,7 +38,8 @@ import time
 # More hardware queues than HIP's default 4, so the compute stream, RCCL's stream
 # and the sharded exchange's side streams do not share (and serialise on) one
 # AQL queue. Must be set before the HIP runtime initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+HW_QUEUES_GIVEN = os.environ.get("GPU_MAX_HW_QUEUES")
+if int(HW_QUEUES_GIVEN or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np
@@ -915,6 +916,11 @@ def main():
         "partition": ("columns" if columns else "users") if dist_mode else
                      (f"one column shard of {emulate}" if emulate else "single GPU"),
         "graph_replay": use_graph,
+        "hw_queues": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"),
+                      "given": HW_QUEUES_GIVEN,
+                      "note": "bench.py raises HIP's hardware queues per process to 8 (from "
+                              "the given value, default 4) before the runtime starts, so the "
+                              "compute, RCCL and side streams do not share one queue"},
         "value_note": "value = SpMM edges actually gathered (source row read and "
                       "multiply-added) per second, whole job: every launch's edges counted "
                       f"on the device over {count_steps} steps after the timed region "

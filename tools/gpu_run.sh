@@ -9,7 +9,7 @@
 #
 # steps:
 #   box        GPU / driver / partition / clock facts of this box (box.txt)
-#   tests      the whole `pytest -m gpu` suite (TESTS=<pytest args> narrows it)
+#   tests      the whole `pytest -m gpu` suite (TESTS="<files / -k ...>" narrows it)
 #   smoke      __graft_entry__.smoke()
 #   bench      the default bench line (BENCH_ARGS appended), bench.json
 #   quick      bench --steps 10 without the CPU / stock-torch / drop-in legs
@@ -46,8 +46,8 @@ for step in "$@"; do
       } > "$O/box.txt" 2>&1
       grep -E "Memory Partition|Compute Partition|sclk|mclk|fclk" "$O/box.txt" | head -12 ;;
     tests)
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 500 \
-        --timeout-method thread ${TESTS:-} > "$O/gpu_tests.log" 2>&1
+      timeout -k 10 1100 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --durations=15 --timeout 500 \
+        --timeout-method thread > "$O/gpu_tests.log" 2>&1
       rc=$?; hard $rc tests "$O/gpu_tests.log"
       echo "TESTS rc=$rc"; grep -E "passed|failed" "$O/gpu_tests.log" | tail -1
       grep FAILED "$O/gpu_tests.log" | head
@@ -122,7 +122,7 @@ for step in "$@"; do
       [ $rc -eq 0 ] || { tail -20 "$O/rehearsal_gloo$n.log"; exit 1; }
       python tools/bench_brief.py "$O/rehearsal_gloo$n.json" ;;
     dropin)    # the drop-in module step (FusedAdam, torch foreach Adam) + a kernel trace
-      for a in bbgr foreach; do
+      for a in ${DROPIN_ADAMS:-bbgr bbgr_bwd foreach}; do
         timeout -k 10 400 python tools/dropin_probe.py --adam $a > "$O/dropin_$a.json" \
           2> "$O/dropin_$a.log"
         rc=$?; hard $rc "dropin $a" "$O/dropin_$a.log"
@@ -130,7 +130,7 @@ for step in "$@"; do
         cat "$O/dropin_$a.json"
       done
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$O/dropin_trace" \
-        -o run -- python3 tools/dropin_probe.py --adam bbgr --steps 5 --warmup 2 \
+        -o run -- python3 tools/dropin_probe.py --adam ${DROPIN_TRACE:-bbgr_bwd} --steps 5 --warmup 2 \
         > "$O/dropin_trace.json" 2> "$O/dropin_trace.log"
       rc=$?; hard $rc dropin_trace "$O/dropin_trace.log"; [ $rc -eq 0 ] || exit 1
       tr=$(find "$O/dropin_trace" -name "*kernel_trace.csv" | head -1)
