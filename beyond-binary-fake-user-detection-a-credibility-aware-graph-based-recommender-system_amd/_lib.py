@@ -203,6 +203,9 @@ _SIGNATURES = {
     "bbgr_rows_gather": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_rows_copy": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, _P], c_int32),
     "bbgr_first_slot": ([c_int64, _P, c_int64, _P, _P, _P], c_int32),
+    "bbgr_ego_slots": ([c_int64, _P, _P, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P],
+                       c_int32),
+    "bbgr_graph_rows": ([c_int64, _P, c_int64, _P, _P, _P], c_int32),
     "bbgr_rows_add_unique": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P],
                              c_int32),
     # blueprint names, thin forms of the entry points above
@@ -238,7 +241,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 7:
+        if handle.bbgr_abi_version() != 8:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

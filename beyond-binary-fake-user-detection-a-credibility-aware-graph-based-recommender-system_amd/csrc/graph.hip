@@ -843,11 +843,12 @@ struct DegreeSortWs {
 static DegreeSortWs degree_sort_ws(long n_ids, int n, int end_bit) {
   DegreeSortWs w = {};
   size_t t_sort = 0, t_rle = 0;
-  hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, (const unsigned *)nullptr,
-                                    (unsigned *)nullptr, (int)n_ids, 0, end_bit);
-  hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, (const unsigned *)nullptr,
-                                        (unsigned *)nullptr, (int *)nullptr, (int *)nullptr,
-                                        (int)n_ids);
+  // size queries (no launch; the sizes are what they return)
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, (const unsigned *)nullptr,
+                                          (unsigned *)nullptr, (int)n_ids, 0, end_bit);
+  (void)hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, (const unsigned *)nullptr,
+                                              (unsigned *)nullptr, (int *)nullptr, (int *)nullptr,
+                                              (int)n_ids);
   w.keys = align_up(4 * (size_t)n_ids);
   w.uniq = align_up(4 * (size_t)n);
   w.cnt = align_up(4 * (size_t)n);

@@ -120,6 +120,10 @@ struct Pair {
   };
   mutable std::mutex fb_mu;
   mutable std::map<int64_t, FrontierBufs> fb;
+  // 0..U-1 / 0..I-1 (int32): the identity acc_in_map of the last layer of an
+  // input-order chain, made once instead of two fills per call
+  mutable std::once_flag iota_once;
+  mutable Tensor iota_u, iota_i;
 };
 
 static std::mutex g_mu;
@@ -281,6 +285,18 @@ static Tensor iota32(int64_t n, const Tensor &like) {
   return at::arange(n, at::TensorOptions().dtype(at::kInt).device(like.device()));
 }
 
+// the pair's cached identity maps; a graph capture makes its own (the fill
+// then replays with it)
+static std::pair<Tensor, Tensor> pair_iotas(const Pair &P, const Tensor &like) {
+  if (capturing()) return {iota32(P.U, like), iota32(P.I, like)};
+  std::call_once(P.iota_once, [&] {
+    P.iota_u = iota32(P.U, like);
+    P.iota_i = iota32(P.I, like);
+    check(bbgr_sync(cur_stream()), "bbgr_sync");   // once: filled before any stream reads it
+  });
+  return {P.iota_u, P.iota_i};
+}
+
 static AccPlan acc_plan(int64_t k, int64_t K, const Tensor &x0, const Tensor &caller,
                         Tensor &internal, const int32_t *map, const Tensor &iota) {
   AccPlan a;
@@ -324,8 +340,7 @@ static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0,
   if (P.io && K >= 2) {
     int_u = at::empty({U, d}, f32(u0));
     int_i = at::empty({I, d}, f32(u0));
-    iota_u = iota32(U, u0);
-    iota_i = iota32(I, u0);
+    std::tie(iota_u, iota_i) = pair_iotas(P, u0);
   }
   if (gs) {   // Version-2:482-487: i_k = M_iu u_{k-1}; u_k = M_ui i_k
     Tensor bufU = at::empty({U, d}, f32(u0)), bufI = at::empty({I, d}, f32(u0));
@@ -376,19 +391,35 @@ static std::tuple<Tensor, Tensor> forward_chain(const Pair &P, const Tensor &u0,
   return {acc_u, acc_i};
 }
 
-// A zeroed byte mask of n rows in whole 4-byte words (bbgr_mark_list sets its
-// bytes with word atomics).
-static Tensor byte_mask(int64_t n, const Tensor &like) {
-  return at::zeros({(std::max<int64_t>(n, 1) + 3) / 4 * 4}, u8(like)).narrow(0, 0, n);
-}
+// Several zeroed byte regions from ONE fill (a launch each costs ~5 us at the
+// drop-in step's batch sizes): region k holds sizes[k] bytes at a 256-byte
+// aligned offset, so a region also views as a wider type, and a byte mask's
+// last word lies inside its region (bbgr_mark_list sets bytes with word
+// atomics).
+struct ZeroArena {
+  Tensor buf;
+  std::vector<int64_t> off, len;
+  ZeroArena(const Tensor &like, std::initializer_list<int64_t> sizes) {
+    int64_t o = 0;
+    for (int64_t n : sizes) {
+      off.push_back(o);
+      len.push_back(n);
+      o += (std::max<int64_t>(n, 1) + 255) / 256 * 256;
+    }
+    buf = at::zeros({o}, u8(like));
+  }
+  Tensor bytes(size_t k) const { return buf.narrow(0, off[k], len[k]); }
+};
 
 // ids in [0, n) -> rank[ids] (graph order), anything else -> -1 (skipped by
 // the marking kernels)
 static Tensor to_graph_rows(const Tensor &ids, int64_t n, const Tensor &rank64) {
-  if (n == 0) return at::full_like(ids, -1);
-  Tensor ok = (ids >= 0).logical_and(ids < n);
-  if (!rank64.defined()) return at::where(ok, ids, at::full_like(ids, -1));
-  return at::where(ok, rank64.index_select(0, ids.clamp(0, n - 1)), at::full_like(ids, -1));
+  Tensor out = at::empty_like(ids);
+  check(bbgr_graph_rows(ids.numel(), ids.data_ptr<int64_t>(), n,
+                        rank64.defined() ? rank64.data_ptr<int64_t>() : nullptr,
+                        out.data_ptr<int64_t>(), cur_stream()),
+        "bbgr_graph_rows");
+  return out;
 }
 
 // The GS finals at the listed rows only (bbgr::propagate_rows): u_final at
@@ -417,10 +448,14 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
   // graph's (mu / mi); non-io pairs: one order
   Tensor ui = to_graph_rows(users, U, P.io ? P.user_rank64 : Tensor());
   Tensor ii = to_graph_rows(items, I, P.io ? P.item_rank64 : Tensor());
-  Tensor mu = byte_mask(U, u0), mi = byte_mask(I, u0), fr = byte_mask(I, u0);
+  // every zeroed mask and counter of the call in one fill: mu, mi, fr (+ the
+  // caller-order mu_in, mi_in of an input-order pair), ucount, fcount
+  ZeroArena za(u0, {U, I, I, P.io ? U : 0, P.io ? I : 0, 16});
+  Tensor mu = za.bytes(0), mi = za.bytes(1), fr = za.bytes(2);
   Tensor ulist = at::empty({std::max<int64_t>(users.numel(), 1)}, users.options());
   Tensor flist = at::empty({std::max<int64_t>(I, 1)}, users.options());
-  Tensor ucount = at::zeros({1}, users.options()), fcount = at::zeros({1}, users.options());
+  Tensor counts = za.bytes(5).view(at::kLong);
+  Tensor ucount = counts.narrow(0, 0, 1), fcount = counts.narrow(0, 1, 1);
   // the distinct listed users (a list of distinct rows for the last user product)
   check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), nullptr, nullptr,
                        mu.data_ptr<uint8_t>(), U, ulist.data_ptr<int64_t>(),
@@ -440,8 +475,8 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
         "bbgr_mark_list");
   Tensor mu_in = mu, mi_in = mi;
   if (P.io) {
-    mu_in = byte_mask(U, u0);
-    mi_in = byte_mask(I, u0);
+    mu_in = za.bytes(3);
+    mi_in = za.bytes(4);
     check(bbgr_mark_rows(users.numel(), users.data_ptr<int64_t>(), 1, mu_in.data_ptr<uint8_t>(),
                          U, st),
           "bbgr_mark_rows");
@@ -456,8 +491,7 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
   if (P.io && K >= 2) {
     int_u = at::empty({U, d}, f32(u0));
     int_i = at::empty({I, d}, f32(u0));
-    iota_u = iota32(U, u0);
-    iota_i = iota32(I, u0);
+    std::tie(iota_u, iota_i) = pair_iotas(P, u0);
   }
   Tensor bufU = at::empty({U, d}, f32(u0)), bufI = at::empty({I, d}, f32(u0));
   for (int64_t k = 1; k <= K; ++k) {
@@ -933,13 +967,14 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
     gU.index_fill_(0, ru, 0.0);
   }
   index_add_rows(gU, ru, vu.contiguous());
-  Tensor mu = at::zeros({std::max<int64_t>(U, 1)}, u8(vu));
-  Tensor mi = at::empty({std::max<int64_t>(I, 1)}, u8(vu));
+  // mu (and mi when it is marked from the list) zeroed by one fill
+  ZeroArena za(vu, {U, gi_rows ? I : 0});
+  Tensor mu = za.bytes(0);
+  Tensor mi = gi_rows ? za.bytes(1) : at::empty({std::max<int64_t>(I, 1)}, u8(vu)).narrow(0, 0, I);
   check(bbgr_mark_rows(ru.numel(), ru.data_ptr<int64_t>(), 1, mu.data_ptr<uint8_t>(), U,
                        cur_stream()),
         "bbgr_mark_rows");
   if (gi_rows) {
-    mi.zero_();
     check(bbgr_mark_rows(ii.numel(), ii.data_ptr<int64_t>(), 1, mi.data_ptr<uint8_t>(), I,
                          cur_stream()),
           "bbgr_mark_rows");
@@ -1144,36 +1179,35 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_cuda(
 // new stream at a recycled address is still all INT32_MAX once the old
 // stream's work has drained, which destroying a stream waits for.
 static constexpr size_t kFirstSlotScratch = 8;
-static Tensor first_slot(const Tensor &ids_, int64_t n_rows) {
-  Tensor ids = ids_.to(at::kLong).contiguous();
-  Tensor slot = at::empty_like(ids);
+static Tensor slot_scratch(int64_t n_rows, const at::Device &dev) {
   static std::mutex mu;
   static std::map<std::tuple<int64_t, int64_t, int64_t>, std::pair<Tensor, uint64_t>> scratch;
   static uint64_t tick = 0;
-  Tensor first;
   const auto fresh = [&] {
     return at::full({std::max<int64_t>(n_rows, 1)}, 0x7fffffff,
-                    at::TensorOptions().dtype(at::kInt).device(ids.device()));
+                    at::TensorOptions().dtype(at::kInt).device(dev));
   };
-  if (capturing()) {   // a captured step fills its own (the fill replays with it)
-    first = fresh();
-  } else {
-    std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_tuple((int64_t)ids.device().index(), n_rows,
-                                     (int64_t)(intptr_t)cur_stream());
-    auto it = scratch.find(key);
-    if (it == scratch.end()) {
-      if (scratch.size() >= kFirstSlotScratch) {
-        auto lru = scratch.begin();
-        for (auto j = scratch.begin(); j != scratch.end(); ++j)
-          if (j->second.second < lru->second.second) lru = j;
-        scratch.erase(lru);
-      }
-      it = scratch.emplace(key, std::make_pair(fresh(), uint64_t(0))).first;
+  if (capturing()) return fresh();   // a captured step fills its own (the fill replays with it)
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_tuple((int64_t)dev.index(), n_rows, (int64_t)(intptr_t)cur_stream());
+  auto it = scratch.find(key);
+  if (it == scratch.end()) {
+    if (scratch.size() >= kFirstSlotScratch) {
+      auto lru = scratch.begin();
+      for (auto j = scratch.begin(); j != scratch.end(); ++j)
+        if (j->second.second < lru->second.second) lru = j;
+      scratch.erase(lru);
     }
-    it->second.second = ++tick;
-    first = it->second.first;
+    it = scratch.emplace(key, std::make_pair(fresh(), uint64_t(0))).first;
   }
+  it->second.second = ++tick;
+  return it->second.first;
+}
+
+static Tensor first_slot(const Tensor &ids_, int64_t n_rows) {
+  Tensor ids = ids_.to(at::kLong).contiguous();
+  Tensor slot = at::empty_like(ids);
+  Tensor first = slot_scratch(n_rows, ids.device());
   check(bbgr_first_slot(ids.numel(), ids.data_ptr<int64_t>(), n_rows, first.data_ptr<int32_t>(),
                         slot.data_ptr<int64_t>(), cur_stream()),
         "bbgr_first_slot");
@@ -1190,14 +1224,21 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
                                                                 const Tensor &ue,
                                                                 const Tensor &ie, double reg) {
   const int64_t B = users.numel(), d = ue.size(1), U = ue.size(0), I = ie.size(0);
-  Tensor valid = (users >= 0) & (users < U) & (pos >= 0) & (pos < I) & (neg >= 0) & (neg < I);
-  Tensor iu = users.clamp(0, U - 1);
-  Tensor ii = at::cat({pos, neg}).clamp(0, I - 1);
-  Tensor su = first_slot(iu, U), si = first_slot(ii, I);
+  TORCH_CHECK(U > 0 && I > 0, "ego_grad_rows: empty table");
+  // one int64 block: iu [B], ii [2B], cu [B], sp [B], sn [B]
+  Tensor ix = at::empty({6 * B}, users.options());
+  Tensor iu = ix.narrow(0, 0, B), ii = ix.narrow(0, B, 2 * B), cu = ix.narrow(0, 3 * B, B),
+         sp = ix.narrow(0, 4 * B, B), sn = ix.narrow(0, 5 * B, B);
+  Tensor fu = slot_scratch(U, users.device()), fi = slot_scratch(I, users.device());
+  check(bbgr_ego_slots(B, users.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
+                       neg.data_ptr<int64_t>(), U, I, fu.data_ptr<int32_t>(),
+                       fi.data_ptr<int32_t>(), iu.data_ptr<int64_t>(), ii.data_ptr<int64_t>(),
+                       cu.data_ptr<int64_t>(), sp.data_ptr<int64_t>(), sn.data_ptr<int64_t>(),
+                       cur_stream()),
+        "bbgr_ego_slots");
   Tensor ue_c = ue.index_select(0, iu).contiguous(), ie_c = ie.index_select(0, ii).contiguous();
-  Tensor cu = at::where(valid, su, at::full_like(su, -1)).contiguous();
-  Tensor gu = at::zeros({B, d}, f32(ue)), gi = at::zeros({2 * B, d}, f32(ue));
-  Tensor sp = si.narrow(0, 0, B).contiguous(), sn = si.narrow(0, B, B).contiguous();
+  Tensor g = at::zeros({3 * B, d}, f32(ue));
+  Tensor gu = g.narrow(0, 0, B), gi = g.narrow(0, B, 2 * B);
   bbgr_bpr_args a = bpr_args(cu, sp, sn, ue_c, ie_c, ue_c, ie_c, reg, c10::nullopt, 0.0);
   a.dloss = dl.data_ptr<float>();
   a.g_ue = gu.data_ptr<float>();
@@ -1240,7 +1281,10 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   Tensor uf = uf_.contiguous(), itf = itf_.contiguous();
   const int64_t B = users.numel();
   Tensor dl = dloss.to(at::kFloat).contiguous().reshape({});
-  Tensor contrib = at::empty({3 * B, d}, f32(uf));
+  // [user rows | pos rows | neg rows | (K+1)-scaled ego item rows]: the item
+  // gradient's addends lie contiguous, in the order they are summed
+  Tensor rows = at::empty({5 * B, d}, f32(uf));
+  Tensor contrib = rows.narrow(0, 0, 3 * B);
   bbgr_bpr_args a = bpr_args(users, pos, neg, uf, itf, u0, i0, reg, c10::nullopt, 0.0);
   a.dloss = dl.data_ptr<float>();
   a.contrib = contrib.data_ptr<float>();
@@ -1259,8 +1303,10 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   // the item gradient / gl: the BPR rows, then the ego rows, per item in
   // ascending source order
   Tensor vi = contrib.narrow(0, B, 2 * B);
+  Tensor ego_i = rows.narrow(0, 3 * B, 2 * B);
+  at::mul_out(ego_i, ri, kp1);
   sa.item_grad = at::zeros({std::max<int64_t>(I, 1), d}, f32(uf)).narrow(0, 0, I);
-  index_add_rows(sa.item_grad, at::cat({ii, ii}), at::cat({vi, at::mul(ri, kp1)}));
+  index_add_rows(sa.item_grad, at::cat({ii, ii}), rows.narrow(0, B, 4 * B));
   rows_backward(P, iu, contrib.narrow(0, 0, B), i0, K, true, ii, vi, &sa);
 }
 

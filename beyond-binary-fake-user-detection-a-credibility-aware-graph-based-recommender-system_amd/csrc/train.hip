@@ -492,6 +492,58 @@ __global__ void first_slot_reset_kernel(long n, const long *ids, long n_rows, in
   if (r >= 0 && r < n_rows) first[r] = 0x7fffffff;
 }
 
+// bbgr_ego_slots: the first_slot passes of a (user, pos, neg) batch at once.
+// Thread t < B handles user t, thread B + j item j of cat(pos, neg).
+__device__ __forceinline__ long clamp_row(long r, long n) { return r < 0 ? 0 : (r >= n ? n - 1 : r); }
+
+__global__ void ego_slots_min_kernel(long B, const long *users, const long *pos, const long *neg,
+                                     long U, long I, int *first_u, int *first_i, long *iu,
+                                     long *ii) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * B) return;
+  if (t < B) {
+    const long r = clamp_row(users[t], U);
+    iu[t] = r;
+    atomicMin(first_u + r, (int)t);
+  } else {
+    const long j = t - B;
+    const long r = clamp_row(j < B ? pos[j] : neg[j - B], I);
+    ii[j] = r;
+    atomicMin(first_i + r, (int)j);
+  }
+}
+__global__ void ego_slots_read_kernel(long B, const long *users, const long *pos, const long *neg,
+                                      long U, long I, const int *first_u, const int *first_i,
+                                      const long *iu, const long *ii, long *cu, long *sp,
+                                      long *sn) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * B) return;
+  if (t < B) {
+    const long u = users[t], p = pos[t], n = neg[t];
+    const bool ok = u >= 0 && u < U && p >= 0 && p < I && n >= 0 && n < I;
+    cu[t] = ok ? (long)first_u[iu[t]] : -1;
+  } else {
+    const long j = t - B;
+    const long s = first_i[ii[j]];
+    if (j < B) sp[j] = s; else sn[j - B] = s;
+  }
+}
+__global__ void ego_slots_reset_kernel(long B, int *first_u, int *first_i, const long *iu,
+                                       const long *ii) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * B) return;
+  if (t < B) first_u[iu[t]] = 0x7fffffff;
+  else first_i[ii[t - B]] = 0x7fffffff;
+}
+
+__global__ void graph_rows_kernel(long n, const long *ids, long n_rows, const long *rank,
+                                  long *out) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const long r = ids[k];
+  out[k] = (r >= 0 && r < n_rows) ? (rank ? rank[r] : r) : -1;
+}
+
 // dst[idx[k]] = src[idx[k]] (idx < 0 skipped; repeats write the same row).
 __global__ __launch_bounds__(256) void rows_copy_kernel(long n, const long *idx,
                                                         const float4 *src, long lds4,
@@ -936,6 +988,43 @@ extern "C" int bbgr_first_slot(int64_t n, const int64_t *ids, int64_t n_rows, in
   hipLaunchKernelGGL(first_slot_reset_kernel, dim3(g), dim3(256), 0, st, (long)n,
                      (const long *)ids, (long)n_rows, first);
   BBGR_LAUNCHED("first_slot_reset_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_ego_slots(int64_t B, const int64_t *users, const int64_t *pos,
+                              const int64_t *neg, int64_t n_users, int64_t n_items,
+                              int32_t *first_u, int32_t *first_i, int64_t *iu, int64_t *ii,
+                              int64_t *cu, int64_t *sp, int64_t *sn, bbgr_stream_t stream) {
+  BBGR_REQUIRE(B >= 0 && 3 * B < (1LL << 31) && n_users > 0 && n_items > 0,
+               "bbgr_ego_slots: bad sizes");
+  if (B == 0) return BBGR_OK;
+  BBGR_REQUIRE(users && pos && neg && first_u && first_i && iu && ii && cu && sp && sn,
+               "bbgr_ego_slots: null arrays");
+  hipStream_t st = as_stream(stream);
+  const unsigned g = (unsigned)((3 * B + 255) / 256);
+  const long *u = (const long *)users, *p = (const long *)pos, *n = (const long *)neg;
+  hipLaunchKernelGGL(ego_slots_min_kernel, dim3(g), dim3(256), 0, st, (long)B, u, p, n,
+                     (long)n_users, (long)n_items, first_u, first_i, (long *)iu, (long *)ii);
+  BBGR_LAUNCHED("ego_slots_min_kernel");
+  hipLaunchKernelGGL(ego_slots_read_kernel, dim3(g), dim3(256), 0, st, (long)B, u, p, n,
+                     (long)n_users, (long)n_items, (const int *)first_u, (const int *)first_i,
+                     (const long *)iu, (const long *)ii, (long *)cu, (long *)sp, (long *)sn);
+  BBGR_LAUNCHED("ego_slots_read_kernel");
+  hipLaunchKernelGGL(ego_slots_reset_kernel, dim3(g), dim3(256), 0, st, (long)B, first_u,
+                     first_i, (const long *)iu, (const long *)ii);
+  BBGR_LAUNCHED("ego_slots_reset_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_graph_rows(int64_t n, const int64_t *ids, int64_t n_rows, const int64_t *rank,
+                               int64_t *out, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n_rows >= 0, "bbgr_graph_rows: bad sizes");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(ids && out, "bbgr_graph_rows: null arrays");
+  hipLaunchKernelGGL(graph_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)ids, (long)n_rows,
+                     (const long *)rank, (long *)out);
+  BBGR_LAUNCHED("graph_rows_kernel");
   return BBGR_OK;
 }
 

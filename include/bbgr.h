@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 7
+#define BBGR_ABI_VERSION 8
 
 typedef enum {
   BBGR_OK = 0,
@@ -500,6 +500,27 @@ int bbgr_rows_add_unique(int64_t n, const int64_t *idx, const float *src, int64_
 /* deterministic), a gather, and a reset of the touched rows.              */
 int bbgr_first_slot(int64_t n, const int64_t *ids, int64_t n_rows, int32_t *first,
                     int64_t *slot, bbgr_stream_t stream);
+
+/* The ego rows' slots of a batch of B (user, pos, neg) triples in three     */
+/* launches (ABI 8; bpr.ego_grad_rows, the drop-in step's BPR backward,      */
+/* Version-2/lighgcn_cu_pop.py:389-397):                                      */
+/*   iu[b] = clamp(users[b], 0, n_users - 1);                                 */
+/*   ii[b] = clamp(pos[b], 0, n_items - 1), ii[B + b] = clamp(neg[b], ...);   */
+/*   cu[b] = the first b' with iu[b'] == iu[b], or -1 when any id of triple  */
+/*           b lies outside its table;                                        */
+/*   sp[b] / sn[b] = the first j with ii[j] == ii[b] / ii[B + b].             */
+/* first_u [n_users] / first_i [n_items]: int32 scratch holding INT32_MAX at */
+/* every row (left so on return), as bbgr_first_slot's.                       */
+int bbgr_ego_slots(int64_t B, const int64_t *users, const int64_t *pos, const int64_t *neg,
+                   int64_t n_users, int64_t n_items, int32_t *first_u, int32_t *first_i,
+                   int64_t *iu, int64_t *ii, int64_t *cu, int64_t *sp, int64_t *sn,
+                   bbgr_stream_t stream);
+
+/* out[k] = rank[ids[k]] (rank NULL: ids[k]) for ids[k] in [0, n_rows), else */
+/* -1 (ABI 8): a caller's row ids as graph rows in one launch                */
+/* (bbgr::propagate_rows' batch lists; the marking kernels skip the -1).     */
+int bbgr_graph_rows(int64_t n, const int64_t *ids, int64_t n_rows, const int64_t *rank,
+                    int64_t *out, bbgr_stream_t stream);
 
 /* Deterministic index_add_: dst[idx[k], :d] += src[k, :d] for k < n, with   */
 /* the addends of each destination row summed in ascending k and added once  */

@@ -117,6 +117,17 @@ int main(void) {
   expect_error("first_slot bad n", bbgr_first_slot(-1, NULL, 4, NULL, NULL, NULL));
   expect_error("first_slot null", bbgr_first_slot(4, NULL, 4, NULL, NULL, NULL));
   expect_ok("first_slot empty", bbgr_first_slot(0, NULL, 4, NULL, NULL, NULL));
+  expect_error("ego_slots bad B", bbgr_ego_slots(-1, NULL, NULL, NULL, 4, 4, NULL, NULL, NULL, NULL,
+                                                  NULL, NULL, NULL, NULL));
+  expect_error("ego_slots empty table", bbgr_ego_slots(0, NULL, NULL, NULL, 0, 4, NULL, NULL, NULL,
+                                                       NULL, NULL, NULL, NULL, NULL));
+  expect_error("ego_slots null", bbgr_ego_slots(4, NULL, NULL, NULL, 4, 4, NULL, NULL, NULL, NULL,
+                                                NULL, NULL, NULL, NULL));
+  expect_ok("ego_slots empty", bbgr_ego_slots(0, NULL, NULL, NULL, 4, 4, NULL, NULL, NULL, NULL,
+                                              NULL, NULL, NULL, NULL));
+  expect_error("graph_rows bad n", bbgr_graph_rows(-1, NULL, 4, NULL, NULL, NULL));
+  expect_error("graph_rows null", bbgr_graph_rows(4, NULL, 4, NULL, NULL, NULL));
+  expect_ok("graph_rows empty", bbgr_graph_rows(0, NULL, 4, NULL, NULL, NULL));
   expect_error("rows_copy bad d", bbgr_rows_copy(4, NULL, f4, 64, f4, 64, 6, NULL));
   expect_ok("rows_copy empty", bbgr_rows_copy(0, NULL, NULL, 64, NULL, 64, 64, NULL));
   expect_error("rows_add_unique bad ld", bbgr_rows_add_unique(4, NULL, f4, 32, f4, 64, 64, 8,

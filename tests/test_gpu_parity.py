@@ -865,6 +865,67 @@ def test_first_slot_kernel_is_the_first_occurrence(n, hi):
         assert bool((first == 0x7fffffff).all())
 
 
+@pytest.mark.parametrize("B,U,I", [(1, 3, 2), (8192, 5_000_000, 1_000_000), (4096, 50, 30),
+                                   (300, 300, 7)])
+def test_ego_slots_kernel_is_the_torch_formulation(B, U, I):
+    """bbgr_ego_slots (the drop-in BPR backward's ego-row slots in three
+    launches) equals the torch formulation it replaced: clamped ids, the first
+    occurrence of each clamped id (bbgr_first_slot semantics, an invalid
+    triple's clamped id included), -1 for a triple with any id out of range;
+    both scratch tables are left all INT32_MAX."""
+    from bbgr import _lib
+    g = torch.Generator().manual_seed(B + U + I)
+    users = torch.randint(-1, U + 1, (B,), generator=g)
+    pos = torch.randint(-1, I + 1, (B,), generator=g)
+    neg = torch.randint(-1, I + 1, (B,), generator=g)
+    if B > 1000:   # mostly valid, as a sampler's batch
+        users, pos, neg = users.clamp(0, U - 1), pos.clamp(0, I - 1), neg.clamp(0, I - 1)
+        users[::97], neg[::89] = -1, I
+    valid = (users >= 0) & (users < U) & (pos >= 0) & (pos < I) & (neg >= 0) & (neg < I)
+    iu = users.clamp(0, U - 1)
+    ii = torch.cat([pos, neg]).clamp(0, I - 1)
+
+    def first(ids):
+        seen = {}
+        return torch.tensor([seen.setdefault(v, b) for b, v in enumerate(ids.tolist())])
+
+    su, si = first(iu), first(ii)
+    want_cu = torch.where(valid, su, torch.full_like(su, -1))
+    fu = torch.full((U,), 0x7fffffff, dtype=torch.int32, device=DEV)
+    fi = torch.full((I,), 0x7fffffff, dtype=torch.int32, device=DEV)
+    out = torch.empty(6 * B, dtype=torch.int64, device=DEV)
+    du, dp, dn = users.to(DEV), pos.to(DEV), neg.to(DEV)
+    for _ in range(2):   # reusable scratch
+        out.fill_(-7)
+        _lib.call("bbgr_ego_slots", B, _lib.ptr(du), _lib.ptr(dp), _lib.ptr(dn), U, I,
+                  _lib.ptr(fu), _lib.ptr(fi), _lib.ptr(out), _lib.ptr(out[B:]), _lib.ptr(out[3 * B:]),
+                  _lib.ptr(out[4 * B:]), _lib.ptr(out[5 * B:]), _lib.stream_handle())
+        torch.cuda.synchronize()
+        o = out.cpu()
+        assert torch.equal(o[:B], iu) and torch.equal(o[B:3 * B], ii)
+        assert torch.equal(o[3 * B:4 * B], want_cu)
+        assert torch.equal(o[4 * B:5 * B], si[:B]) and torch.equal(o[5 * B:], si[B:])
+        assert bool((fu == 0x7fffffff).all()) and bool((fi == 0x7fffffff).all())
+
+
+@pytest.mark.parametrize("ranked", [False, True])
+def test_graph_rows_kernel(ranked):
+    """bbgr_graph_rows: rank[id] (or the id) inside [0, n), -1 outside."""
+    from bbgr import _lib
+    n_rows = 1000
+    ids = torch.randint(-5, n_rows + 5, (5000,), generator=torch.Generator().manual_seed(3))
+    rank = torch.randperm(n_rows, generator=torch.Generator().manual_seed(4))
+    ok = (ids >= 0) & (ids < n_rows)
+    base = rank[ids.clamp(0, n_rows - 1)] if ranked else ids
+    want = torch.where(ok, base, torch.full_like(ids, -1))
+    di, dr = ids.to(DEV), rank.to(DEV)
+    out = torch.empty_like(di)
+    _lib.call("bbgr_graph_rows", ids.numel(), _lib.ptr(di), n_rows,
+              _lib.ptr(dr) if ranked else None, _lib.ptr(out), _lib.stream_handle())
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), want)
+
+
 @pytest.mark.parametrize("d", [16, 64, 256])
 def test_rows_add_unique_is_bitwise_the_sorted_scatter(d):
     """bbgr_rows_add_unique (distinct indices, no sort) == bbgr_scatter_add_rows

@@ -71,6 +71,7 @@ def main():
     runs = [(int(x), int(ch), int(fp)) for ch in a.column_chains.split(",")
             for x in a.exchange_parts.split(",") for fp in a.frontier_parts.split(",")]
     for xp, chains, fparts in runs:
+        torch.cuda.reset_peak_memory_stats()
         tr = ShardedTrainer(local, hi - lo, I, "v2_pop", cred=cred, emb_dim=d, num_layers=K,
                             batch_size=max(1, B // a.parts_of), device="cuda",
                             vertex_order="degree", exchange_parts=xp,
@@ -107,7 +108,10 @@ def main():
                           "column_chains": chains, "frontier_parts": fparts,
                           "native_comm": a.native_comm,
                           "item_rows_owned": tr.ib - tr.ia,
-                          "ms_per_step": ms, "host_issue_ms": 1000.0 * issue / a.steps}),
+                          "ms_per_step": ms, "host_issue_ms": 1000.0 * issue / a.steps,
+                          # device memory one such rank holds at its peak (whether
+                          # N ranks of it fit one GPU for a gloo rehearsal)
+                          "peak_allocated_gib": torch.cuda.max_memory_allocated() / 2**30}),
               flush=True)
         tr.close()
         del tr
