@@ -182,8 +182,11 @@ def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop",
     (Version-2:835-849), then loss = bpr(propagate()) (2K torch.sparse.mm over
     every edge), loss.backward() (autograd's 2K transposed products) and
     torch.optim.Adam.step() over all (U+I) x d parameters (V2:858-863), each
-    part timed. One run, no warm-up (a step takes minutes of host time); whole
-    reference steps of the same variant at C2 and C1 are timed beside."""
+    part timed. One run (a step takes minutes of host time); the whole
+    reference steps of the same variant at C2 and C1 are timed FIRST, so
+    torch's CPU thread pool, sparse kernels and allocator are warm when the C4
+    step starts (its large tensors are fresh mmaps in every step of the
+    reference too, so their first-touch cost belongs to the step)."""
     from oracle import ref_numpy as R
     from oracle import ref_torch as T
     cores = cpu_threads()
@@ -200,6 +203,7 @@ def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop",
                            f"1 warm-up: {med:.3f}s"),
                 "whole_step_s": {cfg_name: {"median": med, "runs": ts, "edges_per_s": work / med,
                                             **_spread(ts)}}}
+    whole = {n: _reference_step_s(n, variant, whole_reps) for n in whole_steps}
     t_setup = time.perf_counter()
     torch.manual_seed(seed)
     model, popmix = T.reference_model(variant, edges, U, I, d, K, cred)
@@ -231,12 +235,12 @@ def cpu_baseline(edges, cfg, cfg_name, cred, variant: str = "v2_pop",
     del loss, opt, model
     t_fwd, t_bwd, t_adam = t1 - t0, t2 - t1, t3 - t2
     t_step = t_samp + t_fwd + t_bwd + t_adam
-    whole = {n: _reference_step_s(n, variant, whole_reps) for n in whole_steps}
     return {
         "value": 4 * K * E / t_step, "unit": "edges/s", "cores": cores, "kind": "port",
         "bpr_steps_per_s": 1.0 / t_step,
-        "sample": (f"ONE whole {cfg_name} {variant} reference step, measured (one run, no "
-                   f"warm-up): {'pop-mix' if popmix else 'uniform'} sampler loop over B={B} "
+        "sample": (f"ONE whole {cfg_name} {variant} reference step, measured (one run, after "
+                   f"the C2 / C1 whole steps warmed torch's CPU machinery): "
+                   f"{'pop-mix' if popmix else 'uniform'} sampler loop over B={B} "
                    f"users {t_samp:.1f}s (1 thread), propagate + BPR {t_fwd:.1f}s (2K={2 * K} "
                    f"torch.sparse.mm over all {E} edges), loss.backward() {t_bwd:.1f}s, torch "
                    f"Adam over {U + I} rows {t_adam:.2f}s: {t_step:.1f}s/step on {cores} "

@@ -172,6 +172,9 @@ _SIGNATURES = {
                             ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_scatter_add_rows": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P,
                                ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_scatter_plan": ([c_int64, _P, c_int64, _P, ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_scatter_apply": ([c_int64, c_int64, _P, _P, c_int64, _P, c_int64, _P, c_int64, c_int32,
+                            _P], c_int32),
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
     "bbgr_mark_slots": ([c_int64, _P, _P, _P, _P, c_int32, _P], c_int32),
     "bbgr_mark_list": ([c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P], c_int32),

@@ -669,11 +669,55 @@ static void release_bits(const Pair &P, const Support &s, const Tensor &ui) {
 // ego[r], so G = out * T + gl * gU carries them), as FusedTrainer does.
 static void index_add_rows(Tensor &dst, const Tensor &index, const Tensor &src);
 
+// The sort of a deterministic row scatter, kept to apply to several tables
+// over the same index list (bbgr_scatter_plan / bbgr_scatter_apply).
+struct RowPlan {
+  Tensor ws, idx;
+  int64_t n = 0, n_dst = 0;
+  bool defined() const { return ws.defined(); }
+};
+
+static RowPlan plan_rows(const Tensor &index, int64_t n_dst) {
+  RowPlan r;
+  r.idx = index.to(at::kLong).contiguous();
+  r.n = r.idx.numel();
+  r.n_dst = n_dst;
+  size_t need = 0;
+  check(bbgr_scatter_plan(r.n, r.idx.data_ptr<int64_t>(), n_dst, nullptr, &need, cur_stream()),
+        "bbgr_scatter_plan (size)");
+  r.ws = at::empty({(int64_t)std::max<size_t>(need, 1)},
+                   at::TensorOptions().dtype(at::kByte).device(index.device()));
+  size_t have = (size_t)r.ws.numel();
+  check(bbgr_scatter_plan(r.n, r.idx.data_ptr<int64_t>(), n_dst, r.ws.data_ptr(), &have,
+                          cur_stream()),
+        "bbgr_scatter_plan");
+  return r;
+}
+
+// dst.index_add_(0, idx, src) (then src2 continuing each row's sum) in the
+// plan's order: bitwise index_add_rows over [src; src2] with [idx; idx]
+static void apply_rows(const RowPlan &r, Tensor &dst, const Tensor &src_,
+                       const Tensor &src2_ = Tensor()) {
+  TORCH_CHECK(dst.size(0) == r.n_dst, "apply_rows: destination rows differ from the plan's");
+  const Tensor src = src_.contiguous(), src2 = src2_.defined() ? src2_.contiguous() : Tensor();
+  TORCH_CHECK(src.size(0) >= r.n && src.size(1) == dst.size(1) &&
+                  (!src2.defined() || (src2.size(0) >= r.n && src2.size(1) == dst.size(1))),
+              "apply_rows: shapes");
+  check(bbgr_scatter_apply(r.n, r.n_dst, r.ws.data_ptr(), src.data_ptr<float>(), ld(src),
+                           src2.defined() ? src2.data_ptr<float>() : nullptr,
+                           src2.defined() ? ld(src2) : 0, dst.data_ptr<float>(), ld(dst),
+                           (int32_t)dst.size(1), cur_stream()),
+        "bbgr_scatter_apply");
+}
+
 struct StepAdam {
   AdamTable user, item;
   Tensor item_grad;                 // [I, d], caller's row order
   Tensor ego_u_vals;                // (K+1) * ego rows, aligned with the users' rows
-  Tensor ego_u_rows;                // their gU rows (set by rows_backward)
+  // the sorts of the step's two index lists: the batch items (gI and the
+  // item gradient) and the batch users' gU rows (set by rows_backward; gU
+  // and the ego rows added before the user Adam)
+  RowPlan item_plan, user_plan;
 };
 
 static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU, const Tensor &gI,
@@ -740,7 +784,7 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
         ou.add_scale = P.bi.in_scale;
       } else if (sa) {   // the user Adam: no gradient table, ego rows in gU first
         Tensor g = gU;
-        index_add_rows(g, sa->ego_u_rows, sa->ego_u_vals);
+        apply_rows(sa->user_plan, g, sa->ego_u_vals);
         ou.y_scale = P.bu.out_scale;
         ou.y_map = um;   // the Adam's rows: the caller's order
         ou.adam = &sa->user;
@@ -949,7 +993,8 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
     TORCH_CHECK(vi_->dim() == 2 && vi_->size(0) == ii.numel() && vi_->size(1) == d,
                 "propagate_backward_rows: vi must be [len(ii), d]");
     gI = at::zeros({std::max<int64_t>(I, 1), d}, f32(vu)).narrow(0, 0, I);
-    index_add_rows(gI, ii, vi_->contiguous());
+    if (sa && sa->item_plan.defined()) apply_rows(sa->item_plan, gI, *vi_);
+    else index_add_rows(gI, ii, vi_->contiguous());
   } else {
     gI = gI_.contiguous();
   }
@@ -958,7 +1003,6 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
   // (Support.gu_internal); the same values at the same rows of the products
   const bool gu_int = P->io && K >= 1;
   Tensor ru = gu_int ? P->user_rank64.index_select(0, iu).contiguous() : iu;
-  if (sa) sa->ego_u_rows = ru;   // the ego rows land on the same gU rows as vu
   Tensor gU;
   if (K == 0) {
     gU = at::zeros({std::max<int64_t>(U, 1), d}, f32(vu)).narrow(0, 0, U);
@@ -966,7 +1010,12 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
     gU = at::empty({std::max<int64_t>(U, 1), d}, f32(vu)).narrow(0, 0, U);
     gU.index_fill_(0, ru, 0.0);
   }
-  index_add_rows(gU, ru, vu.contiguous());
+  if (sa) {   // the ego rows land on the same gU rows as vu: one sort for both
+    sa->user_plan = plan_rows(ru, U);
+    apply_rows(sa->user_plan, gU, vu);
+  } else {
+    index_add_rows(gU, ru, vu.contiguous());
+  }
   // mu (and mi when it is marked from the list) zeroed by one fill
   ZeroArena za(vu, {U, gi_rows ? I : 0});
   Tensor mu = za.bytes(0);
@@ -1281,10 +1330,7 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   Tensor uf = uf_.contiguous(), itf = itf_.contiguous();
   const int64_t B = users.numel();
   Tensor dl = dloss.to(at::kFloat).contiguous().reshape({});
-  // [user rows | pos rows | neg rows | (K+1)-scaled ego item rows]: the item
-  // gradient's addends lie contiguous, in the order they are summed
-  Tensor rows = at::empty({5 * B, d}, f32(uf));
-  Tensor contrib = rows.narrow(0, 0, 3 * B);
+  Tensor contrib = at::empty({3 * B, d}, f32(uf));
   bbgr_bpr_args a = bpr_args(users, pos, neg, uf, itf, u0, i0, reg, c10::nullopt, 0.0);
   a.dloss = dl.data_ptr<float>();
   a.contrib = contrib.data_ptr<float>();
@@ -1302,11 +1348,11 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   sa.ego_u_vals = at::mul(ru, kp1);
   // the item gradient / gl: the BPR rows, then the ego rows, per item in
   // ascending source order
+  // (one sort of the 2B item ids serves this scatter and rows_backward's gI)
   Tensor vi = contrib.narrow(0, B, 2 * B);
-  Tensor ego_i = rows.narrow(0, 3 * B, 2 * B);
-  at::mul_out(ego_i, ri, kp1);
+  sa.item_plan = plan_rows(ii, I);
   sa.item_grad = at::zeros({std::max<int64_t>(I, 1), d}, f32(uf)).narrow(0, 0, I);
-  index_add_rows(sa.item_grad, at::cat({ii, ii}), rows.narrow(0, B, 4 * B));
+  apply_rows(sa.item_plan, sa.item_grad, vi, at::mul(ri, kp1));
   rows_backward(P, iu, contrib.narrow(0, 0, B), i0, K, true, ii, vi, &sa);
 }
 

@@ -610,11 +610,15 @@ __global__ void scatter_keys_kernel(long n, const long *idx, long n_dst, unsigne
 // is a prefix, its length a ballot), then up to 8 of its rows are gathered
 // before they are added in order: a hot destination (a popular item drawn
 // many times as a negative) no longer costs one dependent load chain per
-// element. The additions are the same, in the same order (bitwise).
+// element. The additions are the same, in the same order (bitwise). src2
+// (nullable): the run is summed over src, then the same sum continues over
+// src2's rows of the run — one ascending sum over [src; src2], as if the two
+// tables were concatenated with their index lists (bbgr_scatter_apply).
 template <int D>
 __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const unsigned *keys,
                                                                const int *vals,
                                                                const float *src, long lds,
+                                                               const float *src2, long lds2,
                                                                float *dst, long ldd,
                                                                unsigned skip) {
   constexpr int V = RowShape<D>::V;
@@ -628,6 +632,10 @@ __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const uns
   float4 acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int pass = 0; pass < 2; ++pass) {
+  const float *sp = pass ? src2 : src;
+  const long lp = pass ? lds2 : lds;
+  if (!sp) break;
   for (long t0 = s;; t0 += 16) {
     const long tj = t0 + lane;
     const bool in = tj < n && keys[tj] == key;
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const uns
       for (int g = 0; g < G; ++g) {
         const int v = __shfl(vj, j0 + g, 16);
         if (cols && j0 + g < cnt) {
-          const float4 *row = reinterpret_cast<const float4 *>(src + (long)v * lds) + lane;
+          const float4 *row = reinterpret_cast<const float4 *>(sp + (long)v * lp) + lane;
 #pragma unroll
           for (int k = 0; k < V; ++k) x[g][k] = row[16 * k];
         }
@@ -657,6 +665,7 @@ __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const uns
     }
     if (cnt < 16) break;
   }
+  }
   if (!cols) return;
   float4 *out = reinterpret_cast<float4 *>(dst + (long)key * ldd) + lane;
 #pragma unroll
@@ -670,6 +679,88 @@ __global__ __launch_bounds__(256) void scatter_segments_kernel(long n, const uns
 
 using namespace bbgr;
 
+// the plan of a scatter over n rows: [k1 | k2 | v1 | v2 | sort scratch], the
+// sorted (key, position) pairs in k2 / v2
+static size_t scatter_plan_bytes(int64_t n, int64_t n_dst, int *end_bit_out, size_t *temp_out,
+                                 hipStream_t st) {
+  int end_bit = 1;   // keys are in [0, n_dst] (n_dst marks skipped rows)
+  while (end_bit < 32 && (1ull << end_bit) <= (unsigned long long)n_dst) ++end_bit;
+  size_t temp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (unsigned *)nullptr, (unsigned *)nullptr,
+                                           (int *)nullptr, (int *)nullptr,
+                                           (int)(n > 0 ? n : 1), 0, end_bit, st);
+  if (end_bit_out) *end_bit_out = end_bit;
+  if (temp_out) *temp_out = temp;
+  return 4 * align_up(4 * (size_t)(n > 0 ? n : 1)) + align_up(temp);
+}
+
+extern "C" int bbgr_scatter_plan(int64_t n, const int64_t *idx, int64_t n_dst, void *plan,
+                                 size_t *plan_bytes, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n < (1ll << 31) && n_dst >= 0 && n_dst < 0xFFFFFFFFll && plan_bytes,
+               "bbgr_scatter_plan: bad sizes");
+  hipStream_t st = as_stream(stream);
+  int end_bit = 1;
+  size_t temp = 0;
+  const size_t need = scatter_plan_bytes(n, n_dst, &end_bit, &temp, st);
+  if (!plan) {
+    *plan_bytes = need;
+    return BBGR_OK;
+  }
+  if (*plan_bytes < need) {
+    set_error("bbgr_scatter_plan: plan %zu < %zu bytes", *plan_bytes, need);
+    return BBGR_ERR_WORKSPACE;
+  }
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(idx, "bbgr_scatter_plan: null idx");
+  const size_t a = align_up(4 * (size_t)n);
+  char *ws = static_cast<char *>(plan);
+  unsigned *k1 = reinterpret_cast<unsigned *>(ws), *k2 = reinterpret_cast<unsigned *>(ws + a);
+  int *v1 = reinterpret_cast<int *>(ws + 2 * a), *v2 = reinterpret_cast<int *>(ws + 3 * a);
+  hipLaunchKernelGGL(scatter_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (long)n, (const long *)idx, (long)n_dst, k1, v1);
+  BBGR_LAUNCHED("scatter_keys_kernel");
+  BBGR_HIP(hipcub::DeviceRadixSort::SortPairs(ws + 4 * a, temp, k1, k2, v1, v2, (int)n, 0,
+                                              end_bit, st));
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_scatter_apply(int64_t n, int64_t n_dst, const void *plan, const float *src,
+                                  int64_t ldsrc, const float *src2, int64_t ldsrc2, float *dst,
+                                  int64_t lddst, int32_t d, bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n < (1ll << 31) && n_dst >= 0 && n_dst < 0xFFFFFFFFll,
+               "bbgr_scatter_apply: bad sizes");
+  if (!supported_width(d)) {
+    set_error("bbgr_scatter_apply: d = %d unsupported (8, 16, 32, 64, 128, 256)", d);
+    return BBGR_ERR_UNSUPPORTED;
+  }
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(plan && src && dst, "bbgr_scatter_apply: null arrays");
+  BBGR_REQUIRE(aligned16(src) && aligned16(dst) && ldsrc >= d && lddst >= d &&
+                   (ldsrc & 3) == 0 && (lddst & 3) == 0 &&
+                   (!src2 || (aligned16(src2) && ldsrc2 >= d && (ldsrc2 & 3) == 0)),
+               "bbgr_scatter_apply: tables must be 16-byte aligned, ld >= d, ld % 4 == 0");
+  hipStream_t st = as_stream(stream);
+  const size_t a = align_up(4 * (size_t)n);
+  const char *ws = static_cast<const char *>(plan);
+  const unsigned *k2 = reinterpret_cast<const unsigned *>(ws + a);
+  const int *v2 = reinterpret_cast<const int *>(ws + 3 * a);
+  const unsigned grid = (unsigned)((n + 15) / 16);
+#define BBGR_SEGMENTS(DD)                                                                        \
+  hipLaunchKernelGGL(scatter_segments_kernel<DD>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, \
+                     src, (long)ldsrc, src2, (long)ldsrc2, dst, (long)lddst, (unsigned)n_dst)
+  switch (d) {
+    case 8: BBGR_SEGMENTS(8); break;
+    case 16: BBGR_SEGMENTS(16); break;
+    case 32: BBGR_SEGMENTS(32); break;
+    case 64: BBGR_SEGMENTS(64); break;
+    case 128: BBGR_SEGMENTS(128); break;
+    default: BBGR_SEGMENTS(256); break;
+  }
+#undef BBGR_SEGMENTS
+  BBGR_LAUNCHED("scatter_segments_kernel");
+  return BBGR_OK;
+}
+
 extern "C" int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float *src,
                                      int64_t ldsrc, float *dst, int64_t lddst, int32_t d,
                                      int64_t n_dst, void *workspace, size_t *workspace_bytes,
@@ -680,15 +771,7 @@ extern "C" int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float 
     set_error("bbgr_scatter_add_rows: d = %d unsupported (8, 16, 32, 64, 128, 256)", d);
     return BBGR_ERR_UNSUPPORTED;
   }
-  int end_bit = 1;   // keys are in [0, n_dst] (n_dst marks skipped rows)
-  while (end_bit < 32 && (1ull << end_bit) <= (unsigned long long)n_dst) ++end_bit;
-  size_t temp = 0;
-  BBGR_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (unsigned *)nullptr,
-                                              (unsigned *)nullptr, (int *)nullptr,
-                                              (int *)nullptr, (int)(n > 0 ? n : 1), 0, end_bit,
-                                              as_stream(stream)));
-  const size_t a = align_up(4 * (size_t)(n > 0 ? n : 1));
-  const size_t need = 4 * a + align_up(temp);
+  const size_t need = scatter_plan_bytes(n, n_dst, nullptr, nullptr, as_stream(stream));
   if (!workspace) {
     *workspace_bytes = need;
     return BBGR_OK;
@@ -702,26 +785,10 @@ extern "C" int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float 
   BBGR_REQUIRE(aligned16(src) && aligned16(dst) && ldsrc >= d && lddst >= d &&
                    (ldsrc & 3) == 0 && (lddst & 3) == 0,
                "bbgr_scatter_add_rows: tables must be 16-byte aligned, ld >= d, ld % 4 == 0");
-  hipStream_t st = as_stream(stream);
-  char *ws = static_cast<char *>(workspace);
-  unsigned *k1 = reinterpret_cast<unsigned *>(ws), *k2 = reinterpret_cast<unsigned *>(ws + a);
-  int *v1 = reinterpret_cast<int *>(ws + 2 * a), *v2 = reinterpret_cast<int *>(ws + 3 * a);
-  hipLaunchKernelGGL(scatter_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                     (long)n, (const long *)idx, (long)n_dst, k1, v1);
-  BBGR_LAUNCHED("scatter_keys_kernel");
-  BBGR_HIP(hipcub::DeviceRadixSort::SortPairs(ws + 4 * a, temp, k1, k2, v1, v2, (int)n, 0,
-                                              end_bit, st));
-  const unsigned grid = (unsigned)((n + 15) / 16);
-  switch (d) {
-    case 8: hipLaunchKernelGGL(scatter_segments_kernel<8>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
-    case 16: hipLaunchKernelGGL(scatter_segments_kernel<16>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
-    case 32: hipLaunchKernelGGL(scatter_segments_kernel<32>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
-    case 64: hipLaunchKernelGGL(scatter_segments_kernel<64>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
-    case 128: hipLaunchKernelGGL(scatter_segments_kernel<128>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
-    default: hipLaunchKernelGGL(scatter_segments_kernel<256>, dim3(grid), dim3(256), 0, st, (long)n, k2, v2, src, (long)ldsrc, dst, (long)lddst, (unsigned)n_dst); break;
-  }
-  BBGR_LAUNCHED("scatter_segments_kernel");
-  return BBGR_OK;
+  size_t have = *workspace_bytes;
+  const int rc = bbgr_scatter_plan(n, idx, n_dst, workspace, &have, stream);
+  if (rc != BBGR_OK) return rc;
+  return bbgr_scatter_apply(n, n_dst, workspace, src, ldsrc, nullptr, 0, dst, lddst, d, stream);
 }
 
 extern "C" int bbgr_bpr(const bbgr_bpr_args *a, bbgr_stream_t stream) {

@@ -530,6 +530,21 @@ int bbgr_graph_rows(int64_t n, const int64_t *ids, int64_t n_rows, const int64_t
 int bbgr_scatter_add_rows(int64_t n, const int64_t *idx, const float *src, int64_t ldsrc,
                           float *dst, int64_t lddst, int32_t d, int64_t n_dst,
                           void *workspace, size_t *workspace_bytes, bbgr_stream_t stream);
+/* bbgr_scatter_add_rows in two halves (ABI 8), so one sort serves several  */
+/* scatters over the same index list (the drop-in backward scatters its     */
+/* item rows into two tables and its user rows twice).                      */
+/* bbgr_scatter_plan: the stable order of idx into `plan` (device; query    */
+/* plan_bytes with plan == NULL: bbgr_scatter_add_rows' workspace size).    */
+int bbgr_scatter_plan(int64_t n, const int64_t *idx, int64_t n_dst, void *plan,
+                      size_t *plan_bytes, bbgr_stream_t stream);
+/* bbgr_scatter_apply: dst[r, :d] += (the ascending sum over k with         */
+/* idx[k] == r of src[k, :d], continued over src2[k, :d] when src2 is not    */
+/* NULL), each row added once: bitwise bbgr_scatter_add_rows over the        */
+/* concatenation [src; src2] with the index list [idx; idx]. n, n_dst and    */
+/* idx as planned; the plan may be applied any number of times.             */
+int bbgr_scatter_apply(int64_t n, int64_t n_dst, const void *plan, const float *src,
+                       int64_t ldsrc, const float *src2, int64_t ldsrc2, float *dst,
+                       int64_t lddst, int32_t d, bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Credibility-GNN edge weights, main.py:677-701:       */

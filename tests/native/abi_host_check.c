@@ -126,6 +126,17 @@ int main(void) {
   expect_ok("ego_slots empty", bbgr_ego_slots(0, NULL, NULL, NULL, 4, 4, NULL, NULL, NULL, NULL,
                                               NULL, NULL, NULL, NULL));
   expect_error("graph_rows bad n", bbgr_graph_rows(-1, NULL, 4, NULL, NULL, NULL));
+  {
+    size_t sz = 0;
+    expect_error("scatter_plan no size", bbgr_scatter_plan(4, NULL, 4, NULL, NULL, NULL));
+    expect_error("scatter_plan bad n", bbgr_scatter_plan(-1, NULL, 4, NULL, &sz, NULL));
+  }
+  expect_error("scatter_apply bad d", bbgr_scatter_apply(4, 4, NULL, NULL, 8, NULL, 0, NULL, 8, 12,
+                                                         NULL));
+  expect_error("scatter_apply null", bbgr_scatter_apply(4, 4, NULL, NULL, 64, NULL, 0, NULL, 64, 64,
+                                                        NULL));
+  expect_ok("scatter_apply empty", bbgr_scatter_apply(0, 4, NULL, NULL, 64, NULL, 0, NULL, 64, 64,
+                                                      NULL));
   expect_error("graph_rows null", bbgr_graph_rows(4, NULL, 4, NULL, NULL, NULL));
   expect_ok("graph_rows empty", bbgr_graph_rows(0, NULL, 4, NULL, NULL, NULL));
   expect_error("rows_copy bad d", bbgr_rows_copy(4, NULL, f4, 64, f4, 64, 6, NULL));

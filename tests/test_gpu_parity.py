@@ -946,15 +946,19 @@ def test_rows_add_unique_is_bitwise_the_sorted_scatter(d):
                                       a.cpu().numpy().view(np.uint32))
 
 
-@pytest.mark.parametrize("d", [8, 16, 32, 64, 128, 256])
-def test_scatter_add_rows_matches_index_add(d):
+@pytest.mark.parametrize("d,n,n_dst", [(d, 20000, 700) for d in (8, 16, 32, 64, 128, 256)]
+                         + [(64, 16384, 700), (16, 16384, 1_000_000), (16, 8192, 5_000_000),
+                            (16, 4000, 300), (256, 600, 50), (64, 1, 3)])
+def test_scatter_add_rows_matches_index_add(d, n, n_dst):
     """bbgr_scatter_add_rows == numpy add.at (sequential ascending order) bit
-    for bit on a zero destination; invalid indices skipped; repeatable."""
+    for bit on a zero destination; invalid indices skipped; repeatable; from
+    one row to 20000, onto tables of up to 5M rows."""
     from bbgr.scatter import index_add_rows
-    rng = np.random.default_rng(d)
-    n, n_dst = 20000, 700
+    rng = np.random.default_rng(d + n)
     idx = rng.integers(-3, n_dst + 3, n)          # duplicates + out-of-range rows
-    idx[:500] = 5                                 # one long run
+    if n_dst > 100_000:                           # a batch's rows: Zipf-like repeats
+        idx = np.minimum(rng.zipf(1.3, n) - 1, n_dst + 2)
+    idx[:min(500, n // 2)] = 5                    # one long run
     src = rng.normal(size=(n, d)).astype(np.float32)
     want = np.zeros((n_dst, d), np.float32)
     ok = (idx >= 0) & (idx < n_dst)
@@ -968,6 +972,42 @@ def test_scatter_add_rows_matches_index_add(d):
     np.testing.assert_array_equal(got2, got3)
     empty = index_add_rows(t(base), torch.empty(0, dtype=torch.int64, device=DEV), t(src))
     np.testing.assert_array_equal(empty.cpu().numpy(), base)
+
+
+@pytest.mark.parametrize("d,n,n_dst", [(64, 16384, 1_000_000), (16, 3000, 200), (256, 5, 3)])
+def test_scatter_plan_applies_like_the_concatenated_scatter(d, n, n_dst):
+    """bbgr_scatter_plan + bbgr_scatter_apply: one sort applied to two tables
+    gives bbgr_scatter_add_rows' bits each time, and with a second source it
+    equals the scatter of [src; src2] over [idx; idx] bit for bit (the drop-in
+    backward's item gradient: BPR rows, then ego rows, one sum per item)."""
+    import ctypes
+    from bbgr import _lib
+    from bbgr.scatter import index_add_rows
+    rng = np.random.default_rng(n + d)
+    idx = np.minimum(rng.zipf(1.2, n) - 1, n_dst + 1)   # repeats + out-of-range rows
+    idx[: n // 3] = rng.integers(-2, n_dst + 2, n // 3)
+    src = rng.normal(size=(n, d)).astype(np.float32)
+    src2 = rng.normal(size=(n, d)).astype(np.float32)
+    src2[::3] = 0.0
+    di, ds, ds2 = t(idx, torch.int64), t(src), t(src2)
+    need = ctypes.c_size_t(0)
+    _lib.call("bbgr_scatter_plan", n, _lib.ptr(di), n_dst, None, ctypes.byref(need),
+              _lib.stream_handle())
+    plan = torch.empty(max(need.value, 1), dtype=torch.uint8, device=DEV)
+    _lib.call("bbgr_scatter_plan", n, _lib.ptr(di), n_dst, _lib.ptr(plan), ctypes.byref(need),
+              _lib.stream_handle())
+    base = rng.normal(size=(n_dst, d)).astype(np.float32)
+    for s2 in (None, ds2):
+        want = index_add_rows(t(base), di if s2 is None else torch.cat([di, di]),
+                              ds if s2 is None else torch.cat([ds, ds2]))
+        for _ in range(2):   # the plan is reusable
+            got = t(base)
+            _lib.call("bbgr_scatter_apply", n, n_dst, _lib.ptr(plan), _lib.ptr(ds), d,
+                      None if s2 is None else _lib.ptr(s2), d, _lib.ptr(got), d, d,
+                      _lib.stream_handle())
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32),
+                                          want.cpu().numpy().view(np.uint32))
 
 
 def test_training_step_is_bitwise_reproducible():
