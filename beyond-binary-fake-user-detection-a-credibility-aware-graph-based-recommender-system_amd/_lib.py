@@ -91,6 +91,7 @@ class SpmmArgs(ctypes.Structure):
         ("acc_in_map", c_void_p),
         ("adam_grad", c_void_p), ("adam_grad_ld", c_int64), ("adam_grad_scale", c_float),
         ("adam_map", c_void_p),
+        ("adam_moments_unmapped", c_int32),
     ]
 
 
@@ -244,7 +245,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 8:
+        if handle.bbgr_abi_version() != 9:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

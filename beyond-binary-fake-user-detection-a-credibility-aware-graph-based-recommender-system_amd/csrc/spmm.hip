@@ -86,6 +86,7 @@ struct SpmmParams {
   long adam_g_ld;
   float adam_g_scale;
   const int *adam_map;         // the fused Adam's row map (args.adam_map; NULL: y_map's)
+  int adam_mrow;               // moments at the launch row (args.adam_moments_unmapped)
 };
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -600,13 +601,13 @@ __device__ __forceinline__ AdamConsts launch_adam_consts(const SpmmParams &P) {
 }
 
 template <int D>
-__device__ __forceinline__ void adam_row(const SpmmParams &P, long row, int lane,
+__device__ __forceinline__ void adam_row(const SpmmParams &P, long row, long mrow, int lane,
                                          const float4 (&G)[RowShape<D>::V]) {
   constexpr int V = RowShape<D>::V;
   const AdamConsts ac = launch_adam_consts(P);
   float4 *pp = reinterpret_cast<float4 *>(P.adam_p + (long)row * P.adam_ld) + lane;
-  float4 *pm = reinterpret_cast<float4 *>(P.adam_m + (long)row * P.adam_ld) + lane;
-  float4 *pv = reinterpret_cast<float4 *>(P.adam_v + (long)row * P.adam_ld) + lane;
+  float4 *pm = reinterpret_cast<float4 *>(P.adam_m + (long)mrow * P.adam_ld) + lane;
+  float4 *pv = reinterpret_cast<float4 *>(P.adam_v + (long)mrow * P.adam_ld) + lane;
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     const bool ntm = P.nt_out_from != 0x7fffffff;   // moments: streamed once per step
@@ -659,6 +660,7 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
       }
     }
     const long ra_ = P.adam_map ? (long)P.adam_map[row] : ry;   // the Adam's rows
+    const long rm_ = P.adam_mrow ? (long)row : ra_;                // its moments' rows
     if (P.adam_p && P.adam_g) {   // Adam of another table riding on this row write
       const float4 *gr = reinterpret_cast<const float4 *>(P.adam_g + ra_ * P.adam_g_ld) + lane;
       float4 Ga[V];
@@ -668,9 +670,9 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
         Ga[k] = make_float4(P.adam_g_scale * g4.x, P.adam_g_scale * g4.y,
                             P.adam_g_scale * g4.z, P.adam_g_scale * g4.w);
       }
-      adam_row<D>(P, ra_, lane, Ga);
+      adam_row<D>(P, ra_, rm_, lane, Ga);
     } else if (P.adam_p) {
-      adam_row<D>(P, ra_, lane, G);
+      adam_row<D>(P, ra_, rm_, lane, G);
     }
   }
   const long rc = P.acc_map ? (long)P.acc_map[row] : (long)row;
@@ -1240,6 +1242,7 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.adam_g_ld = a->adam_grad_ld;
   P.adam_g_scale = a->adam_grad_scale;
   P.adam_map = a->adam_map;
+  P.adam_mrow = a->adam_moments_unmapped != 0;
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {

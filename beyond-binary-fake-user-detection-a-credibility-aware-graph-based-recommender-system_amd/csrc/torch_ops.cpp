@@ -163,6 +163,7 @@ struct AdamTable {
   Tensor p, m, v;
   float lr = 1e-3f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, wd = 0.f;
   float bc1 = 1.f, bc2s = 1.f;
+  bool moments_graph = false;   // m, v in the graph's row order (adam_moments_unmapped)
 };
 
 struct Opts {
@@ -254,6 +255,7 @@ static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) 
     a.adam_grad_ld = o.adam_grad_ld;
     a.adam_grad_scale = o.adam_grad_scale;
     a.adam_map = o.adam_map;
+    a.adam_moments_unmapped = A.moments_graph ? 1 : 0;
   }
   // input-order source rows carry no hot prefix; mapped output rows neither
   a.stream_from = o.src_input ? 0 : pr.stream_from(d);
@@ -1314,7 +1316,8 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
                                    int64_t key, int64_t K, const Tensor &m_u, const Tensor &v_u,
                                    const Tensor &m_i, const Tensor &v_i, double lr, double beta1,
                                    double beta2, double eps, double wd, double bc1_u,
-                                   double bc2s_u, double bc1_i, double bc2s_i) {
+                                   double bc2s_u, double bc1_i, double bc2s_i,
+                                   bool moments_graph) {
   auto P = pair_of(key);
   TORCH_CHECK(K >= 2, "bpr_adam_backward: the in-backward Adam needs num_layers >= 2");
   const int64_t d = u0.size(1), U = P->U, I = P->I;
@@ -1345,6 +1348,10 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
                       (float)bc1_u, (float)bc2s_u};
   sa.item = AdamTable{i0, m_i, v_i, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
                       (float)bc1_i, (float)bc2s_i};
+  // moments in the graph's row order: only the caller-order weight rows are
+  // read and written through the row maps (an input-order pair; otherwise the
+  // two orders are one)
+  sa.user.moments_graph = sa.item.moments_graph = moments_graph && P->io;
   sa.ego_u_vals = at::mul(ru, kp1);
   // the item gradient / gl: the BPR rows, then the ego rows, per item in
   // ascending source order
@@ -1789,7 +1796,7 @@ TORCH_LIBRARY(bbgr, m) {
         "Tensor users, Tensor pos, Tensor neg, float reg, int pair_key, int num_layers, "
         "Tensor(c!) m_u, Tensor(d!) v_u, Tensor(e!) m_i, Tensor(f!) v_i, float lr, float beta1, "
         "float beta2, float eps, float weight_decay, float bc1_u, float bc2s_u, float bc1_i, "
-        "float bc2s_i) -> ()");
+        "float bc2s_i, bool moments_graph=False) -> ()");
   m.def("_register_pair(int key, Tensor?[] tensors, int[] meta) -> ()",
         &bbgr_torch::register_pair);
   m.def("_unregister_pair(int key) -> ()", &bbgr_torch::unregister_pair);

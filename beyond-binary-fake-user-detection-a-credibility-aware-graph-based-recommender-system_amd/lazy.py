@@ -43,7 +43,7 @@ class _Pending:
     def __init__(self, full_fn, rows_fn, u0: torch.Tensor, i0: torch.Tensor, step=None):
         self.full_fn, self.rows_fn = full_fn, rows_fn
         self.u0, self.i0 = u0, i0
-        self.step = step   # (pair_key, num_layers) of a GS chain: the in-backward Adam
+        self.step = step   # (pair_key, num_layers, row maps or None) of a GS chain: the in-backward Adam
         self.version = (u0._version, i0._version)
         self.grad = torch.is_grad_enabled()
         self.out = None
@@ -180,7 +180,7 @@ class _BprAdamStep(torch.autograd.Function):
     def backward(ctx, g):
         from . import ops
         uf, itf, u0, i0, users, pos, neg = ctx.saved_tensors
-        key, K = ctx.chain
+        key, K, maps = ctx.chain
 
         def run(states, group, corr):
             su, si = states
@@ -190,9 +190,11 @@ class _BprAdamStep(torch.autograd.Function):
                                   si["exp_avg"], si["exp_avg_sq"], float(group["lr"]),
                                   float(b1), float(b2), float(group["eps"]),
                                   float(group["weight_decay"]), corr[0][0], corr[0][1],
-                                  corr[1][0], corr[1][1])
+                                  corr[1][0], corr[1][1], maps is not None)
 
-        ctx.opt.step_in_backward([u0, i0], run)
+        # an input-order pair: the moments live in the graph's row order
+        # (FusedAdam converts them once, and back at its state_dict boundary)
+        ctx.opt.step_in_backward([u0, i0], run, row_maps=maps)
         return (None,) * 8
 
 

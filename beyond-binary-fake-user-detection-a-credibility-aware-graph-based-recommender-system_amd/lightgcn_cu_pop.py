@@ -82,7 +82,8 @@ class LightGCN(torch.nn.Module):
             return _lazy.deferred_pair(
                 lambda: _propagate(pair, u0, i0, K, ORDER_GS),
                 lambda users, items: _propagate_rows(pair, u0, i0, K, ORDER_GS, users, items),
-                u0, i0, step=(pair_key(pair), K))
+                u0, i0, step=(pair_key(pair), K,
+                              (pair.io.user_map64, pair.io.item_map64) if pair.io else None))
         return _propagate(pair, u0, i0, K, ORDER_GS)
 
     def get_user_item_emb(self):

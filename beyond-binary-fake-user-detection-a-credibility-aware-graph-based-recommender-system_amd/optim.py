@@ -164,7 +164,14 @@ class FusedAdam(torch.optim.Optimizer):
     step: Version-2/lighgcn_cu_pop.py:861-863) runs unchanged. Each backward
     through bpr_loss is one optimizer step. The update equals the separate
     step's up to rounding: the ego-L2 rows join the gradient before the last
-    products' epilogues, not after them (FusedTrainer's order)."""
+    products' epilogues, not after them (FusedTrainer's order).
+
+    On a degree-ordered drop-in graph (the default) the in-backward step keeps
+    those two tables' exp_avg / exp_avg_sq in the graph's row order, so the
+    fused epilogue streams them and reads only the weight rows through the row
+    map. The optimizer converts them once, and back wherever they leave it:
+    state_dict(), moments(), and a step() that updates them outside the
+    backward. load_state_dict() takes the caller's order, as torch's Adam."""
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, fuse_backward: bool = False):
@@ -173,6 +180,9 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.fuse_backward = bool(fuse_backward)
         self._stepped: set = set()   # ids of parameters stepped in the last backward
+        # id(param) -> map[graph row] = caller row: its moments are held in the
+        # graph's row order (in-backward steps on an input-order drop-in pair)
+        self._graph_rows: dict = {}
         if self.fuse_backward:
             import weakref
             me = weakref.ref(self)
@@ -195,19 +205,80 @@ class FusedAdam(torch.optim.Optimizer):
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return st
 
+    def _to_caller_rows(self, p) -> None:
+        """Moments of p back in the caller's row order (if held in the graph's)."""
+        m = self._graph_rows.pop(id(p), None)
+        if m is None:
+            return
+        st = self.state[p]
+        for k in ("exp_avg", "exp_avg_sq"):
+            out = torch.empty_like(st[k])
+            out.index_copy_(0, m, st[k])   # caller row m[r] <- graph row r
+            st[k] = out
+
+    def _to_graph_rows(self, p, m) -> None:
+        """Moments of p in the graph's row order of map m (m[graph row] = caller row)."""
+        have = self._graph_rows.get(id(p))
+        if have is m:
+            return
+        self._to_caller_rows(p)
+        st = self.state[p]
+        for k in ("exp_avg", "exp_avg_sq"):
+            st[k] = st[k].index_select(0, m)
+        self._graph_rows[id(p)] = m
+
+    def moments(self, p):
+        """(exp_avg, exp_avg_sq) of p in the caller's row order (copies when
+        they are held in the graph's)."""
+        st = self.state[p]
+        m = self._graph_rows.get(id(p))
+        if m is None:
+            return st["exp_avg"], st["exp_avg_sq"]
+        out = []
+        for k in ("exp_avg", "exp_avg_sq"):
+            t = torch.empty_like(st[k])
+            t.index_copy_(0, m, st[k])
+            out.append(t)
+        return tuple(out)
+
+    def state_dict(self):
+        """torch's state_dict, moments in the caller's row order."""
+        sd = super().state_dict()
+        if self._graph_rows:
+            index = {}
+            for g, gs in zip(self.param_groups, sd["param_groups"]):
+                index.update(zip((id(p) for p in g["params"]), gs["params"]))
+            for g in self.param_groups:
+                for p in g["params"]:
+                    if id(p) in self._graph_rows:
+                        entry = dict(sd["state"][index[id(p)]])
+                        entry["exp_avg"], entry["exp_avg_sq"] = self.moments(p)
+                        sd["state"][index[id(p)]] = entry
+        return sd
+
+    def load_state_dict(self, state_dict):
+        self._graph_rows.clear()   # a loaded state is in the caller's order
+        super().load_state_dict(state_dict)
+
     @torch.no_grad()
-    def step_in_backward(self, params, run) -> None:
+    def step_in_backward(self, params, run, row_maps=None) -> None:
         """One Adam step of `params` (one param group) carried out by `run(states,
         group, corrections)` inside a backward pass: the step counts advance,
         corrections = [(1 - beta1^t, sqrt(1 - beta2^t)) per parameter] (host
-        double, as adam_step), and step() then skips these parameters."""
+        double, as adam_step), and step() then skips these parameters.
+        row_maps (one int64 map per parameter, map[graph row] = caller row):
+        `run` takes the moments in the graph's row order."""
         g = self._group_of(params)
         if g is None:
             raise RuntimeError("FusedAdam.step_in_backward: parameters not in one group")
         b1, b2 = g["betas"]
         states, corr = [], []
-        for p in params:
+        for i, p in enumerate(params):
             st = self._init_state(p)
+            if row_maps is not None:
+                self._to_graph_rows(p, row_maps[i])
+            else:
+                self._to_caller_rows(p)
             st["step"] += 1
             t = int(st["step"].item())
             states.append(st)
@@ -233,6 +304,7 @@ class FusedAdam(torch.optim.Optimizer):
                     continue
                 _lib.require_gpu(p)
                 st = self._init_state(p)
+                self._to_caller_rows(p)
                 st["step"] += 1
                 adam_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"],
                           int(st["step"].item()), group["lr"], b1, b2, group["eps"],

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 8
+#define BBGR_ABI_VERSION 9
 
 typedef enum {
   BBGR_OK = 0,
@@ -281,6 +281,11 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   exp_avg, exp_avg_sq and adam_grad) of CSR row r are row adam_map[r]      */
 /*   instead of y_map's: a product that writes y in the graph's order while  */
 /*   the weights live in the caller's (the drop-in's in-backward item Adam). */
+/* adam_moments_unmapped (ABI 9): nonzero keeps exp_avg / exp_avg_sq at the  */
+/*   launch's own row r (the graph's order) while the param and adam_grad    */
+/*   follow adam_map: the drop-in optimizer stores its moments in the graph's */
+/*   order, so only the caller-order weight row is read and written at       */
+/*   random (bbgr.optim.FusedAdam converts them at its state_dict boundary). */
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
@@ -344,6 +349,7 @@ typedef struct {
   int64_t adam_grad_ld;
   float adam_grad_scale;
   const int32_t *adam_map;
+  int32_t adam_moments_unmapped;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,

@@ -161,9 +161,8 @@ def test_fused_backward_adam_matches_the_separate_step(module):
         if k == 0:
             assert ls[0] == ls[1]
             for pa, pb in zip(a.parameters(), b.parameters()):
-                for key in ("exp_avg", "exp_avg_sq"):
-                    x, y = oa.state[pa][key], ob.state[pb][key]
-                    assert float((x - y).norm() / y.norm()) < 1e-6, key
+                for x, y in zip(oa.moments(pa), ob.moments(pb)):
+                    assert float((x - y).norm() / y.norm()) < 1e-6
         else:
             assert abs(ls[0] - ls[1]) <= 1e-6 * abs(ls[1])
     for pa, pb, p0 in zip(a.parameters(), b.parameters(), w0):
@@ -192,3 +191,50 @@ def test_fused_backward_adam_falls_back_where_it_does_not_apply():
     c.bpr_loss(*batches[0], uf, itf, 1e-4).backward()
     assert c.user_emb.weight.grad is not None and c.item_emb.weight.grad is not None
     oc.step()
+
+
+def test_fused_backward_adam_moments_leave_in_the_callers_order():
+    """On the degree-ordered drop-in graph the in-backward step holds the two
+    tables' moments in the graph's row order (the fused epilogue streams them,
+    only the weight rows go through the row map). state_dict() and moments()
+    hand them out in the caller's order: after one step they equal the
+    separate step's within 1e-6; a step() outside the backward (a loss that
+    read the whole tables) converts them back and continues; a loaded state
+    dict restarts in the caller's order and round-trips."""
+    from bbgr.optim import FusedAdam
+    a, b = _model(3), _model(3)
+    oa = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
+    ob = FusedAdam(b.parameters(), lr=1e-3)
+    users, pos, neg = _batch(0)
+    for m, o in ((a, oa), (b, ob)):
+        uf, itf = m.get_user_item_emb()
+        o.zero_grad()
+        m.bpr_loss(users, pos, neg, uf, itf, 1e-4).backward()
+        o.step()
+    assert len(oa._graph_rows) == 2 and not ob._graph_rows
+    sa, sb = oa.state_dict(), ob.state_dict()
+    for k in sa["state"]:
+        for key in ("exp_avg", "exp_avg_sq"):
+            x, y = sa["state"][k][key], sb["state"][k][key]
+            assert float((x - y).norm() / y.norm()) < 1e-6, key
+    # the internal tables are still graph-ordered (state_dict made copies)
+    pa = next(a.parameters())
+    assert not torch.equal(oa.state[pa]["exp_avg"], oa.moments(pa)[0])
+    users, pos, neg = _batch(1)
+    for m, o in ((a, oa), (b, ob)):
+        uf, itf = m.get_user_item_emb()
+        uf[0]   # the whole tables: bpr_loss takes the usual path, step() steps
+        o.zero_grad()
+        m.bpr_loss(users, pos, neg, uf, itf, 1e-4).backward()
+        assert all(p.grad is not None for p in m.parameters())
+        o.step()
+    assert not oa._graph_rows
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert int(oa.state[pa]["step"]) == 2
+        assert float((pa - pb).norm() / pb.norm()) < 1e-5
+        for x, y in zip(oa.moments(pa), ob.moments(pb)):
+            assert float((x - y).norm() / y.norm()) < 1e-5
+    oc = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
+    oc.load_state_dict(oa.state_dict())
+    for pa in a.parameters():
+        assert all(torch.equal(x, y) for x, y in zip(oc.moments(pa), oa.moments(pa)))
