@@ -747,13 +747,32 @@ def main():
         todo.append((other, xp))
         if other == "users" and args.chain_beside and inline_xp is not None:
             todo.append(("users", inline_xp))
+    beside_errors = []
     for part, xq in todo:
-        trainer.close()
-        del trainer
+        if trainer is not None:
+            trainer.close()
+        trainer = None
         torch.cuda.empty_cache()
-        trainer = build(part, xq)
-        r = measure(trainer, part, args.dense_check)
-        r["xp"] = xq
+        # a beside run that fails on every rank alike (an RCCL communicator
+        # that will not come up, memory) is reported, not fatal: the ranks
+        # agree on it and the line keeps the runs that finished
+        try:
+            if os.environ.get("BBGR_BENCH_FAIL_BESIDE") == part:   # the error path's test
+                raise RuntimeError("injected beside failure")
+            trainer = build(part, xq)
+            r = measure(trainer, part, args.dense_check)
+            r["xp"] = xq
+            ok = 1.0
+        except Exception as ex:   # noqa: BLE001
+            ok, err = 0.0, f"{part} ({chain_mode(xq) if part == 'users' else 'columns'}): " \
+                           f"{type(ex).__name__}: {ex}"[:400]
+            log(f"[bench] rank {rank}: beside run failed: {err}")
+        if _allreduce(ok, dev, torch.distributed.ReduceOp.MIN) < 1.0:
+            beside_errors.append(err if ok < 1.0 else f"{part}: failed on another rank")
+            if trainer is not None:
+                trainer.close()
+            trainer = None
+            continue
         runs.append(r)
     # every rank holds the same max-over-ranks times: the same choice everywhere
     res = min(runs, key=lambda r: r["elapsed"])
@@ -796,7 +815,8 @@ def main():
     dense_ms, frontier_on = res["dense_ms"], res["frontier_on"]
     if dist_mode:
         del edges   # the cpu_baseline leg (rank 0, N=1 only) is the only later user
-        trainer.close()                    # the native exchange's communicator, if any
+        if trainer is not None:
+            trainer.close()                # the native exchange's communicator, if any
     groups = roofline_groups(timer, counts, timer_steps, count_steps, I)
     weak_beside = None
     if world > 1 and not weak and args.weak_beside > 0 and not sharded_gen:
@@ -804,7 +824,14 @@ def main():
         # every rank a full config-sized user shard over the shared items
         del trainer
         torch.cuda.empty_cache()
-        weak_beside = measure_weak(args, cfg, rank, world, dev, xp, frontier)
+        try:
+            weak_beside, ok = measure_weak(args, cfg, rank, world, dev, xp, frontier), 1.0
+        except Exception as ex:   # noqa: BLE001
+            ok, err = 0.0, f"weak: {type(ex).__name__}: {ex}"[:400]
+            log(f"[bench] rank {rank}: weak beside run failed: {err}")
+        if _allreduce(ok, dev, torch.distributed.ReduceOp.MIN) < 1.0:
+            weak_beside = None
+            beside_errors.append(err if ok < 1.0 else "weak: failed on another rank")
     # the dominant kernel: full-CSR item<-user products (spmm_kernel)
     dom = [g for g in groups if g["kind"] == "full" and g["side"] == "item<-user"]
     dom_n = sum(g["launches_per_step"] for g in dom)
@@ -916,6 +943,7 @@ def main():
         "dropin_backward_adam_step": dropin_bwd,
         "weak_beside": weak_beside,
         "partition_beside": partition_beside,
+        "beside_errors": beside_errors or None,
         "chain_beside": chain_beside,
         "partition": ("columns" if columns else "users") if dist_mode else
                      (f"one column shard of {emulate}" if emulate else "single GPU"),

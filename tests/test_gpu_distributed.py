@@ -248,6 +248,26 @@ def test_bench_two_ranks_on_c2(tmp_path, partition):
     assert j["partition_beside"] is None
 
 
+def test_bench_two_ranks_survives_a_failed_beside_run(tmp_path):
+    """A beside run that fails on every rank (here injected into the user-row
+    runs: an RCCL communicator that will not come up would fail the same way)
+    does not cost the line: the ranks agree on it, the line is the run that
+    finished, and the failures are listed in beside_errors."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "2",
+           "--warmup", "1", "--dense-check", "0", "--frontier", "on", "--weak-beside", "0",
+           "--partition", "columns"]
+    env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo",
+               BBGR_BENCH_FAIL_BESIDE="users")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    j = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert j["partition"] == "columns" and j["value"] > 0
+    assert j["partition_beside"] is None and j["chain_beside"] is None
+    assert len(j["beside_errors"]) == 2 and all("injected" in e for e in j["beside_errors"])
+
+
 def test_bench_sharded_single_rank_with_inline_collectives(tmp_path):
     """bench.py's user-row step at world size 1 over RCCL (--sharded) with
     every collective inline on the compute stream (--native-comm inline): one
