@@ -1,9 +1,10 @@
 """GPU: the reference's training loops, end to end, over several steps.
 
 Each family's loop — Version-2/lighgcn_cu_pop.py:786-863 (GS, pop-mix
-negatives), lightgcn_cu.py:586-652 (Jacobi, uniform negatives, the
-credibility-fair loss written inline) and lightgcn.py:540-590 (symmetric
-adjacency, uniform negatives): the operators, the model, torch's Adam, the
+negatives), version_1/lightgcn_cu_pop_long_tail_exposure.py:630-685 (Method
+A: popularity-damped GS, uniform negatives), lightgcn_cu.py:586-652 (Jacobi,
+uniform negatives, the credibility-fair loss written inline) and
+lightgcn.py:540-590 (symmetric adjacency, uniform negatives): the operators, the model, torch's Adam, the
 seeded numpy stream, the per-epoch shuffle of the train users, the per-user
 sampler loop and the step — runs twice on the C1 graph:
 
@@ -31,6 +32,7 @@ from bbgr import host_sampler as HS  # noqa: E402
 from bbgr import lightgcn as SYM  # noqa: E402
 from bbgr import lightgcn_cu as CU  # noqa: E402
 from bbgr import lightgcn_cu_pop as V2  # noqa: E402
+from bbgr import lightgcn_cu_pop_long_tail_exposure as MA  # noqa: E402
 from bbgr.synthetic import CONFIGS, config_edges, synthetic_credibility  # noqa: E402
 from oracle import ref_numpy as R  # noqa: E402
 from oracle import ref_torch as T  # noqa: E402
@@ -62,6 +64,23 @@ def _v2(e, U, I, d, K, cred, optimizer, lr):
     if optimizer == "fused_backward":
         from bbgr.optim import FusedAdam
         return ref, m, tables, step, lambda ps: FusedAdam(ps, lr=lr, fuse_backward=True)
+    return ref, m, tables, step, None
+
+
+def _method_a(e, U, I, d, K, cred, optimizer, lr):
+    """version_1/lightgcn_cu_pop_long_tail_exposure.py:630-685: Version-2's
+    model on the popularity-damped operators, uniform negatives."""
+    torch.manual_seed(42)
+    Tui, Tiu = T.gs_operators(e, U, I, cred, method_a=True)
+    ref = T.GSModel(U, I, d, K, Tui, Tiu)
+    M_ui, M_iu = MA.build_message_passing_mats(e, U, I, torch.as_tensor(cred), DEV)
+    m = MA.LightGCN(U, I, d, K, M_ui, M_iu).to(DEV)
+    tables = {"user_emb": (m.user_emb, ref.user_emb), "item_emb": (m.item_emb, ref.item_emb)}
+
+    def step(users_t, pos_t, neg_t, reg):
+        user_emb, item_emb = m.get_user_item_emb()
+        return m.bpr_loss(users_t, pos_t, neg_t, user_emb, item_emb, reg)
+
     return ref, m, tables, step, None
 
 
@@ -98,11 +117,13 @@ def _sym(e, U, I, d, K, cred, optimizer, lr):
     return ref, m, tables, step, None
 
 
-FAMILIES = {"v2_pop": (_v2, True), "cu_fair": (_cu, False), "plain": (_sym, False)}
+FAMILIES = {"v2_pop": (_v2, True), "method_a": (_method_a, False), "cu_fair": (_cu, False),
+            "plain": (_sym, False)}
 
 
 @pytest.mark.parametrize("family,optimizer", [("v2_pop", "torch"), ("v2_pop", "fused_backward"),
-                                              ("cu_fair", "torch"), ("plain", "torch")])
+                                              ("method_a", "torch"), ("cu_fair", "torch"),
+                                              ("plain", "torch")])
 def test_reference_training_loop_two_epochs(family, optimizer):
     c = CONFIGS["C1"]
     U, I, d, K = c["num_users"], c["num_items"], c["emb_dim"], c["num_layers"]
