@@ -165,3 +165,83 @@ def evaluate_full(user_emb: torch.Tensor, item_emb: torch.Tensor, train_csr: Csr
         results["_raw"] = dict(users=users, topk=topk.view(n, max(Ks)),
                                topk_score=topk_score.view(n, max(Ks)), groups=groups)
     return results
+
+
+# -- the reference scripts' evaluate_* signatures ------------------------------
+# Version-2/lighgcn_cu_pop.py:536-752 take (model, train_csr, test_csr,
+# num_items, device, item_pop, total_train_interactions, cred_np) with host
+# (indptr, indices) CSRs from edges_to_user_csr and read cfg.Ks /
+# cfg.sampled_negatives / cfg.cred_group_pct / cfg.seed; the older scripts
+# (version_1/*.py:486-610, lightgcn_cu.py:488-560, lightgcn.py:398-520) take
+# the first five only and return precision / recall / ndcg per K. The
+# wrappers below keep those signatures (the cfg fields as keyword arguments
+# with the reference's defaults) and return the same dictionaries. Sampled
+# candidates are drawn on the device (Philox), not from the host Generator.
+_V1_KEYS = ("precision", "recall", "ndcg", "users_eval", "mode")
+
+
+def csr_from_host(csr, n_cols: int, device) -> Csr:
+    """A host (indptr, indices) CSR (edges_to_user_csr) as a device Csr."""
+    indptr, indices = csr
+    indptr = np.asarray(indptr, dtype=np.int64)
+    n_rows = indptr.size - 1
+    rows = np.repeat(np.arange(n_rows, dtype=np.int32), np.diff(indptr))
+    return Csr(rows, np.asarray(indices).astype(np.int32), n_rows, n_cols, device)
+
+
+def _model_tables(model, device):
+    """The final tables as each reference evaluate_* reads them:
+    final_embeddings() (CredLightGCN, lightgcn_cu.py:492) or get_user_item_emb()."""
+    with torch.no_grad():
+        if hasattr(model, "final_embeddings"):
+            ue, ie = model.final_embeddings()
+        else:
+            ue, ie = model.get_user_item_emb()
+        dev = torch.device(device)
+        return ue.to(dev), ie.to(dev)
+
+
+def _host_defaults(train_csr, num_items, n_users):
+    """item_pop / total interactions / credibility for the five-argument
+    scripts, whose results carry none of the metrics they feed."""
+    pop = np.bincount(np.asarray(train_csr[1], np.int64), minlength=num_items)
+    return pop.astype(np.float32), int(pop.sum()), np.ones(n_users, np.float32)
+
+
+def evaluate_sampled_reference(model, train_csr, test_csr, num_items: int, device,
+                               item_pop=None, total_train_interactions=None, cred_np=None, *,
+                               Ks=(10, 20), sampled_negatives: int = 99,
+                               cred_group_pct: float = 0.20, seed: int = 42):
+    """evaluate_sampled with the reference scripts' signature (see above)."""
+    ue, ie = _model_tables(model, device)
+    v1 = item_pop is None
+    if v1:
+        item_pop, total_train_interactions, cred_np = _host_defaults(train_csr, num_items,
+                                                                     ue.shape[0])
+    tr = csr_from_host(train_csr, num_items, ue.device)
+    te = csr_from_host(test_csr, num_items, ue.device)
+    res = evaluate_sampled(ue, ie, tr, te, num_items, item_pop, total_train_interactions,
+                           cred_np, Ks=Ks, sampled_negatives=sampled_negatives,
+                           cred_group_pct=cred_group_pct, seed=seed + 999)
+    if v1:
+        res = {K: {**{k: r[k] for k in _V1_KEYS}, "negatives": r["negatives"]}
+               for K, r in res.items()}
+    return res
+
+
+def evaluate_full_ranking_reference(model, train_csr, test_csr, num_items: int, device,
+                                    item_pop=None, total_train_interactions=None, cred_np=None,
+                                    *, Ks=(10, 20), cred_group_pct: float = 0.20):
+    """evaluate_full_ranking with the reference scripts' signature (see above)."""
+    ue, ie = _model_tables(model, device)
+    v1 = item_pop is None
+    if v1:
+        item_pop, total_train_interactions, cred_np = _host_defaults(train_csr, num_items,
+                                                                     ue.shape[0])
+    tr = csr_from_host(train_csr, num_items, ue.device)
+    te = csr_from_host(test_csr, num_items, ue.device)
+    res = evaluate_full(ue, ie, tr, te, num_items, item_pop, total_train_interactions, cred_np,
+                        Ks=Ks, cred_group_pct=cred_group_pct)
+    if v1:
+        res = {K: {k: r[k] for k in _V1_KEYS} for K, r in res.items()}
+    return res

@@ -63,3 +63,17 @@ class LightGCN(torch.nn.Module):
         W = self.emb.weight
         return _bpr.bpr_loss(users, pos_items, neg_items, user_emb, item_emb,
                              W[: self.num_users], W[self.num_users:], reg_weight)
+
+
+def evaluate_sampled(model, train_csr, test_csr, num_items: int, device: str, **cfg):
+    """lightgcn.py:397-457 (same arguments; precision / recall / ndcg per K):
+    bbgr.evaluation.evaluate_sampled, candidates drawn on the device."""
+    from .evaluation import evaluate_sampled_reference
+    return evaluate_sampled_reference(model, train_csr, test_csr, num_items, device, **cfg)
+
+
+def evaluate_full_ranking(model, train_csr, test_csr, num_items: int, device: str, **cfg):
+    """lightgcn.py:459-520 (same arguments; precision / recall / ndcg per K):
+    bbgr.evaluation.evaluate_full."""
+    from .evaluation import evaluate_full_ranking_reference
+    return evaluate_full_ranking_reference(model, train_csr, test_csr, num_items, device, **cfg)

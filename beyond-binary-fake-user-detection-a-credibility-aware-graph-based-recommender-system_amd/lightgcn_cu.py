@@ -103,4 +103,11 @@ def _propagate_one(pair: OperatorPair, u: torch.Tensor, i: torch.Tensor):
     return ops.jacobi_layer(u, i, ops.pair_key(pair))
 
 
-__all__ = ["build_cred_weighted_mats", "CredLightGCN"]
+__all__ = ["build_cred_weighted_mats", "CredLightGCN", "evaluate_sampled"]
+
+
+def evaluate_sampled(model, train_csr, test_csr, num_items: int, device: str, **cfg):
+    """lightgcn_cu.py:487-547 (same arguments; precision / recall / ndcg per K):
+    bbgr.evaluation.evaluate_sampled, candidates drawn on the device."""
+    from .evaluation import evaluate_sampled_reference
+    return evaluate_sampled_reference(model, train_csr, test_csr, num_items, device, **cfg)

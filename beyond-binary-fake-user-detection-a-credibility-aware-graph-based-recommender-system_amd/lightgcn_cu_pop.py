@@ -100,3 +100,24 @@ class LightGCN(torch.nn.Module):
             user_emb, item_emb, users, pos_items, neg_items)
         return _bpr.bpr_loss(users, pos_items, neg_items, user_emb, item_emb,
                              self.user_emb.weight, self.item_emb.weight, reg_weight)
+
+
+def evaluate_sampled(model, train_csr, test_csr, num_items: int, device: str, item_pop,
+                     total_train_interactions: int, cred_np, **cfg):
+    """Version-2/lighgcn_cu_pop.py:536-650 (same arguments, the same result
+    dictionary per K; cfg.Ks / sampled_negatives / cred_group_pct / seed as
+    keyword arguments): one device launch for all users
+    (bbgr.evaluation.evaluate_sampled; candidates drawn by Philox)."""
+    from .evaluation import evaluate_sampled_reference
+    return evaluate_sampled_reference(model, train_csr, test_csr, num_items, device, item_pop,
+                                      total_train_interactions, cred_np, **cfg)
+
+
+def evaluate_full_ranking(model, train_csr, test_csr, num_items: int, device: str, item_pop,
+                          total_train_interactions: int, cred_np, **cfg):
+    """Version-2/lighgcn_cu_pop.py:653-752 (same arguments and result
+    dictionary): fp32 MFMA scores with the train items masked and a running
+    top-K (bbgr.evaluation.evaluate_full)."""
+    from .evaluation import evaluate_full_ranking_reference
+    return evaluate_full_ranking_reference(model, train_csr, test_csr, num_items, device,
+                                           item_pop, total_train_interactions, cred_np, **cfg)

@@ -156,3 +156,71 @@ def test_eval_full_matches_reference_ranking():
         u = users[b]
         a, r = np.sort(s64[u, topk[b]])[::-1], np.sort(s64[u, ref[b]])[::-1]
         np.testing.assert_allclose(a, r, rtol=1e-5, atol=1e-5)
+
+
+V2_KEYS = {"precision", "recall", "ndcg", "item_coverage", "avg_log_popularity",
+           "avg_self_information", "cred_utility", "high_cred_recall", "low_cred_recall",
+           "high_users", "low_users", "users_eval", "mode"}
+
+
+@pytest.mark.parametrize("family", ["v2_pop", "method_a", "cu_fair", "plain"])
+def test_evaluate_with_the_reference_signatures(family):
+    """evaluate_sampled / evaluate_full_ranking exported by each drop-in module
+    with its script's signature: (model, train_csr, test_csr, num_items,
+    device[, item_pop, total_train_interactions, cred_np]) with host
+    (indptr, indices) CSRs from edges_to_user_csr, returning the script's
+    dictionary per K (Version-2: the full set of keys; the older scripts:
+    precision / recall / ndcg / users_eval / mode). The values are
+    bbgr.evaluation's on the model's final tables and device CSRs built from
+    the edges, bit for bit (the host-CSR conversion loses nothing)."""
+    from bbgr import evaluation as EV
+    from bbgr import host_sampler as HS
+    from bbgr import lightgcn as SYM
+    from bbgr import lightgcn_cu as CU
+    from bbgr import lightgcn_cu_pop as V2
+    from bbgr import lightgcn_cu_pop_long_tail_exposure as MA
+    U, I, d = 600, 900, 64
+    tr, te = _split(U, I, 12000, 31)
+    cred = synthetic_credibility(U, 31)
+    if family == "v2_pop":
+        mod, m = V2, V2.LightGCN(U, I, d, 3, *V2.build_message_passing_mats(
+            tr, U, I, torch.as_tensor(cred), DEV)).to(DEV)
+    elif family == "method_a":
+        mod, m = MA, MA.LightGCN(U, I, d, 3, *MA.build_message_passing_mats(
+            tr, U, I, torch.as_tensor(cred), DEV)).to(DEV)
+    elif family == "cu_fair":
+        M_ui, M_iu, _ = CU.build_cred_weighted_mats(tr, U, I, cred, DEV)
+        mod, m = CU, CU.CredLightGCN(U, I, d, 3, M_ui, M_iu).to(DEV)
+    else:
+        mod, m = SYM, SYM.LightGCN(U, I, d, 3, SYM.build_norm_adj(tr, U, I, DEV)).to(DEV)
+    tr_csr, te_csr = HS.edges_to_user_csr(tr, U), HS.edges_to_user_csr(te, U)
+    pop = np.bincount(tr[1].astype(np.int64), minlength=I).astype(np.float32)
+    with torch.no_grad():
+        ue, ie = m.final_embeddings() if family == "cu_fair" else m.get_user_item_emb()
+        ue, ie = torch.as_tensor(ue).clone(), torch.as_tensor(ie).clone()
+    trc, tec = Csr(tr[0], tr[1], U, I, DEV), Csr(te[0], te[1], U, I, DEV)
+    v2 = family == "v2_pop"
+    extra = (pop, int(tr.shape[1]), cred) if v2 else ()
+    want_pop, want_total, want_cred = (pop, int(tr.shape[1]), cred) if v2 else \
+        (pop, int(tr.shape[1]), np.ones(U, np.float32))
+    got = mod.evaluate_sampled(m, tr_csr, te_csr, I, DEV, *extra)
+    want = EV.evaluate_sampled(ue, ie, trc, tec, I, want_pop, want_total, want_cred,
+                               seed=42 + 999)
+    checks = [(got, want, "sampled(1pos+neg)")]
+    if hasattr(mod, "evaluate_full_ranking"):
+        checks.append((mod.evaluate_full_ranking(m, tr_csr, te_csr, I, DEV, *extra),
+                       EV.evaluate_full(ue, ie, trc, tec, I, want_pop, want_total, want_cred),
+                       "full"))
+    for got, want, mode in checks:
+        assert sorted(got) == [10, 20]
+        for K in (10, 20):
+            keys = V2_KEYS | ({"negatives"} if mode != "full" else set()) if v2 else \
+                {"precision", "recall", "ndcg", "users_eval", "mode"} | \
+                ({"negatives"} if mode != "full" else set())
+            assert set(got[K]) == keys, (family, mode)
+            assert got[K]["mode"] == mode
+            for k in got[K]:
+                assert got[K][k] == want[K][k], (family, mode, K, k)
+    with pytest.raises(RuntimeError, match="No users with test interactions"):
+        empty = (np.zeros(U + 1, np.int64), np.zeros(0, np.int64))
+        mod.evaluate_sampled(m, tr_csr, empty, I, DEV, *extra)
