@@ -132,8 +132,8 @@ def test_method_a_module_defers_too():
             assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("module", [V2, MA])
-def test_fused_backward_adam_matches_the_separate_step(module):
+@pytest.mark.parametrize("module,K", [(V2, 3), (MA, 3), (V2, 2), (V2, 4)])
+def test_fused_backward_adam_matches_the_separate_step(module, K):
     """bbgr.optim.FusedAdam(fuse_backward=True): the reference's loop body
     (Version-2:858-863) unchanged, the optimizer step carried out inside
     loss.backward() by bbgr::bpr_adam_backward (Adam in the last backward
@@ -145,7 +145,7 @@ def test_fused_backward_adam_matches_the_separate_step(module):
     from bbgr.optim import FusedAdam
     batches = [_batch(s) for s in range(3)]
     batches[1][0][5] = batches[1][0][6]   # a repeated user
-    a, b = _model(3, module), _model(3, module)
+    a, b = _model(K, module), _model(K, module)
     w0 = [p.detach().clone() for p in b.parameters()]
     oa = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
     ob = FusedAdam(b.parameters(), lr=1e-3)
