@@ -888,7 +888,8 @@ def main():
         common = ("Version-2 LightGCN drop-in (bbgr ops: propagate, bpr_loss and their "
                   "registered backward; get_user_item_emb() tables deferred, so bpr_loss "
                   "computes the batch rows only, bbgr::propagate_rows), input vertex order, "
-                  "uniform batches (tools/dropin_probe.py)")
+                  "the reference loop's batches (epoch shuffle of the train users, "
+                  "bbgr.host_sampler's positive / pop-mix negative draws; tools/dropin_probe.py)")
         dropin["note"] = common + " + torch.optim.Adam(foreach), the reference's optimizer"
         dropin_fused["note"] = (common + " + bbgr.optim.FusedAdam (same state keys), on the "
                                 "same model right after the foreach timing")

@@ -1,8 +1,12 @@
 """Probe: the reference's own training step through the drop-in module API
 (Version-2/lighgcn_cu_pop.py:858-863 — propagate, bpr_loss, zero_grad,
 backward, torch.optim.Adam.step) on a BASELINE config, beside the fused
-trainer's step on the same graph. Batches are drawn on the device up front
-(uniform users / items: the sampler is not what this times).
+trainer's step on the same graph. The batches are drawn up front, as the
+reference's loop draws them (`--batches reference`, the default: the epoch
+shuffle of the train users and the per-user positive / pop-mix negative
+draws of Version-2:821-849, through bbgr.host_sampler with the numpy
+Generator seeded 42) or uniformly on the device (`--batches uniform`, the
+rounds 2-5 figures); the sampler itself is not what this times.
 
     python tools/dropin_probe.py [--config C4] [--steps 10] [--adam foreach|fused|bbgr]
 
@@ -36,17 +40,48 @@ def timed(fn, steps: int) -> float:
     return 1000.0 * (time.perf_counter() - t0) / steps
 
 
+def reference_batches(edges, U: int, I: int, B: int, n_b: int, seed: int = 42,
+                      gamma: float = 0.75, mix_pop: float = 0.7):
+    """n_b batches of the reference's loop (Version-2:805-849): pop_prob from
+    the train degrees, the shuffled train users sliced by B, a positive from
+    each user's row and a pop-mix negative (bbgr.host_sampler, bit for bit
+    the reference's numpy stream); int64 [n_b, B] each (a short last slice
+    wraps into the next epoch's shuffle, as later epochs would)."""
+    from bbgr import host_sampler as HS
+    e = np.asarray(edges)
+    indptr, indices = HS.edges_to_user_csr(e, U)
+    deg = np.bincount(e[1].astype(np.int64), minlength=I).astype(np.float64)
+    pop = np.power(deg + 1.0, gamma)
+    pop_prob = pop / (pop.sum() + 1e-12)
+    rng = np.random.default_rng(seed)
+    train_users = np.where(np.diff(indptr) > 0)[0]
+    out_u, out_p, out_n, order, at = [], [], [], np.empty(0, np.int64), 0
+    while len(out_u) < n_b:
+        if at + B > order.size:   # a new epoch
+            rng.shuffle(train_users)
+            order, at = train_users.copy(), 0
+        u, p, n = HS.sample_batch(indptr, indices, order[at:at + B], I, rng, pop_prob,
+                                  mix_pop=mix_pop)
+        at += B
+        out_u.append(u)
+        out_p.append(p)
+        out_n.append(n)
+    return (np.stack(out_u), np.stack(out_p), np.stack(out_n))
+
+
 def run(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
         adam: str = "foreach", device=None, pre_ordered: bool = False,
-        items_ordered: bool = False, dense_finals: bool = False) -> dict:
+        items_ordered: bool = False, dense_finals: bool = False,
+        batches: str = "reference") -> dict:
     """One optimizer (module docstring)."""
     return run_many(cfg_name, edges, cred_np, steps, warmup, (adam,), device, pre_ordered,
-                    items_ordered, dense_finals)[adam]
+                    items_ordered, dense_finals, batches)[adam]
 
 
 def run_many(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: int = 3,
              adams=("foreach",), device=None, pre_ordered: bool = False,
-             items_ordered: bool = False, dense_finals: bool = False) -> dict:
+             items_ordered: bool = False, dense_finals: bool = False,
+             batches: str = "reference") -> dict:
     """{adam: result} for each optimizer in `adams`, on ONE model built once
     (each optimizer starts fresh on the weights the previous one left: the
     timings do not depend on the values)."""
@@ -80,11 +115,18 @@ def run_many(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: i
         model.propagate()   # first call: operator pair registration + first-layer values
     torch.cuda.synchronize()
     first_call_s = time.perf_counter() - t1
-    g = torch.Generator(device=dev).manual_seed(1)
     n_b = warmup + steps
-    users = torch.randint(0, U, (n_b, B), device=dev, generator=g)
-    pos = torch.randint(0, I, (n_b, B), device=dev, generator=g)
-    neg = torch.randint(0, I, (n_b, B), device=dev, generator=g)
+    if batches == "reference":   # in the ids the model was built on
+        t2 = time.perf_counter()
+        users, pos, neg = (torch.as_tensor(x).to(dev) for x in
+                           reference_batches(e, U, I, B, n_b))
+        batches_s = time.perf_counter() - t2
+    else:
+        g = torch.Generator(device=dev).manual_seed(1)
+        users = torch.randint(0, U, (n_b, B), device=dev, generator=g)
+        pos = torch.randint(0, I, (n_b, B), device=dev, generator=g)
+        neg = torch.randint(0, I, (n_b, B), device=dev, generator=g)
+        batches_s = 0.0
     it = iter(range(10**9))
     opt = None
 
@@ -123,7 +165,8 @@ def run_many(cfg_name: str, edges=None, cred_np=None, steps: int = 10, warmup: i
         for _ in range(warmup):
             step()
         out = {"config": cfg_name, "adam": adam, "pre_ordered": pre_ordered,
-               "items_ordered": items_ordered,
+               "items_ordered": items_ordered, "batches": batches,
+               "batches_s": batches_s,
                "setup_s": setup_s, "build_s": build_s, "model_init_s": setup_s - build_s,
                "first_call_s": first_call_s, "steps": steps,
                "lazy_finals": bool(model.lazy_finals),
@@ -154,10 +197,13 @@ def main():
                     help="only the item ids handed over in descending-degree order")
     ap.add_argument("--dense-finals", action="store_true",
                     help="LightGCN.lazy_finals = False: whole final tables at every call")
+    ap.add_argument("--batches", default="reference", choices=["reference", "uniform"],
+                    help="the reference loop's batches (host sampler, pop-mix) or uniform "
+                         "device draws (module docstring)")
     a = ap.parse_args()
     print(json.dumps(run(a.config, steps=a.steps, warmup=a.warmup, adam=a.adam,
                          pre_ordered=a.pre_ordered, items_ordered=a.items_ordered,
-                         dense_finals=a.dense_finals)),
+                         dense_finals=a.dense_finals, batches=a.batches)),
           flush=True)
 
 

@@ -123,7 +123,7 @@ for step in "$@"; do
       python tools/bench_brief.py "$O/rehearsal_gloo$n.json" ;;
     dropin)    # the drop-in module step (FusedAdam, torch foreach Adam) + a kernel trace
       for a in ${DROPIN_ADAMS:-bbgr bbgr_bwd foreach}; do
-        timeout -k 10 400 python tools/dropin_probe.py --adam $a > "$O/dropin_$a.json" \
+        timeout -k 10 400 python tools/dropin_probe.py --adam $a ${DROPIN_ARGS:-} > "$O/dropin_$a.json" \
           2> "$O/dropin_$a.log"
         rc=$?; hard $rc "dropin $a" "$O/dropin_$a.log"
         [ $rc -eq 0 ] || { tail -20 "$O/dropin_$a.log"; exit 1; }
