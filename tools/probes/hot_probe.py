@@ -2,7 +2,7 @@
 degree order (graph.HOT_BYTES and the rows/8 cap), on one C4 trainer. The
 rule is swapped between runs on the same trainer (it is evaluated per launch).
 
-    python tools/probes/hot_probe.py [--steps 15]
+    python tools/probes/hot_probe.py [--steps 15] [--cases 8:8:192,8:64:192]
 """
 from __future__ import annotations
 
@@ -41,6 +41,8 @@ def rule(user_div, item_div, budget_mb, U):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=15)
+    ap.add_argument("--cases", default="",
+                    help="user_div:item_div:budget_mb,... (default: the round-2 sweep)")
     a = ap.parse_args()
     c = CONFIGS["C4"]
     U, I, d, K, B = (c[k] for k in ("num_users", "num_items", "emb_dim", "num_layers", "batch"))
@@ -49,6 +51,8 @@ def main():
                       num_layers=K, batch_size=B)
     cases = [(8, 8, 192), (8, 4, 192), (8, 2, 192), (16, 8, 192), (4, 8, 256), (8, 1, 256),
              (0, 0, 0), (8, 8, 192)]
+    if a.cases:
+        cases = [tuple(int(v) for v in c.split(":")) for c in a.cases.split(",")]
     for ud, idv, mb in cases:
         G.Csr.stream_from, G.Csr.stream_out_from = rule(ud, idv, mb, U)
         for _ in range(3):
