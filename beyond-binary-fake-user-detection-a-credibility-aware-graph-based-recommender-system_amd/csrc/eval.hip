@@ -10,7 +10,7 @@
 //
 // Full-ranking protocol, :652-752: every item is scored for every evaluated
 // user. That is a U_eval x I x d product: fp32 MFMA (v_mfma_f32_32x32x2_f32,
-// exact fp32 fma chains) over LDS-staged 128-item tiles, 128 users per
+// exact fp32 fma chains) over LDS-staged 128-item tiles, 256 users per
 // workgroup (32 per wave, the user fragment kept in registers for the whole
 // sweep). The reference's `scores[train] = -1e9; argsort` is fused: every lane
 // keeps the running top-KM of the items it owns in registers (score desc,
@@ -283,7 +283,8 @@ __global__ __launch_bounds__(FULL_THREADS) void eval_full_kernel(FullParams P) {
   // inserts every lane's buffer at once, so the compare-swap insertion runs
   // SIMD-parallel instead of once per passing lane.
   int cnt = 0;
-  float thr = -INFINITY;
+  // (+inf for a lane without a user: nothing ever passes its threshold)
+  float thr = valid ? -INFINITY : INFINITY;
   auto flush = [&]() {
     for (int j = 0; j < cnt; ++j) {
       const float2 c = cbuf[j * FULL_THREADS + threadIdx.x];
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(FULL_THREADS) void eval_full_kernel(FullParams P) {
       }
     }
     cnt = 0;
-    thr = tv[KM - 1];
+    thr = valid ? tv[KM - 1] : INFINITY;
   };
   const int n_tiles = item_hi > item_lo ? (item_hi - item_lo + TILE - 1) / TILE : 0;
   float4 stage[F4];
@@ -320,68 +321,122 @@ __global__ __launch_bounds__(FULL_THREADS) void eval_full_kernel(FullParams P) {
       *reinterpret_cast<float4 *>(T + row * LDT + 4 * c4) = stage[j];
     }
   };
+  // Scores of sub-tiles [lo, hi) of tile T: per sub-tile one chain of H
+  // MFMAs over the components in order (the same chain for every tiling).
+  // Sub-tiles [plo, phi) (already scored, not written here) have their
+  // maxima folded into mxp a few elements per component step, between the
+  // MFMAs, so the check's VALU work issues while the matrix pipe is busy.
+  f32x16 acc[M];
+  float mxp[M];
+  constexpr int EPS = 16 / (H / 4);   // max elements folded per component step
+  auto score_rows = [&](const float *T, int lo, int hi, int plo, int phi) {
+#pragma unroll
+    for (int m = lo; m < hi; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+#pragma unroll
+    for (int m = plo; m < phi; ++m) mxp[m] = acc[m][0];
+#pragma unroll
+    for (int s4 = 0; s4 < H / 4; ++s4) {
+#pragma unroll
+      for (int m = plo; m < phi; ++m)
+#pragma unroll
+        for (int q = 0; q < EPS; ++q)
+          if (s4 * EPS + q > 0) mxp[m] = fmaxf(mxp[m], acc[m][s4 * EPS + q]);
+      float4 a[M];
+#pragma unroll
+      for (int m = lo; m < hi; ++m)
+        a[m] = *reinterpret_cast<const float4 *>(T + (m * 32 + r) * LDT + h * H + 4 * s4);
+      // independent accumulators back to back
+#pragma unroll
+      for (int m = lo; m < hi; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].x, ub[4 * s4 + 0], acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = lo; m < hi; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].y, ub[4 * s4 + 1], acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = lo; m < hi; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].z, ub[4 * s4 + 2], acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = lo; m < hi; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].w, ub[4 * s4 + 3], acc[m], 0, 0, 0);
+    }
+  };
+  // Sub-tile m's scores against the threshold; acc[m][e] = score of user b,
+  // item i0 + 32m + (e&3) + 8(e>>2) + 4h.
+  auto scan = [&](int m, int i0, bool folded) {
+    float mx = acc[m][0];
+    if (folded) {
+      mx = mxp[m];
+    } else {
+#pragma unroll
+      for (int e = 1; e < 16; ++e) mx = fmaxf(mx, acc[m][e]);
+    }
+    if (mx > thr) {
+      unsigned pass = 0;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) pass |= (acc[m][e] > thr ? 1u : 0u) << e;
+      while (pass) {
+        const int e = __builtin_ctz(pass);
+        pass &= pass - 1;
+        float sc = acc[m][0];
+#pragma unroll
+        for (int e2 = 1; e2 < 16; ++e2) sc = e2 == e ? acc[m][e2] : sc;
+        const int it = i0 + 32 * m + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (it < item_hi) {
+          if (cnt == CB) flush();      // this lane only (early tiles: all lanes together)
+          cbuf[cnt * FULL_THREADS + threadIdx.x] = make_float2(sc, __int_as_float(it));
+          ++cnt;
+        }
+      }
+    }
+    if (__any(cnt > CB - 4)) flush();   // batch the insertions across lanes
+  };
   if (n_tiles > 0) {
     load_tile(0);
     store_tile(0);
   }
   __syncthreads();
-  for (int t = 0; t < n_tiles; ++t) {
-    if (t + 1 < n_tiles) load_tile(t + 1);
-    const float *T = tile + (t & 1) * TILE * LDT;
-    f32x16 acc[M];
+  // Software pipeline (KM <= 24): the second half of tile t-1's sub-tiles is
+  // checked while the first half of tile t is on the MFMA pipe, the first
+  // half of tile t while its second half is. Candidates still reach each
+  // lane's buffer in ascending item order. (Before the first tile the pending
+  // half holds -inf scores: nothing passes.) The 32-deep list leaves no
+  // registers for it and checks each tile after its MFMAs.
+  if constexpr (KM <= 24) {
+    constexpr int M2 = M / 2;
 #pragma unroll
-    for (int m = 0; m < M; ++m)
+    for (int m = M2; m < M; ++m)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+      for (int e = 0; e < 16; ++e) acc[m][e] = -INFINITY;
+    int i_prev = item_lo;
+    for (int t = 0; t < n_tiles; ++t) {
+      if (t + 1 < n_tiles) load_tile(t + 1);
+      const float *T = tile + (t & 1) * TILE * LDT;
+      const int i0 = item_lo + t * TILE;
+      score_rows(T, 0, M2, M2, M);
 #pragma unroll
-    for (int s4 = 0; s4 < H / 4; ++s4) {
-      float4 a[M];
+      for (int m = M2; m < M; ++m) scan(m, i_prev, true);
+      score_rows(T, M2, M, 0, M2);
 #pragma unroll
-      for (int m = 0; m < M; ++m)
-        a[m] = *reinterpret_cast<const float4 *>(T + (m * 32 + r) * LDT + h * H + 4 * s4);
-      // independent accumulators back to back
-#pragma unroll
-      for (int m = 0; m < M; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].x, ub[4 * s4 + 0], acc[m], 0, 0, 0);
-#pragma unroll
-      for (int m = 0; m < M; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].y, ub[4 * s4 + 1], acc[m], 0, 0, 0);
-#pragma unroll
-      for (int m = 0; m < M; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].z, ub[4 * s4 + 2], acc[m], 0, 0, 0);
-#pragma unroll
-      for (int m = 0; m < M; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].w, ub[4 * s4 + 3], acc[m], 0, 0, 0);
+      for (int m = 0; m < M2; ++m) scan(m, i0, true);
+      i_prev = i0;
+      if (t + 1 < n_tiles) store_tile((t + 1) & 1);
+      __syncthreads();
     }
-    // acc[m][e] = score of user b, item i0 + 32m + (e&3) + 8(e>>2) + 4h
-    const int i0 = item_lo + t * TILE;
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      float mx = acc[m][0];
+    for (int m = M2; m < M; ++m) scan(m, i_prev, false);
+  } else {
+    for (int t = 0; t < n_tiles; ++t) {
+      if (t + 1 < n_tiles) load_tile(t + 1);
+      const float *T = tile + (t & 1) * TILE * LDT;
+      score_rows(T, 0, M, 0, 0);
+      const int i0 = item_lo + t * TILE;
 #pragma unroll
-      for (int e = 1; e < 16; ++e) mx = fmaxf(mx, acc[m][e]);
-      if (valid && mx > thr) {
-        unsigned pass = 0;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) pass |= (acc[m][e] > thr ? 1u : 0u) << e;
-        while (pass) {
-          const int e = __builtin_ctz(pass);
-          pass &= pass - 1;
-          float sc = acc[m][0];
-#pragma unroll
-          for (int e2 = 1; e2 < 16; ++e2) sc = e2 == e ? acc[m][e2] : sc;
-          const int it = i0 + 32 * m + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (it < item_hi) {
-            if (cnt == CB) flush();      // this lane only (early tiles: all lanes together)
-            cbuf[cnt * FULL_THREADS + threadIdx.x] = make_float2(sc, __int_as_float(it));
-            ++cnt;
-          }
-        }
-      }
-      if (__any(cnt > CB - 4)) flush();   // batch the insertions across lanes
+      for (int m = 0; m < M; ++m) scan(m, i0, false);
+      if (t + 1 < n_tiles) store_tile((t + 1) & 1);
+      __syncthreads();
     }
-    if (t + 1 < n_tiles) store_tile((t + 1) & 1);
-    __syncthreads();
   }
   flush();
   if (valid) {

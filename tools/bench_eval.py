@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--negatives", type=int, default=99)
     ap.add_argument("--cpu-users", type=int, default=40000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ks", type=int, nargs="+", default=[10, 20],
+                    help="--full: the cutoffs (the top-K list is max(ks) deep)")
     ap.add_argument("--full", action="store_true",
                     help="full-ranking protocol (evaluate_full_ranking) instead of sampled")
     ap.add_argument("--max-users", type=int, default=0,
@@ -89,7 +91,8 @@ def main():
         te = te[:, np.isin(te[0], keep_u)]
         tec = Csr(te[0], te[1], U, I, dev)
     if args.full:
-        run = lambda c: evaluate_full(uf, itf, trc, tec, I, pop_t, T, cred_t)  # noqa: E731
+        run = lambda c: evaluate_full(uf, itf, trc, tec, I, pop_t, T, cred_t,  # noqa: E731
+                                      Ks=tuple(args.ks))
     else:
         run = lambda c: evaluate_sampled(uf, itf, trc, tec, I, pop_t, T, cred_t,  # noqa: E731
                                          sampled_negatives=args.negatives, counter=c)
@@ -111,7 +114,8 @@ def main():
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t1)
         evs.append(a.elapsed_time(b) / 1e3)
-    n_eval = int(res[10]["users_eval"])
+    k0 = args.ks[0] if args.full else 10
+    n_eval = int(res[k0]["users_eval"])
     wall = float(np.median(walls))
     dev_s = float(np.median(evs))
     nc = 1 + args.negatives
@@ -127,7 +131,7 @@ def main():
                 "unit": "GB/s", "frac": alg / dev_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
                 "note": "whole evaluate_sampled device time (sample+score+rank, metrics)"}
     log(f"[eval] users {n_eval}  wall {wall*1e3:.2f} ms  device {dev_s*1e3:.2f} ms  "
-        f"ndcg@10 {res[10]['ndcg']:.4f}")
+        f"ndcg@{k0} {res[k0]['ndcg']:.4f}")
     cpu = None
     if not args.no_cpu_baseline:
         from oracle import ref_numpy as R
@@ -149,7 +153,8 @@ def main():
                "sample": f"reference per-user loop (oracle restatement) on the first "
                          f"{users.size} evaluated users of the same split: {el:.1f} s"}
         log(f"[eval] cpu {users.size} users {el:.1f}s -> {users.size/el:.0f} users/s")
-    proto = "full ranking (all items, K=10,20)" if args.full else \
+    kstr = ",".join(str(k) for k in args.ks)
+    proto = f"full ranking (all items, K={kstr})" if args.full else \
         f"sampled eval (1 pos + {args.negatives} neg, K=10,20)"
     line = {
         "metric": "eval_users_per_s", "value": n_eval / wall, "unit": "users/s",
