@@ -6,7 +6,6 @@ with the float64 oracle; the partition, the edge sharding, the global item
 degree all-reduce and the per-layer partial-sum all-reduce are the product's
 own functions / schedule and must reproduce the unsharded propagation."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -18,11 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from _ports import free_port
+    return free_port()
 
 
 def _worker(rank, world, port, out):

@@ -5,7 +5,6 @@ at round end on 8 GPUs. Checked against the float64 oracle on the union of
 the ranks' batches."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -18,11 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from _ports import free_port
+    return free_port()
 
 
 @pytest.mark.parametrize("variant,mode,frontier,world,order", [
