@@ -69,6 +69,41 @@ def test_eval_sampled_vs_oracle(d):
     assert res2[20]["ndcg"] == res[20]["ndcg"] and res2[10]["item_coverage"] == res[10]["item_coverage"]
 
 
+@pytest.mark.parametrize("K", [(10, 20), (3,), (1, 64)])
+def test_eval_sampled_ranks_and_lists_exact_with_ties(K):
+    """Integer-valued embeddings make every score an exact fp32 integer (any
+    summation order), with many ties: the kernel's positive rank and top-k
+    lists must be exactly the stable descending order of the candidates
+    (score desc, candidate slot asc; Version-2:612-620 argsort). Pins the
+    rank count's early stop for candidates outside the top k_max."""
+    from bbgr.evaluation import evaluate_sampled
+    U, I, d = 600, 900, 64
+    tr, te = _split(U, I, 12000, 5)
+    rng = np.random.default_rng(6)
+    uf = rng.integers(-2, 3, size=(U, d)).astype(np.float32)
+    itf = rng.integers(-2, 3, size=(I, d)).astype(np.float32)
+    res = evaluate_sampled(torch.tensor(uf, device=DEV), torch.tensor(itf, device=DEV),
+                           Csr(tr[0], tr[1], U, I, DEV), Csr(te[0], te[1], U, I, DEV), I,
+                           np.bincount(tr[1], minlength=I), int(tr.shape[1]),
+                           synthetic_credibility(U, 5), Ks=K, return_raw=True)
+    raw = res.pop("_raw")
+    assert raw["fails"] == 0
+    users = raw["users"].cpu().numpy()
+    nc = 100
+    cand = raw["cand"].cpu().numpy().reshape(users.size, nc)
+    pos_rank = raw["pos_rank"].cpu().numpy()
+    topk = raw["topk"].cpu().numpy()
+    km = max(K)
+    ties = 0
+    for n, u in enumerate(users):
+        s = itf[cand[n]].astype(np.int64) @ uf[u].astype(np.int64)
+        order = np.lexsort((np.arange(nc), -s))          # score desc, slot asc
+        ties += nc - np.unique(s).size
+        assert pos_rank[n] == int(np.nonzero(order == 0)[0][0]), n
+        np.testing.assert_array_equal(topk[n], cand[n][order[:km]])
+    assert ties > users.size * 10          # the case really is tie-heavy
+
+
 def test_eval_known_ranking():
     """Hand case: one user, item scores fixed, pos guaranteed top-1."""
     from bbgr.evaluation import evaluate_sampled
