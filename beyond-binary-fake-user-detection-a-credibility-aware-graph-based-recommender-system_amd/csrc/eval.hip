@@ -329,6 +329,7 @@ __global__ __launch_bounds__(FULL_THREADS) void eval_full_kernel(FullParams P) {
   f32x16 acc[M];
   float mxp[M];
   constexpr int EPS = 16 / (H / 4);   // max elements folded per component step
+  static_assert(EPS >= 1 && EPS * (H / 4) == 16, "the folds must cover the 16 scores");
   auto score_rows = [&](const float *T, int lo, int hi, int plo, int phi) {
 #pragma unroll
     for (int m = lo; m < hi; ++m)
