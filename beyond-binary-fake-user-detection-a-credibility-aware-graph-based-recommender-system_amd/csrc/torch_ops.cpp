@@ -124,6 +124,15 @@ struct Pair {
   // input-order chain, made once instead of two fills per call
   mutable std::once_flag iota_once;
   mutable Tensor iota_u, iota_i;
+  // the in-backward Adam's two [I, d] item tables (the rows backward's gI and
+  // the item Adam's gradient side table), one set per stream, all-zero between
+  // calls: a call writes the batch items' rows only and clears them again, so
+  // no step pays two 256 MB (C4) zero fills (bpr_adam_backward)
+  struct ItemTables {
+    Tensor gi, grad;
+  };
+  mutable std::mutex it_mu;
+  mutable std::map<int64_t, ItemTables> it;
 };
 
 static std::mutex g_mu;
@@ -961,7 +970,8 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
                                                 const Tensor &vu, const Tensor &gI_, int64_t K,
                                                 bool gs, const c10::optional<Tensor> &ii_,
                                                 const c10::optional<Tensor> &vi_,
-                                                StepAdam *sa = nullptr);
+                                                StepAdam *sa = nullptr,
+                                                const Tensor &gi_zeroed = Tensor());
 
 static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
     const Tensor &iu_, const Tensor &vu, const Tensor &gI_, int64_t num_users, int64_t key,
@@ -973,11 +983,13 @@ static std::tuple<Tensor, Tensor> propagate_backward_rows_cuda(
 }
 
 // the body of propagate_backward_rows; `sa`: the in-backward Adam (no gradient
-// tables returned)
+// tables returned); `gi_zeroed`: an all-zero [I, d] table to form gI in (rows
+// ii only) instead of a fresh zero fill
 static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, const Tensor &iu_,
                                                 const Tensor &vu, const Tensor &gI_, int64_t K,
                                                 bool gs, const c10::optional<Tensor> &ii_,
-                                                const c10::optional<Tensor> &vi_, StepAdam *sa) {
+                                                const c10::optional<Tensor> &vi_, StepAdam *sa,
+                                                const Tensor &gi_zeroed) {
   const int64_t U = P->U, I = P->I, d = vu.size(1);
   Tensor iu = iu_.to(at::kLong).contiguous();
   // dL/d(i_final) as rows too (vi[k] adds to item ii[k]; gI_ is then only a
@@ -994,7 +1006,8 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
     ii = ii_->to(at::kLong).contiguous();
     TORCH_CHECK(vi_->dim() == 2 && vi_->size(0) == ii.numel() && vi_->size(1) == d,
                 "propagate_backward_rows: vi must be [len(ii), d]");
-    gI = at::zeros({std::max<int64_t>(I, 1), d}, f32(vu)).narrow(0, 0, I);
+    gI = gi_zeroed.defined() ? gi_zeroed
+                             : at::zeros({std::max<int64_t>(I, 1), d}, f32(vu)).narrow(0, 0, I);
     if (sa && sa->item_plan.defined()) apply_rows(sa->item_plan, gI, *vi_);
     else index_add_rows(gI, ii, vi_->contiguous());
   } else {
@@ -1358,9 +1371,41 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   // (one sort of the 2B item ids serves this scatter and rows_backward's gI)
   Tensor vi = contrib.narrow(0, B, 2 * B);
   sa.item_plan = plan_rows(ii, I);
-  sa.item_grad = at::zeros({std::max<int64_t>(I, 1), d}, f32(uf)).narrow(0, 0, I);
+  // the two [I, d] item tables: kept all-zero per stream and cleared again at
+  // the batch items' rows (ii, clamped to [0, I)), the only rows written
+  // (eager only; a table set is dropped, not reused, when the chain throws)
+  // (a graph capture gets fresh tables: their fills are then part of the graph)
+  const bool cached = !capturing();
+  const int64_t skey = (int64_t)(intptr_t)cur_stream();
+  std::unique_lock<std::mutex> lk(P->it_mu, std::defer_lock);
+  Pair::ItemTables fresh, *tp = &fresh;
+  if (cached) {
+    lk.lock();
+    tp = &P->it[skey];
+  }
+  Pair::ItemTables &t = *tp;
+  if (!t.gi.defined() || t.gi.size(1) != d || t.gi.device() != uf.device()) {
+    t.gi = at::zeros({std::max<int64_t>(I, 1), d}, f32(uf));
+    t.grad = at::zeros({std::max<int64_t>(I, 1), d}, f32(uf));
+  }
+  Tensor gi = t.gi.narrow(0, 0, I);
+  sa.item_grad = t.grad.narrow(0, 0, I);
+  struct Drop {   // a throw leaves rows written: forget the set (fresh zeros next call)
+    const Pair &P;
+    int64_t key;
+    bool armed = true;
+    ~Drop() {
+      if (armed) P.it.erase(key);
+    }
+  } drop{*P, skey, cached};
   apply_rows(sa.item_plan, sa.item_grad, vi, at::mul(ri, kp1));
-  rows_backward(P, iu, contrib.narrow(0, 0, B), i0, K, true, ii, vi, &sa);
+  rows_backward(P, iu, contrib.narrow(0, 0, B), i0, K, true, ii, vi, &sa, gi);
+  if (cached)
+    for (Tensor *z : {&gi, &sa.item_grad})
+      check(bbgr_rows_zero(ii.numel(), ii.data_ptr<int64_t>(), z->data_ptr<float>(), ld(*z),
+                           (int32_t)d, cur_stream()),
+            "bbgr_rows_zero");
+  drop.armed = false;
 }
 
 // -- Meta kernels (shapes only; torch.compile traces through them) ---------------
