@@ -399,6 +399,22 @@ def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> d
                     "after the strong line in the same run"}
 
 
+def step_summary(ms, dense_ms, torch_ref, dropin, dropin_fused, dropin_bwd) -> dict:
+    """The step times of the line and of the runs beside it, in one small
+    object printed last (the driver keeps the tail of stdout)."""
+    def ms_of(r):
+        return None if r is None else round(r["step_ms"], 3)
+    return {"ms_per_step": round(ms, 3),
+            "dense_ms_per_step": None if not dense_ms else round(dense_ms, 3),
+            "torch_gpu_reference_step_ms": ms_of(torch_ref),
+            "dropin_module_step_ms": ms_of(dropin),
+            "dropin_fused_adam_step_ms": ms_of(dropin_fused),
+            "dropin_backward_adam_step_ms": ms_of(dropin_bwd),
+            "note": "ms per step: the fused trainer (the line), its dense form, the reference's "
+                    "step in stock PyTorch-ROCm, the drop-in module with torch's foreach Adam / "
+                    "FusedAdam / FusedAdam(fuse_backward=True)"}
+
+
 def main():
     global cfg_name_global
     out_stream = _quiet_stdout()
@@ -938,6 +954,7 @@ def main():
                                       if dist_mode and not columns and sel_native != "off"
                                       else ""))},
         "bpr_steps_per_s": steps_per_s,
+        "roofline_per_kernel": groups,
         "torch_gpu_reference": torch_ref,
         "dropin_module_step": dropin,
         "dropin_fused_adam_step": dropin_fused,
@@ -1022,9 +1039,11 @@ def main():
                      / HBM_PEAK_GBS,
                      "step_traffic_source": None if stp is None else
                      {k: stp.get(k) for k in ("tag", "commit", "steps", "kernel_us_per_step_pmc",
-                                              "source")},
-                     "per_kernel": groups},
+                                              "source")}},
         "cpu_baseline": None if cpu is None else {k: v for k, v in cpu.items() if k != "step_s"},
+        # last: the compact figures, where the driver's stdout tail keeps them
+        "step_summary": step_summary(1000.0 * elapsed / args.steps, dense_ms, torch_ref, dropin,
+                                     dropin_fused, dropin_bwd),
     }
     print(json.dumps(out), file=out_stream, flush=True)
     if dist_mode:

@@ -128,6 +128,17 @@ class EvalArgs(ctypes.Structure):
         ("item_pop", c_void_p), ("self_info_denom", c_float), ("group", c_void_p),
         ("pos_rank", c_void_p), ("topk", c_void_p), ("topk_score", c_void_p),
         ("cand_out", c_void_p), ("fail_count", c_void_p), ("sums", c_void_p),
+        ("cand_in", c_void_p),
+    ]
+
+
+class Pcg64State(ctypes.Structure):
+    """bbgr_pcg64: numpy's PCG64 bit_generator.state (128-bit state and
+    increment as two 64-bit halves, the buffered 32-bit output)."""
+    _fields_ = [
+        ("state_hi", c_uint64), ("state_lo", c_uint64),
+        ("inc_hi", c_uint64), ("inc_lo", c_uint64),
+        ("has_uint32", c_int32), ("uinteger", ctypes.c_uint32),
     ]
 
 
@@ -199,6 +210,8 @@ _SIGNATURES = {
     "bbgr_eval_sampled": ([ctypes.POINTER(EvalArgs), _P, ctypes.POINTER(c_size_t), _P],
                           c_int32),
     "bbgr_eval_full": ([ctypes.POINTER(EvalArgs), _P, ctypes.POINTER(c_size_t), _P], c_int32),
+    "bbgr_eval_draw_candidates": ([ctypes.POINTER(Pcg64State), c_int64, _P, _P, _P, _P, _P,
+                                   c_int64, c_int32, _P], c_int32),
     "bbgr_nonempty_rows": ([c_int32, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P],
                            c_int32),
     "bbgr_mask_to_list": ([c_int64, _P, _P, _P, _P, ctypes.POINTER(c_size_t), _P], c_int32),
@@ -245,7 +258,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 9:
+        if handle.bbgr_abi_version() != 10:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

@@ -26,6 +26,9 @@
 // per-user P/R/NDCG/novelty/group terms, marks covered items and reduces a
 // fixed chunk of users per workgroup; eval_sum_kernel sums the chunks in a
 // fixed order and counts covered items. Deterministic bit for bit.
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 
 namespace bbgr {
@@ -82,6 +85,7 @@ struct EvalParams {
   int *topk;
   int *cand_out;
   int *fail_count;
+  const int *cand_in;   // candidates supplied (the reference's numpy stream) instead of drawn
 };
 
 // MC: LDS candidate capacity per user (128 covers the reference's 1 + 99;
@@ -114,8 +118,11 @@ __global__ __launch_bounds__(256) void eval_sampled_kernel(EvalParams P) {
   __syncthreads();
   const int *te_row = te_lds ? rows[g][0] : P.te_indices + tb;
   const int *tr_row = tr_lds ? rows[g][1] : P.tr_indices + rb;
-  // ---- candidates: lane 0 of each group draws pos; lanes split the negatives
-  if (active && nte > 0) {
+  // ---- candidates: supplied (cand_in), or lane 0 of each group draws pos and
+  // the lanes split the negatives
+  if (active && nte > 0 && P.cand_in) {
+    for (int c = lane; c < nc; c += 16) cand[g][c] = P.cand_in[b * nc + c];
+  } else if (active && nte > 0) {
     const uint32_t k0 = (uint32_t)P.seed, k1 = (uint32_t)(P.seed >> 32) ^ 0x2545F491u;
     const uint32_t c1 = (uint32_t)b, c2 = (uint32_t)P.counter;
     const uint32_t c3 = (uint32_t)(P.counter >> 32) ^ (uint32_t)((unsigned long long)b >> 32);
@@ -754,9 +761,141 @@ static int launch_merge(const FullParams &P, long b0, const bbgr_eval_args *a, h
   return BBGR_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The reference's candidate stream on the host (bbgr_eval_draw_candidates):
+// numpy's PCG64 (XSL-RR 128/64: advance the LCG, then output
+// rotr64(hi ^ lo, hi >> 58)), its buffered 32-bit outputs (the low half of a
+// 64-bit output first, the high half kept for the next call), and
+// Generator.integers' scalar int64 path (random_bounded_uint64_fill with
+// Lemire's multiply-and-reject; a range of one value draws nothing).
+// ---------------------------------------------------------------------------
+typedef unsigned __int128 u128;
+
+struct Pcg64 {
+  u128 state, inc;
+  bool has32;
+  uint32_t buf32;
+
+  uint64_t next64() {
+    const u128 mult = ((u128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull;
+    state = state * mult + inc;
+    const uint64_t x = (uint64_t)(state >> 64) ^ (uint64_t)state;
+    const unsigned rot = (unsigned)(state >> 122);
+    return (x >> rot) | (x << ((-rot) & 63u));
+  }
+  uint32_t next32() {
+    if (has32) {
+      has32 = false;
+      return buf32;
+    }
+    const uint64_t v = next64();
+    has32 = true;
+    buf32 = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+  }
+  // rng.integers(0, n) for an int64 result, n >= 1: off + a value in [0, rng]
+  uint64_t bounded(uint64_t rng) {
+    if (rng == 0) return 0;
+    if (rng <= 0xFFFFFFFFull) {
+      if (rng == 0xFFFFFFFFull) return next32();
+      const uint32_t excl = (uint32_t)rng + 1u;
+      uint64_t m = (uint64_t)next32() * excl;
+      uint32_t left = (uint32_t)m;
+      if (left < excl) {
+        const uint32_t thr = (UINT32_MAX - (uint32_t)rng) % excl;
+        while (left < thr) {
+          m = (uint64_t)next32() * excl;
+          left = (uint32_t)m;
+        }
+      }
+      return m >> 32;
+    }
+    if (rng == UINT64_MAX) return next64();
+    const uint64_t excl = rng + 1;
+    u128 m = (u128)next64() * excl;
+    uint64_t left = (uint64_t)m;
+    if (left < excl) {
+      const uint64_t thr = (UINT64_MAX - rng) % excl;
+      while (left < thr) {
+        m = (u128)next64() * excl;
+        left = (uint64_t)m;
+      }
+    }
+    return (uint64_t)(m >> 64);
+  }
+};
+
+// np.searchsorted(arr, x) (side='left') exactly as numpy's binary search runs
+// it, so user_has_item (Version-2:330-336) agrees even on an unsorted row
+static inline bool user_has_item_host(const int64_t *arr, int64_t n, int64_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = lo + ((hi - lo) >> 1);
+    if (arr[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < n && arr[lo] == x;
+}
+
 }  // namespace bbgr
 
 using namespace bbgr;
+
+extern "C" int bbgr_eval_draw_candidates(bbgr_pcg64 *rng, int64_t n_users, const int64_t *users,
+                                         const int64_t *te_indptr, const int64_t *te_indices,
+                                         const int64_t *tr_indptr, const int64_t *tr_indices,
+                                         int64_t n_items, int32_t n_neg, int32_t *cand) {
+  BBGR_REQUIRE(rng && n_users >= 0 && n_items > 0 && n_items <= INT32_MAX && n_neg >= 0,
+               "bbgr_eval_draw_candidates: bad sizes (n_items in [1, 2^31), n_neg >= 0)");
+  BBGR_REQUIRE(n_users == 0 || (users && te_indptr && te_indices && tr_indptr && tr_indices && cand),
+               "bbgr_eval_draw_candidates: null array");
+  BBGR_REQUIRE((rng->inc_lo & 1ull) == 1ull, "bbgr_eval_draw_candidates: PCG64 increment must be odd");
+  Pcg64 g;
+  g.state = ((u128)rng->state_hi << 64) | rng->state_lo;
+  g.inc = ((u128)rng->inc_hi << 64) | rng->inc_lo;
+  g.has32 = rng->has_uint32 != 0;
+  g.buf32 = rng->uinteger;
+  const int64_t nc = 1 + (int64_t)n_neg;
+  std::vector<int64_t> gt;   // the test row, sorted: `j in gt_set`
+  for (int64_t b = 0; b < n_users; ++b) {
+    const int64_t u = users[b];
+    const int64_t tb = te_indptr[u], te = te_indptr[u + 1];
+    const int64_t rb = tr_indptr[u], re = tr_indptr[u + 1];
+    if (te <= tb) {
+      set_error("bbgr_eval_draw_candidates: user %lld has an empty test row", (long long)u);
+      return BBGR_ERR_INVALID;
+    }
+    gt.assign(te_indices + tb, te_indices + te);
+    std::sort(gt.begin(), gt.end());
+    const int64_t *tr = tr_indices + rb;
+    const int64_t ntr = re - rb;
+    // the reference's while loop ends only if some item passes both tests: each
+    // row rejects at most its own values, so a shortfall needs an exact count
+    if ((te - tb) + ntr >= n_items) {
+      bool any = false;
+      for (int64_t j = 0; j < n_items && !any; ++j)
+        any = !std::binary_search(gt.begin(), gt.end(), j) && !user_has_item_host(tr, ntr, j);
+      if (!any && n_neg > 0) {
+        set_error("bbgr_eval_draw_candidates: user %lld has no admissible negative item",
+                  (long long)u);
+        return BBGR_ERR_INVALID;
+      }
+    }
+    int32_t *out = cand + b * nc;
+    out[0] = (int32_t)te_indices[tb + (int64_t)g.bounded((uint64_t)(te - tb - 1))];
+    for (int64_t s = 1; s < nc;) {
+      const int64_t j = (int64_t)g.bounded((uint64_t)(n_items - 1));
+      if (std::binary_search(gt.begin(), gt.end(), j)) continue;
+      if (user_has_item_host(tr, ntr, j)) continue;
+      out[s++] = (int32_t)j;
+    }
+  }
+  rng->state_hi = (uint64_t)(g.state >> 64);
+  rng->state_lo = (uint64_t)g.state;
+  rng->has_uint32 = g.has32 ? 1 : 0;
+  rng->uinteger = g.buf32;
+  return BBGR_OK;
+}
 
 extern "C" int bbgr_eval_sampled(const bbgr_eval_args *a, void *workspace,
                                  size_t *workspace_bytes, bbgr_stream_t stream) {
@@ -801,6 +940,7 @@ extern "C" int bbgr_eval_sampled(const bbgr_eval_args *a, void *workspace,
     P.topk = a->topk;
     P.cand_out = a->cand_out;
     P.fail_count = a->fail_count;
+    P.cand_in = a->cand_in;
     BBGR_HIP(hipMemsetAsync(a->topk, 0xff, sizeof(int) * (size_t)a->n_users * a->k_max, st));
     const unsigned grid = (unsigned)((a->n_users + 15) / 16);
     const bool small = 1 + a->n_neg <= 128;

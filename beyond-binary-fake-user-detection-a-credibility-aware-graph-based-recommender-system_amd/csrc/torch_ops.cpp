@@ -127,12 +127,33 @@ struct Pair {
   // the in-backward Adam's two [I, d] item tables (the rows backward's gI and
   // the item Adam's gradient side table), one set per stream, all-zero between
   // calls: a call writes the batch items' rows only and clears them again, so
-  // no step pays two 256 MB (C4) zero fills (bpr_adam_backward)
+  // no step pays two 256 MB (C4) zero fills (bpr_adam_backward). At most
+  // kItemTableSets sets are kept (the least recently used stream's set is
+  // dropped): a caller that steps on a new stream per epoch or worker holds a
+  // bounded 2 x [I, d] each, not one more set per stream.
   struct ItemTables {
     Tensor gi, grad;
+    uint64_t tick = 0;
   };
+  static constexpr size_t kItemTableSets = 2;
   mutable std::mutex it_mu;
   mutable std::map<int64_t, ItemTables> it;
+  mutable uint64_t it_tick = 0;
+  // the set for stream `skey` (it_mu held), evicting the LRU set first when full
+  ItemTables &item_tables(int64_t skey) const {
+    auto f = it.find(skey);
+    if (f == it.end()) {
+      if (it.size() >= kItemTableSets) {
+        auto lru = it.begin();
+        for (auto j = it.begin(); j != it.end(); ++j)
+          if (j->second.tick < lru->second.tick) lru = j;
+        it.erase(lru);
+      }
+      f = it.emplace(skey, ItemTables{}).first;
+    }
+    f->second.tick = ++it_tick;
+    return f->second;
+  }
 };
 
 static std::mutex g_mu;
@@ -1242,10 +1263,14 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_cuda(
 // holds a bounded n_rows int32 each (20 MB for U = 5M). An entry inherited by a
 // new stream at a recycled address is still all INT32_MAX once the old
 // stream's work has drained, which destroying a stream waits for.
+// `role` keeps tables a single launch uses side by side apart: bbgr_ego_slots
+// takes a user and an item table at once, which must not be one buffer when
+// U == I (0 = first_slot, 1 = ego users, 2 = ego items).
 static constexpr size_t kFirstSlotScratch = 8;
-static Tensor slot_scratch(int64_t n_rows, const at::Device &dev) {
+static Tensor slot_scratch(int64_t n_rows, const at::Device &dev, int64_t role = 0) {
   static std::mutex mu;
-  static std::map<std::tuple<int64_t, int64_t, int64_t>, std::pair<Tensor, uint64_t>> scratch;
+  static std::map<std::tuple<int64_t, int64_t, int64_t, int64_t>, std::pair<Tensor, uint64_t>>
+      scratch;
   static uint64_t tick = 0;
   const auto fresh = [&] {
     return at::full({std::max<int64_t>(n_rows, 1)}, 0x7fffffff,
@@ -1253,7 +1278,8 @@ static Tensor slot_scratch(int64_t n_rows, const at::Device &dev) {
   };
   if (capturing()) return fresh();   // a captured step fills its own (the fill replays with it)
   std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_tuple((int64_t)dev.index(), n_rows, (int64_t)(intptr_t)cur_stream());
+  const auto key =
+      std::make_tuple((int64_t)dev.index(), n_rows, (int64_t)(intptr_t)cur_stream(), role);
   auto it = scratch.find(key);
   if (it == scratch.end()) {
     if (scratch.size() >= kFirstSlotScratch) {
@@ -1293,7 +1319,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
   Tensor ix = at::empty({6 * B}, users.options());
   Tensor iu = ix.narrow(0, 0, B), ii = ix.narrow(0, B, 2 * B), cu = ix.narrow(0, 3 * B, B),
          sp = ix.narrow(0, 4 * B, B), sn = ix.narrow(0, 5 * B, B);
-  Tensor fu = slot_scratch(U, users.device()), fi = slot_scratch(I, users.device());
+  Tensor fu = slot_scratch(U, users.device(), 1), fi = slot_scratch(I, users.device(), 2);
   check(bbgr_ego_slots(B, users.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
                        neg.data_ptr<int64_t>(), U, I, fu.data_ptr<int32_t>(),
                        fi.data_ptr<int32_t>(), iu.data_ptr<int64_t>(), ii.data_ptr<int64_t>(),
@@ -1381,7 +1407,7 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   Pair::ItemTables fresh, *tp = &fresh;
   if (cached) {
     lk.lock();
-    tp = &P->it[skey];
+    tp = &P->item_tables(skey);
   }
   Pair::ItemTables &t = *tp;
   if (!t.gi.defined() || t.gi.size(1) != d || t.gi.device() != uf.device()) {
@@ -1816,6 +1842,13 @@ static void unregister_pair(int64_t key) {
 // backward the autograd graph took
 static std::vector<int64_t> counters() { return {g_rows_backward.load(), g_dense_backward.load()}; }
 
+// the in-backward Adam's cached item table sets of a pair (tests bound it)
+static int64_t item_table_sets(int64_t key) {
+  auto P = pair_of(key);
+  std::lock_guard<std::mutex> lk(P->it_mu);
+  return (int64_t)P->it.size();
+}
+
 }  // namespace bbgr_torch
 
 TORCH_LIBRARY(bbgr, m) {
@@ -1846,6 +1879,7 @@ TORCH_LIBRARY(bbgr, m) {
         &bbgr_torch::register_pair);
   m.def("_unregister_pair(int key) -> ()", &bbgr_torch::unregister_pair);
   m.def("_counters() -> int[]", &bbgr_torch::counters);
+  m.def("_item_table_sets(int key) -> int", &bbgr_torch::item_table_sets);
 }
 
 TORCH_LIBRARY_IMPL(bbgr, CUDA, m) {

@@ -9,6 +9,7 @@ Bias corrections are computed on the host in double, as torch does.
 from __future__ import annotations
 
 import math
+import warnings
 
 import numpy as np
 import torch
@@ -171,7 +172,15 @@ class FusedAdam(torch.optim.Optimizer):
     fused epilogue streams them and reads only the weight rows through the row
     map. The optimizer converts them once, and back wherever they leave it:
     state_dict(), moments(), and a step() that updates them outside the
-    backward. load_state_dict() takes the caller's order, as torch's Adam."""
+    backward. load_state_dict() takes the caller's order, as torch's Adam.
+
+    The fused step assumes bpr_loss is the only consumer of the two tables in
+    the loss. A gradient that reaches them by another path (e.g. a term
+    `lam * W.norm()` added to the loss) lands in .grad and cannot join the
+    update already made inside the backward: step() raises on it rather than
+    drop it. A parameter is owned by the last FusedAdam(fuse_backward=True)
+    built over it; building a second one over a parameter a live one owns
+    warns (the first then steps it outside the backward)."""
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, fuse_backward: bool = False):
@@ -188,6 +197,12 @@ class FusedAdam(torch.optim.Optimizer):
             me = weakref.ref(self)
             for g in self.param_groups:
                 for p in g["params"]:
+                    e = _IN_BACKWARD.get(id(p))
+                    if e is not None and e[0]() is p and e[1]() is not None:
+                        warnings.warn("FusedAdam(fuse_backward=True): a parameter owned by "
+                                      "another live in-backward FusedAdam moves to this one; "
+                                      "the other steps it outside the backward from now on",
+                                      RuntimeWarning, stacklevel=2)
                     _IN_BACKWARD[id(p)] = (weakref.ref(p), me)
 
     def _group_of(self, params):
@@ -299,6 +314,15 @@ class FusedAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 if id(p) in self._stepped:   # stepped inside the backward already
                     self._stepped.discard(id(p))
+                    # a gradient from another term of the loss cannot join the
+                    # update already made: refuse to drop it silently (a zero
+                    # .grad from zero_grad(set_to_none=False) is fine)
+                    if p.grad is not None and bool(p.grad.ne(0).any()):
+                        raise RuntimeError(
+                            "FusedAdam(fuse_backward=True): a parameter stepped inside "
+                            "the backward also has a .grad from another term of the loss; "
+                            "the in-backward step assumes bpr_loss is its only consumer "
+                            "(use fuse_backward=False for such losses)")
                     continue
                 if p.grad is None:
                     continue

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 9
+#define BBGR_ABI_VERSION 10
 
 typedef enum {
   BBGR_OK = 0,
@@ -725,6 +725,9 @@ int bbgr_list_positions(int64_t n_max, const int64_t *list, const int64_t *count
 /*   1+n_neg candidates scored <uf[u], itf[c]> and ranked descending, ties    */
 /*   in candidate order (pos first). Writes pos_rank[n_users],                */
 /*   topk[n_users*k_max] (-1 padded), optional cand_out[n_users*(1+n_neg)].   */
+/*   cand_in (nullable, ABI 10): the candidates are taken from                */
+/*   cand_in[b*(1+n_neg) + c] (c = 0 the positive) instead of drawn; the      */
+/*   reference's own numpy stream, drawn by bbgr_eval_draw_candidates.        */
 /* Full: every item scored <uf[u], itf[i]> with fp32 MFMA (one fmaf chain    */
 /*   per score, components in the order 0, d/2, 1, d/2+1, ...), train items   */
 /*   set to -1e9, ranked by (score desc, item asc); topk[n_users*k_max] and   */
@@ -763,12 +766,40 @@ typedef struct {
   int32_t *cand_out;       /* sampled only, nullable */
   int32_t *fail_count;     /* sampled only, nullable */
   double *sums;
+  const int32_t *cand_in;  /* sampled only, nullable (ABI 10) */
 } bbgr_eval_args;
 
 int bbgr_eval_sampled(const bbgr_eval_args *args, void *workspace, size_t *workspace_bytes,
                       bbgr_stream_t stream);
 int bbgr_eval_full(const bbgr_eval_args *args, void *workspace, size_t *workspace_bytes,
                    bbgr_stream_t stream);
+
+/* The reference's candidate draws, bit for bit (HOST code, host arrays; ABI  */
+/* 10). evaluate_sampled (Version-2/lighgcn_cu_pop.py:554-589, the same loop  */
+/* in lightgcn.py:406-429, lightgcn_cu.py:496-519,                            */
+/* version_1/lightgcn_cu_pop_long_tail_exposure.py:494-517) draws from        */
+/* np.random.default_rng(seed + 999), per evaluated user u in order:          */
+/*   pos = gt[rng.integers(0, len(gt))]  (gt = the user's test row)           */
+/*   repeat until n_neg: j = rng.integers(0, n_items); skip j if j is in gt   */
+/*   or user_has_item(train, u, j) (np.searchsorted in the train row, :330);  */
+/*   otherwise append j (duplicates kept).                                    */
+/* rng is numpy's PCG64 bit generator state (bit_generator.state: the 128-bit */
+/* state and increment, has_uint32, uinteger), advanced in place exactly as   */
+/* numpy advances it: scalar integers(0, n) on int64 is Lemire's bounded      */
+/* draw on buffered 32-bit outputs (n - 1 < 2^32; 64-bit outputs above).      */
+/* cand[b*(1+n_neg) + c]: c = 0 the positive, 1.. the negatives. users must   */
+/* have non-empty test rows. Returns BBGR_ERR_INVALID if a user cannot get    */
+/* n_neg negatives (the reference's loop would not end).                      */
+typedef struct {
+  uint64_t state_hi, state_lo;   /* the 128-bit LCG state */
+  uint64_t inc_hi, inc_lo;       /* the 128-bit increment (odd) */
+  int32_t has_uint32;
+  uint32_t uinteger;
+} bbgr_pcg64;
+int bbgr_eval_draw_candidates(bbgr_pcg64 *rng, int64_t n_users, const int64_t *users,
+                              const int64_t *te_indptr, const int64_t *te_indices,
+                              const int64_t *tr_indptr, const int64_t *tr_indices,
+                              int64_t n_items, int32_t n_neg, int32_t *cand);
 
 /* ------------------------------------------------------------------------- */
 /* Blueprint names (SURVEY §8(b)'s ABI sketch), thin forms of the above.      */

@@ -446,14 +446,38 @@ def make_cred_groups(users, cred, pct):
     return users[order[-k:]], users[order[:k]]
 
 
+def sampled_candidates_reference_style(rng, users, tr_ptr, tr_idx, te_ptr, te_idx, num_items,
+                                       n_neg=99):
+    """The candidate draws of the reference's loop (Version-2:575-589), literal:
+    per user in order, pos = gt[rng.integers(0, len(gt))], then negatives by
+    rejection on gt_set and user_has_item. Advances `rng` as the reference
+    does; returns [n_users, 1 + n_neg] int64."""
+    cands = []
+    for u in users:
+        gt = te_idx[te_ptr[u]:te_ptr[u + 1]]
+        gt_set = set(map(int, gt.tolist()))
+        pos = int(gt[rng.integers(0, len(gt))])
+        negs = []
+        while len(negs) < n_neg:
+            j = int(rng.integers(0, num_items))
+            if j in gt_set:
+                continue
+            if user_has_item(tr_ptr, tr_idx, int(u), j):
+                continue
+            negs.append(j)
+        cands.append([pos] + negs)
+    return np.asarray(cands, np.int64).reshape(len(users), 1 + n_neg)
+
+
 def evaluate_sampled_reference_style(tr_ptr, tr_idx, te_ptr, te_idx, uf, itf, num_items, item_pop,
                                      total_train, cred, Ks=(10, 20), n_neg=99, pct=0.2, seed=1041,
-                                     users=None):
+                                     users=None, rng=None):
     """The whole reference loop (Version-2:536-650) including its numpy
     sampling stream (default_rng(seed); pos via integers(0, len(gt)); negatives
     by rejection on gt_set and user_has_item). `users` restricts the loop to a
-    subset (the CPU-baseline sample); returns (results, candidates)."""
-    rng = np.random.default_rng(seed)
+    subset (the CPU-baseline sample); `rng` (optional) is the Generator to draw
+    from, left in its end state; returns (results, candidates)."""
+    rng = np.random.default_rng(seed) if rng is None else rng
     if users is None:
         users = np.where(np.diff(te_ptr) > 0)[0].astype(np.int64)
     cands = []

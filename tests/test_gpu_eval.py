@@ -1,11 +1,14 @@
 """GPU: sampled evaluation (bbgr_eval_sampled) vs the oracle restatement of
 Version-2/lighgcn_cu_pop.py:536-650 on the SAME candidates.
 
-The candidates come from the device Philox stream (numpy's PCG64 stream is not
-reproduced: distributional parity), so the test (1) checks every candidate
-invariant exactly and (2) feeds the device's candidates to the float64 oracle
-and compares the metrics. fp32 vs float64 scores can swap a near-tie, so
-per-user hit metrics may differ for at most 2 users."""
+The native evaluate_sampled draws its candidates from the device Philox
+stream, so those tests (1) check every candidate invariant exactly and (2) feed
+the device's candidates to the float64 oracle and compare the metrics (fp32 vs
+float64 scores can swap a near-tie, so per-user hit metrics may differ for at
+most 2 users). The reference-signature wrappers draw the reference's own
+numpy stream on the host (bbgr_eval_draw_candidates): their results are
+checked against the whole reference loop, sampling included
+(test_reference_signature_evaluation_is_the_reference_loop)."""
 import numpy as np
 import pytest
 import torch
@@ -239,12 +242,20 @@ def test_evaluate_with_the_reference_signatures(family):
     want_pop, want_total, want_cred = (pop, int(tr.shape[1]), cred) if v2 else \
         (pop, int(tr.shape[1]), np.ones(U, np.float32))
     got = mod.evaluate_sampled(m, tr_csr, te_csr, I, DEV, *extra)
+    # the wrapper's host parts: the reference's users, groups, credibility mean
+    # and numpy candidate stream
+    users = np.where(np.diff(te_csr[0]) > 0)[0].astype(np.int64)
+    flags = EV.cred_group_flags(users, want_cred, 0.2)
+    cu = float(np.add.accumulate(want_cred[users].astype(np.float64))[-1]) / users.size
+    cand = EV.draw_candidates(np.random.default_rng(42 + 999), users, tr_csr, te_csr, I, 99)
+    host = dict(users=torch.from_numpy(users), groups=torch.from_numpy(flags), cred_utility=cu)
     want = EV.evaluate_sampled(ue, ie, trc, tec, I, want_pop, want_total, want_cred,
-                               seed=42 + 999)
+                               cand=cand, **host)
     checks = [(got, want, "sampled(1pos+neg)")]
     if hasattr(mod, "evaluate_full_ranking"):
         checks.append((mod.evaluate_full_ranking(m, tr_csr, te_csr, I, DEV, *extra),
-                       EV.evaluate_full(ue, ie, trc, tec, I, want_pop, want_total, want_cred),
+                       EV.evaluate_full(ue, ie, trc, tec, I, want_pop, want_total, want_cred,
+                                        **host),
                        "full"))
     for got, want, mode in checks:
         assert sorted(got) == [10, 20]
@@ -259,3 +270,93 @@ def test_evaluate_with_the_reference_signatures(family):
     with pytest.raises(RuntimeError, match="No users with test interactions"):
         empty = (np.zeros(U + 1, np.int64), np.zeros(0, np.int64))
         mod.evaluate_sampled(m, tr_csr, empty, I, DEV, *extra)
+
+
+@pytest.mark.parametrize("family", ["v2_pop", "method_a", "cu_fair", "plain"])
+def test_reference_signature_evaluation_is_the_reference_loop(family):
+    """Each drop-in module's evaluate_sampled / evaluate_full_ranking against the
+    reference's whole loop restated on the CPU (Version-2/lighgcn_cu_pop.py:
+    536-752; lightgcn.py:398-520, lightgcn_cu.py:488-560 and version_1 for the
+    older families), on a C1-sized model (943 users x 1682 items, 100K edges,
+    80/20 split) with heavily tied credibilities (0.0 / 1.0 / 0.5):
+    - sampled: the restatement draws pos and negatives from
+      np.random.default_rng(seed + 999) itself (numpy's integers, gt_set and
+      user_has_item rejection), groups by np.argsort: the package's candidates
+      equal it exactly, its Generator ends in the same state, the integer
+      results (users, group sizes, coverage counts) are equal and the floats
+      agree to 1e-6 relative;
+    - full ranking: the restatement ranks by the kernel's score arithmetic
+      (oracle/csrc/eval_full.c, one fp32 fma chain per score; the reference's
+      own torch reduction order is unspecified), then runs the reference's
+      metric loop with its groups: integers equal, floats to 1e-6."""
+    from bbgr import evaluation as EV
+    from bbgr import host_sampler as HS
+    from bbgr import lightgcn as SYM
+    from bbgr import lightgcn_cu as CU
+    from bbgr import lightgcn_cu_pop as V2
+    from bbgr import lightgcn_cu_pop_long_tail_exposure as MA
+    from oracle import native as N
+    U, I, d = 943, 1682, 64
+    tr, te = _split(U, I, 100_000, 41)
+    rng = np.random.default_rng(41)
+    cred = rng.choice(np.array([0.0, 1.0, 0.5], np.float32), U, p=[0.45, 0.45, 0.1])
+    torch.manual_seed(41)
+    if family == "v2_pop":
+        mod, m = V2, V2.LightGCN(U, I, d, 3, *V2.build_message_passing_mats(
+            tr, U, I, torch.as_tensor(cred), DEV)).to(DEV)
+    elif family == "method_a":
+        mod, m = MA, MA.LightGCN(U, I, d, 3, *MA.build_message_passing_mats(
+            tr, U, I, torch.as_tensor(cred), DEV)).to(DEV)
+    elif family == "cu_fair":
+        M_ui, M_iu, _ = CU.build_cred_weighted_mats(tr, U, I, cred, DEV)
+        mod, m = CU, CU.CredLightGCN(U, I, d, 3, M_ui, M_iu).to(DEV)
+    else:
+        mod, m = SYM, SYM.LightGCN(U, I, d, 3, SYM.build_norm_adj(tr, U, I, DEV)).to(DEV)
+    tr_csr, te_csr = HS.edges_to_user_csr(tr, U), HS.edges_to_user_csr(te, U)
+    pop = np.bincount(tr[1].astype(np.int64), minlength=I)
+    total = int(tr.shape[1])
+    v2 = family == "v2_pop"
+    extra = (pop, total, cred) if v2 else ()
+    r_cred = cred if v2 else np.ones(U, np.float32)
+    with torch.no_grad():
+        ue, ie = m.final_embeddings() if family == "cu_fair" else m.get_user_item_emb()
+        uf, itf = (torch.as_tensor(x).clone().cpu().numpy() for x in (ue, ie))
+    users = np.where(np.diff(te_csr[0]) > 0)[0].astype(np.int64)
+    hi, lo = R.make_cred_groups(users, r_cred, 0.2)
+    # -- sampled
+    got = EV.evaluate_sampled_reference(m, tr_csr, te_csr, I, DEV, *extra, return_raw=True)
+    raw = got.pop("_raw")
+    r_rng = np.random.default_rng(42 + 999)
+    want, cands = R.evaluate_sampled_reference_style(*tr_csr, *te_csr, uf, itf, I, pop, total,
+                                                     r_cred, Ks=(10, 20), n_neg=99, pct=0.2,
+                                                     rng=r_rng)
+    np.testing.assert_array_equal(raw["cand"].cpu().numpy(), np.asarray(cands))
+    assert raw["rng_state"] == r_rng.bit_generator.state
+    flags = raw["groups"].cpu().numpy()
+    assert set(users[flags & 1 > 0].tolist()) == set(hi.tolist())
+    assert set(users[flags & 2 > 0].tolist()) == set(lo.tolist())
+    # the module export is the same call
+    exp = mod.evaluate_sampled(m, tr_csr, te_csr, I, DEV, *extra)
+    for K in (10, 20):
+        assert exp[K] == got[K]
+    # -- full ranking (the scripts that have it)
+    checks = [(got, want)]
+    if hasattr(mod, "evaluate_full_ranking"):
+        fgot = mod.evaluate_full_ranking(m, tr_csr, te_csr, I, DEV, *extra)
+        o_items, o_scores = N.full_topk(users, *tr_csr, uf, itf, 20)
+        o_items = np.where(np.isneginf(o_scores), -1, o_items)
+        fwant = R.evaluate_given_topk(users, o_items, *te_csr, pop, total, I, r_cred, hi, lo,
+                                      Ks=(10, 20))
+        checks.append((fgot, fwant))
+    for g, w in checks:
+        for K in (10, 20):
+            for k, v in g[K].items():
+                if k in ("mode", "negatives"):
+                    continue
+                if k in w[K] and isinstance(w[K][k], int):
+                    assert v == w[K][k], (family, K, k)
+                elif k in w[K]:
+                    assert v == pytest.approx(w[K][k], rel=1e-6, abs=1e-12), (family, K, k)
+            if "item_coverage" in g[K]:   # the coverage numerator is an integer
+                assert round(g[K]["item_coverage"] * I) == round(w[K]["item_coverage"] * I)
+            assert g[K]["users_eval"] == users.size

@@ -23,12 +23,12 @@ DEV = "cuda"
 U, I, E, D, B = 1500, 700, 20000, 64, 512
 
 
-def _model(K, module=V2, lazy_on=True, seed=0):
-    e = synthetic_edges(U, I, E, seed=4, items="zipf")
+def _model(K, module=V2, lazy_on=True, seed=0, n_items=I):
+    e = synthetic_edges(U, n_items, E, seed=4, items="zipf")
     torch.manual_seed(seed)
     cred = torch.as_tensor(synthetic_credibility(U, 4))
-    M_ui, M_iu = module.build_message_passing_mats(e, U, I, cred, DEV)
-    m = module.LightGCN(U, I, D, K, M_ui, M_iu).to(DEV)
+    M_ui, M_iu = module.build_message_passing_mats(e, U, n_items, cred, DEV)
+    m = module.LightGCN(U, n_items, D, K, M_ui, M_iu).to(DEV)
     m.lazy_finals = lazy_on
     return m
 
@@ -234,7 +234,89 @@ def test_fused_backward_adam_moments_leave_in_the_callers_order():
         assert float((pa - pb).norm() / pb.norm()) < 1e-5
         for x, y in zip(oa.moments(pa), ob.moments(pb)):
             assert float((x - y).norm() / y.norm()) < 1e-5
-    oc = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
+    with pytest.warns(RuntimeWarning, match="another live in-backward FusedAdam"):
+        oc = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)   # takes them from oa
     oc.load_state_dict(oa.state_dict())
     for pa in a.parameters():
         assert all(torch.equal(x, y) for x, y in zip(oc.moments(pa), oa.moments(pa)))
+
+
+def test_fused_backward_adam_with_as_many_items_as_users(monkeypatch):
+    """num_users == num_items: the ego rows' first-slot tables of the users and
+    of the items are two buffers (one launch fills both; a shared buffer sent
+    ego-L2 rows to wrong rows). The in-backward step and the
+    deferred sparse-ego loss against the dense separate step."""
+    from bbgr.optim import FusedAdam
+    batches = [_batch(s) for s in range(3)]
+    batches[1][0][5] = batches[1][0][6]   # a repeated user
+    for bt in batches:                    # items drawn from [0, U) too
+        g = torch.Generator().manual_seed(int(bt[0][0]))
+        bt[1][:] = torch.randint(0, U, (B,), generator=g).to(DEV)
+        bt[2][:] = torch.randint(0, U, (B,), generator=g).to(DEV)
+        bt[1][:8] = bt[0][:8]             # item ids equal to user ids of the batch
+    # the deferred loss (bpr_loss_sparse_ego's backward) vs the dense ego table
+    from bbgr import bpr
+    a, b = _model(3, n_items=U), _model(3, n_items=U, lazy_on=False)
+    ra = _steps(a, batches)
+    monkeypatch.setattr(bpr, "_receives_dense_grad", lambda *x: False)
+    rb = _steps(b, batches)
+    monkeypatch.undo()
+    for (la, ga), (lb, gb) in zip(ra, rb):
+        assert la == lb
+        for x, y in zip(ga, gb):
+            assert torch.equal(x, y)
+    # the in-backward Adam vs the separate step
+    c, d = _model(3, n_items=U), _model(3, n_items=U)
+    w0 = [p.detach().clone() for p in d.parameters()]
+    oc = FusedAdam(c.parameters(), lr=1e-3, fuse_backward=True)
+    od = FusedAdam(d.parameters(), lr=1e-3)
+    for k, (users, pos, neg) in enumerate(batches):
+        for m, o in ((c, oc), (d, od)):
+            uf, itf = m.get_user_item_emb()
+            loss = m.bpr_loss(users, pos, neg, uf, itf, 1e-2)   # a large ego term
+            o.zero_grad()
+            loss.backward()
+            o.step()
+        if k == 0:
+            for pc, pd in zip(c.parameters(), d.parameters()):
+                for x, y in zip(oc.moments(pc), od.moments(pd)):
+                    assert float((x - y).norm() / y.norm()) < 1e-6
+    for pc, pd, p0 in zip(c.parameters(), d.parameters(), w0):
+        dc, dd = pc.detach() - p0, pd.detach() - p0
+        assert float((dc - dd).norm() / dd.norm()) < 1e-3
+
+
+def test_fused_backward_item_tables_bounded_over_streams():
+    """The in-backward Adam keeps its two [I, d] item tables per stream; a
+    caller stepping on a new stream each time holds at most two sets."""
+    from bbgr.optim import FusedAdam
+    from bbgr.ops import pair_key
+    a = _model(3)
+    oa = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
+    key = pair_key(a._operator_pair())
+    for s in range(4):
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            uf, itf = a.get_user_item_emb()
+            oa.zero_grad()
+            a.bpr_loss(*_batch(s), uf, itf, 1e-4).backward()
+            oa.step()
+        torch.cuda.current_stream().wait_stream(st)
+        assert torch.ops.bbgr._item_table_sets(key) == min(s + 1, 2)
+    assert all(int(oa.state[p]["step"]) == 4 for p in a.parameters())
+    assert all(torch.isfinite(p).all() for p in a.parameters())
+
+
+def test_fused_backward_adam_refuses_a_second_gradient_path():
+    """A loss term that reads the weights directly puts a .grad on a table the
+    in-backward step already updated: step() raises instead of dropping it."""
+    from bbgr.optim import FusedAdam
+    a = _model(3)
+    oa = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
+    uf, itf = a.get_user_item_emb()
+    loss = a.bpr_loss(*_batch(0), uf, itf, 1e-4) + 1e-3 * a.user_emb.weight.norm()
+    oa.zero_grad()
+    loss.backward()
+    with pytest.raises(RuntimeError, match="only consumer"):
+        oa.step()

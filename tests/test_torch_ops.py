@@ -23,7 +23,7 @@ SCHEMAS = {
 NAMES = ["propagate", "propagate_backward", "propagate_backward_rows", "jacobi_layer",
          "jacobi_layer_backward", "propagate_sym", "propagate_sym_backward", "bpr_loss",
          "bpr_loss_backward", "bpr_loss_sparse_ego", "_register_pair", "_unregister_pair",
-         "_counters"]
+         "_counters", "_item_table_sets"]
 
 
 def test_every_operator_is_registered_from_cpp():

@@ -10,7 +10,7 @@ run() {  # tag, parts, lib
   env ${lib:+BBGR_LIB=$PWD/$L/$lib/libbbgr.so} timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-torch-reference --dense-check 0 --emulate-columns $parts > gpurun_out/abn/$tag.json 2> gpurun_out/abn/$tag.log || { echo "BENCH $tag FAILED"; tail -20 gpurun_out/abn/$tag.log; exit 1; }
   python -c "
 import json;j=json.load(open('gpurun_out/abn/$tag.json'))
-print('$tag', round(j['ms_per_step'],3), [(k['kind'],k['side'][:4],k.get('masks',''),round(k['avg_ms'],3)) for k in j['roofline']['per_kernel']])"
+print('$tag', round(j['ms_per_step'],3), [(k['kind'],k['side'][:4],k.get('masks',''),round(k['avg_ms'],3)) for k in j['roofline_per_kernel']])"
 }
 VARIANTS=${VARIANTS:-"c4base:4: c4w16:4:w16 c4mw16:4:mw16 c4r3:4:r3s16 c4base_b:4:"}
 for v in $VARIANTS; do

@@ -10,7 +10,7 @@ run() {  # tag, args, env...
   env "$@" timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-torch-reference --dense-check 0 $args > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.log || { echo "BENCH $tag FAILED"; tail -20 gpurun_out/ab/$tag.log; exit 1; }
   python -c "
 import json;j=json.load(open('gpurun_out/ab/$tag.json'))
-print('$tag', round(j['ms_per_step'],3), [(k['kind'],k['side'],k['d'],round(k['avg_ms'],3)) for k in j['roofline']['per_kernel'] if k['kind']=='adam'])"
+print('$tag', round(j['ms_per_step'],3), [(k['kind'],k['side'],k['d'],round(k['avg_ms'],3)) for k in j['roofline_per_kernel'] if k['kind']=='adam'])"
 }
 NOPF="BBGR_LIB=$PWD/beyond-binary-fake-user-detection-a-credibility-aware-graph-based-recommender-system_amd/lib/ab/nopf/libbbgr.so"
 run pf1 "" && run nopf1 "" $NOPF && run pf2 "" && run nopf2 "" $NOPF && \
