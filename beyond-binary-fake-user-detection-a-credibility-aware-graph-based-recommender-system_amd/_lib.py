@@ -148,6 +148,7 @@ _SIGNATURES = {
     "bbgr_last_error": ([], ctypes.c_char_p),
     "bbgr_device_info": ([ctypes.c_int, _P, ctypes.c_char_p, ctypes.c_int], c_int32),
     "bbgr_sync": ([_P], c_int32),
+    "bbgr_profile_marker": ([c_int32, _P], c_int32),
     "bbgr_csr_build": ([c_int64, _P, _P, c_int32, c_int32, _P, _P, _P, _P,
                         ctypes.POINTER(c_size_t), _P], c_int32),
     "bbgr_csr_plan_count": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(c_int32),

@@ -382,6 +382,9 @@ struct Flagged {
   __host__ __device__ bool operator()(const long &r) const { return mask[r] != 0; }
 };
 
+// bbgr_profile_marker: does nothing; its dispatches mark a trace window
+__global__ __launch_bounds__(64) void profile_marker_kernel() {}
+
 }  // namespace bbgr
 
 using namespace bbgr;
@@ -406,6 +409,13 @@ extern "C" int bbgr_device_info(int device, int *cu_count, char *arch_name,
 
 extern "C" int bbgr_sync(bbgr_stream_t stream) {
   BBGR_HIP(hipStreamSynchronize(as_stream(stream)));
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_profile_marker(int32_t tag, bbgr_stream_t stream) {
+  BBGR_REQUIRE(tag >= 1 && tag <= 1024, "bbgr_profile_marker: tag in [1, 1024]");
+  hipLaunchKernelGGL(profile_marker_kernel, dim3((unsigned)tag), dim3(64), 0, as_stream(stream));
+  BBGR_LAUNCHED("profile_marker_kernel");
   return BBGR_OK;
 }
 

@@ -51,6 +51,11 @@ const char *bbgr_last_error(void);
 int bbgr_device_info(int device, int *cu_count, char *arch_name, int arch_name_len);
 /* Blocks until `stream` has drained (the one explicit sync). */
 int bbgr_sync(bbgr_stream_t stream);
+/* An empty kernel, profile_marker_kernel, of `tag` workgroups (1 <= tag <=   */
+/* 1024; ABI 10): bench.py brackets its timed steps with tags 1 / 2 so a      */
+/* rocprofv3 trace can be cut at them by dispatch order                       */
+/* (tools/summarize_profile.py).                                              */
+int bbgr_profile_marker(int32_t tag, bbgr_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* CSR structure                                                              */

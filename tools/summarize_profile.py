@@ -32,6 +32,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def round_dir(tag: str) -> str:
     """profiles/ keeps each round's records in its own directory (r5x: round5)."""
     import re
+    if re.match(r"r6[a-z]", tag):
+        return "round6"
     if re.match(r"r5[a-z]", tag):
         return "round5"
     if re.match(r"r4[a-z]", tag):
@@ -39,6 +41,37 @@ def round_dir(tag: str) -> str:
     if re.match(r"r3([a-z]|$)", tag):
         return "round3"
     return "round1-2"
+
+
+def commit_id():
+    """BBGR_COMMIT, else this checkout's HEAD (the profile's tree is the one
+    gpurun sent; summarise right after the run), '+dirty' if files differ."""
+    c = os.environ.get("BBGR_COMMIT")
+    if c:
+        return c
+    import subprocess
+    try:
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"],
+                              capture_output=True, text=True, check=True).stdout.strip()
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no"],
+                               capture_output=True, text=True, check=True).stdout.strip()
+        return head + ("+dirty" if dirty else "")
+    except (OSError, subprocess.CalledProcessError):
+        return None
+
+
+def _bench_line(src: str) -> dict:
+    lines = open(os.path.join(src, "trace_bench.json")).read().strip().splitlines()
+    return json.loads(lines[-1])
+
+
+def bench_steps(src: str) -> int:
+    """The timed steps of the trace pass's bench run (its own JSON line)."""
+    return int(_bench_line(src)["steps"])
+
+
+def bench_ms_per_step(src: str) -> float:
+    return float(_bench_line(src)["ms_per_step"])
 
 
 def main(tag: str):
@@ -51,18 +84,39 @@ def main(tag: str):
     stats = {r["Name"]: r for r in csv.DictReader(
         open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
 
-    def pmc(kind):
-        d = collections.defaultdict(list)
-        for r in csv.DictReader(open(os.path.join(src, kind, "run_counter_collection.csv"))):
-            d[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
-        return d
+    def marked(rows, grid_of):
+        """(begin, end) dispatch ids of bench.py's two profile_marker_kernel
+        launches (grids of 1 and 2 workgroups of 64) around the timed steps."""
+        ids = {}
+        for r in rows:
+            if "profile_marker_kernel" in r["Kernel_Name"]:
+                ids[grid_of(r)] = int(r["Dispatch_Id"])
+        return (ids[64], ids[128]) if 64 in ids and 128 in ids else None
 
-    fetch, write = pmc("fetch"), pmc("write")
-    # per-dispatch durations by (kernel, grid) from the trace pass
-    dur = collections.defaultdict(list)
-    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
-        g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-        dur[(r["Kernel_Name"], g)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    def pmc(kind):
+        rows = list(csv.DictReader(open(os.path.join(src, kind, "run_counter_collection.csv"))))
+        win = marked(rows, lambda r: int(r["Grid_Size"]))
+        d, dw = collections.defaultdict(list), collections.defaultdict(list)
+        for r in rows:
+            key = (r["Kernel_Name"], int(r["Grid_Size"]))
+            d[key].append(float(r["Counter_Value"]))
+            if win and win[0] < int(r["Dispatch_Id"]) < win[1]:
+                dw[key].append(float(r["Counter_Value"]))
+        return d, dw, win
+
+    (fetch, fetch_w, fwin), (write, write_w, wwin) = pmc("fetch"), pmc("write")
+    # per-dispatch durations by (kernel, grid) from the trace pass; those
+    # between the markers (the timed steps) kept apart
+    trows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
+    tgrid = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])  # noqa: E731
+    twin = marked(trows, tgrid)
+    dur, dur_w = collections.defaultdict(list), collections.defaultdict(list)
+    for r in trows:
+        key = (r["Kernel_Name"], tgrid(r))
+        t = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        dur[key].append(t)
+        if twin and twin[0] < int(r["Dispatch_Id"]) < twin[1]:
+            dur_w[key].append(t)
     kernels = {}
     for key in sorted(set(fetch) | set(dur)):
         name, grid = key
@@ -96,7 +150,7 @@ def main(tag: str):
         n = sum(e["dispatches"] for e in dom)
         avg = sum(e["hbm_bytes_corrected"] * e["dispatches"] for e in dom) / n
         avg_us = sum(e["avg_us"] * e["dispatches"] for e in dom) / n
-        json.dump({"tag": tag, "commit": os.environ.get("BBGR_COMMIT"),
+        json.dump({"tag": tag, "commit": commit_id(),
                    "kernel": "spmm_kernel (full-CSR item<-user product)",
                    "hbm_bytes_per_launch_corrected": avg,
                    "fetch_KiB_per_launch": sum(e["FETCH_SIZE_KiB"] * e["dispatches"]
@@ -108,25 +162,41 @@ def main(tag: str):
                                 for e in dom},
                    "source": f"profiles/{round_dir(tag)}/{tag}_summary.json"},
                   open(os.path.join(top, "spmm_traffic.json"), "w"), indent=1)
-    # the whole step: every PMC-profiled kernel dispatched at least once per
-    # profiled step (one-time setup kernels dispatch fewer times), its bytes x
-    # dispatches / steps. BBGR_PROFILE_STEPS = the bench's warmup + timed +
-    # count steps under the profiler (profile_box.sh default 2 + 5 + 3).
-    steps = int(os.environ.get("BBGR_PROFILE_STEPS", "10"))
-    per_step = [e for e in kernels.values()
-                if "hbm_bytes_corrected" in e and e["dispatches"] >= steps]
-    if per_step and os.environ.get("BBGR_TRAFFIC_JSON", "1") != "0":
-        tot_b = sum(e["hbm_bytes_corrected"] * e["dispatches"] for e in per_step) / steps
-        tot_us = sum((e["avg_us"] or 0.0) * e["dispatches"] for e in per_step) / steps
-        json.dump({"tag": tag, "commit": os.environ.get("BBGR_COMMIT"), "steps": steps,
+    # the whole step: the dispatches between bench.py's two marker kernels
+    # (the timed steps; BBGR_PROFILE_MARKS=1 in profile_box.sh) in each pass,
+    # counted per (kernel, grid): per_step = count / steps must be an integer
+    # for every kernel, the bytes are the window's own dispatches' mean x
+    # count / steps, the time the trace pass's window durations / steps.
+    if twin and fwin and wwin and os.environ.get("BBGR_TRAFFIC_JSON", "1") != "0":
+        steps = int(os.environ.get("BBGR_PROFILE_STEPS") or bench_steps(src))
+        step_k, irregular = {}, {}
+        for key in sorted(dur_w):
+            name, grid = key
+            n = len(dur_w[key])
+            f, w = fetch_w.get(key, []), write_w.get(key, [])
+            e = {"per_step": n / steps, "avg_us": sum(dur_w[key]) / n / 1e3,
+                 "dispatches_in_window": {"trace": n, "fetch": len(f), "write": len(w)}}
+            if f and w:
+                e["hbm_bytes_corrected"] = (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024
+            (step_k if n % steps == 0 and len(f) == n and len(w) == n
+             else irregular)[f"{name}@{grid}"] = e
+        tot_b = sum(e["hbm_bytes_corrected"] * e["per_step"] for e in step_k.values()
+                    if "hbm_bytes_corrected" in e)
+        tot_us = sum(e["avg_us"] * e["per_step"] for e in step_k.values())
+        step_ms = bench_ms_per_step(src)
+        json.dump({"tag": tag, "commit": commit_id(), "steps": steps,
+                   "selection": "dispatches between the bench's two profile markers (the timed "
+                                "steps), per (kernel, grid); per_step an exact integer",
                    "hbm_bytes_per_step_corrected": tot_b,
                    "kernel_us_per_step_pmc": tot_us,
-                   "kernels": {f'{e["kernel"]}@{e["grid"]}': {
-                       "per_step": e["dispatches"] / steps, "avg_us": e["avg_us"],
-                       "hbm_bytes_corrected": e["hbm_bytes_corrected"]} for e in per_step},
+                   "trace_ms_per_step": step_ms,
+                   "kernels": {k: {**e, "per_step": int(e["per_step"])}
+                               for k, e in step_k.items()},
+                   "irregular": irregular or None,
                    "note": "2*FETCH_SIZE+WRITE_SIZE (gfx950 read correction) summed over the "
-                           "PMC-profiled kernels of one step; FETCH_SIZE counts Infinity-Cache "
-                           "hits, so this bounds the step's HBM bytes from above",
+                           "kernels of one timed step; FETCH_SIZE counts Infinity-Cache hits, "
+                           "so this bounds the step's HBM bytes from above; kernel_us_per_step "
+                           "<= trace_ms_per_step (the trace pass's own bench line)",
                    "source": f"profiles/{round_dir(tag)}/{tag}_summary.json"},
                   open(os.path.join(top, "step_traffic.json"), "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
