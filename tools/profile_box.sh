@@ -10,6 +10,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export BBGR_PROFILE_MARKS=1
+echo "${BBGR_COMMIT:-unknown}" > $OUT/commit.txt   # set by the caller: the box has no .git
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run \
   -- python3 bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace_bench.log
 # every kernel (no include filter): profiles/step_traffic.json sums a whole step

@@ -43,12 +43,16 @@ def round_dir(tag: str) -> str:
     return "round1-2"
 
 
-def commit_id():
+def commit_id(src=None):
     """BBGR_COMMIT, else this checkout's HEAD (the profile's tree is the one
     gpurun sent; summarise right after the run), '+dirty' if files differ."""
     c = os.environ.get("BBGR_COMMIT")
     if c:
         return c
+    if src and os.path.exists(os.path.join(src, "commit.txt")):   # written by profile_box.sh
+        c = open(os.path.join(src, "commit.txt")).read().strip()
+        if c and c != "unknown":
+            return c
     import subprocess
     try:
         head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"],
@@ -79,6 +83,7 @@ def main(tag: str):
     top = os.path.join(ROOT, "profiles")
     dst = os.path.join(top, round_dir(tag))
     os.makedirs(dst, exist_ok=True)
+    commit = commit_id(src)   # before this run rewrites the tracked traffic files
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(
@@ -150,7 +155,7 @@ def main(tag: str):
         n = sum(e["dispatches"] for e in dom)
         avg = sum(e["hbm_bytes_corrected"] * e["dispatches"] for e in dom) / n
         avg_us = sum(e["avg_us"] * e["dispatches"] for e in dom) / n
-        json.dump({"tag": tag, "commit": commit_id(),
+        json.dump({"tag": tag, "commit": commit,
                    "kernel": "spmm_kernel (full-CSR item<-user product)",
                    "hbm_bytes_per_launch_corrected": avg,
                    "fetch_KiB_per_launch": sum(e["FETCH_SIZE_KiB"] * e["dispatches"]
@@ -164,29 +169,36 @@ def main(tag: str):
                   open(os.path.join(top, "spmm_traffic.json"), "w"), indent=1)
     # the whole step: the dispatches between bench.py's two marker kernels
     # (the timed steps; BBGR_PROFILE_MARKS=1 in profile_box.sh) in each pass,
-    # counted per (kernel, grid): per_step = count / steps must be an integer
-    # for every kernel, the bytes are the window's own dispatches' mean x
-    # count / steps, the time the trace pass's window durations / steps.
+    # counted per kernel: per_step = count / steps must be an integer for every
+    # kernel (a row-list launch's grid follows its list, so grids vary from
+    # step to step: they are listed per kernel, not counted apart); bytes and
+    # time are the window's own dispatches summed / steps.
     if twin and fwin and wwin and os.environ.get("BBGR_TRAFFIC_JSON", "1") != "0":
         steps = int(os.environ.get("BBGR_PROFILE_STEPS") or bench_steps(src))
+        by_name = collections.defaultdict(list)
+        for key in dur_w:
+            by_name[key[0]].append(key)
         step_k, irregular = {}, {}
-        for key in sorted(dur_w):
-            name, grid = key
-            n = len(dur_w[key])
-            f, w = fetch_w.get(key, []), write_w.get(key, [])
-            e = {"per_step": n / steps, "avg_us": sum(dur_w[key]) / n / 1e3,
-                 "dispatches_in_window": {"trace": n, "fetch": len(f), "write": len(w)}}
-            if f and w:
-                e["hbm_bytes_corrected"] = (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024
-            (step_k if n % steps == 0 and len(f) == n and len(w) == n
-             else irregular)[f"{name}@{grid}"] = e
-        tot_b = sum(e["hbm_bytes_corrected"] * e["per_step"] for e in step_k.values()
-                    if "hbm_bytes_corrected" in e)
-        tot_us = sum(e["avg_us"] * e["per_step"] for e in step_k.values())
+        for name, keys in sorted(by_name.items()):
+            n = sum(len(dur_w[k]) for k in keys)
+            nf = sum(len(fetch_w.get(k, [])) for k in keys)
+            nw = sum(len(write_w.get(k, [])) for k in keys)
+            e = {"per_step": n / steps,
+                 "us_per_step": sum(sum(dur_w[k]) for k in keys) / steps / 1e3,
+                 "grids": sorted(k[1] for k in keys for _ in dur_w[k]),
+                 "dispatches_in_window": {"trace": n, "fetch": nf, "write": nw}}
+            if nf == n and nw == n:
+                e["hbm_bytes_per_step_corrected"] = sum(
+                    2 * sum(fetch_w[k]) + sum(write_w[k]) for k in keys) * 1024 / steps
+            if len(e["grids"]) > 8:
+                e["grids"] = sorted(set(e["grids"]))
+            (step_k if n % steps == 0 and nf == n and nw == n else irregular)[name] = e
+        tot_b = sum(e["hbm_bytes_per_step_corrected"] for e in step_k.values())
+        tot_us = sum(e["us_per_step"] for e in step_k.values())
         step_ms = bench_ms_per_step(src)
-        json.dump({"tag": tag, "commit": commit_id(), "steps": steps,
-                   "selection": "dispatches between the bench's two profile markers (the timed "
-                                "steps), per (kernel, grid); per_step an exact integer",
+        json.dump({"tag": tag, "commit": commit, "steps": steps,
+                   "selection": "kernels dispatched between the bench's two profile markers "
+                                "(the timed steps); per_step an exact integer per kernel",
                    "hbm_bytes_per_step_corrected": tot_b,
                    "kernel_us_per_step_pmc": tot_us,
                    "trace_ms_per_step": step_ms,
