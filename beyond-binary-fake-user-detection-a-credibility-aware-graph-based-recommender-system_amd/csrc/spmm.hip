@@ -14,9 +14,11 @@
 //     edges; each chunk is one 256-thread workgroup (16 groups on contiguous
 //     edge sub-ranges, fixed-order LDS reduction). Chunk blocks come first in
 //     the grid so the heavy (power-law) rows start early.
-//   * rows cut into >1 chunk write per-chunk partials; a fix-up launch sums
-//     them in chunk order. Every reduction order is fixed: the result is
-//     bitwise deterministic (no atomics).
+//   * rows cut into >1 chunk write per-chunk partials (write-through) and take
+//     an arrival ticket; the last-arriving chunk workgroup of the row sums the
+//     partials in chunk order and runs the epilogue, inside the same launch.
+//     Every reduction order is fixed: the result is bitwise deterministic (no
+//     floating-point atomics).
 #include <stdarg.h>
 #include <stdlib.h>
 

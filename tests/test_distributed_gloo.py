@@ -16,9 +16,12 @@ import torch.multiprocessing as mp
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _free_port():
-    from _ports import free_port
-    return free_port()
+def _spawn(fn, world, out):
+    """mp.spawn over a rendezvous store this process holds (tests/_ports.py)."""
+    from _ports import host_store
+    store, port = host_store(world)
+    mp.spawn(fn, args=(world, port, out), nprocs=world, join=True)
+    del store
 
 
 def _worker(rank, world, port, out):
@@ -27,8 +30,9 @@ def _worker(rank, world, port, out):
     import bbgr  # noqa: F401
     from bbgr.distributed import global_item_indptr, partition_users, shard_edges
     from oracle import ref_numpy as R
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                            world_size=world)
+    sys.path.insert(0, HERE)
+    from _ports import init_worker
+    init_worker(rank, world, port)
     g = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
     U, I, E, DUP, D, K, B = (int(x) for x in g["meta"])
     e, cred, u0, i0 = g["edges"], g["cred"], g["u0"], g["i0"]
@@ -63,7 +67,7 @@ def _worker(rank, world, port, out):
 
 def test_two_rank_schedule_matches_unsharded(tmp_path):
     from oracle import ref_numpy as R
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    _spawn(_worker, 2, str(tmp_path))
     r = [np.load(tmp_path / f"r{k}.npz") for k in range(2)]
     g = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
     U, I, E, DUP, D, K, B = (int(x) for x in g["meta"])
@@ -127,8 +131,9 @@ def _owner_worker(rank, world, port, out):
     sys.path.insert(0, os.path.dirname(HERE))
     import bbgr  # noqa: F401
     from bbgr.distributed import gather_owned, owner_bounds, refresh_from_owners
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                            world_size=world)
+    sys.path.insert(0, HERE)
+    from _ports import init_worker
+    init_worker(rank, world, port)
     I, d = 23, 5
     bounds = owner_bounds(I, world)
     g = torch.Generator().manual_seed(0)
@@ -149,7 +154,7 @@ def _owner_worker(rank, world, port, out):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_item_ownership_refresh_and_gather_are_exact(tmp_path, world):
-    mp.spawn(_owner_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    _spawn(_owner_worker, world, str(tmp_path))
     for k in range(world):
         z = np.load(tmp_path / f"own{k}.npz")
         rows = np.unique(np.clip(z["rows"], 0, None))

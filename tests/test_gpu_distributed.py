@@ -16,11 +16,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _free_port():
-    from _ports import free_port
-    return free_port()
-
-
 @pytest.mark.parametrize("variant,mode,frontier,world,order", [
     ("v2_pop", "strong", "frontier", 2, "input"), ("cu_fair", "strong", "frontier", 2, "input"),
     ("v2_pop", "strong", "dense", 2, "input"), ("v2_pop", "weak", "frontier", 2, "input"),
@@ -34,7 +29,7 @@ def test_sharded_step_vs_oracle(tmp_path, variant, mode, frontier, world, order)
     from oracle import ref_numpy as R
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--standalone", "--local-addr=127.0.0.1",
            os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, mode, frontier, order]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
@@ -102,7 +97,7 @@ def test_sharded_fused_adam_and_sparse_exchange(tmp_path, variant):
     gradient) == separate gradient + Adam, and the frontier-row (compacted)
     exchange == the dense item-table exchange, over three sharded steps."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--standalone", "--local-addr=127.0.0.1",
            os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, "fused"]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
@@ -159,7 +154,7 @@ def test_sharded_trainer_over_rccl_single_rank_matches_fused(tmp_path, variant, 
     """The sharded step with its collectives on RCCL (world size 1: the one
     RCCL configuration a 1-GPU box can run) equals the single-GPU step."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--standalone", "--local-addr=127.0.0.1",
            os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, "rccl1", "frontier",
            order]
     env = dict(os.environ, OMP_NUM_THREADS="4")
@@ -196,7 +191,7 @@ def test_column_sharded_step_matches_single_gpu(tmp_path, variant, frontier, ord
     products are summed per shard then across shards, and narrow rows (64/4 =
     16 columns) sum their edges in slot order."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={world}", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           f"--nproc-per-node={world}", "--standalone", "--local-addr=127.0.0.1",
            os.path.join(HERE, "dist_worker.py"), str(tmp_path), variant, "columns", frontier,
            order]
     env = dict(os.environ, OMP_NUM_THREADS="4")
@@ -224,7 +219,7 @@ def test_bench_two_ranks_on_c2(tmp_path, partition):
     chains = partition.endswith("+chains")
     partition = partition.split("+")[0]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--standalone", "--local-addr=127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "3",
            "--warmup", "1", "--dense-check", "1", "--frontier", "on", "--partition", partition,
            "--weak-beside", "2", "--partition-beside", "0", "--chain-beside", "0"] + \
@@ -250,7 +245,7 @@ def test_bench_two_ranks_survives_a_failed_beside_run(tmp_path):
     does not cost the line: the ranks agree on it, the line is the run that
     finished, and the failures are listed in beside_errors."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--standalone", "--local-addr=127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "2",
            "--warmup", "1", "--dense-check", "0", "--frontier", "on", "--weak-beside", "0",
            "--partition", "columns"]
@@ -269,7 +264,7 @@ def test_bench_sharded_single_rank_with_inline_collectives(tmp_path):
     every collective inline on the compute stream (--native-comm inline): one
     chain, no ranges, a JSON line with the step's value."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--standalone", "--local-addr=127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "1", "--sharded", "--config", "C2",
            "--steps", "3", "--warmup", "1", "--dense-check", "0", "--frontier", "on",
            "--native-comm", "inline", "--no-cpu-baseline", "--no-torch-reference"]
@@ -287,7 +282,7 @@ def test_bench_two_ranks_measures_both_partitions(tmp_path):
     graph is timed the same way in the same run; the faster is the line and the
     other is reported beside it."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--standalone", "--local-addr=127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "3",
            "--warmup", "1", "--dense-check", "1", "--frontier", "on", "--weak-beside", "0"]
     env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo")
