@@ -400,6 +400,74 @@ def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> d
                     "after the strong line in the same run"}
 
 
+# per-rank compute of the C4 user-row step at N = 8, measured alone (DESIGN
+# §6: one chain with inline collectives / two column chains): the constants of
+# the chain-setting rule; other (config, N) have no measured constants
+RANK_COMPUTE_MS = {("C4", 8): {"inline": 2.39, "two_chains": 2.90}}
+
+
+def allreduce_probe(dev, world: int, native: bool, sizes, iters: int = 5) -> dict:
+    """The item exchange's all-reduce alone: `sizes` bytes of fp32 through
+    torch's process group and (RCCL only) the C ABI's communicator inline on
+    the current stream, each timed over `iters` calls between a barrier + sync
+    on both sides, max over ranks. t_ar per call; bus bandwidth = 2(P-1)/P x
+    bytes / t_ar (a ring all-reduce's per-rank wire bytes), algorithm
+    bandwidth = bytes / t_ar."""
+    from bbgr.distributed import RcclItemComm
+    out = {"world": world, "iters": iters, "sizes_bytes": list(sizes)}
+    comm = RcclItemComm(device=dev, inline=True) if native else None
+    try:
+        for S in sizes:
+            t = torch.ones(S // 4, dtype=torch.float32, device=dev)
+            ways = [("torch", lambda: torch.distributed.all_reduce(t))]
+            if comm is not None:
+                ways.append(("cabi", lambda: comm.all_reduce(t)))
+            for name, run in ways:
+                for _ in range(2):
+                    run()
+                torch.cuda.synchronize()
+                torch.distributed.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    run()
+                torch.cuda.synchronize()
+                torch.distributed.barrier()
+                el = _allreduce(time.perf_counter() - t0, dev, torch.distributed.ReduceOp.MAX)
+                t_ar = el / iters
+                out[f"{name}_{S >> 20}MB"] = {
+                    "t_ar_ms": 1e3 * t_ar,
+                    "busbw_GBps": 2.0 * (world - 1) / world * S / t_ar / 1e9,
+                    "algbw_GBps": S / t_ar / 1e9}
+            del t
+    finally:
+        if comm is not None:
+            comm.close()
+    return out
+
+
+def chain_rule(probe: dict, config: str, world: int, K: int, dense_bytes: int,
+               frontier_bytes: int) -> dict | None:
+    """DESIGN §6 / §8 item 1 on the measured t_ar: one inline chain takes
+    n_dense t_ar(dense) + n_frontier t_ar(frontier) + its compute; two column
+    chains overlap the exchange with the other chain's products,
+    max(exchange, compute). The predicted faster setting runs first; both
+    are timed and the measured faster is the line."""
+    c = RANK_COMPUTE_MS.get((config, world))
+    if c is None or probe is None:
+        return None
+    key = lambda how, S: probe.get(f"{how}_{S >> 20}MB", {}).get("t_ar_ms")  # noqa: E731
+    n_dense, n_front = 2 * (K - 1), 2
+    inline_how = "cabi" if key("cabi", dense_bytes) is not None else "torch"
+    wire_inline = n_dense * key(inline_how, dense_bytes) + n_front * key(inline_how, frontier_bytes)
+    wire_two = n_dense * key("torch", dense_bytes) + n_front * key("torch", frontier_bytes)
+    pred_inline = wire_inline + c["inline"]
+    pred_two = max(wire_two, c["two_chains"])
+    return {"exchanges_per_step": {"dense": n_dense, "frontier": n_front},
+            "rank_compute_ms": c, "wire_ms": {"inline": wire_inline, "two_chains": wire_two},
+            "predicted_ms": {"inline": pred_inline, "two_chains": pred_two},
+            "predicted": "inline" if pred_inline < pred_two else "two_chains"}
+
+
 def step_summary(ms, dense_ms, torch_ref, dropin, dropin_fused, dropin_bwd) -> dict:
     """The step times of the line and of the runs beside it, in one small
     object printed last (the driver keeps the tail of stdout)."""
@@ -487,6 +555,8 @@ def main():
                     help="N>1 strong runs: afterwards time this many weak-scaled steps "
                          "(each rank a full config-sized shard) and report them beside "
                          "the strong line (0 = skip)")
+    ap.add_argument("--ar-probe", type=int, default=1,
+                    help="N > 1: time the item all-reduce alone first (allreduce_probe)")
     ap.add_argument("--dist-timeout", type=float, default=180.0,
                     help="N>1: seconds before a stuck collective aborts the run (every rank "
                          "draws its graph in parallel first: C4 ~25 s)")
@@ -570,6 +640,15 @@ def main():
     log(f"[bench] rank {rank}: {args.config} U={U} I={I} d={d} K={K} B={B} "
         f"scaling={scaling} generated in {time.perf_counter() - t0:.1f}s")
 
+    # the item all-reduce alone (dense payload I*d*4, frontier 16 MB) before any
+    # step: t_ar and bus bandwidth on this machine's links (DESIGN §6 assumed
+    # 76.8 GB/s per link)
+    ar_probe = None
+    if world > 1 and args.ar_probe:
+        ar_probe = allreduce_probe(dev, world, backend == "nccl", (I * d * 4, 16 << 20))
+        log(f"[bench] rank {rank}: all-reduce probe {json.dumps(ar_probe)}")
+    rule = chain_rule(ar_probe, args.config, world, K, I * d * 4, 16 << 20) \
+        if (args.column_chains is None and args.native_comm == "off" and not weak) else None
     if args.native_comm == "inline":   # one chain, no ranges: nothing overlaps the wire
         args.column_chains = 1
         args.exchange_parts = 1 if args.exchange_parts is None else args.exchange_parts
@@ -753,15 +832,20 @@ def main():
         how = ("C ABI RCCL on a comm stream" if nc else "torch collectives")
         return f"{c} chain{'s' if c > 1 else ''}, {xq['exchange_parts']} item-row range(s), {how}"
 
-    trainer = build(partition)
+    # the user-row chain settings: the main run and the one beside it (the
+    # probe's rule, when it has constants, decides which runs first)
+    main_xp, beside_xp = xp, inline_xp
+    if rule is not None and rule["predicted"] == "inline" and inline_xp is not None:
+        main_xp, beside_xp = inline_xp, xp
+    trainer = build(partition, main_xp if partition == "users" else None)
     res = measure(trainer, partition, args.dense_check)
-    res["xp"] = xp
+    res["xp"] = main_xp if partition == "users" else xp
     runs = [res]
     U_job = U * (world if weak else 1)
     strong_multi = dist_mode and world > 1 and not weak
     todo = []
-    if strong_multi and partition == "users" and args.chain_beside and inline_xp is not None:
-        todo.append(("users", inline_xp))
+    if strong_multi and partition == "users" and args.chain_beside and beside_xp is not None:
+        todo.append(("users", beside_xp))
     other = {"columns": "users", "users": "columns"}.get(partition)
     if (strong_multi and not sharded_gen and args.partition_beside
             and (other == "users" or can_shard_columns(d, world))):
@@ -769,8 +853,8 @@ def main():
         # the faster one is the line, the other is reported beside it (the
         # per-link exchange model cannot settle N = 2 / 4 without the links)
         todo.append((other, xp))
-        if other == "users" and args.chain_beside and inline_xp is not None:
-            todo.append(("users", inline_xp))
+        if other == "users" and args.chain_beside and beside_xp is not None:
+            todo.append(("users", beside_xp))
     beside_errors = []
     for part, xq in todo:
         if trainer is not None:
@@ -971,6 +1055,11 @@ def main():
         "partition_beside": partition_beside,
         "beside_errors": beside_errors or None,
         "chain_beside": chain_beside,
+        "allreduce_probe": ar_probe,
+        "chain_rule": None if rule is None else dict(
+            rule, measured=None if chain_beside is None else
+            ("inline" if chain_beside["faster_chain_mode"].startswith("1 chain")
+             else "two_chains")),
         "partition": ("columns" if columns else "users") if dist_mode else
                      (f"one column shard of {emulate}" if emulate else "single GPU"),
         "graph_replay": use_graph,

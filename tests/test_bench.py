@@ -154,3 +154,24 @@ def test_edges_per_step_weights_column_slices(bench):
     assert bench.edges_per_step(halves, 64, 2) == (400.0, 400.0)
     masked = {("masked", "src", 1000, 500, 64): [1, 10, 90, 30]}
     assert bench.edges_per_step(masked, 64, 1) == (30.0, 90.0)
+
+
+def test_chain_rule_from_the_measured_allreduce(bench):
+    """at C4, N = 8 one inline chain wins only while the step's
+    exchanges take less than the two-chain compute minus the inline compute;
+    other configs have no constants and no rule."""
+    dense, front = 1_000_000 * 64 * 4, 16 << 20
+
+    def probe(t_dense, t_front, cabi=True):
+        p = {"torch_244MB": {"t_ar_ms": t_dense}, "torch_16MB": {"t_ar_ms": t_front}}
+        if cabi:
+            p.update({"cabi_244MB": {"t_ar_ms": t_dense}, "cabi_16MB": {"t_ar_ms": t_front}})
+        return p
+    fast = bench.chain_rule(probe(0.05, 0.01), "C4", 8, 3, dense, front)
+    assert fast["predicted"] == "inline"
+    assert fast["wire_ms"]["inline"] == pytest.approx(4 * 0.05 + 2 * 0.01)
+    slow = bench.chain_rule(probe(1.0, 0.1, cabi=False), "C4", 8, 3, dense, front)
+    assert slow["predicted"] == "two_chains"
+    assert slow["predicted_ms"]["two_chains"] == pytest.approx(4.2)
+    assert bench.chain_rule(probe(0.05, 0.01), "C4", 4, 3, dense, front) is None
+    assert bench.chain_rule(None, "C4", 8, 3, dense, front) is None

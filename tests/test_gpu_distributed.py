@@ -304,3 +304,13 @@ def test_bench_two_ranks_measures_both_partitions(tmp_path):
     assert "gloo" in c["backend_note"]
     users_ms = (j["ms_per_step"] if j["partition"] == "users" else b["ms_per_step"])
     assert users_ms == c["faster_users_ms_per_step"]
+    # the item all-reduce timed alone before the steps (dense payload I*d*4 =
+    # 12.8 MB at C2, and 16 MB): t_ar and bus bandwidth through torch's group
+    # (gloo here: no RCCL communicator, so no C ABI figures)
+    p = j["allreduce_probe"]
+    assert p["world"] == 2 and p["sizes_bytes"] == [50_000 * 64 * 4, 16 << 20]
+    for mb in (12, 16):
+        e = p[f"torch_{mb}MB"]
+        assert e["t_ar_ms"] > 0 and e["busbw_GBps"] == pytest.approx(e["algbw_GBps"])  # P = 2
+    assert not any(k.startswith("cabi_") for k in p)
+    assert j["chain_rule"] is None   # constants only for C4 at N = 8
