@@ -13,6 +13,11 @@ value = evaluated users / wall time of one bbgr.evaluation.evaluate_sampled
 roofline = eval_sampled_kernel: algorithmic bytes per user = (1 + n_neg + 1)
         rows of d fp32 (the user row and every candidate's item row) / launch
         time, timed with HIP events on the launching stream.
+--stream numpy: the candidates of the reference's own numpy stream
+        (np.random.default_rng(seed + 999), drawn on the host by
+        bbgr_eval_draw_candidates, bit for bit the reference loop's), uploaded
+        and scored by the same kernel; the host draw is timed apart
+        (host_draw_s) and included in the wall time.
 --full: the full-ranking protocol; roofline = fp32 MFMA (2*d flops per
         (user, item) score) over the whole evaluate_full device time.
 cpu_baseline = the reference's per-user loop restated in oracle/ref_numpy.py
@@ -65,6 +70,8 @@ def main():
                     help="--full: the cutoffs (the top-K list is max(ks) deep)")
     ap.add_argument("--full", action="store_true",
                     help="full-ranking protocol (evaluate_full_ranking) instead of sampled")
+    ap.add_argument("--stream", default="philox", choices=["philox", "numpy"],
+                    help="sampled: device Philox candidates, or the reference's numpy stream")
     ap.add_argument("--max-users", type=int, default=0,
                     help="evaluate only the first N users with test items (0 = all)")
     args = ap.parse_args()
@@ -93,6 +100,24 @@ def main():
     if args.full:
         run = lambda c: evaluate_full(uf, itf, trc, tec, I, pop_t, T, cred_t,  # noqa: E731
                                       Ks=tuple(args.ks))
+    elif args.stream == "numpy":
+        from bbgr import evaluation as EV
+        from bbgr.host_sampler import edges_to_user_csr
+        tr_csr, te_csr = edges_to_user_csr(tr, U), edges_to_user_csr(te, U)
+        host_users = np.where(np.diff(te_csr[0]) > 0)[0].astype(np.int64)
+        users_t = torch.from_numpy(host_users).to(dev)
+        groups_t = torch.from_numpy(EV.cred_group_flags(host_users, cred, 0.2)).to(dev)
+        draw_s = []
+
+        def run(c):
+            t = time.perf_counter()
+            cand = EV.draw_candidates(np.random.default_rng(42 + 999), host_users, tr_csr,
+                                      te_csr, I, args.negatives)
+            draw_s.append(time.perf_counter() - t)
+            return evaluate_sampled(uf, itf, trc, tec, I, pop_t, T, cred_t,
+                                    sampled_negatives=args.negatives,
+                                    cand=torch.from_numpy(cand).pin_memory(), users=users_t,
+                                    groups=groups_t)
     else:
         run = lambda c: evaluate_sampled(uf, itf, trc, tec, I, pop_t, T, cred_t,  # noqa: E731
                                          sampled_negatives=args.negatives, counter=c)
@@ -155,7 +180,7 @@ def main():
         log(f"[eval] cpu {users.size} users {el:.1f}s -> {users.size/el:.0f} users/s")
     kstr = ",".join(str(k) for k in args.ks)
     proto = f"full ranking (all items, K={kstr})" if args.full else \
-        f"sampled eval (1 pos + {args.negatives} neg, K=10,20)"
+        f"sampled eval (1 pos + {args.negatives} neg, K=10,20; {args.stream} candidates)"
     line = {
         "metric": "eval_users_per_s", "value": n_eval / wall, "unit": "users/s",
         "n_gpus": 1, "steps": args.reps, "warmup": args.warmup, "ms_per_step": wall * 1e3,
@@ -165,6 +190,9 @@ def main():
                    "users_eval": n_eval, "num_items": I, "emb_dim": d,
                    "train_edges": T, "test_edges": int(te.shape[1])},
         "device_ms": dev_s * 1e3,
+        "host_draw_s": (float(np.median(draw_s)) if not args.full and args.stream == "numpy"
+                        else None),
+        "candidate_stream": None if args.full else args.stream,
         "roofline": roof,
         "cpu_baseline": cpu,
     }

@@ -24,6 +24,8 @@
 #   pmc        PMC passes over the SpMM kernels (PMC_SETS: one pass per word)
 #   dropin     the drop-in module step (FusedAdam / torch foreach Adam) + trace
 #   configs    one bench line per config (CONFIGS="C1 C2 C3 C5")
+#   evalnp     sampled evaluation at C4 on the reference's numpy candidate stream
+#   frontierab C2 / C1 step with the frontier masks on and off (graph replay)
 set -o pipefail
 T=$1; shift
 O=gpurun_out/$T
@@ -146,6 +148,22 @@ for step in "$@"; do
         rc=$?; hard $rc "bench $c" "$O/${c,,}_bench.log"
         [ $rc -eq 0 ] || { tail -20 "$O/${c,,}_bench.log"; exit 1; }
         echo "$c: $(python tools/bench_brief.py "$O/${c,,}_bench.json" | head -1)"
+      done ;;
+    evalnp)
+      timeout -k 10 600 python -u tools/bench_eval.py --stream numpy --no-cpu-baseline --reps 2 \
+        --warmup 1 ${EVAL_ARGS:-} > "$O/eval_numpy.json" 2> "$O/eval_numpy.log"
+      rc=$?; hard $rc evalnp "$O/eval_numpy.log"; echo "EVALNP rc=$rc"
+      [ $rc -eq 0 ] || { tail -20 "$O/eval_numpy.log"; exit 1; }
+      tail -c 700 "$O/eval_numpy.json" ;;
+    frontierab)
+      for c in ${FCONFIGS:-C2 C1}; do
+        for f in on off; do
+          timeout -k 10 400 python -u bench.py --config $c --frontier $f $quick_args --steps 50 \
+            --warmup 5 > "$O/${c,,}_frontier_$f.json" 2> "$O/${c,,}_frontier_$f.log"
+          rc=$?; hard $rc "frontier $c $f" "$O/${c,,}_frontier_$f.log"
+          [ $rc -eq 0 ] || { tail -20 "$O/${c,,}_frontier_$f.log"; exit 1; }
+          echo "$c frontier $f: $(python tools/bench_brief.py "$O/${c,,}_frontier_$f.json" | head -1)"
+        done
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
