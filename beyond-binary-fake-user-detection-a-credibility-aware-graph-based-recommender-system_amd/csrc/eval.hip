@@ -837,6 +837,30 @@ static inline bool user_has_item_host(const int64_t *arr, int64_t n, int64_t x) 
   return lo < n && arr[lo] == x;
 }
 
+// Membership in a SORTED row without data-dependent branches (a rejection is
+// rare, so the searches' branches would mispredict on most draws): the same
+// answer as any search of a sorted row, hence as user_has_item's.
+static inline bool sorted_contains(const int64_t *a, int64_t n, int64_t x) {
+  if (n <= 32) {   // short rows: a fixed-length scan (the trip count is the row's)
+    bool f = false;
+    for (int64_t k = 0; k < n; ++k) f |= a[k] == x;
+    return f;
+  }
+  const int64_t *base = a;
+  while (n > 1) {   // the trip count depends on n only; the step is arithmetic
+    const int64_t half = n >> 1;
+    base += (int64_t)(base[half - 1] < x) * half;
+    n -= half;
+  }
+  return *base == x;
+}
+
+static inline bool is_sorted_row(const int64_t *a, int64_t n) {
+  for (int64_t k = 1; k < n; ++k)
+    if (a[k] < a[k - 1]) return false;
+  return true;
+}
+
 }  // namespace bbgr
 
 using namespace bbgr;
@@ -869,6 +893,11 @@ extern "C" int bbgr_eval_draw_candidates(bbgr_pcg64 *rng, int64_t n_users, const
     std::sort(gt.begin(), gt.end());
     const int64_t *tr = tr_indices + rb;
     const int64_t ntr = re - rb;
+    // a sorted train row (edges_to_user_csr sorts every row) is searched
+    // without branches; any other row exactly as numpy's searchsorted runs
+    const bool tr_sorted = is_sorted_row(tr, ntr);
+    const int64_t *gtp = gt.data();
+    const int64_t ngt = (int64_t)gt.size();
     // the reference's while loop ends only if some item passes both tests: each
     // row rejects at most its own values, so a shortfall needs an exact count
     if ((te - tb) + ntr >= n_items) {
@@ -885,8 +914,8 @@ extern "C" int bbgr_eval_draw_candidates(bbgr_pcg64 *rng, int64_t n_users, const
     out[0] = (int32_t)te_indices[tb + (int64_t)g.bounded((uint64_t)(te - tb - 1))];
     for (int64_t s = 1; s < nc;) {
       const int64_t j = (int64_t)g.bounded((uint64_t)(n_items - 1));
-      if (std::binary_search(gt.begin(), gt.end(), j)) continue;
-      if (user_has_item_host(tr, ntr, j)) continue;
+      if (sorted_contains(gtp, ngt, j)) continue;   // j in gt_set
+      if (tr_sorted ? sorted_contains(tr, ntr, j) : user_has_item_host(tr, ntr, j)) continue;
       out[s++] = (int32_t)j;
     }
   }
