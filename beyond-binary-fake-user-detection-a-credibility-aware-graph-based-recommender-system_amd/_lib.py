@@ -92,6 +92,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_grad", c_void_p), ("adam_grad_ld", c_int64), ("adam_grad_scale", c_float),
         ("adam_map", c_void_p),
         ("adam_moments_unmapped", c_int32),
+        ("tag_out", c_void_p), ("tag_mask", c_void_p), ("src_tagged", c_void_p),
     ]
 
 

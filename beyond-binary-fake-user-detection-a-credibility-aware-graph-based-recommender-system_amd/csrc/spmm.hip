@@ -89,7 +89,21 @@ struct SpmmParams {
   float adam_g_scale;
   const int *adam_map;         // the fused Adam's row map (args.adam_map; NULL: y_map's)
   int adam_mrow;               // moments at the launch row (args.adam_moments_unmapped)
+  int *tag_out;                // tagged-index copy written by a full launch (args.tag_out)
+  const unsigned char *tag_mask;
 };
+
+// Tagged column indices (ABI 10): a full launch over a CSR can write a copy of
+// its column indices with bit 31 set where the column is dead in tag_mask
+// (TAG_WRITE); a masked launch over the same CSR then reads liveness from the
+// index itself (TAG_READ: indices = the copy, no src_mask load), which takes
+// the mask byte's dependent load out of every batch's index -> gather chain.
+constexpr int TAG_NONE = 0, TAG_WRITE = 1, TAG_READ = 2;
+
+__device__ __forceinline__ void tag_store(const SpmmParams &P, long e, int col) {
+  __builtin_nontemporal_store(P.tag_mask[col] ? col : (int)((unsigned)col | 0x80000000u),
+                              P.tag_out + e);
+}
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
   return make_float4(fmaf(a, x.x, y.x), fmaf(a, x.y, y.y), fmaf(a, x.z, y.z),
@@ -300,7 +314,7 @@ __device__ __forceinline__ int compact_live(int &my, float &mw) {
 }
 
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
-template <int D, int WMODE, bool MASKED, bool BITS = false>
+template <int D, int WMODE, bool MASKED, bool BITS = false, int TAG = TAG_NONE>
 __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee,
                                              int lane, float4 (&acc)[D / 64]) {
   constexpr int V = D / 64;
@@ -326,7 +340,9 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     float mw = 0.f;
     if (lane < n && ((live >> lane) & 1u)) {
       my = ld_edge(P.indices + e0 + lane);
-      if (MASKED && !BITS && P.src_mask && !P.src_mask[my]) my = -1;   // exact-zero source row
+      if constexpr (TAG == TAG_WRITE) tag_store(P, (long)e0 + lane, my);
+      // exact-zero source row (a tagged index carries it in its sign)
+      if (MASKED && !BITS && TAG != TAG_READ && P.src_mask && !P.src_mask[my]) my = -1;
       if (my >= 0) {
         if (WMODE == 1) mw = ld_edge(P.edge_val + e0 + lane);
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
@@ -334,7 +350,7 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     }
     if constexpr (MASKED && BITS) {   // live edges first (sparse: ~1 of 16 live)
       n = compact_live<WMODE>(my, mw);
-    } else if (MASKED && P.src_mask) {   // skip 16-edge batches with no live source (group-uniform)
+    } else if (MASKED && (TAG == TAG_READ || P.src_mask)) {   // skip 16-edge batches with no live source (group-uniform)
       const unsigned long long lv = __ballot(my >= 0);
       if (((lv >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
     }
@@ -483,13 +499,13 @@ __device__ __forceinline__ void gather_slot(const SpmmParams &P, int eb, int ee,
 }
 
 // A row's gather for any width: the narrow form below 64 columns.
-template <int D, int WMODE, bool MASKED, bool BITS = false>
+template <int D, int WMODE, bool MASKED, bool BITS = false, int TAG = TAG_NONE>
 __device__ __forceinline__ void gather_row(const SpmmParams &P, int eb, int ee, int lane,
                                            float4 (&acc)[RowShape<D>::V]) {
   if constexpr (D < 64) {
     gather_range_narrow<D, WMODE, MASKED>(P, eb, ee, lane, acc[0]);
   } else {
-    gather_range<D, WMODE, MASKED, BITS>(P, eb, ee, lane, acc);
+    gather_range<D, WMODE, MASKED, BITS, TAG>(P, eb, ee, lane, acc);
   }
 }
 
@@ -499,7 +515,7 @@ __device__ __forceinline__ void gather_row(const SpmmParams &P, int eb, int ee, 
 // for the same registers. Per row the operation sequence is gather_range's
 // (edges in CSR order from zero; dead batches skipped), so results match the
 // one-row path bitwise (up to the sign of an exact zero).
-template <int D, int WMODE, bool MASKED>
+template <int D, int WMODE, bool MASKED, int TAG = TAG_NONE>
 __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int eeA, int ebB,
                                             int eeB, int lane, float4 (&accA)[D / 64],
                                             float4 (&accB)[D / 64]) {
@@ -513,7 +529,8 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     float mwA = 0.f, mwB = 0.f;
     if (lane < na) {
       myA = ld_edge(P.indices + ebA + o + lane);
-      if (MASKED && P.src_mask && !P.src_mask[myA]) myA = -1;
+      if constexpr (TAG == TAG_WRITE) tag_store(P, (long)ebA + o + lane, myA);
+      if (MASKED && TAG != TAG_READ && P.src_mask && !P.src_mask[myA]) myA = -1;
       if (myA >= 0) {
         if (WMODE == 1) mwA = ld_edge(P.edge_val + ebA + o + lane);
         if (WMODE == 2) mwA = P.col_scale[myA] * P.col_scale_s;
@@ -521,13 +538,14 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     }
     if (lane < nb) {
       myB = ld_edge(P.indices + ebB + o + lane);
-      if (MASKED && P.src_mask && !P.src_mask[myB]) myB = -1;
+      if constexpr (TAG == TAG_WRITE) tag_store(P, (long)ebB + o + lane, myB);
+      if (MASKED && TAG != TAG_READ && P.src_mask && !P.src_mask[myB]) myB = -1;
       if (myB >= 0) {
         if (WMODE == 1) mwB = ld_edge(P.edge_val + ebB + o + lane);
         if (WMODE == 2) mwB = P.col_scale[myB] * P.col_scale_s;
       }
     }
-    if (MASKED && P.src_mask) {   // a batch with no live source adds nothing
+    if (MASKED && (TAG == TAG_READ || P.src_mask)) {   // a batch with no live source adds nothing
       const unsigned long long la = __ballot(myA >= 0), lb = __ballot(myB >= 0);
       if (((la >> (threadIdx.x & 48)) & 0xffffull) == 0) na = 0;
       if (((lb >> (threadIdx.x & 48)) & 0xffffull) == 0) nb = 0;
@@ -917,7 +935,7 @@ __device__ __forceinline__ bool serial_long(const SpmmParams &P, int len) {
 
 // Short-row workgroup sb of a launch: rows sb*per_block.. of the row range or
 // of the row list (whose length is n_list).
-template <int D, int WMODE, bool MASKED, bool PAIR, bool BITS>
+template <int D, int WMODE, bool MASKED, bool PAIR, bool BITS, int TAG>
 __device__ __forceinline__ void short_rows(const SpmmParams &P, long sb, long n_list, int g,
                                            int lane) {
   constexpr int V = RowShape<D>::V;
@@ -956,7 +974,7 @@ __device__ __forceinline__ void short_rows(const SpmmParams &P, long sb, long n_
     float4 accB[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) accB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    gather_pair<D, WMODE, MASKED>(P, ser[0] ? 0 : eb[0], ser[0] ? 0 : ee[0],
+    gather_pair<D, WMODE, MASKED, TAG>(P, ser[0] ? 0 : eb[0], ser[0] ? 0 : ee[0],
                                   ser[1] ? 0 : eb[1], ser[1] ? 0 : ee[1], lane, acc, accB);
     if (rr[0] >= 0 && !ser[0]) epilogue<D>(P, (int)rr[0], lane, acc);
     if (rr[1] >= 0 && !ser[1]) epilogue<D>(P, (int)rr[1], lane, accB);
@@ -1010,12 +1028,12 @@ __device__ __forceinline__ void short_rows(const SpmmParams &P, long sb, long n_
     if (!serial_long<D, BITS>(P, ee - eb)) return;  // owned by chunk blocks
     chunk_row_serial<D, WMODE>(P, eb, ee, lane, acc);
   } else {
-    gather_row<D, WMODE, MASKED, BITS>(P, eb, ee, lane, acc);
+    gather_row<D, WMODE, MASKED, BITS, TAG>(P, eb, ee, lane, acc);
   }
   epilogue<D>(P, (int)row, lane, acc);
 }
 
-template <int D, int WMODE, bool MASKED, bool PAIR, bool BITS = false>
+template <int D, int WMODE, bool MASKED, bool PAIR, bool BITS = false, int TAG = TAG_NONE>
 __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   constexpr int V = RowShape<D>::V;
   __shared__ float4 red[16 * (D / 4)];
@@ -1035,7 +1053,7 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     const int per = (((len + 15) >> 4) + 15) & ~15;  // multiple of 16
     const int gb = ch.y + g * per;
     const int ge = min(ch.z, gb + per);
-    if (gb < ge) gather_row<D, WMODE, MASKED, BITS>(P, gb, ge, lane, acc);
+    if (gb < ge) gather_row<D, WMODE, MASKED, BITS, TAG>(P, gb, ge, lane, acc);
     block_reduce16<D>(red, g, lane, acc);
     if (ch.w < 0) {   // the row's only chunk
       if (g == 0 && lane < RowShape<D>::LANES) {
@@ -1054,7 +1072,7 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
   // list length in device memory (a list built on the stream, e.g. inside a
   // captured step; n_row_list is its capacity): workgroups past it exit
   if (MASKED && P.row_list && P.row_count) n = min(n, *P.row_count);
-  short_rows<D, WMODE, MASKED, PAIR, BITS>(P, sb, n, g, lane);
+  short_rows<D, WMODE, MASKED, PAIR, BITS, TAG>(P, sb, n, g, lane);
 }
 
 // Full-CSR launches (the roofline kernel) and masked / row-list launches are
@@ -1088,6 +1106,24 @@ __global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::pair_waves_ma
                                                      : Tune<D>::pair_waves_masked) void
 spmm_masked_pair_kernel(SpmmParams P) {
   spmm_body<D, WMODE, true, true>(P);
+}
+
+// The tagged-index forms (two-row CSRs, d >= 64): the full product that also
+// writes the tagged copy of its column indices, and the src-masked product that
+// reads liveness from that copy (args.tag_out / src_tagged). Symbols of their
+// own: the plain kernels keep their register budgets.
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::pair_waves0
+                                                     : Tune<D>::pair_waves) void spmm_pair_tag_kernel(
+    SpmmParams P) {
+  spmm_body<D, WMODE, false, true, false, TAG_WRITE>(P);
+}
+
+template <int D, int WMODE>
+__global__ __launch_bounds__(256) BBGR_WAVES(WMODE == 0 ? Tune<D>::pair_waves_masked0
+                                                     : Tune<D>::pair_waves_masked) void
+spmm_masked_pair_tagged_kernel(SpmmParams P) {
+  spmm_body<D, WMODE, true, true, false, TAG_READ>(P);
 }
 
 // Slot-bitmap launches (args.src_bits, d >= 64, one row per group): liveness
@@ -1141,18 +1177,24 @@ __global__ __launch_bounds__(256) void epilogue_kernel(SpmmParams P, const float
 }
 
 template <int D, int WMODE>
-static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
-  const bool masked = P.src_mask || P.row_mask || P.row_list;
+static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st, bool tag_read) {
+  const bool masked = P.src_mask || P.row_mask || P.row_list || tag_read;
   const long short_rows = P.row_list ? P.n_row_list : (long)(P.row_end - P.row_begin);
   const bool pair = D >= 64 && P.pair_rows;
   const long per_block = D < 64 ? 16 * (16 / (D / 4)) : (pair ? 32 : 16);
   const long short_blocks = (short_rows + per_block - 1) / per_block;
   const long grid = (long)P.n_chunks + short_blocks;
+  if ((P.tag_out || tag_read) && !(D >= 64 && pair)) {
+    set_error("bbgr_spmm: tagged indices need a two-row CSR (average degree <= 24) and d >= 64");
+    return BBGR_ERR_UNSUPPORTED;
+  }
   if (grid > 0) {
     const dim3 gd((unsigned)grid), bd(256);
     if constexpr (D >= 64) {
       if (pair) {
-        if (masked) hipLaunchKernelGGL((spmm_masked_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
+        if (tag_read) hipLaunchKernelGGL((spmm_masked_pair_tagged_kernel<D, WMODE>), gd, bd, 0, st, P);
+        else if (P.tag_out) hipLaunchKernelGGL((spmm_pair_tag_kernel<D, WMODE>), gd, bd, 0, st, P);
+        else if (masked) hipLaunchKernelGGL((spmm_masked_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
         else if (P.adam_p) hipLaunchKernelGGL((spmm_adam_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
         else hipLaunchKernelGGL((spmm_pair_kernel<D, WMODE>), gd, bd, 0, st, P);
         BBGR_LAUNCHED("spmm_kernel");
@@ -1177,11 +1219,11 @@ static int launch_spmm(const SpmmParams &P, int n_split, hipStream_t st) {
 
 template <int D>
 static int dispatch_wmode(const SpmmParams &P, int wmode, int n_split,
-                          hipStream_t st) {
+                          hipStream_t st, bool tag_read) {
   switch (wmode) {
-    case 0: return launch_spmm<D, 0>(P, n_split, st);
-    case 1: return launch_spmm<D, 1>(P, n_split, st);
-    case 2: return launch_spmm<D, 2>(P, n_split, st);
+    case 0: return launch_spmm<D, 0>(P, n_split, st, tag_read);
+    case 1: return launch_spmm<D, 1>(P, n_split, st, tag_read);
+    case 2: return launch_spmm<D, 2>(P, n_split, st, tag_read);
   }
   set_error("bbgr_spmm: weight_mode %d not in {0,1,2}", wmode);
   return BBGR_ERR_INVALID;
@@ -1376,16 +1418,27 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
   BBGR_REQUIRE(!a->row_list || a->row_mask || csr->n_chunks == 0,
                "bbgr_spmm: row_list needs row_mask when the plan has long-row chunks");
   P.pair_rows = d >= 64 && pair_rows(csr);
+  // tagged indices: a full launch writes the copy, a masked one reads it
+  BBGR_REQUIRE(!a->tag_out || (a->tag_mask && !a->src_tagged && !a->src_mask && !a->row_mask &&
+                               !a->row_list && !a->use_range && !a->adam_param),
+               "bbgr_spmm: tag_out needs tag_mask and a full launch (no masks, list, range or "
+               "fused Adam)");
+  BBGR_REQUIRE(!a->src_tagged || (!a->src_mask && !a->src_bits && !a->adam_param),
+               "bbgr_spmm: src_tagged replaces src_mask (no src_mask / src_bits / fused Adam)");
+  const bool tag_read = a->src_tagged != nullptr;
+  P.tag_out = a->tag_out;
+  P.tag_mask = a->tag_mask;
+  if (tag_read) P.indices = a->src_tagged;
   P.nt_from = a->stream_from > 0 ? a->stream_from : 0x7fffffff;
   P.nt_out_from = a->stream_out_from > 0 ? a->stream_out_from : 0x7fffffff;
   hipStream_t st = as_stream(stream);
   switch (d) {
-    case 8: return dispatch_wmode<8>(P, a->weight_mode, n_split, st);
-    case 16: return dispatch_wmode<16>(P, a->weight_mode, n_split, st);
-    case 32: return dispatch_wmode<32>(P, a->weight_mode, n_split, st);
-    case 64: return dispatch_wmode<64>(P, a->weight_mode, n_split, st);
-    case 128: return dispatch_wmode<128>(P, a->weight_mode, n_split, st);
-    default: return dispatch_wmode<256>(P, a->weight_mode, n_split, st);
+    case 8: return dispatch_wmode<8>(P, a->weight_mode, n_split, st, tag_read);
+    case 16: return dispatch_wmode<16>(P, a->weight_mode, n_split, st, tag_read);
+    case 32: return dispatch_wmode<32>(P, a->weight_mode, n_split, st, tag_read);
+    case 64: return dispatch_wmode<64>(P, a->weight_mode, n_split, st, tag_read);
+    case 128: return dispatch_wmode<128>(P, a->weight_mode, n_split, st, tag_read);
+    default: return dispatch_wmode<256>(P, a->weight_mode, n_split, st, tag_read);
   }
 }
 

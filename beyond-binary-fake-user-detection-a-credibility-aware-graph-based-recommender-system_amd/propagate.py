@@ -359,7 +359,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          acc_in=None, acc_out=None, acc_scale=None, acc_scale_s: float = 1.0,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
          add_mask=None, row_list=None, rng=None, adam=None, y_map=None, acc_map=None,
-         add_map=None, src_input: bool = False, src_bits=None, row_count=None) -> None:
+         add_map=None, src_input: bool = False, src_bits=None, row_count=None,
+         tag_out=None, tag_mask=None, tagged=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream. `adam`
     (optim.AdamRows): apply Adam to each row's y value in the epilogue.
     `y_map` / `acc_map` / `add_map`: row maps of those tables (input-order
@@ -369,7 +370,11 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     `row_count` (device int64): row_list holds that many rows (its numel() is
     the capacity; bbgr_spmm_args.row_count) — a list built on the stream, the
     rows row_mask flags; a ListLength passes the list at its published length
-    instead when there is one."""
+    instead when there is one. `tag_out` / `tag_mask` (a full launch): also
+    write the CSR's column indices with bit 31 set where tag_mask is 0;
+    `tagged` (with src_mask, the same mask): read liveness from such a copy
+    instead of loading src_mask per edge (bbgr_spmm_args.tag_out /
+    src_tagged; bitwise the src_mask launch)."""
     listed_on_device = row_count is not None
     if isinstance(row_count, ListLength):
         n = row_count.length()
@@ -397,6 +402,12 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     a.gamma = gamma
     a.partial = ptr(prod.workspace(d))
     a.src_mask, a.row_mask = ptr(src_mask), ptr(row_mask)
+    if tag_out is not None:
+        a.tag_out, a.tag_mask = ptr(tag_out), ptr(tag_mask)
+    if tagged is not None:
+        if src_mask is None:
+            raise ValueError("spmm: tagged indices stand for a src_mask; pass it too")
+        a.src_tagged, a.src_mask = ptr(tagged), None
     a.acc_mask, a.add_mask = ptr(acc_mask), ptr(add_mask)
     if row_list is not None:
         a.row_list, a.n_row_list = ptr(row_list), row_list.numel()
@@ -527,7 +538,7 @@ def drain(steps):
 def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
                   order: str = ORDER_GS, out_u: torch.Tensor | None = None,
                   out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None,
-                  final_rows=None):
+                  final_rows=None, tag=None):
     """Final (layer-mean) user and item tables. u0 [U,d], i0 [I,d] fp32.
     A generator: it yields after issuing each item-row product (with `reduce`,
     each exchange point), so the caller can interleave the issue of several
@@ -544,7 +555,10 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
     last item product visits them instead of testing every row's mask byte.
     `item_acc_mask`: the item rows whose FINAL value is read (the batch items;
     default item_mask): the item layer-mean accumulator is formed on those
-    rows only (item_mask must cover them)."""
+    rows only (item_mask must cover them).
+    `tag=(tag_out, tag_mask)` (GS, K >= 2): the first user product, a full
+    launch, also writes the user CSR's column indices tagged with tag_mask
+    (bit 31 = dead item) for backward_steps(tagged=...)."""
     U, I = pair.num_users, pair.num_items
     d = u0.shape[1]
     _check_table("user table", u0, U, d)
@@ -584,10 +598,13 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
                           row_mask=mi if last else None, acc_mask=ami, acc_map=am_i,
                           src_input=io is not None and k == 1, **(il if last else {}))
             yield
+            tk = {}
+            if tag is not None and k == 1 and not last:
+                tk = dict(tag_out=tag[0], tag_mask=tag[1])
             spmm(FU, bufI, False, y=bufU if k < K else None, y_scale=pair.feed_fwd_ui,
                  acc_in=u0 if k == 1 else acc_u, acc_out=acc_u,
                  acc_scale=FU.out_scale, gamma=g, row_mask=mu if last else None,
-                 acc_mask=mu, row_list=ulist if last else None, acc_map=am_u)
+                 acc_mask=mu, row_list=ulist if last else None, acc_map=am_u, **tk)
     elif order == ORDER_J:
         bufU, bufI = [new("u0", U), new("u1", U)], [new("i0", I), new("i1", I)]
         cur = 0
@@ -616,10 +633,10 @@ def forward_steps(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_la
 def forward(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,
             order: str = ORDER_GS, out_u: torch.Tensor | None = None,
             out_i: torch.Tensor | None = None, ws: dict | None = None, reduce=None,
-            final_rows=None):
+            final_rows=None, tag=None):
     """forward_steps run to completion: the final (u, i) tables."""
     return drain(forward_steps(pair, u0, i0, num_layers, order, out_u, out_i, ws, reduce,
-                               final_rows))
+                               final_rows, tag))
 
 
 def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers: int,
@@ -627,7 +644,7 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                    out_i: torch.Tensor | None = None, ws: dict | None = None,
                    grad_i0_dense: bool = True, reduce=None, grad_support=None,
                    adam_u=None, before_last=None, adam_i=None, src_bits=None,
-                   frontier_list=None):
+                   frontier_list=None, tagged=None):
     """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final); a
     generator yielding after each item-row product, like forward_steps.
     `adam_u` (optim.AdamRows) fuses the user-table Adam step into the last
@@ -652,7 +669,10 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     `frontier_list=(rows, count)`: GS, no `reduce` — the flagged items as a
     row list of capacity rows.numel() whose length is the device int64 count
     (bbgr_mark_list): the first item product then visits those rows only
-    instead of testing every row's mask byte."""
+    instead of testing every row's mask byte.
+    `tagged` (GS): the user CSR's column indices tagged with grad_support's
+    item mask (forward_steps(tag=...)): the first user product reads the item
+    support from them instead of loading the mask per edge (bitwise)."""
     U, I = pair.num_users, pair.num_items
     d = gU.shape[1]
     _check_table("user grad", gU, U, d)
@@ -705,10 +725,11 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                           src_input=inp and first, src_bits=src_bits if first else None,
                           **(fl if first else {}), **ka)
             yield
+            tg = tagged if (first and si_int is not None) else None
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
                      add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl,
-                     src_mask=si_int if first else None, add_map=um)
+                     src_mask=si_int if first else None, add_map=um, tagged=tg)
             else:
                 if before_last is not None:
                     before_last()
@@ -716,7 +737,8 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                 fused = adam_u is not None and src is None   # fused Adam needs every row
                 spmm(BU, bufI, False, y=None if fused else gu0, y_scale=BU.out_scale,
                      add=gU, add_mask=su, add_scale=None, add_scale_s=gl,
-                     src_mask=src, adam=adam_u if fused else None, add_map=um, y_map=um)
+                     src_mask=src, adam=adam_u if fused else None, add_map=um, y_map=um,
+                     tagged=tg)
                 if adam_u is not None and not fused:   # K == 1: masked product, Adam apart
                     adam_u.apply(gu0)
         if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
@@ -772,11 +794,11 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
              out_i: torch.Tensor | None = None, ws: dict | None = None,
              grad_i0_dense: bool = True, reduce=None, grad_support=None,
              adam_u=None, before_last=None, adam_i=None, src_bits=None,
-             frontier_list=None):
+             frontier_list=None, tagged=None):
     """backward_steps run to completion: (grad u0, grad i0)."""
     return drain(backward_steps(pair, gU, gI, num_layers, order, out_u, out_i, ws,
                                 grad_i0_dense, reduce, grad_support, adam_u, before_last,
-                                adam_i, src_bits, frontier_list))
+                                adam_i, src_bits, frontier_list, tagged))
 
 
 def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,

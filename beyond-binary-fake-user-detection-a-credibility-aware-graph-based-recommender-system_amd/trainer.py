@@ -15,6 +15,7 @@ into them and the step re-zeroes exactly the touched rows afterwards.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -148,6 +149,16 @@ class FusedTrainer:
         # (63k at C4) instead of testing the mask byte of every item row.
         # Its launches take the list at its length (P.ListLength) when the step
         # runs eagerly, at its capacity with the device count when captured.
+        # GS, K >= 2, a two-row user CSR: the first forward user product writes
+        # the user CSR's column indices tagged with the item frontier (bit 31 =
+        # dead item, bbgr_spmm_args.tag_out), and the first backward user
+        # product reads the frontier from them instead of loading the mask byte
+        # of every edge (src_tagged; bitwise the mask launch). 4 B per edge.
+        self.tagged = None
+        uc = graph.user_csr
+        if (self.frontier and order == ORDER_GS and num_layers >= 2 and emb_dim >= 64
+                and uc.nnz <= 24 * uc.n_rows and os.environ.get("BBGR_TAGGED", "1") != "0"):
+            self.tagged = torch.empty(max(uc.nnz, 1), dtype=torch.int32, device=dev)
         self.item_list = self.item_count = self.item_len = None
         if self.frontier and order == ORDER_GS:
             self.item_list = torch.empty(max(self.I, 1), dtype=torch.int64, device=dev)
@@ -217,7 +228,8 @@ class FusedTrainer:
         forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
                 out_i=self.itf, ws=self.ws,
                 final_rows=None if masks is None else
-                (masks[0], masks[1], users if listed else None, self._flist(masks)))
+                (masks[0], masks[1], users if listed else None, self._flist(masks)),
+                tag=self._tag(masks))
         # (a caller's batch may repeat a user: its last user layer then runs on
         # the de-duplicated mask instead of a row list, whose repeated rows
         # would update the in-place accumulator twice)
@@ -235,7 +247,8 @@ class FusedTrainer:
         else:
             backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                      out_i=self.g_i0, ws=self.ws, grad_support=masks,
-                     src_bits=self._bits(masks), frontier_list=self._flist(masks))
+                     src_bits=self._bits(masks), frontier_list=self._flist(masks),
+                     tagged=self._tagged(masks))
             # ego L2 term goes straight to the weight grads (Version-2:503-507):
             # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
             call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
@@ -303,7 +316,8 @@ class FusedTrainer:
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                  ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
                  src_bits=self._bits(masks), frontier_list=self._flist(masks),
-                 before_last=before_last, reduce=reduce, adam_i=adam_i)
+                 before_last=before_last, reduce=reduce, adam_i=adam_i,
+                 tagged=self._tagged(masks))
         if side:   # the side table is all-zero between steps
             call("bbgr_rows_zero", item_rows.numel(), ptr(item_rows), ptr(ga), ld(ga), self.d,
                  st)
@@ -385,6 +399,18 @@ class FusedTrainer:
             call("bbgr_mark_slots", B, ptr(users), ptr(uc.indptr), ptr(self.slot_map),
                  ptr(self.slot_bits), value, st)
         return self.mask_u, self.mask_i
+
+    def _tag(self, masks):
+        """forward(tag=...): the tagged user-CSR index copy and the item mask."""
+        t = getattr(self, "tagged", None)
+        self._tag_fresh = masks is not None and t is not None and self.K >= 2
+        return (t, masks[1]) if self._tag_fresh else None
+
+    def _tagged(self, masks):
+        """backward(tagged=...): the copy, only if this step's forward wrote it
+        (a subclass step that runs its own forward never reads a stale copy)."""
+        fresh, self._tag_fresh = getattr(self, "_tag_fresh", False), False
+        return self.tagged if (fresh and masks is not None) else None
 
     def _bits(self, masks):
         """The slot bitmap for backward(src_bits=...) when the masks are on."""

@@ -291,6 +291,16 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   follow adam_map: the drop-in optimizer stores its moments in the graph's */
 /*   order, so only the caller-order weight row is read and written at       */
 /*   random (bbgr.optim.FusedAdam converts them at its state_dict boundary). */
+/* tag_out (nullable, int32 [nnz], with tag_mask [n_cols] bytes; ABI 10): a  */
+/*   full launch (no masks, list, range or fused Adam) also writes            */
+/*   tag_out[e] = indices[e] with bit 31 set where tag_mask[indices[e]] == 0, */
+/*   for every slot e of the CSR. src_tagged (nullable, ABI 10): a launch     */
+/*   reads its column indices from src_tagged instead, an index with bit 31   */
+/*   set being a dead source skipped as src_mask would skip it (so src_mask   */
+/*   and src_bits must be NULL): the src-masked backward user product reads   */
+/*   the frontier from the copy the forward's first user product wrote, with  */
+/*   no mask load between an index and its gather. Bitwise the src_mask       */
+/*   launch. Both need a two-row CSR (nnz <= 24 n_rows) and d >= 64.          */
 /* partial: n_chunks*d floats followed by n_chunks int32 arrival counters     */
 /*   (zero when allocated; each launch leaves them zero): the last chunk of a */
 /*   split row to arrive sums the row's partials in chunk order in the same  */
@@ -355,6 +365,9 @@ typedef struct {
   float adam_grad_scale;
   const int32_t *adam_map;
   int32_t adam_moments_unmapped;
+  int32_t *tag_out;
+  const uint8_t *tag_mask;
+  const int32_t *src_tagged;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,

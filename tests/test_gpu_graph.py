@@ -185,3 +185,30 @@ def test_slot_bitmap_first_item_product_is_bitwise_the_mask(variant, bits, liste
             assert int(a.item_count.item()) == 0
     for x, y in ((a.user_w, b.user_w), (a.item_w, b.item_w), (a.m_u, b.m_u), (a.v_i, b.v_i)):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("fuse,K", [(True, 3), (False, 3), (True, 2)])
+def test_tagged_user_indices_step_is_bitwise_the_mask_step(fuse, K, monkeypatch):
+    """GS with the frontier: the first forward user product writes the user
+    CSR's indices tagged with the item frontier and the first backward user
+    product reads them (bbgr_spmm_args.tag_out / src_tagged) instead of the
+    mask byte per edge: losses, weights and moments equal the mask step's bit
+    for bit over five steps (BBGR_TAGGED=0 keeps the mask)."""
+    e, g = _graph()
+    kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=64, num_layers=K, batch_size=256,
+              frontier=True, fuse_adam=fuse, seed=7)
+    a = FusedTrainer(g, "v2_pop", **kw)
+    monkeypatch.setenv("BBGR_TAGGED", "0")
+    b = FusedTrainer(g, "v2_pop", **kw)
+    assert a.tagged is not None and b.tagged is None
+    for _ in range(5):
+        assert float(a.step()) == float(b.step())
+    _assert_same(a, b)
+    # the copy holds this step's frontier: bit 31 exactly off the item mask
+    uc = g.user_csr
+    a._set_masks(a._last_users, a.pos, a.neg, 1)
+    idx = uc.indices[:uc.nnz].long()
+    live = a.mask_i[idx].bool()
+    a._set_masks(a._last_users, a.pos, a.neg, 0)
+    want = torch.where(live, idx, idx | (1 << 31)).to(torch.int64) & 0xFFFFFFFF
+    assert torch.equal(a.tagged[:uc.nnz].to(torch.int64) & 0xFFFFFFFF, want)

@@ -1183,6 +1183,51 @@ def test_src_masked_launch_is_bitwise_the_dense_product(d, mode, monkeypatch):
                                               err_msg=f"frac={frac} pair={pair} rng={rg}")
 
 
+@pytest.mark.parametrize("d,mode", [(64, 0), (64, 1), (64, 2), (128, 0), (256, 1)])
+def test_tagged_indices_launch_is_bitwise_the_src_masked_launch(d, mode, monkeypatch):
+    """bbgr_spmm_args.tag_out: a full two-row launch also writes the column
+    indices with bit 31 set off tag_mask, and its product is unchanged;
+    src_tagged: a masked launch reading liveness from that copy is bitwise the
+    src_mask launch (live fractions 0 .. 1, chunked long rows, every weight
+    mode). One-row CSRs refuse both."""
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(700 + d + mode)
+    Rn, Cn = 2500, 900
+    deg = rng.geometric(0.1, Rn) - 1
+    deg[rng.choice(Rn, 5, replace=False)] = [16, 17, 31, 200, 900]
+    rows = np.repeat(np.arange(Rn), deg).astype(np.int32)
+    cols = rng.integers(0, Cn, rows.size).astype(np.int32)
+    vals = rng.uniform(0.1, 1.0, rows.size).astype(np.float32)
+    cs = rng.uniform(0.5, 2.0, Cn).astype(np.float32)
+    c = Csr(rows, cols, Rn, Cn, DEV, edge_values=t(vals) if mode == 1 else None,
+            long_threshold=64, chunk_edges=128)
+    prod = Product(c, c.values if mode == 1 else None, t(cs) if mode == 2 else None, None, {})
+    x = rng.uniform(-1, 1, (Cn, d)).astype(np.float32)
+    monkeypatch.setenv("BBGR_SPMM_PAIR", "1")
+    idx = c.indices[:c.nnz].long()
+    for frac in (0.0, 0.05, 0.41, 0.9, 1.0):
+        m = t((rng.random(Cn) < frac).astype(np.uint8), torch.uint8)
+        xm = t(x) * m[:, None].float()
+        tag = torch.full((c.nnz,), 12345, dtype=torch.int32, device=DEV)
+        ref = torch.full((Rn, d), 7.0, device=DEV)
+        got = torch.full((Rn, d), 7.0, device=DEV)
+        spmm(prod, xm, True, y=ref, y_scale_s=0.5)
+        spmm(prod, xm, True, y=got, y_scale_s=0.5, tag_out=tag, tag_mask=m)
+        assert torch.equal(got, ref), f"writer frac={frac}"
+        want = torch.where(m[idx].bool(), idx, idx | (1 << 31)) & 0xFFFFFFFF
+        assert torch.equal(tag.long() & 0xFFFFFFFF, want), f"tags frac={frac}"
+        ref.fill_(7.0)
+        got.fill_(7.0)
+        spmm(prod, xm, True, y=ref, y_scale_s=0.5, src_mask=m)
+        spmm(prod, xm, True, y=got, y_scale_s=0.5, src_mask=m, tagged=tag)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(got.cpu().numpy(), ref.cpu().numpy(),
+                                      err_msg=f"reader frac={frac}")
+    monkeypatch.setenv("BBGR_SPMM_PAIR", "0")
+    with pytest.raises(_lib.BbgrError, match="two-row CSR"):
+        spmm(prod, t(x), True, y=got, src_mask=m, tagged=tag)
+
+
 @pytest.mark.parametrize("variant", ["gs", "method_a", "jacobi"])
 def test_every_layer_vs_oracle(gold, variant):
     """SURVEY §8(d) parity, per layer k and side: the operators' products
