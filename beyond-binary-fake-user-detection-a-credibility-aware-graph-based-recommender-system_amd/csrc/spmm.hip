@@ -100,9 +100,16 @@ struct SpmmParams {
 // the mask byte's dependent load out of every batch's index -> gather chain.
 constexpr int TAG_NONE = 0, TAG_WRITE = 1, TAG_READ = 2;
 
-__device__ __forceinline__ void tag_store(const SpmmParams &P, long e, int col) {
-  __builtin_nontemporal_store(P.tag_mask[col] ? col : (int)((unsigned)col | 0x80000000u),
-                              P.tag_out + e);
+// The writer loads the mask byte of an edge's column right after the index
+// and stores the tagged index only after the batch's gathers are issued, so
+// the dependent mask load never stalls the gather chain (stored before the
+// gathers, its wait exposed an L2 round trip per batch: +0.26 ms per C4 user
+// product). col < 0: no edge in this lane.
+__device__ __forceinline__ int tag_of(const SpmmParams &P, int col) {
+  return col < 0 ? 0 : (int)P.tag_mask[col];
+}
+__device__ __forceinline__ void tag_store(const SpmmParams &P, long e, int col, int live) {
+  __builtin_nontemporal_store(live ? col : (int)((unsigned)col | 0x80000000u), P.tag_out + e);
 }
 
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 y) {
@@ -340,7 +347,6 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     float mw = 0.f;
     if (lane < n && ((live >> lane) & 1u)) {
       my = ld_edge(P.indices + e0 + lane);
-      if constexpr (TAG == TAG_WRITE) tag_store(P, (long)e0 + lane, my);
       // exact-zero source row (a tagged index carries it in its sign)
       if (MASKED && !BITS && TAG != TAG_READ && P.src_mask && !P.src_mask[my]) my = -1;
       if (my >= 0) {
@@ -348,6 +354,8 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
       }
     }
+    int tm = 0;
+    if constexpr (TAG == TAG_WRITE) tm = tag_of(P, my);
     if constexpr (MASKED && BITS) {   // live edges first (sparse: ~1 of 16 live)
       n = compact_live<WMODE>(my, mw);
     } else if (MASKED && (TAG == TAG_READ || P.src_mask)) {   // skip 16-edge batches with no live source (group-uniform)
@@ -385,6 +393,9 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
           for (int k = 0; k < V; ++k) acc[k] = f4_fma(w, v[j][k], acc[k]);
         }
       }
+    }
+    if constexpr (TAG == TAG_WRITE) {
+      if (lane < n) tag_store(P, (long)e0 + lane, my, tm);
     }
   }
 }
@@ -529,7 +540,6 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     float mwA = 0.f, mwB = 0.f;
     if (lane < na) {
       myA = ld_edge(P.indices + ebA + o + lane);
-      if constexpr (TAG == TAG_WRITE) tag_store(P, (long)ebA + o + lane, myA);
       if (MASKED && TAG != TAG_READ && P.src_mask && !P.src_mask[myA]) myA = -1;
       if (myA >= 0) {
         if (WMODE == 1) mwA = ld_edge(P.edge_val + ebA + o + lane);
@@ -538,12 +548,16 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     }
     if (lane < nb) {
       myB = ld_edge(P.indices + ebB + o + lane);
-      if constexpr (TAG == TAG_WRITE) tag_store(P, (long)ebB + o + lane, myB);
       if (MASKED && TAG != TAG_READ && P.src_mask && !P.src_mask[myB]) myB = -1;
       if (myB >= 0) {
         if (WMODE == 1) mwB = ld_edge(P.edge_val + ebB + o + lane);
         if (WMODE == 2) mwB = P.col_scale[myB] * P.col_scale_s;
       }
+    }
+    int tmA = 0, tmB = 0;
+    if constexpr (TAG == TAG_WRITE) {
+      tmA = tag_of(P, myA);
+      tmB = tag_of(P, myB);
     }
     if (MASKED && (TAG == TAG_READ || P.src_mask)) {   // a batch with no live source adds nothing
       const unsigned long long la = __ballot(myA >= 0), lb = __ballot(myB >= 0);
@@ -602,6 +616,10 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
           }
         }
       }
+    }
+    if constexpr (TAG == TAG_WRITE) {
+      if (lane < na) tag_store(P, (long)ebA + o + lane, myA, tmA);
+      if (lane < nb) tag_store(P, (long)ebB + o + lane, myB, tmB);
     }
   }
 }

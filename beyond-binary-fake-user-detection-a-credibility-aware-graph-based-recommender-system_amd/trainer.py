@@ -149,15 +149,18 @@ class FusedTrainer:
         # (63k at C4) instead of testing the mask byte of every item row.
         # Its launches take the list at its length (P.ListLength) when the step
         # runs eagerly, at its capacity with the device count when captured.
-        # GS, K >= 2, a two-row user CSR: the first forward user product writes
-        # the user CSR's column indices tagged with the item frontier (bit 31 =
-        # dead item, bbgr_spmm_args.tag_out), and the first backward user
-        # product reads the frontier from them instead of loading the mask byte
-        # of every edge (src_tagged; bitwise the mask launch). 4 B per edge.
+        # BBGR_TAGGED=1 (GS, K >= 2, a two-row user CSR): the first forward user
+        # product writes the user CSR's column indices tagged with the item
+        # frontier (bit 31 = dead item, bbgr_spmm_args.tag_out), and the first
+        # backward user product reads the frontier from them instead of loading
+        # the mask byte of every edge (src_tagged; bitwise the mask launch).
+        # Off by default: at C4 the reader drops 0.905 -> 0.770 ms but the
+        # writer's 50M extra mask-byte loads cost the forward product +0.26 ms
+        # (1.467 -> 1.723 ms; profiles/round6/r6e_tagged_ab.txt).
         self.tagged = None
         uc = graph.user_csr
         if (self.frontier and order == ORDER_GS and num_layers >= 2 and emb_dim >= 64
-                and uc.nnz <= 24 * uc.n_rows and os.environ.get("BBGR_TAGGED", "1") != "0"):
+                and uc.nnz <= 24 * uc.n_rows and os.environ.get("BBGR_TAGGED", "0") == "1"):
             self.tagged = torch.empty(max(uc.nnz, 1), dtype=torch.int32, device=dev)
         self.item_list = self.item_count = self.item_len = None
         if self.frontier and order == ORDER_GS:

@@ -193,13 +193,14 @@ def test_tagged_user_indices_step_is_bitwise_the_mask_step(fuse, K, monkeypatch)
     CSR's indices tagged with the item frontier and the first backward user
     product reads them (bbgr_spmm_args.tag_out / src_tagged) instead of the
     mask byte per edge: losses, weights and moments equal the mask step's bit
-    for bit over five steps (BBGR_TAGGED=0 keeps the mask)."""
+    for bit over five steps (BBGR_TAGGED=1 turns it on; the default keeps the
+    mask)."""
     e, g = _graph()
     kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=64, num_layers=K, batch_size=256,
               frontier=True, fuse_adam=fuse, seed=7)
-    a = FusedTrainer(g, "v2_pop", **kw)
-    monkeypatch.setenv("BBGR_TAGGED", "0")
     b = FusedTrainer(g, "v2_pop", **kw)
+    monkeypatch.setenv("BBGR_TAGGED", "1")
+    a = FusedTrainer(g, "v2_pop", **kw)
     assert a.tagged is not None and b.tagged is None
     for _ in range(5):
         assert float(a.step()) == float(b.step())
