@@ -191,8 +191,11 @@ class SpmmTimer:
     rows and edges each launch actually processes (bench.py's traversed-edge
     figure; run over extra steps outside the timed region)."""
 
-    def __init__(self, count: bool = False):
+    def __init__(self, count: bool = False, select=None):
         self.count = count
+        # select(kind, prod) -> bool: time only those launches (the others run
+        # without events, so the timer adds no gaps around them)
+        self.select = select
         # (rows, nnz, d, kind, start_event, end_event, table_rows, n_cols, masks)
         self.records = []
         # (kind, masks, table_rows, n_cols, d, rows_t, visited_t, gathered_t): device counts
@@ -432,6 +435,9 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     masked = src_mask is not None or row_mask is not None or row_list is not None
     kind = "masked" if masked else ("full" if adam is None else
                                     "adam" if adam.grad is None else "adam_side")
+    if _timer.select is not None and not _timer.select(kind, prod):
+        call("bbgr_spmm", ctypes.byref(cs), ctypes.byref(a), stream_handle())
+        return
     if listed_on_device:   # the list is row_mask's rows, built on the stream
         row_list = None
     if _timer.count:
