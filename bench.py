@@ -400,6 +400,10 @@ def measure_weak(args, cfg, rank: int, world: int, dev, xp: dict, frontier) -> d
                     "after the strong line in the same run"}
 
 
+# --graph auto: replay the step as one HIP graph below this many edges (C1,
+# C2: launch-bound steps; at C4 replay and eager tie)
+GRAPH_MAX_EDGES = 4_000_000
+
 # per-rank compute of the C4 user-row step at N = 8, measured alone (DESIGN
 # §6: one chain with inline collectives / two column chains): the constants of
 # the chain-setting rule; other (config, N) have no measured constants
@@ -706,7 +710,6 @@ def main():
                                                 emb_dim=d, num_layers=K, batch_size=B,
                                                 device=dev, frontier=frontier, **xq)
 
-    from bbgr.trainer import FRONTIER_MIN_EDGES
     count_steps = max(1, args.count_steps)
 
     def measure(trainer, part: str, dense_check: int) -> dict:
@@ -723,7 +726,7 @@ def main():
         log(f"[bench] rank {rank}: {part} setup done, E={E} (local {E_local}), frontier="
             f"{trainer.frontier}, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB")
         use_graph = not dist_mode and (args.graph == "on" or (args.graph == "auto"
-                                                              and E < FRONTIER_MIN_EDGES))
+                                                              and E < GRAPH_MAX_EDGES))
         step_fn = trainer.step
         if use_graph:
             from bbgr.trainer import GraphedStep

@@ -39,10 +39,12 @@ VARIANTS = {
 }
 
 # frontier="auto": masks pay only on graphs whose full-CSR products take well
-# over the mask build (~0.05 ms of small launches). At C2 (1M edges) the masked
-# step measured 1.092 ms against 1.058 dense (profiles/round1-2/r08_c2_bench.json); at
-# C4 (50M) 17.0 against 23.5. Below this many edges the step runs dense.
-FRONTIER_MIN_EDGES = 4_000_000
+# over the mask build (~0.05 ms of small launches). Round 6, graph-replayed
+# steps: C2 (1M edges) 0.577 ms masked against 0.597 dense, C1 (100K) 0.387
+# against 0.300 (profiles/round6/r6c_c{1,2}_frontier_*.json; round 1 measured C2
+# the other way, 1.092 vs 1.058 ms, before the products got faster); C4 (50M)
+# 16.3 against 22.4. Below this many edges the step runs dense.
+FRONTIER_MIN_EDGES = 500_000
 
 
 def resolve_frontier(frontier, nnz: int) -> bool:
