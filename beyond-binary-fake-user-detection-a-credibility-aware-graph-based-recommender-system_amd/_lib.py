@@ -93,6 +93,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_map", c_void_p),
         ("adam_moments_unmapped", c_int32),
         ("tag_out", c_void_p), ("tag_mask", c_void_p), ("src_tagged", c_void_p),
+        ("adam_mirror", c_void_p),
     ]
 
 

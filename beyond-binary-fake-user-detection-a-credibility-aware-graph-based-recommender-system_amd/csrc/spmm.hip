@@ -91,6 +91,7 @@ struct SpmmParams {
   int adam_mrow;               // moments at the launch row (args.adam_moments_unmapped)
   int *tag_out;                // tagged-index copy written by a full launch (args.tag_out)
   const unsigned char *tag_mask;
+  float *adam_mirror;          // caller-order copy of the updated param rows (args.adam_mirror)
 };
 
 // Tagged column indices (ABI 10): a full launch over a CSR can write a copy of
@@ -638,9 +639,11 @@ __device__ __forceinline__ AdamConsts launch_adam_consts(const SpmmParams &P) {
   return c;
 }
 
+// `row`: the param row; `mrow`: the moments' row; `crow`: the row of the
+// caller-order mirror the updated param row is also stored to (adam_mirror)
 template <int D>
-__device__ __forceinline__ void adam_row(const SpmmParams &P, long row, long mrow, int lane,
-                                         const float4 (&G)[RowShape<D>::V]) {
+__device__ __forceinline__ void adam_row(const SpmmParams &P, long row, long mrow, long crow,
+                                         int lane, const float4 (&G)[RowShape<D>::V]) {
   constexpr int V = RowShape<D>::V;
   const AdamConsts ac = launch_adam_consts(P);
   float4 *pp = reinterpret_cast<float4 *>(P.adam_p + (long)row * P.adam_ld) + lane;
@@ -658,6 +661,8 @@ __device__ __forceinline__ void adam_row(const SpmmParams &P, long row, long mro
     adam_elem(p4.w, G[k].w, m4.w, v4.w, ac);
     if (row >= P.nt_out_from) st_nt(pp + 16 * k, p4);
     else pp[16 * k] = p4;
+    if (P.adam_mirror)   // write-only random rows: streamed
+      st_nt(reinterpret_cast<float4 *>(P.adam_mirror + crow * P.adam_ld) + lane + 16 * k, p4);
     if (ntm) {
       st_nt(pm + 16 * k, m4);
       st_nt(pv + 16 * k, v4);
@@ -699,6 +704,7 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
     }
     const long ra_ = P.adam_map ? (long)P.adam_map[row] : ry;   // the Adam's rows
     const long rm_ = P.adam_mrow ? (long)row : ra_;                // its moments' rows
+    const long rp_ = P.adam_mirror ? rm_ : ra_;                    // its param's rows
     if (P.adam_p && P.adam_g) {   // Adam of another table riding on this row write
       const float4 *gr = reinterpret_cast<const float4 *>(P.adam_g + ra_ * P.adam_g_ld) + lane;
       float4 Ga[V];
@@ -708,9 +714,9 @@ __device__ __forceinline__ void epilogue(const SpmmParams &P, int row, int lane,
         Ga[k] = make_float4(P.adam_g_scale * g4.x, P.adam_g_scale * g4.y,
                             P.adam_g_scale * g4.z, P.adam_g_scale * g4.w);
       }
-      adam_row<D>(P, ra_, rm_, lane, Ga);
+      adam_row<D>(P, rp_, rm_, ra_, lane, Ga);
     } else if (P.adam_p) {
-      adam_row<D>(P, ra_, rm_, lane, G);
+      adam_row<D>(P, rp_, rm_, ra_, lane, G);
     }
   }
   const long rc = P.acc_map ? (long)P.acc_map[row] : (long)row;
@@ -1305,10 +1311,13 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.adam_g_scale = a->adam_grad_scale;
   P.adam_map = a->adam_map;
   P.adam_mrow = a->adam_moments_unmapped != 0;
+  P.adam_mirror = a->adam_mirror;
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {
-  if (!a->adam_param) return true;
+  if (!a->adam_param) return !a->adam_mirror;
+  if (a->adam_mirror && !(a->adam_moments_unmapped && ld_ok(a->adam_mirror, a->adam_ld, d)))
+    return false;
   const bool dev = a->adam_state != nullptr;
   return a->adam_exp_avg && a->adam_exp_avg_sq && ld_ok(a->adam_param, a->adam_ld, d) &&
          ld_ok(a->adam_exp_avg, a->adam_ld, d) && ld_ok(a->adam_exp_avg_sq, a->adam_ld, d) &&

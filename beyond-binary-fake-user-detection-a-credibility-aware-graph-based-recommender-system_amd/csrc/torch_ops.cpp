@@ -194,6 +194,9 @@ struct AdamTable {
   float lr = 1e-3f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, wd = 0.f;
   float bc1 = 1.f, bc2s = 1.f;
   bool moments_graph = false;   // m, v in the graph's row order (adam_moments_unmapped)
+  // p is then graph-ordered too (the optimizer's master copy) and every updated
+  // row is also written to this caller-order table (bbgr_spmm_args.adam_mirror)
+  Tensor mirror;
 };
 
 struct Opts {
@@ -286,6 +289,7 @@ static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) 
     a.adam_grad_scale = o.adam_grad_scale;
     a.adam_map = o.adam_map;
     a.adam_moments_unmapped = A.moments_graph ? 1 : 0;
+    if (A.mirror.defined()) a.adam_mirror = A.mirror.data_ptr<float>();
   }
   // input-order source rows carry no hot prefix; mapped output rows neither
   a.stream_from = o.src_input ? 0 : pr.stream_from(d);
@@ -465,9 +469,17 @@ static Tensor to_graph_rows(const Tensor &ids, int64_t n, const Tensor &rank64) 
 // reads the finals only at its batch rows (the reference's get_user_item_emb
 // -> bpr_loss, Version-2:858-859) skips the two last-layer full products and
 // the full-table accumulator passes. Jacobi order: the dense chain.
+// graph_tables: u0 / i0 are the GRAPH-ordered copies of the caller's tables
+// (the in-backward optimizer's master copies, input-order pair, K >= 2): the
+// first products gather them through the internal column indices (the hot
+// prefix of the degree order) and the layer-1 accumulators read them unmapped;
+// the returned finals are in the caller's order as always. Same values, same
+// per-row arithmetic: bitwise the caller-order call.
 static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, const Tensor &i0,
                                                int64_t K, bool gs, const Tensor &users_,
-                                               const Tensor &items_) {
+                                               const Tensor &items_, bool graph_tables = false) {
+  TORCH_CHECK(!graph_tables || (gs && K >= 2 && P.io),
+              "propagate_rows_graph: an input-order GS pair and num_layers >= 2");
   if (!gs || K == 0) return forward_chain(P, u0, i0, K, gs);
   const int64_t U = P.U, I = P.I, d = u0.size(1);
   check_table("user table", u0, U, d);
@@ -531,12 +543,13 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
     Opts oi;
     oi.y = bufI;
     oi.y_scale = P.feed_fwd_iu;
-    const AccPlan ai = acc_plan(k, K, i0, acc_i, int_i, am_i, iota_i);
+    AccPlan ai = acc_plan(k, K, i0, acc_i, int_i, am_i, iota_i);
+    if (graph_tables && k == 1) ai.in_map = nullptr;   // i0 already in the graph's order
     set_acc(oi, ai);
     oi.acc_mask = (ai.out_map ? mi_in : mi).data_ptr<uint8_t>();
     oi.acc_scale = P.fi.out_scale;
     oi.gamma = g;
-    oi.src_input = P.io && k == 1;
+    oi.src_input = P.io && k == 1 && !graph_tables;
     if (k == K) {   // the item frontier, listed on the device
       oi.row_mask = fr.data_ptr<uint8_t>();
       oi.row_list = flist.data_ptr<int64_t>();
@@ -547,7 +560,8 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
     Opts ou;
     if (k < K) ou.y = bufU;
     ou.y_scale = P.feed_fwd_ui;
-    const AccPlan au = acc_plan(k, K, u0, acc_u, int_u, am_u, iota_u);
+    AccPlan au = acc_plan(k, K, u0, acc_u, int_u, am_u, iota_u);
+    if (graph_tables && k == 1) au.in_map = nullptr;
     set_acc(ou, au);
     ou.acc_mask = (au.out_map ? mu_in : mu).data_ptr<uint8_t>();
     ou.acc_scale = P.fu.out_scale;
@@ -973,6 +987,16 @@ static std::tuple<Tensor, Tensor> propagate_rows_cuda(const Tensor &u0, const Te
   return forward_rows(*P, u0.contiguous(), i0.contiguous(), K, is_gs(order), users, items);
 }
 
+// bbgr::propagate_rows_graph — propagate_rows (GS) from the graph-ordered
+// master copies of the weights (no autograd: the in-backward step's forward)
+static std::tuple<Tensor, Tensor> propagate_rows_graph_cuda(const Tensor &u0g, const Tensor &i0g,
+                                                            const Tensor &users,
+                                                            const Tensor &items, int64_t key,
+                                                            int64_t K) {
+  auto P = pair_of(key);
+  return forward_rows(*P, u0g.contiguous(), i0g.contiguous(), K, true, users, items, true);
+}
+
 static std::tuple<Tensor, Tensor> propagate_backward_cuda(const Tensor &gU_, const Tensor &gI_,
                                                           int64_t key, int64_t K,
                                                           c10::string_view order) {
@@ -1356,7 +1380,8 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
                                    const Tensor &m_i, const Tensor &v_i, double lr, double beta1,
                                    double beta2, double eps, double wd, double bc1_u,
                                    double bc2s_u, double bc1_i, double bc2s_i,
-                                   bool moments_graph) {
+                                   bool moments_graph, const c10::optional<Tensor> &u_graph,
+                                   const c10::optional<Tensor> &i_graph) {
   auto P = pair_of(key);
   TORCH_CHECK(K >= 2, "bpr_adam_backward: the in-backward Adam needs num_layers >= 2");
   const int64_t d = u0.size(1), U = P->U, I = P->I;
@@ -1391,6 +1416,23 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   // read and written through the row maps (an input-order pair; otherwise the
   // two orders are one)
   sa.user.moments_graph = sa.item.moments_graph = moments_graph && P->io;
+  // graph-ordered master copies of the weights: the Adam reads and writes them
+  // with the moments (streamed) and writes the caller's rows only (mirror)
+  const bool masters = u_graph.has_value() && u_graph->defined();
+  TORCH_CHECK(masters == (i_graph.has_value() && i_graph->defined()),
+              "bpr_adam_backward: u_graph and i_graph go together");
+  if (masters) {
+    TORCH_CHECK(sa.user.moments_graph, "bpr_adam_backward: master copies need an input-order "
+                                       "pair with graph-ordered moments");
+    TORCH_CHECK(u_graph->sizes() == u0.sizes() && i_graph->sizes() == i0.sizes() &&
+                    u_graph->is_contiguous() && i_graph->is_contiguous() &&
+                    u_graph->scalar_type() == at::kFloat && i_graph->scalar_type() == at::kFloat,
+                "bpr_adam_backward: master copies shaped like the weights (contiguous fp32)");
+    sa.user.p = *u_graph;
+    sa.user.mirror = u0;
+    sa.item.p = *i_graph;
+    sa.item.mirror = i0;
+  }
   sa.ego_u_vals = at::mul(ru, kp1);
   // the item gradient / gl: the BPR rows, then the ego rows, per item in
   // ascending source order
@@ -1874,7 +1916,10 @@ TORCH_LIBRARY(bbgr, m) {
         "Tensor users, Tensor pos, Tensor neg, float reg, int pair_key, int num_layers, "
         "Tensor(c!) m_u, Tensor(d!) v_u, Tensor(e!) m_i, Tensor(f!) v_i, float lr, float beta1, "
         "float beta2, float eps, float weight_decay, float bc1_u, float bc2s_u, float bc1_i, "
-        "float bc2s_i, bool moments_graph=False) -> ()");
+        "float bc2s_i, bool moments_graph=False, Tensor(g!)? u_graph=None, "
+        "Tensor(h!)? i_graph=None) -> ()");
+  m.def("propagate_rows_graph(Tensor u0g, Tensor i0g, Tensor users, Tensor items, "
+        "int pair_key, int num_layers) -> (Tensor, Tensor)");
   m.def("_register_pair(int key, Tensor?[] tensors, int[] meta) -> ()",
         &bbgr_torch::register_pair);
   m.def("_unregister_pair(int key) -> ()", &bbgr_torch::unregister_pair);
@@ -1895,6 +1940,7 @@ TORCH_LIBRARY_IMPL(bbgr, CUDA, m) {
   m.impl("bpr_loss_backward", &bbgr_torch::bpr_loss_backward_cuda);
   m.impl("bpr_loss_sparse_ego", &bbgr_torch::bpr_loss_sparse_ego_cuda);
   m.impl("bpr_adam_backward", &bbgr_torch::bpr_adam_backward_cuda);
+  m.impl("propagate_rows_graph", &bbgr_torch::propagate_rows_graph_cuda);
 }
 
 TORCH_LIBRARY_IMPL(bbgr, Meta, m) {

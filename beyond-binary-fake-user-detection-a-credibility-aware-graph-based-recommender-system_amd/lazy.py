@@ -170,7 +170,13 @@ class _BprAdamStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, u0, i0, users, pos, neg, reg, pending, opt):
         from . import ops
-        uf, itf = pending.rows_fn(users, torch.cat([pos, neg]))
+        key, K, maps = pending.step
+        mg = opt.masters([u0, i0], maps) if maps is not None else None
+        if mg is not None:   # the optimizer's graph-ordered copies are current
+            uf, itf = ops.propagate_rows_graph(mg[0], mg[1], users, torch.cat([pos, neg]),
+                                               key, K)
+        else:
+            uf, itf = pending.rows_fn(users, torch.cat([pos, neg]))
         loss = ops.bpr_loss(uf, itf, u0, i0, users, pos, neg, float(reg), None, 0.0)
         ctx.save_for_backward(uf, itf, u0, i0, users, pos, neg)
         ctx.reg, ctx.chain, ctx.opt = float(reg), pending.step, opt
@@ -185,12 +191,17 @@ class _BprAdamStep(torch.autograd.Function):
         def run(states, group, corr):
             su, si = states
             b1, b2 = group["betas"]
+            # input-order pair: the Adam updates the graph-ordered master copies
+            # (built now if missing or stale) and writes the caller's rows
+            mg = ctx.opt.masters([u0, i0], maps, create=True) if maps is not None else None
             ops.bpr_adam_backward(g.detach(), uf, itf, u0.detach(), i0.detach(), users, pos,
                                   neg, ctx.reg, key, K, su["exp_avg"], su["exp_avg_sq"],
                                   si["exp_avg"], si["exp_avg_sq"], float(group["lr"]),
                                   float(b1), float(b2), float(group["eps"]),
                                   float(group["weight_decay"]), corr[0][0], corr[0][1],
-                                  corr[1][0], corr[1][1], maps is not None)
+                                  corr[1][0], corr[1][1], maps is not None,
+                                  None if mg is None else mg[0], None if mg is None else mg[1])
+            run.masters_updated = mg is not None
 
         # an input-order pair: the moments live in the graph's row order
         # (FusedAdam converts them once, and back at its state_dict boundary)

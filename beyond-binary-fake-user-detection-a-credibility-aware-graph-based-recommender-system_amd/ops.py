@@ -14,6 +14,9 @@ libtorch / TorchScript caller reaches the same operators as torch.ops.bbgr.*:
   bbgr::propagate_rows(u0, i0, users, items, pair_key, num_layers, order)
                                 -> (u_final, i_final) valid at the listed rows only
                                 (GS; backward: propagate's)
+  bbgr::propagate_rows_graph(u0g, i0g, users, items, pair_key, num_layers)
+                                -> propagate_rows (GS) from graph-ordered copies of
+                                the weights (no autograd; the in-backward step)
   bbgr::propagate_backward(gU, gI, pair_key, num_layers, order) -> (grad_u0, grad_i0)
   bbgr::propagate_backward_rows(iu, vu, gI, num_users, pair_key, num_layers,
                                 order, ii=None, vi=None) -> (grad_u0, grad_i0)
@@ -71,6 +74,7 @@ bpr_loss = torch.ops.bbgr.bpr_loss
 bpr_loss_backward = torch.ops.bbgr.bpr_loss_backward
 bpr_loss_sparse_ego = torch.ops.bbgr.bpr_loss_sparse_ego
 bpr_adam_backward = torch.ops.bbgr.bpr_adam_backward
+propagate_rows_graph = torch.ops.bbgr.propagate_rows_graph
 
 # autograd node name of bbgr::propagate (bpr.py reads the graph)
 PROPAGATE_NODE = "torch::autograd::CppNode<bbgr_torch::PropagateFn>"

@@ -173,6 +173,14 @@ class FusedAdam(torch.optim.Optimizer):
     map. The optimizer converts them once, and back wherever they leave it:
     state_dict(), moments(), and a step() that updates them outside the
     backward. load_state_dict() takes the caller's order, as torch's Adam.
+    There it also keeps a graph-ordered master copy of each of the two weight
+    tables (masters()): the in-backward Adam streams it with the moments and
+    only WRITES the caller's rows (bbgr_spmm_args.adam_mirror), and the next
+    step's forward gathers the master copies through the graph's own column
+    indices (bbgr::propagate_rows_graph). A copy is used only while its
+    table's version is the one the optimizer left (any other in-place write to
+    the weights makes it stale; the next in-backward step rebuilds it); it
+    costs one more table of each size in device memory.
 
     The fused step assumes bpr_loss is the only consumer of the two tables in
     the loss. A gradient that reaches them by another path (e.g. a term
@@ -192,6 +200,8 @@ class FusedAdam(torch.optim.Optimizer):
         # id(param) -> map[graph row] = caller row: its moments are held in the
         # graph's row order (in-backward steps on an input-order drop-in pair)
         self._graph_rows: dict = {}
+        # id(param) -> [graph-ordered copy, its row map, the param's version it matches]
+        self._masters: dict = {}
         if self.fuse_backward:
             import weakref
             me = weakref.ref(self)
@@ -275,6 +285,29 @@ class FusedAdam(torch.optim.Optimizer):
         self._graph_rows.clear()   # a loaded state is in the caller's order
         super().load_state_dict(state_dict)
 
+    # False: no master copies (the in-backward step reads and writes the
+    # caller-order weight rows through the row map, as before round 6)
+    use_masters = True
+
+    def masters(self, params, row_maps, create: bool = False):
+        """The graph-ordered master copies of `params` (copy[r] = p[map[r]]),
+        or None unless every one is current with its parameter (same row map,
+        the version the optimizer left). create=True builds the missing or
+        stale ones from the parameters first."""
+        if not self.use_masters:
+            return None
+        out = []
+        for p, m in zip(params, row_maps):
+            e = self._masters.get(id(p))
+            ok = (e is not None and e[1] is m and e[2] == p._version
+                  and e[0].device == p.device and e[0].shape == p.shape)
+            if not ok:
+                if not create:
+                    return None
+                e = self._masters[id(p)] = [p.detach().index_select(0, m), m, p._version]
+            out.append(e[0])
+        return out
+
     @torch.no_grad()
     def step_in_backward(self, params, run, row_maps=None) -> None:
         """One Adam step of `params` (one param group) carried out by `run(states,
@@ -302,6 +335,11 @@ class FusedAdam(torch.optim.Optimizer):
         for p in params:
             self._stepped.add(id(p))
             torch.autograd.graph.increment_version(p)
+            e = self._masters.get(id(p))
+            if e is not None and getattr(run, "masters_updated", False):
+                e[2] = p._version   # the copy was updated with the weights
+            elif e is not None:
+                del self._masters[id(p)]
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -291,6 +291,12 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   follow adam_map: the drop-in optimizer stores its moments in the graph's */
 /*   order, so only the caller-order weight row is read and written at       */
 /*   random (bbgr.optim.FusedAdam converts them at its state_dict boundary). */
+/* adam_mirror (nullable, with adam_moments_unmapped; ABI 10): adam_param is */
+/*   then in the launch's row order as well (row r, like the moments), and   */
+/*   every updated param row is also stored to adam_mirror row adam_map[r]   */
+/*   (y_map[r] without adam_map), stride adam_ld: the drop-in optimizer keeps */
+/*   a graph-ordered master copy of a weight table, streamed with its        */
+/*   moments, and the caller's table is only written (no random row read).   */
 /* tag_out (nullable, int32 [nnz], with tag_mask [n_cols] bytes; ABI 10): a  */
 /*   full launch (no masks, list, range or fused Adam) also writes            */
 /*   tag_out[e] = indices[e] with bit 31 set where tag_mask[indices[e]] == 0, */
@@ -368,6 +374,7 @@ typedef struct {
   int32_t *tag_out;
   const uint8_t *tag_mask;
   const int32_t *src_tagged;
+  float *adam_mirror;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,

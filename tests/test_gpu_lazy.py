@@ -320,3 +320,46 @@ def test_fused_backward_adam_refuses_a_second_gradient_path():
     loss.backward()
     with pytest.raises(RuntimeError, match="only consumer"):
         oa.step()
+
+
+def test_fused_backward_adam_master_copies_are_bitwise_the_caller_order_step():
+    """FusedAdam(fuse_backward=True) on the degree-ordered drop-in graph keeps
+    graph-ordered master copies of the two weight tables: the in-backward Adam
+    updates them with the moments and writes the caller's rows (adam_mirror),
+    and the next forward gathers them (bbgr::propagate_rows_graph). Against the
+    same optimizer without them: losses, weights and moments bit for bit over
+    five steps, including a step after an outside in-place write to the
+    weights (the copies are stale then and are rebuilt, not used)."""
+    from bbgr.optim import FusedAdam
+    batches = [_batch(s) for s in range(5)]
+    a, b = _model(3), _model(3)
+    oa = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
+    ob = FusedAdam(b.parameters(), lr=1e-3, fuse_backward=True)
+    ob.use_masters = False
+    for k, (users, pos, neg) in enumerate(batches):
+        if k == 3:   # an outside write: both models, the same rows
+            with torch.no_grad():
+                for m in (a, b):
+                    m.user_emb.weight[:7] *= 0.5
+                    m.item_emb.weight[3] += 0.25
+            assert oa.masters([a.user_emb.weight, a.item_emb.weight],
+                              [a._pair.io.user_map64, a._pair.io.item_map64]) is None
+        ls = []
+        for m, o in ((a, oa), (b, ob)):
+            uf, itf = m.get_user_item_emb()
+            loss = m.bpr_loss(users, pos, neg, uf, itf, 1e-4)
+            o.zero_grad()
+            loss.backward()
+            o.step()
+            ls.append(float(loss))
+        assert ls[0] == ls[1], k
+        if k >= 1:
+            assert len(oa._masters) == 2 and not ob._masters
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)
+        for x, y in zip(oa.moments(pa), ob.moments(pb)):
+            assert torch.equal(x, y)
+    ug, ig = oa.masters([a.user_emb.weight, a.item_emb.weight],
+                        [a._pair.io.user_map64, a._pair.io.item_map64])
+    assert torch.equal(ug, a.user_emb.weight.detach()[a._pair.io.user_map64])
+    assert torch.equal(ig, a.item_emb.weight.detach()[a._pair.io.item_map64])
