@@ -173,14 +173,14 @@ class FusedAdam(torch.optim.Optimizer):
     map. The optimizer converts them once, and back wherever they leave it:
     state_dict(), moments(), and a step() that updates them outside the
     backward. load_state_dict() takes the caller's order, as torch's Adam.
-    There it also keeps a graph-ordered master copy of each of the two weight
-    tables (masters()): the in-backward Adam streams it with the moments and
-    only WRITES the caller's rows (bbgr_spmm_args.adam_mirror), and the next
-    step's forward gathers the master copies through the graph's own column
-    indices (bbgr::propagate_rows_graph). A copy is used only while its
-    table's version is the one the optimizer left (any other in-place write to
-    the weights makes it stale; the next in-backward step rebuilds it); it
-    costs one more table of each size in device memory.
+    With use_masters = True it also keeps a graph-ordered master copy of each
+    of the two weight tables (masters()): the in-backward Adam streams it with
+    the moments and only WRITES the caller's rows (bbgr_spmm_args.adam_mirror),
+    and the next step's forward gathers the master copies through the graph's
+    own column indices (bbgr::propagate_rows_graph). A copy is used only while
+    its table's version is the one the optimizer left (any other in-place
+    write to the weights makes it stale; the next in-backward step rebuilds
+    it); it costs one more table of each size in device memory.
 
     The fused step assumes bpr_loss is the only consumer of the two tables in
     the loss. A gradient that reaches them by another path (e.g. a term
@@ -285,9 +285,12 @@ class FusedAdam(torch.optim.Optimizer):
         self._graph_rows.clear()   # a loaded state is in the caller's order
         super().load_state_dict(state_dict)
 
-    # False: no master copies (the in-backward step reads and writes the
-    # caller-order weight rows through the row map, as before round 6)
-    use_masters = True
+    # True: keep the graph-ordered master copies (off by default: measured at
+    # C4, the next forward's first item product gains 1.963 -> 1.888 ms but the
+    # user Adam product loses 2.563 -> 2.607 ms — the caller's rows are still
+    # written, so the copy adds a 1.28 GB stream where the random read it
+    # replaces cost little more; profiles/round6/r6g_masters_ab.txt)
+    use_masters = False
 
     def masters(self, params, row_maps, create: bool = False):
         """The graph-ordered master copies of `params` (copy[r] = p[map[r]]),

@@ -323,8 +323,9 @@ def test_fused_backward_adam_refuses_a_second_gradient_path():
 
 
 def test_fused_backward_adam_master_copies_are_bitwise_the_caller_order_step():
-    """FusedAdam(fuse_backward=True) on the degree-ordered drop-in graph keeps
-    graph-ordered master copies of the two weight tables: the in-backward Adam
+    """FusedAdam(fuse_backward=True, use_masters=True) on the degree-ordered
+    drop-in graph keeps graph-ordered master copies of the two weight tables:
+    the in-backward Adam
     updates them with the moments and writes the caller's rows (adam_mirror),
     and the next forward gathers them (bbgr::propagate_rows_graph). Against the
     same optimizer without them: losses, weights and moments bit for bit over
@@ -335,7 +336,7 @@ def test_fused_backward_adam_master_copies_are_bitwise_the_caller_order_step():
     a, b = _model(3), _model(3)
     oa = FusedAdam(a.parameters(), lr=1e-3, fuse_backward=True)
     ob = FusedAdam(b.parameters(), lr=1e-3, fuse_backward=True)
-    ob.use_masters = False
+    oa.use_masters, ob.use_masters = True, False
     for k, (users, pos, neg) in enumerate(batches):
         if k == 3:   # an outside write: both models, the same rows
             with torch.no_grad():
