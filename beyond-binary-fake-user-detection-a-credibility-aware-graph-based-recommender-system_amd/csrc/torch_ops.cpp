@@ -1289,15 +1289,17 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_cuda(
 // stream's work has drained, which destroying a stream waits for.
 // `role` keeps tables a single launch uses side by side apart: bbgr_ego_slots
 // takes a user and an item table at once, which must not be one buffer when
-// U == I (0 = first_slot, 1 = ego users, 2 = ego items).
+// U == I (0 = first_slot, 1 = ego users, 2 = ego items; 3 = bbgr_ego_rows'
+// zero-filled counts, whose fill value the role fixes).
 static constexpr size_t kFirstSlotScratch = 8;
-static Tensor slot_scratch(int64_t n_rows, const at::Device &dev, int64_t role = 0) {
+static Tensor slot_scratch(int64_t n_rows, const at::Device &dev, int64_t role = 0,
+                           int32_t fill = 0x7fffffff) {
   static std::mutex mu;
   static std::map<std::tuple<int64_t, int64_t, int64_t, int64_t>, std::pair<Tensor, uint64_t>>
       scratch;
   static uint64_t tick = 0;
   const auto fresh = [&] {
-    return at::full({std::max<int64_t>(n_rows, 1)}, 0x7fffffff,
+    return at::full({std::max<int64_t>(n_rows, 1)}, fill,
                     at::TensorOptions().dtype(at::kInt).device(dev));
   };
   if (capturing()) return fresh();   // a captured step fills its own (the fill replays with it)
@@ -1350,16 +1352,18 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
                        cu.data_ptr<int64_t>(), sp.data_ptr<int64_t>(), sn.data_ptr<int64_t>(),
                        cur_stream()),
         "bbgr_ego_slots");
-  Tensor ue_c = ue.index_select(0, iu).contiguous(), ie_c = ie.index_select(0, ii).contiguous();
-  Tensor g = at::zeros({3 * B, d}, f32(ue));
+  // every row written (zero off the first slots): no fill; the counts scratch
+  // is zero between calls
+  Tensor g = at::empty({3 * B, d}, f32(ue));
   Tensor gu = g.narrow(0, 0, B), gi = g.narrow(0, B, 2 * B);
-  bbgr_bpr_args a = bpr_args(cu, sp, sn, ue_c, ie_c, ue_c, ie_c, reg, c10::nullopt, 0.0);
-  a.dloss = dl.data_ptr<float>();
-  a.g_ue = gu.data_ptr<float>();
-  a.ldgue = ld(gu);
-  a.g_ie = gi.data_ptr<float>();
-  a.ldgie = ld(gi);
-  check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr (ego rows)");
+  Tensor cnt = slot_scratch(3 * B, users.device(), 3, 0);
+  const Tensor uec = ue.contiguous(), iec = ie.contiguous();
+  check(bbgr_ego_rows(B, (int32_t)d, cu.data_ptr<int64_t>(), sp.data_ptr<int64_t>(),
+                      sn.data_ptr<int64_t>(), iu.data_ptr<int64_t>(), ii.data_ptr<int64_t>(),
+                      uec.data_ptr<float>(), ld(uec), iec.data_ptr<float>(), ld(iec),
+                      dl.data_ptr<float>(), (float)reg, cnt.data_ptr<int32_t>(),
+                      gu.data_ptr<float>(), ld(gu), gi.data_ptr<float>(), ld(gi), cur_stream()),
+        "bbgr_ego_rows");
   return {gu, gi, iu, ii};
 }
 

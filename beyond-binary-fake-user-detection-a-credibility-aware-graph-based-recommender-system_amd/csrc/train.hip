@@ -536,6 +536,59 @@ __global__ void ego_slots_reset_kernel(long B, int *first_u, int *first_i, const
   else first_i[ii[t - B]] = 0x7fffffff;
 }
 
+// bbgr_ego_rows: the ego-L2 rows in first-slot form. ego_count_kernel counts
+// each first slot's occurrences among the valid triples (int atomics: one per
+// occurrence, not d float atomics); ego_rows_kernel gives every slot s (one
+// 16-lane group each) y = gr * e added n times from +0.0 and re-zeroes its
+// count. All addends of a row are the same y, so the atomics' sum in any
+// order is this sequential sum, bit for bit.
+__global__ void ego_count_kernel(long B, const long *cu, const long *sp, const long *sn,
+                                 int *counts) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B || cu[t] < 0) return;
+  atomicAdd(counts + cu[t], 1);
+  atomicAdd(counts + B + sp[t], 1);
+  atomicAdd(counts + B + sn[t], 1);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ego_rows_kernel(long B, const long *iu, const long *ii,
+                                                       const float *ue, long ldue,
+                                                       const float *ie, long ldie,
+                                                       const float *dloss, float inv_b,
+                                                       float reg, int *counts, float *g_u,
+                                                       long ldgu, float *g_i, long ldgi) {
+  constexpr int V = D / 64;
+  const long s = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  if (s >= 3 * B) return;
+  const int n = counts[s];
+  const bool user = s < B;
+  float4 *dst = reinterpret_cast<float4 *>(user ? g_u + s * ldgu : g_i + (s - B) * ldgi) + lane;
+  float4 acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n > 0) {
+    // bbgr_bpr's G and gr, in its order
+    const float G = (dloss ? *dloss : 1.0f) * inv_b;
+    const float gr = 2.0f * reg * G;
+    const float4 *src = reinterpret_cast<const float4 *>(
+                            user ? ue + iu[s] * ldue : ie + ii[s - B] * ldie) + lane;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float4 e = src[16 * k];
+      const float4 y = make_float4(__fmul_rn(gr, e.x), __fmul_rn(gr, e.y), __fmul_rn(gr, e.z),
+                                   __fmul_rn(gr, e.w));
+      for (int j = 0; j < n; ++j)
+        acc[k] = make_float4(__fadd_rn(acc[k].x, y.x), __fadd_rn(acc[k].y, y.y),
+                             __fadd_rn(acc[k].z, y.z), __fadd_rn(acc[k].w, y.w));
+    }
+    if (lane == 0) counts[s] = 0;
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) dst[16 * k] = acc[k];
+}
+
 __global__ void graph_rows_kernel(long n, const long *ids, long n_rows, const long *rank,
                                   long *out) {
   const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1080,6 +1133,42 @@ extern "C" int bbgr_ego_slots(int64_t B, const int64_t *users, const int64_t *po
   hipLaunchKernelGGL(ego_slots_reset_kernel, dim3(g), dim3(256), 0, st, (long)B, first_u,
                      first_i, (const long *)iu, (const long *)ii);
   BBGR_LAUNCHED("ego_slots_reset_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int64_t *sp,
+                             const int64_t *sn, const int64_t *iu, const int64_t *ii,
+                             const float *ue, int64_t ldue, const float *ie, int64_t ldie,
+                             const float *dloss, float reg, int32_t *counts, float *g_u,
+                             int64_t ldgu, float *g_i, int64_t ldgi, bbgr_stream_t stream) {
+  BBGR_REQUIRE(B >= 0 && 3 * B < (1LL << 31), "bbgr_ego_rows: bad batch");
+  if (d != 64 && d != 128 && d != 256) {
+    set_error("bbgr_ego_rows: embedding dim %d unsupported (64, 128, 256)", d);
+    return BBGR_ERR_UNSUPPORTED;
+  }
+  if (B == 0) return BBGR_OK;
+  BBGR_REQUIRE(cu && sp && sn && iu && ii && ue && ie && counts && g_u && g_i,
+               "bbgr_ego_rows: null arrays");
+  BBGR_REQUIRE(aligned16(ue) && aligned16(ie) && aligned16(g_u) && aligned16(g_i) &&
+                   (ldue & 3) == 0 && (ldie & 3) == 0 && (ldgu & 3) == 0 && (ldgi & 3) == 0,
+               "bbgr_ego_rows: tables must be 16-byte aligned, ld % 4 == 0");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(ego_count_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
+                     (long)B, (const long *)cu, (const long *)sp, (const long *)sn, counts);
+  BBGR_LAUNCHED("ego_count_kernel");
+  const dim3 g((unsigned)((3 * B + 15) / 16));
+  const float inv_b = 1.0f / (float)B;
+#define BBGR_EGO_ROWS(DD)                                                                   \
+  hipLaunchKernelGGL(ego_rows_kernel<DD>, g, dim3(256), 0, st, (long)B, (const long *)iu, \
+                     (const long *)ii, ue, (long)ldue, ie, (long)ldie, dloss, inv_b, reg,   \
+                     counts, g_u, (long)ldgu, g_i, (long)ldgi)
+  switch (d) {
+    case 64: BBGR_EGO_ROWS(64); break;
+    case 128: BBGR_EGO_ROWS(128); break;
+    default: BBGR_EGO_ROWS(256); break;
+  }
+#undef BBGR_EGO_ROWS
+  BBGR_LAUNCHED("ego_rows_kernel");
   return BBGR_OK;
 }
 

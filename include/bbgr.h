@@ -547,6 +547,20 @@ int bbgr_ego_slots(int64_t B, const int64_t *users, const int64_t *pos, const in
                    int64_t *iu, int64_t *ii, int64_t *cu, int64_t *sp, int64_t *sn,
                    bbgr_stream_t stream);
 
+/* The ego-L2 gradient rows of a batch in first-slot form (ABI 10; the       */
+/* drop-in step's BPR backward), from bbgr_ego_slots' outputs: slot s of     */
+/* g_u [B, d] (s < B, user iu[s]) and of g_i [2B, d] (item ii[s]) receives    */
+/* y = (2 reg dloss / B) * e, e its ego row (ue[iu[s]] / ie[ii[s]]), added n  */
+/* times from +0.0, n = the slot's occurrences as a first slot (cu / sp / sn) */
+/* among the valid triples (cu[b] >= 0); other slots are written zero. Bitwise */
+/* bbgr_bpr's ego rows over the compact tables (identical addends, so its     */
+/* float atomics' order cannot matter) without their serialisation on a       */
+/* popular item's row. counts: int32 [3B] scratch, zero on entry and return.  */
+int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int64_t *sp, const int64_t *sn,
+                  const int64_t *iu, const int64_t *ii, const float *ue, int64_t ldue,
+                  const float *ie, int64_t ldie, const float *dloss, float reg, int32_t *counts,
+                  float *g_u, int64_t ldgu, float *g_i, int64_t ldgi, bbgr_stream_t stream);
+
 /* out[k] = rank[ids[k]] (rank NULL: ids[k]) for ids[k] in [0, n_rows), else */
 /* -1 (ABI 8): a caller's row ids as graph rows in one launch                */
 /* (bbgr::propagate_rows' batch lists; the marking kernels skip the -1).     */

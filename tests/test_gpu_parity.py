@@ -865,6 +865,46 @@ def test_first_slot_kernel_is_the_first_occurrence(n, hi):
         assert bool((first == 0x7fffffff).all())
 
 
+@pytest.mark.parametrize("B,U,I,d", [(1, 3, 2, 64), (8192, 50_000, 20_000, 64), (4096, 50, 30, 64),
+                                     (300, 300, 7, 128), (512, 900, 40, 256)])
+def test_ego_rows_kernel_is_the_atomic_formulation(B, U, I, d):
+    """bbgr_ego_rows (first-slot counts, then each slot's y added n times from
+    +0.0) is bitwise the bbgr_bpr ego rows it replaced (float atomics of the
+    identical addends, bpr.ego_grad_rows): Zipf-hot items repeated hundreds of
+    times, repeated users, invalid triples; the counts scratch is zero again."""
+    from bbgr import _lib
+    from bbgr import bpr
+    g = torch.Generator().manual_seed(B + U + I + d)
+    users = torch.randint(0, U, (B,), generator=g)
+    zipf = torch.distributions.Categorical(1.0 / torch.arange(1, I + 1, dtype=torch.float64) ** 1.1)
+    pos, neg = zipf.sample((B,)), zipf.sample((B,))
+    if B > 1:
+        users[::7] = users[0]
+        users[::97], neg[::89] = -1, I
+    du, dp, dn = (x.to(DEV) for x in (users, pos, neg))
+    ue = torch.randn(U, d, generator=g).to(DEV)
+    ie = torch.randn(I, d, generator=g).to(DEV)
+    dl = torch.tensor(0.37, device=DEV)
+    want_u, want_i, iu, ii = bpr.ego_grad_rows(dl, du, dp, dn, ue, ie, 1e-2)
+    fu = torch.full((U,), 0x7fffffff, dtype=torch.int32, device=DEV)
+    fi = torch.full((I,), 0x7fffffff, dtype=torch.int32, device=DEV)
+    out = torch.empty(6 * B, dtype=torch.int64, device=DEV)
+    P = _lib.ptr
+    _lib.call("bbgr_ego_slots", B, P(du), P(dp), P(dn), U, I, P(fu), P(fi), P(out), P(out[B:]),
+              P(out[3 * B:]), P(out[4 * B:]), P(out[5 * B:]), _lib.stream_handle())
+    cnt = torch.zeros(3 * B, dtype=torch.int32, device=DEV)
+    got = torch.full((3 * B, d), 7.0, device=DEV)
+    for _ in range(2):   # the counts come back zero: reusable
+        _lib.call("bbgr_ego_rows", B, d, P(out[3 * B:]), P(out[4 * B:]), P(out[5 * B:]), P(out),
+                  P(out[B:]), P(ue), d, P(ie), d, P(dl), 1e-2, P(cnt), P(got), d, P(got[B:]), d,
+                  _lib.stream_handle())
+        torch.cuda.synchronize()
+        assert torch.equal(got[:B], want_u) and torch.equal(got[B:], want_i)
+        assert int(cnt.abs().sum()) == 0
+    if B > 1000:   # the case really repeats rows
+        assert int(torch.bincount(torch.cat([pos, neg])).max()) > 100
+
+
 @pytest.mark.parametrize("B,U,I", [(1, 3, 2), (8192, 5_000_000, 1_000_000), (4096, 50, 30),
                                    (300, 300, 7)])
 def test_ego_slots_kernel_is_the_torch_formulation(B, U, I):
