@@ -39,7 +39,7 @@ import time
 # and the sharded exchange's side streams do not share (and serialise on) one
 # AQL queue. Must be set before the HIP runtime initialises.
 HW_QUEUES_GIVEN = os.environ.get("GPU_MAX_HW_QUEUES")
-if int(HW_QUEUES_GIVEN or 0) < 8:
+if int(HW_QUEUES_GIVEN or 0) < 8 and os.environ.get("BBGR_KEEP_HW_QUEUES") != "1":
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np
