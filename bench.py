@@ -419,7 +419,17 @@ def allreduce_probe(dev, world: int, native: bool, sizes, iters: int = 5) -> dic
     bandwidth = bytes / t_ar."""
     from bbgr.distributed import RcclItemComm
     out = {"world": world, "iters": iters, "sizes_bytes": list(sizes)}
-    comm = RcclItemComm(device=dev, inline=True) if native else None
+    comm, err = None, None
+    if native:   # a communicator that will not come up costs the C ABI figures only
+        try:
+            comm = RcclItemComm(device=dev, inline=True)
+        except Exception as ex:   # noqa: BLE001
+            err = f"{type(ex).__name__}: {ex}"[:300]
+        if _allreduce(0.0 if comm is None else 1.0, dev, torch.distributed.ReduceOp.MIN) < 1.0:
+            out["cabi_error"] = err or "the C ABI communicator failed on another rank"
+            if comm is not None:
+                comm.close()
+            comm = None
     try:
         for S in sizes:
             t = torch.ones(S // 4, dtype=torch.float32, device=dev)
