@@ -1289,8 +1289,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> bpr_loss_backward_cuda(
 // stream's work has drained, which destroying a stream waits for.
 // `role` keeps tables a single launch uses side by side apart: bbgr_ego_slots
 // takes a user and an item table at once, which must not be one buffer when
-// U == I (0 = first_slot, 1 = ego users, 2 = ego items; 3 = bbgr_ego_rows'
-// zero-filled counts, whose fill value the role fixes).
+// U == I (0 = first_slot, 1 = ego users, 2 = ego items). Role 3 holds
+// bbgr_ego_rows' counts, filled with (and left at) 0 instead of INT32_MAX.
 static constexpr size_t kFirstSlotScratch = 8;
 static Tensor slot_scratch(int64_t n_rows, const at::Device &dev, int64_t role = 0,
                            int32_t fill = 0x7fffffff) {

@@ -417,6 +417,91 @@ __global__ void mark_slots_kernel(long n, const long *rows, const int *indptr, c
   }
 }
 
+// bbgr_batch_begin / bbgr_batch_end: one 16-lane group per batch entry b.
+struct BatchParams {
+  long B, U, I;
+  const long *users, *pos, *neg;
+  const int *indptr, *indices;
+  unsigned char *mask_u, *mask_i;
+  long *list;
+  unsigned long long *count;
+  const int *tmap;
+  unsigned *bits;
+  float *g_u, *g_i, *g_side;
+  long ld_gu, ld_gi, ld_side;
+  int d;
+};
+
+__device__ __forceinline__ void batch_flag_item(const BatchParams &P, MarkListLds &s, long r) {
+  if (P.list) {
+    if (mark_first(r, P.mask_i)) mark_list_push(s, r, P.list, P.count);
+  } else {
+    P.mask_i[r] = 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void batch_begin_kernel(BatchParams P) {
+  __shared__ MarkListLds s;
+  if (threadIdx.x == 0) s.n = 0;
+  __syncthreads();
+  const long b = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  if (b < P.B) {
+    const long u = P.users[b];
+    const bool uok = u >= 0 && u < P.U;
+    if (lane == 0 && uok) P.mask_u[u] = 1;
+    if (lane < 2) {
+      const long r = lane == 0 ? P.pos[b] : P.neg[b];
+      if (r >= 0 && r < P.I) batch_flag_item(P, s, r);
+    }
+    if (uok && P.indptr) {
+      const int ee = P.indptr[u + 1];
+      for (int e = P.indptr[u] + lane; e < ee; e += 16) {
+        batch_flag_item(P, s, (long)P.indices[e]);
+        if (P.bits) {
+          const int sl = P.tmap[e];
+          atomicOr(P.bits + (sl >> 5), 1u << (sl & 31));
+        }
+      }
+    }
+  }
+  if (P.list) mark_list_flush(s, P.list, P.count);   // block-uniform
+}
+
+__device__ __forceinline__ void zero_row(float *t, long ld, long r, int d, int lane) {
+  if (!t) return;
+  float4 *row = reinterpret_cast<float4 *>(t + r * ld);
+  for (int c = lane; c < d / 4; c += 16) row[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ __launch_bounds__(256) void batch_end_kernel(BatchParams P) {
+  const long b = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  if (b == 0 && lane == 0 && P.count) *P.count = 0ull;
+  if (b >= P.B) return;
+  const long u = P.users[b];
+  const bool uok = u >= 0 && u < P.U;
+  if (uok) {
+    zero_row(P.g_u, P.ld_gu, u, P.d, lane);
+    if (lane == 0) P.mask_u[u] = 0;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const long r = h == 0 ? P.pos[b] : P.neg[b];
+    if (r < 0 || r >= P.I) continue;
+    zero_row(P.g_i, P.ld_gi, r, P.d, lane);
+    zero_row(P.g_side, P.ld_side, r, P.d, lane);
+    if (lane == 0) P.mask_i[r] = 0;
+  }
+  if (uok && P.indptr) {
+    const int ee = P.indptr[u + 1];
+    for (int e = P.indptr[u] + lane; e < ee; e += 16) {
+      P.mask_i[P.indices[e]] = 0;
+      if (P.bits) P.bits[P.tmap[e] >> 5] = 0u;
+    }
+  }
+}
+
 // every neighbour of a row flagged in row_mask (indexed through row_map when
 // given: CSR row r is flagged by row_mask[row_map[r]]) is set to v in mask
 __global__ void mark_neighbors_of_mask_kernel(long n_rows, const unsigned char *row_mask,
@@ -1042,6 +1127,65 @@ extern "C" int bbgr_mark_slots(int64_t n, const int64_t *rows, const int32_t *in
   hipLaunchKernelGGL(mark_slots_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
                      as_stream(stream), (long)n, (const long *)rows, indptr, tmap, bits, (int)set);
   BBGR_LAUNCHED("mark_slots_kernel");
+  return BBGR_OK;
+}
+
+static int batch_params(const bbgr_batch_args *a, BatchParams &P, const char *who) {
+  BBGR_REQUIRE(a && a->batch >= 0 && a->n_users > 0 && a->n_items > 0, "bbgr_batch: bad sizes");
+  BBGR_REQUIRE(a->batch == 0 || (a->users && a->pos && a->neg && a->mask_u && a->mask_i),
+               "bbgr_batch: null arrays");
+  BBGR_REQUIRE(!a->user_indptr == !a->user_indices, "bbgr_batch: user CSR half given");
+  BBGR_REQUIRE(!a->list == !a->count, "bbgr_batch: list and count go together");
+  BBGR_REQUIRE(!a->slot_bits == !a->slot_map && (!a->slot_bits || a->user_indptr),
+               "bbgr_batch: slot_bits needs slot_map and the user CSR");
+  BBGR_REQUIRE(!(a->g_u || a->g_i || a->g_side) || (a->d > 0 && a->d % 4 == 0),
+               "bbgr_batch: gradient rows need d % 4 == 0");
+  for (const float *t : {a->g_u, a->g_i, a->g_side})
+    BBGR_REQUIRE(!t || aligned16(t), "bbgr_batch: gradient tables must be 16-byte aligned");
+  BBGR_REQUIRE((a->ld_gu & 3) == 0 && (a->ld_gi & 3) == 0 && (a->ld_side & 3) == 0,
+               "bbgr_batch: ld % 4 == 0");
+  (void)who;
+  P.B = a->batch;
+  P.U = a->n_users;
+  P.I = a->n_items;
+  P.users = (const long *)a->users;
+  P.pos = (const long *)a->pos;
+  P.neg = (const long *)a->neg;
+  P.indptr = a->user_indptr;
+  P.indices = a->user_indices;
+  P.mask_u = a->mask_u;
+  P.mask_i = a->mask_i;
+  P.list = (long *)a->list;
+  P.count = (unsigned long long *)a->count;
+  P.tmap = a->slot_map;
+  P.bits = a->slot_bits;
+  P.g_u = a->g_u;
+  P.g_i = a->g_i;
+  P.g_side = a->g_side;
+  P.ld_gu = a->ld_gu;
+  P.ld_gi = a->ld_gi;
+  P.ld_side = a->ld_side;
+  P.d = a->d;
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_batch_begin(const bbgr_batch_args *a, bbgr_stream_t stream) {
+  BatchParams P;
+  if (int rc = batch_params(a, P, "bbgr_batch_begin")) return rc;
+  if (P.B == 0) return BBGR_OK;
+  hipLaunchKernelGGL(batch_begin_kernel, dim3((unsigned)((P.B + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), P);
+  BBGR_LAUNCHED("batch_begin_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_batch_end(const bbgr_batch_args *a, bbgr_stream_t stream) {
+  BatchParams P;
+  if (int rc = batch_params(a, P, "bbgr_batch_end")) return rc;
+  if (P.B == 0 && !P.count) return BBGR_OK;
+  hipLaunchKernelGGL(batch_end_kernel, dim3((unsigned)((P.B + 15) / 16 > 0 ? (P.B + 15) / 16 : 1)),
+                     dim3(256), 0, as_stream(stream), P);
+  BBGR_LAUNCHED("batch_end_kernel");
   return BBGR_OK;
 }
 

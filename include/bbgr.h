@@ -642,6 +642,31 @@ int bbgr_mark_list(int64_t n, const int64_t *rows, const int32_t *indptr,
 int bbgr_mark_slots(int64_t n, const int64_t *rows, const int32_t *indptr,
                     const int32_t *tmap, uint32_t *bits, int32_t set,
                     bbgr_stream_t stream);
+/* A training step's batch bookkeeping in one launch each (ABI 10; the fused  */
+/* trainer's frontier step). bbgr_batch_begin = bbgr_mark_rows(users, 1,      */
+/* mask_u) + bbgr_mark_list(pos, neg -> mask_i, list) + (user_indptr != NULL) */
+/* bbgr_mark_list(every neighbour of the users -> mask_i, list) +            */
+/* (slot_bits != NULL) bbgr_mark_slots(users, set); the same masks, list SET */
+/* (its order unspecified either way) and bits. bbgr_batch_end restores them:*/
+/* mask_u / mask_i bytes of the users, items and neighbours to 0, the slot    */
+/* words to 0, *count to 0 (list != NULL), and zeroes the step's sparse       */
+/* gradient rows: g_u at the users, g_i and g_side (each nullable) at pos and */
+/* neg (d columns). Ids outside the tables (the sampler's -1) are skipped.    */
+typedef struct {
+  int64_t batch;
+  const int64_t *users, *pos, *neg;   /* internal row ids */
+  int64_t n_users, n_items;
+  const int32_t *user_indptr, *user_indices;   /* user CSR; NULL: no neighbours */
+  uint8_t *mask_u, *mask_i;
+  int64_t *list, *count;              /* item frontier list (nullable together) */
+  const int32_t *slot_map;            /* with slot_bits (nullable together) */
+  uint32_t *slot_bits;
+  float *g_u, *g_i, *g_side;          /* bbgr_batch_end only, nullable */
+  int64_t ld_gu, ld_gi, ld_side;
+  int32_t d;
+} bbgr_batch_args;
+int bbgr_batch_begin(const bbgr_batch_args *args, bbgr_stream_t stream);
+int bbgr_batch_end(const bbgr_batch_args *args, bbgr_stream_t stream);
 /* The same for every CSR row r < n_rows flagged in row_mask: row_mask[r], or
  * row_mask[row_map[r]] when row_map is given (a mask kept in the caller's
  * vertex order over a CSR numbered by descending degree). */
