@@ -144,6 +144,21 @@ class Pcg64State(ctypes.Structure):
     ]
 
 
+class BatchArgs(ctypes.Structure):
+    """bbgr_batch_args (bbgr_batch_begin / bbgr_batch_end)."""
+    _fields_ = [
+        ("batch", c_int64), ("users", c_void_p), ("pos", c_void_p), ("neg", c_void_p),
+        ("n_users", c_int64), ("n_items", c_int64),
+        ("user_indptr", c_void_p), ("user_indices", c_void_p),
+        ("mask_u", c_void_p), ("mask_i", c_void_p),
+        ("list", c_void_p), ("count", c_void_p),
+        ("slot_map", c_void_p), ("slot_bits", c_void_p),
+        ("g_u", c_void_p), ("g_i", c_void_p), ("g_side", c_void_p),
+        ("ld_gu", c_int64), ("ld_gi", c_int64), ("ld_side", c_int64),
+        ("d", c_int32),
+    ]
+
+
 _P = c_void_p
 _SIGNATURES = {
     "bbgr_abi_version": ([], c_int32),
@@ -192,6 +207,8 @@ _SIGNATURES = {
                             _P], c_int32),
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
     "bbgr_mark_slots": ([c_int64, _P, _P, _P, _P, c_int32, _P], c_int32),
+    "bbgr_batch_begin": ([ctypes.POINTER(BatchArgs), _P], c_int32),
+    "bbgr_batch_end": ([ctypes.POINTER(BatchArgs), _P], c_int32),
     "bbgr_mark_list": ([c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P], c_int32),
     "bbgr_slots_from_perms": ([c_int64, _P, _P, _P, _P, _P], c_int32),
     "bbgr_transpose_slots": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(CsrStruct), _P, _P],

@@ -165,6 +165,14 @@ class FusedTrainer:
                 and uc.nnz <= 24 * uc.n_rows and os.environ.get("BBGR_TAGGED", "0") == "1"):
             self.tagged = torch.empty(max(uc.nnz, 1), dtype=torch.int32, device=dev)
         self.item_list = self.item_count = self.item_len = None
+        # GS frontier: the step's bookkeeping (masks, list, slot bits, and the
+        # sparse gradient rows' reset) runs as one launch at each end of the
+        # step (bbgr_batch_begin / bbgr_batch_end) instead of ~11 small ones;
+        # same bytes set and restored (BBGR_BATCH_FUSED=0 keeps the separate
+        # launches for A/B).
+        self.batch_fused = (self.frontier and order == ORDER_GS
+                            and os.environ.get("BBGR_BATCH_FUSED", "1") != "0")
+        self._fused_pending = False
         if self.frontier and order == ORDER_GS:
             self.item_list = torch.empty(max(self.I, 1), dtype=torch.int64, device=dev)
             self.item_count = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -268,12 +276,41 @@ class FusedTrainer:
             adam_step(self.item_w, self.g_i0, self.m_i, self.v_i, self.step_count, self.lr,
                       dev=self.dev_state)
         # restore the all-zero invariant of the sparse gradient tables
+        if self._fused_pending:   # (+ the masks, list, bits and item side table)
+            self._fused_pending = False
+            a = self._batch_args(users, g=True)
+            call("bbgr_batch_end", ctypes.byref(a), st)
+            self.item_len.invalidate()
+            return self.loss
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
         call("bbgr_rows_zero", 2 * B, ptr(self.posneg), ptr(self.g_if), ld(self.g_if), self.d,
              st)   # (pos and neg: posneg[:B], posneg[B:2B])
         if masks is not None:
             self._set_masks(users, pos, neg, 0)
         return self.loss
+
+    def _batch_args(self, users, g: bool = False):
+        """bbgr_batch_args over the trainer's own batch (posneg halves)."""
+        B = users.numel()
+        uc = self.graph.user_csr
+        bits = getattr(self, "slot_bits", None)
+        side = getattr(self, "_g_item_side", None) if g else None
+        a = _lib.BatchArgs()
+        a.batch = B
+        a.users, a.pos, a.neg = ptr(users), ptr(self.posneg), ptr(self.posneg) + 8 * B
+        a.n_users, a.n_items = self.U, self.I
+        a.user_indptr, a.user_indices = ptr(uc.indptr), ptr(uc.indices)
+        a.mask_u, a.mask_i = ptr(self.mask_u), ptr(self.mask_i)
+        a.list, a.count = ptr(self.item_list), ptr(self.item_count)
+        if bits is not None:
+            a.slot_map, a.slot_bits = ptr(self.slot_map), ptr(bits)
+        if g:
+            a.g_u, a.ld_gu = ptr(self.g_uf), ld(self.g_uf)
+            a.g_i, a.ld_gi = ptr(self.g_if), ld(self.g_if)
+            if side is not None:
+                a.g_side, a.ld_side = ptr(side), ld(side)
+        a.d = self.d
+        return a
 
     def _bpr(self, users, pos, neg, B: int) -> None:
         """Fused BPR forward + per-triple gradient rows (bbgr_bpr, contrib mode)."""
@@ -323,7 +360,7 @@ class FusedTrainer:
                  src_bits=self._bits(masks), frontier_list=self._flist(masks),
                  before_last=before_last, reduce=reduce, adam_i=adam_i,
                  tagged=self._tagged(masks))
-        if side:   # the side table is all-zero between steps
+        if side and not self._fused_pending:   # the side table is all-zero between steps
             call("bbgr_rows_zero", item_rows.numel(), ptr(item_rows), ptr(ga), ld(ga), self.d,
                  st)
         elif item_adam:
@@ -382,6 +419,18 @@ class FusedTrainer:
         pn = (pos.data_ptr() == self.posneg.data_ptr()
               and neg.data_ptr() == self.posneg.data_ptr() + 8 * B)
         items = [(2 * B, ptr(self.posneg))] if pn else [(B, ptr(pos)), (B, ptr(neg))]
+        if value and pn and getattr(self, "batch_fused", False) and lst is not None:
+            _lib.check_word_padded(self.mask_i, self.I, "item mask")
+            a = self._batch_args(users)
+            call("bbgr_batch_begin", ctypes.byref(a), st)
+            if getattr(self, "item_len", None) is not None:
+                self.item_len.publish()
+            # (the step's end restores all of it in one bbgr_batch_end; a
+            # subclass ending with _set_masks(..., 0) restores it just as well)
+            self._fused_pending = type(self)._step is FusedTrainer._step
+            return self.mask_u, self.mask_i
+        if not value:
+            self._fused_pending = False
         if value and lst is not None:   # flag + list the frontier (GS)
             _lib.check_word_padded(self.mask_i, self.I, "item mask")
             li = (ptr(self.mask_i), self.I, ptr(lst), ptr(self.item_count), st)

@@ -213,3 +213,51 @@ def test_tagged_user_indices_step_is_bitwise_the_mask_step(fuse, K, monkeypatch)
     a._set_masks(a._last_users, a.pos, a.neg, 0)
     want = torch.where(live, idx, idx | (1 << 31)).to(torch.int64) & 0xFFFFFFFF
     assert torch.equal(a.tagged[:uc.nnz].to(torch.int64) & 0xFFFFFFFF, want)
+
+
+@pytest.mark.parametrize("fuse,K,dim", [(True, 3, 64), (False, 3, 64), (True, 2, 64),
+                                        (True, 1, 64), (True, 3, 32)])
+def test_fused_batch_bookkeeping_is_bitwise_the_separate_launches(fuse, K, dim, monkeypatch):
+    """GS frontier: bbgr_batch_begin / bbgr_batch_end (masks, item list, slot
+    bits and the sparse gradient rows' reset in one launch each) give the
+    separate launches' losses, weights and moments bit for bit, and leave
+    every mask byte, slot word, list count, sparse gradient row and the item
+    side table zero after each step."""
+    e, g = _graph()
+    kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=dim, num_layers=K, batch_size=256,
+              frontier=True, fuse_adam=fuse, seed=11)
+    a = FusedTrainer(g, "v2_pop", **kw)
+    monkeypatch.setenv("BBGR_BATCH_FUSED", "0")
+    b = FusedTrainer(g, "v2_pop", **kw)
+    assert a.batch_fused and not b.batch_fused
+    for _ in range(4):
+        assert float(a.step()) == float(b.step())
+        assert not a._fused_pending
+        for t in (a.mask_u, a.mask_i, a.g_uf, a.g_if, a.item_count):
+            assert int(t.abs().sum()) == 0
+        if a.slot_bits is not None:
+            assert int(a.slot_bits.abs().sum()) == 0
+        side = getattr(a, "_g_item_side", None)
+        if side is not None:
+            assert float(side.abs().sum()) == 0.0
+    _assert_same(a, b)
+    # caller batches (repeated users) take the same launches
+    users = torch.tensor([5, 5, 17, 2999, 0, 17], dtype=torch.int64)
+    assert float(a.step(users)) == float(b.step(users))
+    _assert_same(a, b)
+    assert int(a.mask_i.abs().sum()) == 0 and int(a.item_count.abs().sum()) == 0
+
+
+def test_fused_batch_bookkeeping_graph_replay():
+    """A captured step with the fused bookkeeping replays bitwise the eager
+    steps (the list count is restored on the device inside the graph)."""
+    e, g = _graph()
+    kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=64, num_layers=3, batch_size=256,
+              frontier=True, fuse_adam=True, seed=13)
+    a, b = FusedTrainer(g, "v2_pop", **kw), FusedTrainer(g, "v2_pop", **kw)
+    assert a.batch_fused
+    gs = GraphedStep(a)
+    for _ in range(5):
+        assert float(gs.step()) == float(b.step())
+    _assert_same(a, b)
+    assert int(a.item_count.abs().sum()) == 0 and int(a.mask_i.abs().sum()) == 0

@@ -26,6 +26,7 @@
 #   configs    one bench line per config (CONFIGS="C1 C2 C3 C5")
 #   evalnp     sampled evaluation at C4 on the reference's numpy candidate stream
 #   frontierab C2 / C1 step with the frontier masks on and off (graph replay)
+#   batchab    fused step bookkeeping (BBGR_BATCH_FUSED 1 / 0) at BCONFIGS (C2 default)
 set -o pipefail
 T=$1; shift
 O=gpurun_out/$T
@@ -163,6 +164,16 @@ for step in "$@"; do
           rc=$?; hard $rc "frontier $c $f" "$O/${c,,}_frontier_$f.log"
           [ $rc -eq 0 ] || { tail -20 "$O/${c,,}_frontier_$f.log"; exit 1; }
           echo "$c frontier $f: $(python tools/bench_brief.py "$O/${c,,}_frontier_$f.json" | head -1)"
+        done
+      done ;;
+    batchab)
+      for c in ${BCONFIGS:-C2}; do
+        for f in 1 0; do
+          BBGR_BATCH_FUSED=$f timeout -k 10 400 python -u bench.py --config $c $quick_args \
+            --steps 50 --warmup 5 > "$O/${c,,}_batch_$f.json" 2> "$O/${c,,}_batch_$f.log"
+          rc=$?; hard $rc "batch $c $f" "$O/${c,,}_batch_$f.log"
+          [ $rc -eq 0 ] || { tail -20 "$O/${c,,}_batch_$f.log"; exit 1; }
+          echo "$c fused bookkeeping $f: $(python tools/bench_brief.py "$O/${c,,}_batch_$f.json" | head -1)"
         done
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
