@@ -360,9 +360,10 @@ class FusedTrainer:
                  src_bits=self._bits(masks), frontier_list=self._flist(masks),
                  before_last=before_last, reduce=reduce, adam_i=adam_i,
                  tagged=self._tagged(masks))
-        if side and not self._fused_pending:   # the side table is all-zero between steps
-            call("bbgr_rows_zero", item_rows.numel(), ptr(item_rows), ptr(ga), ld(ga), self.d,
-                 st)
+        if side:   # the side table is all-zero between steps (bbgr_batch_end's rows)
+            if not self._fused_pending:
+                call("bbgr_rows_zero", item_rows.numel(), ptr(item_rows), ptr(ga), ld(ga),
+                     self.d, st)
         elif item_adam:
             self._item_adam(item_rows, self.g_if, a_gl, gl)
 
