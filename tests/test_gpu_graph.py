@@ -256,7 +256,8 @@ def test_fused_batch_bookkeeping_graph_replay():
               frontier=True, fuse_adam=True, seed=13)
     a, b = FusedTrainer(g, "v2_pop", **kw), FusedTrainer(g, "v2_pop", **kw)
     assert a.batch_fused
-    gs = GraphedStep(a)
+    gs = GraphedStep(a)   # (a trainer that has not stepped takes its first step eagerly)
+    assert float(gs.first_loss) == float(b.step())
     for _ in range(5):
         assert float(gs.step()) == float(b.step())
     _assert_same(a, b)
