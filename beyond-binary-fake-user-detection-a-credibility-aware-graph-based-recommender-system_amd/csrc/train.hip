@@ -447,22 +447,27 @@ __global__ __launch_bounds__(256) void batch_begin_kernel(BatchParams P) {
   const long b = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
   if (b < P.B) {
+    // every lane's loads issue before its first returning atomic: the pos /
+    // neg rows ride on the last two lanes (a user's first 14 edges are on the
+    // others), the slot bit is set without waiting on a return, and only the
+    // mask's first-setter test waits
     const long u = P.users[b];
+    const long pn = lane == 14 ? P.pos[b] : lane == 15 ? P.neg[b] : -1;
     const bool uok = u >= 0 && u < P.U;
-    if (lane == 0 && uok) P.mask_u[u] = 1;
-    if (lane < 2) {
-      const long r = lane == 0 ? P.pos[b] : P.neg[b];
-      if (r >= 0 && r < P.I) batch_flag_item(P, s, r);
-    }
+    int e = 0, ee = 0;
     if (uok && P.indptr) {
-      const int ee = P.indptr[u + 1];
-      for (int e = P.indptr[u] + lane; e < ee; e += 16) {
-        batch_flag_item(P, s, (long)P.indices[e]);
-        if (P.bits) {
-          const int sl = P.tmap[e];
-          atomicOr(P.bits + (sl >> 5), 1u << (sl & 31));
-        }
+      e = P.indptr[u] + lane;
+      ee = P.indptr[u + 1];
+    }
+    if (lane == 0 && uok) P.mask_u[u] = 1;
+    if (pn >= 0 && pn < P.I) batch_flag_item(P, s, pn);
+    for (; e < ee; e += 16) {
+      const long c = P.indices[e];
+      if (P.bits) {
+        const int sl = P.tmap[e];
+        atomicOr(P.bits + (sl >> 5), 1u << (sl & 31));
       }
+      batch_flag_item(P, s, c);
     }
   }
   if (P.list) mark_list_flush(s, P.list, P.count);   // block-uniform
