@@ -1338,7 +1338,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
                                                                 const Tensor &pos,
                                                                 const Tensor &neg,
                                                                 const Tensor &ue,
-                                                                const Tensor &ie, double reg) {
+                                                                const Tensor &ie, double reg,
+                                                                double scale = 1.0) {
   const int64_t B = users.numel(), d = ue.size(1), U = ue.size(0), I = ie.size(0);
   TORCH_CHECK(U > 0 && I > 0, "ego_grad_rows: empty table");
   // one int64 block: iu [B], ii [2B], cu [B], sp [B], sn [B]
@@ -1362,7 +1363,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
                       sn.data_ptr<int64_t>(), iu.data_ptr<int64_t>(), ii.data_ptr<int64_t>(),
                       uec.data_ptr<float>(), ld(uec), iec.data_ptr<float>(), ld(iec),
                       dl.data_ptr<float>(), (float)reg, cnt.data_ptr<int32_t>(),
-                      gu.data_ptr<float>(), ld(gu), gi.data_ptr<float>(), ld(gi), cur_stream()),
+                      gu.data_ptr<float>(), ld(gu), gi.data_ptr<float>(), ld(gi), (float)scale,
+                      cur_stream()),
         "bbgr_ego_rows");
   return {gu, gi, iu, ii};
 }
@@ -1407,10 +1409,10 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   a.contrib = contrib.data_ptr<float>();
   a.ldcontrib = ld(contrib);
   check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr");
-  auto eg = ego_grad_rows(dl, users, pos, neg, u0, i0, reg);
+  // the ego rows come scaled by K + 1 (one rounding, as at::mul(rows, K + 1))
+  auto eg = ego_grad_rows(dl, users, pos, neg, u0, i0, reg, (double)(K + 1));
   const Tensor &ru = std::get<0>(eg), &ri = std::get<1>(eg), &iu = std::get<2>(eg),
                &ii = std::get<3>(eg);
-  const Tensor kp1 = at::scalar_tensor((float)(K + 1), at::TensorOptions().dtype(at::kFloat));
   StepAdam sa;
   sa.user = AdamTable{u0, m_u, v_u, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
                       (float)bc1_u, (float)bc2s_u};
@@ -1437,7 +1439,7 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
     sa.item.p = *i_graph;
     sa.item.mirror = i0;
   }
-  sa.ego_u_vals = at::mul(ru, kp1);
+  sa.ego_u_vals = ru;
   // the item gradient / gl: the BPR rows, then the ego rows, per item in
   // ascending source order
   // (one sort of the 2B item ids serves this scatter and rows_backward's gI)
@@ -1470,7 +1472,7 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
       if (armed) P.it.erase(key);
     }
   } drop{*P, skey, cached};
-  apply_rows(sa.item_plan, sa.item_grad, vi, at::mul(ri, kp1));
+  apply_rows(sa.item_plan, sa.item_grad, vi, ri);
   rows_backward(P, iu, contrib.narrow(0, 0, B), i0, K, true, ii, vi, &sa, gi);
   if (cached)
     for (Tensor *z : {&gi, &sa.item_grad})

@@ -647,7 +647,8 @@ __global__ __launch_bounds__(256) void ego_rows_kernel(long B, const long *iu, c
                                                        const float *ie, long ldie,
                                                        const float *dloss, float inv_b,
                                                        float reg, int *counts, float *g_u,
-                                                       long ldgu, float *g_i, long ldgi) {
+                                                       long ldgu, float *g_i, long ldgi,
+                                                       float scale) {
   constexpr int V = D / 64;
   const long s = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
@@ -674,6 +675,11 @@ __global__ __launch_bounds__(256) void ego_rows_kernel(long B, const long *iu, c
                              __fadd_rn(acc[k].z, y.z), __fadd_rn(acc[k].w, y.w));
     }
     if (lane == 0) counts[s] = 0;
+    if (scale != 1.0f)   // (x * 1 == x, -0 included: the unscaled rows are these)
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+        acc[k] = make_float4(__fmul_rn(acc[k].x, scale), __fmul_rn(acc[k].y, scale),
+                             __fmul_rn(acc[k].z, scale), __fmul_rn(acc[k].w, scale));
   }
 #pragma unroll
   for (int k = 0; k < V; ++k) dst[16 * k] = acc[k];
@@ -1289,7 +1295,8 @@ extern "C" int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int6
                              const int64_t *sn, const int64_t *iu, const int64_t *ii,
                              const float *ue, int64_t ldue, const float *ie, int64_t ldie,
                              const float *dloss, float reg, int32_t *counts, float *g_u,
-                             int64_t ldgu, float *g_i, int64_t ldgi, bbgr_stream_t stream) {
+                             int64_t ldgu, float *g_i, int64_t ldgi, float scale,
+                             bbgr_stream_t stream) {
   BBGR_REQUIRE(B >= 0 && 3 * B < (1LL << 31), "bbgr_ego_rows: bad batch");
   if (d != 64 && d != 128 && d != 256) {
     set_error("bbgr_ego_rows: embedding dim %d unsupported (64, 128, 256)", d);
@@ -1310,7 +1317,7 @@ extern "C" int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int6
 #define BBGR_EGO_ROWS(DD)                                                                   \
   hipLaunchKernelGGL(ego_rows_kernel<DD>, g, dim3(256), 0, st, (long)B, (const long *)iu, \
                      (const long *)ii, ue, (long)ldue, ie, (long)ldie, dloss, inv_b, reg,   \
-                     counts, g_u, (long)ldgu, g_i, (long)ldgi)
+                     counts, g_u, (long)ldgu, g_i, (long)ldgi, scale)
   switch (d) {
     case 64: BBGR_EGO_ROWS(64); break;
     case 128: BBGR_EGO_ROWS(128); break;

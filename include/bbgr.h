@@ -556,10 +556,13 @@ int bbgr_ego_slots(int64_t B, const int64_t *users, const int64_t *pos, const in
 /* bbgr_bpr's ego rows over the compact tables (identical addends, so its     */
 /* float atomics' order cannot matter) without their serialisation on a       */
 /* popular item's row. counts: int32 [3B] scratch, zero on entry and return.  */
+/* scale: every written row is that sum times scale (one rounding; 1 = the    */
+/* sum itself; the in-backward Adam's (K+1) * ego rows without a mul launch). */
 int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int64_t *sp, const int64_t *sn,
                   const int64_t *iu, const int64_t *ii, const float *ue, int64_t ldue,
                   const float *ie, int64_t ldie, const float *dloss, float reg, int32_t *counts,
-                  float *g_u, int64_t ldgu, float *g_i, int64_t ldgi, bbgr_stream_t stream);
+                  float *g_u, int64_t ldgu, float *g_i, int64_t ldgi, float scale,
+                  bbgr_stream_t stream);
 
 /* out[k] = rank[ids[k]] (rank NULL: ids[k]) for ids[k] in [0, n_rows), else */
 /* -1 (ABI 8): a caller's row ids as graph rows in one launch                */

@@ -897,9 +897,17 @@ def test_ego_rows_kernel_is_the_atomic_formulation(B, U, I, d):
     for _ in range(2):   # the counts come back zero: reusable
         _lib.call("bbgr_ego_rows", B, d, P(out[3 * B:]), P(out[4 * B:]), P(out[5 * B:]), P(out),
                   P(out[B:]), P(ue), d, P(ie), d, P(dl), 1e-2, P(cnt), P(got), d, P(got[B:]), d,
-                  _lib.stream_handle())
+                  1.0, _lib.stream_handle())
         torch.cuda.synchronize()
         assert torch.equal(got[:B], want_u) and torch.equal(got[B:], want_i)
+        assert int(cnt.abs().sum()) == 0
+    # scale: the rows times scale in one rounding (the in-backward Adam's K + 1)
+    for sc in (3.0, 4.0):
+        _lib.call("bbgr_ego_rows", B, d, P(out[3 * B:]), P(out[4 * B:]), P(out[5 * B:]), P(out),
+                  P(out[B:]), P(ue), d, P(ie), d, P(dl), 1e-2, P(cnt), P(got), d, P(got[B:]), d,
+                  sc, _lib.stream_handle())
+        torch.cuda.synchronize()
+        assert torch.equal(got[:B], want_u * sc) and torch.equal(got[B:], want_i * sc)
         assert int(cnt.abs().sum()) == 0
     if B > 1000:   # the case really repeats rows
         assert int(torch.bincount(torch.cat([pos, neg])).max()) > 100
