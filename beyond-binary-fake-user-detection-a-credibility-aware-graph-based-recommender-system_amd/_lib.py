@@ -93,7 +93,7 @@ class SpmmArgs(ctypes.Structure):
         ("adam_map", c_void_p),
         ("adam_moments_unmapped", c_int32),
         ("tag_out", c_void_p), ("tag_mask", c_void_p), ("src_tagged", c_void_p),
-        ("adam_mirror", c_void_p),
+        ("adam_mirror", c_void_p), ("src_mask_bits", c_void_p),
     ]
 
 
@@ -208,6 +208,7 @@ _SIGNATURES = {
     "bbgr_mark_neighbors": ([c_int64, _P, _P, _P, ctypes.c_uint8, _P, _P], c_int32),
     "bbgr_mark_slots": ([c_int64, _P, _P, _P, _P, c_int32, _P], c_int32),
     "bbgr_batch_begin": ([ctypes.POINTER(BatchArgs), _P], c_int32),
+    "bbgr_mask_pack": ([c_int64, _P, _P, _P], c_int32),
     "bbgr_batch_end": ([ctypes.POINTER(BatchArgs), _P], c_int32),
     "bbgr_mark_list": ([c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P], c_int32),
     "bbgr_slots_from_perms": ([c_int64, _P, _P, _P, _P, _P], c_int32),

@@ -92,7 +92,17 @@ struct SpmmParams {
   int *tag_out;                // tagged-index copy written by a full launch (args.tag_out)
   const unsigned char *tag_mask;
   float *adam_mirror;          // caller-order copy of the updated param rows (args.adam_mirror)
+  const unsigned *src_mask_bits;   // src_mask packed one bit per row (args.src_mask_bits)
 };
+
+// Per-edge liveness of source row c. The packed form (bbgr_mask_pack) puts 1024
+// rows in a 128-B line instead of 128: the degree-ordered hub columns most
+// edges point at share a few lines, so a wave's 64 lookups need fewer L2
+// requests and hit L1 more often. Same liveness, so bitwise the byte test.
+__device__ __forceinline__ bool src_live(const SpmmParams &P, int c) {
+  if (P.src_mask_bits) return (P.src_mask_bits[c >> 5] >> (c & 31)) & 1u;
+  return P.src_mask[c] != 0;
+}
 
 // Tagged column indices (ABI 10): a full launch over a CSR can write a copy of
 // its column indices with bit 31 set where the column is dead in tag_mask
@@ -349,7 +359,7 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     if (lane < n && ((live >> lane) & 1u)) {
       my = ld_edge(P.indices + e0 + lane);
       // exact-zero source row (a tagged index carries it in its sign)
-      if (MASKED && !BITS && TAG != TAG_READ && P.src_mask && !P.src_mask[my]) my = -1;
+      if (MASKED && !BITS && TAG != TAG_READ && P.src_mask && !src_live(P, my)) my = -1;
       if (my >= 0) {
         if (WMODE == 1) mw = ld_edge(P.edge_val + e0 + lane);
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
@@ -421,7 +431,7 @@ __device__ __forceinline__ void gather_range_narrow(const SpmmParams &P, int eb,
     float mw = 0.f;
     if (lane < n) {
       my = P.indices[e0 + lane];
-      if (MASKED && P.src_mask && !P.src_mask[my]) my = -1;
+      if (MASKED && P.src_mask && !src_live(P, my)) my = -1;
       if (my >= 0) {
         if (WMODE == 1) mw = P.edge_val[e0 + lane];
         if (WMODE == 2) mw = P.col_scale[my] * P.col_scale_s;
@@ -483,7 +493,7 @@ __device__ __forceinline__ void gather_slot(const SpmmParams &P, int eb, int ee,
       mw[r] = 0.f;
       if (e < ee) {
         my[r] = P.indices[e];
-        if (MASKED && P.src_mask && !P.src_mask[my[r]]) my[r] = -1;
+        if (MASKED && P.src_mask && !src_live(P, my[r])) my[r] = -1;
         if (my[r] >= 0) {
           if (WMODE == 1) mw[r] = P.edge_val[e];
           if (WMODE == 2) mw[r] = P.col_scale[my[r]] * P.col_scale_s;
@@ -541,7 +551,7 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     float mwA = 0.f, mwB = 0.f;
     if (lane < na) {
       myA = ld_edge(P.indices + ebA + o + lane);
-      if (MASKED && TAG != TAG_READ && P.src_mask && !P.src_mask[myA]) myA = -1;
+      if (MASKED && TAG != TAG_READ && P.src_mask && !src_live(P, myA)) myA = -1;
       if (myA >= 0) {
         if (WMODE == 1) mwA = ld_edge(P.edge_val + ebA + o + lane);
         if (WMODE == 2) mwA = P.col_scale[myA] * P.col_scale_s;
@@ -549,7 +559,7 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     }
     if (lane < nb) {
       myB = ld_edge(P.indices + ebB + o + lane);
-      if (MASKED && TAG != TAG_READ && P.src_mask && !P.src_mask[myB]) myB = -1;
+      if (MASKED && TAG != TAG_READ && P.src_mask && !src_live(P, myB)) myB = -1;
       if (myB >= 0) {
         if (WMODE == 1) mwB = ld_edge(P.edge_val + ebB + o + lane);
         if (WMODE == 2) mwB = P.col_scale[myB] * P.col_scale_s;
@@ -1312,6 +1322,7 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   P.adam_map = a->adam_map;
   P.adam_mrow = a->adam_moments_unmapped != 0;
   P.adam_mirror = a->adam_mirror;
+  P.src_mask_bits = a->src_mask_bits;
 }
 
 static bool adam_ok(const bbgr_spmm_args *a, int d) {
@@ -1384,6 +1395,8 @@ extern "C" int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *a,
                                "(16-byte aligned, adam_ld >= d) and bias corrections > 0");
   BBGR_REQUIRE(!a->adam_param || !(a->src_mask || a->row_mask || a->row_list || a->use_range),
                "bbgr_spmm: fused Adam needs every row (no masks, row list or range)");
+  BBGR_REQUIRE(!a->src_mask_bits || a->src_mask,
+               "bbgr_spmm: src_mask_bits packs src_mask (pass both)");
   BBGR_REQUIRE(!a->src_bits || a->src_mask,
                "bbgr_spmm: src_bits needs src_mask (narrow and two-row kernels read the mask)");
   BBGR_REQUIRE(a->weight_mode != 1 || a->edge_val, "bbgr_spmm: weight_mode 1 needs edge_val");

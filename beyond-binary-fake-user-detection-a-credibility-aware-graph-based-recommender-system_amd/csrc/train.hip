@@ -1141,6 +1141,41 @@ extern "C" int bbgr_mark_slots(int64_t n, const int64_t *rows, const int32_t *in
   return BBGR_OK;
 }
 
+// one thread per 32-bit word: 32 byte loads as eight 4-byte loads
+__global__ __launch_bounds__(256) void mask_pack_kernel(long n, const unsigned char *mask,
+                                                        unsigned *bits) {
+  const long w = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long b0 = w * 32;
+  if (b0 >= n) return;
+  unsigned v = 0;
+  if (b0 + 32 <= n && (reinterpret_cast<uintptr_t>(mask) & 3) == 0) {
+    const unsigned *q = reinterpret_cast<const unsigned *>(mask + b0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const unsigned x = q[k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((x >> (8 * j)) & 0xffu) v |= 1u << (4 * k + j);
+    }
+  } else {
+    for (int j = 0; j < 32 && b0 + j < n; ++j)
+      if (mask[b0 + j]) v |= 1u << j;
+  }
+  bits[w] = v;
+}
+
+extern "C" int bbgr_mask_pack(int64_t n, const uint8_t *mask, uint32_t *bits,
+                              bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0, "bbgr_mask_pack: bad size");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(mask && bits, "bbgr_mask_pack: null arrays");
+  const long words = (long)((n + 31) / 32);
+  hipLaunchKernelGGL(mask_pack_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), (long)n, mask, bits);
+  BBGR_LAUNCHED("mask_pack_kernel");
+  return BBGR_OK;
+}
+
 static int batch_params(const bbgr_batch_args *a, BatchParams &P, const char *who) {
   BBGR_REQUIRE(a && a->batch >= 0 && a->n_users > 0 && a->n_items > 0, "bbgr_batch: bad sizes");
   BBGR_REQUIRE(a->batch == 0 || (a->users && a->pos && a->neg && a->mask_u && a->mask_i),

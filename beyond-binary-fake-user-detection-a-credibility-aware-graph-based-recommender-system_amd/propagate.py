@@ -363,7 +363,7 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
          gamma: float = 1.0, src_mask=None, row_mask=None, acc_mask=None,
          add_mask=None, row_list=None, rng=None, adam=None, y_map=None, acc_map=None,
          add_map=None, src_input: bool = False, src_bits=None, row_count=None,
-         tag_out=None, tag_mask=None, tagged=None) -> None:
+         tag_out=None, tag_mask=None, tagged=None, src_mask_bits=None) -> None:
     """One fused SpMM launch (bbgr_spmm) on the current stream. `adam`
     (optim.AdamRows): apply Adam to each row's y value in the epilogue.
     `y_map` / `acc_map` / `add_map`: row maps of those tables (input-order
@@ -377,7 +377,9 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     write the CSR's column indices with bit 31 set where tag_mask is 0;
     `tagged` (with src_mask, the same mask): read liveness from such a copy
     instead of loading src_mask per edge (bbgr_spmm_args.tag_out /
-    src_tagged; bitwise the src_mask launch)."""
+    src_tagged; bitwise the src_mask launch). `src_mask_bits` (with src_mask):
+    the same mask packed one bit per row (bbgr_mask_pack), read by the
+    per-edge test instead of the bytes (bbgr_spmm_args.src_mask_bits)."""
     listed_on_device = row_count is not None
     if isinstance(row_count, ListLength):
         n = row_count.length()
@@ -425,6 +427,8 @@ def spmm(prod: Product, x: torch.Tensor, first: bool, *, y=None, y_scale=None,
     a.y_map, a.acc_map, a.add_map = ptr(y_map), ptr(acc_map), ptr(add_map)
     if src_bits is not None and src_mask is not None:
         a.src_bits = ptr(src_bits)
+    if src_mask_bits is not None and a.src_mask:
+        a.src_mask_bits = ptr(src_mask_bits)
     # input-order source rows carry no hot prefix; mapped output rows neither
     a.stream_from = 0 if src_input else prod.csr.stream_from(d)
     a.stream_out_from = 0 if y_map is not None else prod.csr.stream_out_from(d)
@@ -650,7 +654,7 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                    out_i: torch.Tensor | None = None, ws: dict | None = None,
                    grad_i0_dense: bool = True, reduce=None, grad_support=None,
                    adam_u=None, before_last=None, adam_i=None, src_bits=None,
-                   frontier_list=None, tagged=None):
+                   frontier_list=None, tagged=None, item_mask_bits=None):
     """Gradients w.r.t. (u0, i0) given dL/d(u_final), dL/d(i_final); a
     generator yielding after each item-row product, like forward_steps.
     `adam_u` (optim.AdamRows) fuses the user-table Adam step into the last
@@ -678,7 +682,10 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     instead of testing every row's mask byte.
     `tagged` (GS): the user CSR's column indices tagged with grad_support's
     item mask (forward_steps(tag=...)): the first user product reads the item
-    support from them instead of loading the mask per edge (bitwise)."""
+    support from them instead of loading the mask per edge (bitwise).
+    `item_mask_bits` (GS): grad_support's item mask packed one bit per item
+    (bbgr_mask_pack): the first user product tests its edges on the bits
+    instead of the bytes (bitwise)."""
     U, I = pair.num_users, pair.num_items
     d = gU.shape[1]
     _check_table("user grad", gU, U, d)
@@ -732,10 +739,12 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                           **(fl if first else {}), **ka)
             yield
             tg = tagged if (first and si_int is not None) else None
+            mb = item_mask_bits if (first and si_int is not None and tg is None) else None
             if k > 1:
                 spmm(BU, bufI, False, y=bufU, y_scale=pair.feed_bwd_ui,
                      add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl,
-                     src_mask=si_int if first else None, add_map=um, tagged=tg)
+                     src_mask=si_int if first else None, add_map=um, tagged=tg,
+                     src_mask_bits=mb)
             else:
                 if before_last is not None:
                     before_last()
@@ -744,7 +753,7 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                 spmm(BU, bufI, False, y=None if fused else gu0, y_scale=BU.out_scale,
                      add=gU, add_mask=su, add_scale=None, add_scale_s=gl,
                      src_mask=src, adam=adam_u if fused else None, add_map=um, y_map=um,
-                     tagged=tg)
+                     tagged=tg, src_mask_bits=mb)
                 if adam_u is not None and not fused:   # K == 1: masked product, Adam apart
                     adam_u.apply(gu0)
         if grad_i0_dense:   # GS: i0 only feeds the layer mean -> grad_i0 = gI/(K+1)
@@ -800,11 +809,11 @@ def backward(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_layers:
              out_i: torch.Tensor | None = None, ws: dict | None = None,
              grad_i0_dense: bool = True, reduce=None, grad_support=None,
              adam_u=None, before_last=None, adam_i=None, src_bits=None,
-             frontier_list=None, tagged=None):
+             frontier_list=None, tagged=None, item_mask_bits=None):
     """backward_steps run to completion: (grad u0, grad i0)."""
     return drain(backward_steps(pair, gU, gI, num_layers, order, out_u, out_i, ws,
                                 grad_i0_dense, reduce, grad_support, adam_u, before_last,
-                                adam_i, src_bits, frontier_list, tagged))
+                                adam_i, src_bits, frontier_list, tagged, item_mask_bits))
 
 
 def propagate(pair: OperatorPair, u0: torch.Tensor, i0: torch.Tensor, num_layers: int,

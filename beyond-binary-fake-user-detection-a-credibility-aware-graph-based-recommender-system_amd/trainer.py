@@ -164,6 +164,14 @@ class FusedTrainer:
         if (self.frontier and order == ORDER_GS and num_layers >= 2 and emb_dim >= 64
                 and uc.nnz <= 24 * uc.n_rows and os.environ.get("BBGR_TAGGED", "0") == "1"):
             self.tagged = torch.empty(max(uc.nnz, 1), dtype=torch.int32, device=dev)
+        # GS frontier: the item mask also packed one bit per item after the
+        # marking (bbgr_mask_pack) for the first backward user product's
+        # per-edge test (bbgr_spmm_args.src_mask_bits; bitwise the byte test;
+        # BBGR_MASK_BITS=0 keeps the bytes for A/B)
+        self.mask_i_bits = None
+        if (self.frontier and order == ORDER_GS and num_layers >= 1
+                and os.environ.get("BBGR_MASK_BITS", "1") != "0"):
+            self.mask_i_bits = torch.zeros(self.I // 32 + 1, dtype=torch.int32, device=dev)
         self.item_list = self.item_count = self.item_len = None
         # GS frontier: the step's bookkeeping (masks, list, slot bits, and the
         # sparse gradient rows' reset) runs as one launch at each end of the
@@ -261,7 +269,7 @@ class FusedTrainer:
             backward(self.pair, self.g_uf, self.g_if, self.K, self.order, out_u=self.g_u0,
                      out_i=self.g_i0, ws=self.ws, grad_support=masks,
                      src_bits=self._bits(masks), frontier_list=self._flist(masks),
-                     tagged=self._tagged(masks))
+                     tagged=self._tagged(masks), item_mask_bits=self._mask_bits(masks))
             # ego L2 term goes straight to the weight grads (Version-2:503-507):
             # d/de0 reg*mean(|e0|^2) = 2*reg/B * e0 on every (u, pos, neg) row
             call("bbgr_rows_axpy", B, ptr(users), alpha, ptr(self.user_w), ld(self.user_w),
@@ -359,9 +367,9 @@ class FusedTrainer:
                  ws=self.ws, grad_support=masks, grad_i0_dense=False, adam_u=adam_u,
                  src_bits=self._bits(masks), frontier_list=self._flist(masks),
                  before_last=before_last, reduce=reduce, adam_i=adam_i,
-                 tagged=self._tagged(masks))
+                 tagged=self._tagged(masks), item_mask_bits=self._mask_bits(masks))
         if side:   # the side table is all-zero between steps (bbgr_batch_end's rows)
-            if not self._fused_pending:
+            if not getattr(self, "_fused_pending", False):
                 call("bbgr_rows_zero", item_rows.numel(), ptr(item_rows), ptr(ga), ld(ga),
                      self.d, st)
         elif item_adam:
@@ -424,6 +432,7 @@ class FusedTrainer:
             _lib.check_word_padded(self.mask_i, self.I, "item mask")
             a = self._batch_args(users)
             call("bbgr_batch_begin", ctypes.byref(a), st)
+            self._pack_item_mask()
             if getattr(self, "item_len", None) is not None:
                 self.item_len.publish()
             # (the step's end restores all of it in one bbgr_batch_end; a
@@ -450,10 +459,22 @@ class FusedTrainer:
                 self.item_count.zero_()
                 if getattr(self, "item_len", None) is not None:
                     self.item_len.invalidate()
+        if value:
+            self._pack_item_mask()
         if getattr(self, "slot_bits", None) is not None:   # set / clear the batch's bits
             call("bbgr_mark_slots", B, ptr(users), ptr(uc.indptr), ptr(self.slot_map),
                  ptr(self.slot_bits), value, st)
         return self.mask_u, self.mask_i
+
+    def _pack_item_mask(self) -> None:
+        """mask_i_bits = mask_i packed (every word rewritten: nothing to clear)."""
+        bits = getattr(self, "mask_i_bits", None)
+        if bits is not None:
+            call("bbgr_mask_pack", self.I, ptr(self.mask_i), ptr(bits), stream_handle())
+
+    def _mask_bits(self, masks):
+        """backward(item_mask_bits=...) when the masks are on."""
+        return getattr(self, "mask_i_bits", None) if masks is not None else None
 
     def _tag(self, masks):
         """forward(tag=...): the tagged user-CSR index copy and the item mask."""

@@ -291,6 +291,11 @@ int bbgr_gather_scale(int64_t nnz, const int32_t *indices, const float *scale,
 /*   follow adam_map: the drop-in optimizer stores its moments in the graph's */
 /*   order, so only the caller-order weight row is read and written at       */
 /*   random (bbgr.optim.FusedAdam converts them at its state_dict boundary). */
+/* src_mask_bits (nullable, with src_mask; ABI 10): the same mask packed one */
+/*   bit per source row (bit c & 31 of word c >> 5; bbgr_mask_pack), read by */
+/*   the per-edge liveness test instead of the bytes: fewer L2 requests for   */
+/*   the same test (degree-ordered hub columns share lines). Bitwise the byte */
+/*   mask's result.                                                            */
 /* adam_mirror (nullable, with adam_moments_unmapped; ABI 10): adam_param is */
 /*   then in the launch's row order as well (row r, like the moments), and   */
 /*   every updated param row is also stored to adam_mirror row adam_map[r]   */
@@ -375,6 +380,7 @@ typedef struct {
   const uint8_t *tag_mask;
   const int32_t *src_tagged;
   float *adam_mirror;
+  const uint32_t *src_mask_bits;
 } bbgr_spmm_args;
 
 int bbgr_spmm(const bbgr_csr *csr, const bbgr_spmm_args *args,
@@ -669,6 +675,10 @@ typedef struct {
   int32_t d;
 } bbgr_batch_args;
 int bbgr_batch_begin(const bbgr_batch_args *args, bbgr_stream_t stream);
+/* bits[w] = OR over b < 32 of (mask[32 w + b] != 0) << b, for every word    */
+/* w < ceil(n / 32) (ABI 10): a byte mask packed for bbgr_spmm_args.         */
+/* src_mask_bits (the bits past n are 0).                                    */
+int bbgr_mask_pack(int64_t n, const uint8_t *mask, uint32_t *bits, bbgr_stream_t stream);
 int bbgr_batch_end(const bbgr_batch_args *args, bbgr_stream_t stream);
 /* The same for every CSR row r < n_rows flagged in row_mask: row_mask[r], or
  * row_mask[row_map[r]] when row_map is given (a mask kept in the caller's

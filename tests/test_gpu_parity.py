@@ -1231,6 +1231,67 @@ def test_src_masked_launch_is_bitwise_the_dense_product(d, mode, monkeypatch):
                                               err_msg=f"frac={frac} pair={pair} rng={rg}")
 
 
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 1_000_003])
+def test_mask_pack(n):
+    """bbgr_mask_pack: bit c & 31 of word c >> 5 is mask[c] != 0 (any nonzero
+    byte), the bits past n zero, every word of ceil(n / 32) rewritten; the
+    unaligned tail and an odd-offset mask included."""
+    from bbgr import _lib
+    rng = np.random.default_rng(n)
+    m = torch.from_numpy((rng.random(n + 1) < 0.3).astype(np.uint8) * rng.integers(1, 255, n + 1)
+                         .astype(np.uint8)).to(DEV)
+    for off in (0, 1):
+        mask = m[off: off + n]
+        words = (n + 31) // 32
+        bits = torch.full((words + 1,), -1, dtype=torch.int32, device=DEV)
+        _lib.call("bbgr_mask_pack", n, _lib.ptr(mask), _lib.ptr(bits), _lib.stream_handle())
+        torch.cuda.synchronize()
+        mb = np.zeros(words * 32, dtype=np.uint8)
+        mb[:n] = (mask.cpu().numpy() != 0)
+        want = (mb.reshape(-1, 32).astype(np.uint64) << np.arange(32, dtype=np.uint64)).sum(1)
+        want = want.astype(np.uint32)
+        got = bits.cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(got[:words], want)
+        assert got[words] == 0xFFFFFFFF   # nothing written past the last word
+
+
+@pytest.mark.parametrize("d,mode", [(64, 0), (64, 1), (64, 2), (128, 0), (256, 1), (32, 0)])
+def test_src_mask_bits_launch_is_bitwise_the_byte_mask_launch(d, mode, monkeypatch):
+    """bbgr_spmm_args.src_mask_bits: the per-edge test on the packed mask gives
+    the byte mask's launch bit for bit (live fractions 0 .. 1, one- and
+    two-row kernels, every weight mode, chunked long rows, row ranges)."""
+    from bbgr import _lib
+    from bbgr.propagate import Product, spmm
+    rng = np.random.default_rng(900 + d + mode)
+    Rn, Cn = 2500, 900
+    deg = rng.geometric(0.1, Rn) - 1
+    deg[rng.choice(Rn, 5, replace=False)] = [16, 17, 31, 200, 900]
+    rows = np.repeat(np.arange(Rn), deg).astype(np.int32)
+    cols = rng.integers(0, Cn, rows.size).astype(np.int32)
+    vals = rng.uniform(0.1, 1.0, rows.size).astype(np.float32)
+    cs = rng.uniform(0.5, 2.0, Cn).astype(np.float32)
+    c = Csr(rows, cols, Rn, Cn, DEV, edge_values=t(vals) if mode == 1 else None,
+            long_threshold=64, chunk_edges=128)
+    prod = Product(c, c.values if mode == 1 else None, t(cs) if mode == 2 else None, None, {})
+    x = rng.uniform(-1, 1, (Cn, d)).astype(np.float32)
+    bits = torch.zeros(Cn // 32 + 1, dtype=torch.int32, device=DEV)
+    for frac in (0.0, 0.05, 0.41, 0.9, 1.0):
+        m = t((rng.random(Cn) < frac).astype(np.uint8), torch.uint8)
+        _lib.call("bbgr_mask_pack", Cn, _lib.ptr(m), _lib.ptr(bits), _lib.stream_handle())
+        xm = t(x) * m[:, None].float()
+        for pair in (0, 1):
+            monkeypatch.setenv("BBGR_SPMM_PAIR", str(pair))
+            for rg in [None] + list(c.row_ranges(2)):
+                kw = {} if rg is None else {"rng": rg}
+                ref = torch.full((Rn, d), 7.0, device=DEV)
+                got = torch.full((Rn, d), 7.0, device=DEV)
+                spmm(prod, xm, True, y=ref, y_scale_s=0.5, src_mask=m, **kw)
+                spmm(prod, xm, True, y=got, y_scale_s=0.5, src_mask=m, src_mask_bits=bits, **kw)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(got.cpu().numpy(), ref.cpu().numpy(),
+                                              err_msg=f"frac={frac} pair={pair} rng={rg}")
+
+
 @pytest.mark.parametrize("d,mode", [(64, 0), (64, 1), (64, 2), (128, 0), (256, 1)])
 def test_tagged_indices_launch_is_bitwise_the_src_masked_launch(d, mode, monkeypatch):
     """bbgr_spmm_args.tag_out: a full two-row launch also writes the column

@@ -27,6 +27,8 @@
 #   evalnp     sampled evaluation at C4 on the reference's numpy candidate stream
 #   frontierab C2 / C1 step with the frontier masks on and off (graph replay)
 #   batchab    fused step bookkeeping (BBGR_BATCH_FUSED 1 / 0) at BCONFIGS (C2 default)
+#   envab      A/B of one environment switch: ENVAB=<name>, ENVAB_VALUES ("1 0"), BCONFIGS,
+#              two interleaved rounds
 set -o pipefail
 T=$1; shift
 O=gpurun_out/$T
@@ -174,6 +176,19 @@ for step in "$@"; do
           rc=$?; hard $rc "batch $c $f" "$O/${c,,}_batch_$f.log"
           [ $rc -eq 0 ] || { tail -20 "$O/${c,,}_batch_$f.log"; exit 1; }
           echo "$c fused bookkeeping $f: $(python tools/bench_brief.py "$O/${c,,}_batch_$f.json" | head -1)"
+        done
+      done ;;
+    envab)
+      for rep in 1 2; do
+        for c in ${BCONFIGS:-C4}; do
+          for f in ${ENVAB_VALUES:-1 0}; do
+            o="$O/${c,,}_${ENVAB}_${f}_$rep"
+            env "$ENVAB=$f" timeout -k 10 400 python -u bench.py --config $c $quick_args \
+              --steps 30 --warmup 3 > "$o.json" 2> "$o.log"
+            rc=$?; hard $rc "envab $c $f" "$o.log"
+            [ $rc -eq 0 ] || { tail -20 "$o.log"; exit 1; }
+            echo "$c $ENVAB=$f #$rep: $(python tools/bench_brief.py "$o.json" | head -1)"
+          done
         done
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
