@@ -116,7 +116,7 @@ struct Pair {
   // the rows backward's frontier buffers, one set per stream (reused: the slot
   // bitmap is cleared again after each use; frontier_bits / release_bits)
   struct FrontierBufs {
-    Tensor bits, list, count, ws;
+    Tensor bits, list, count, ws, mbits;
   };
   mutable std::mutex fb_mu;
   mutable std::map<int64_t, FrontierBufs> fb;
@@ -218,6 +218,7 @@ struct Opts {
   const int64_t *row_list = nullptr, *row_count = nullptr;   // device-length row list
   int64_t n_row_list = 0;
   const uint32_t *src_bits = nullptr;                         // slot bitmap of src_mask
+  const uint32_t *src_mask_bits = nullptr;                    // src_mask packed (bbgr_mask_pack)
   // fused Adam on this launch's rows (bbgr_spmm_args.adam_*; null: none)
   const AdamTable *adam = nullptr;
   const float *adam_grad = nullptr;   // its gradient table (nullable: the row value)
@@ -271,6 +272,7 @@ static void spmm(const Product &pr, const Tensor &x, bool first, const Opts &o) 
   a.n_row_list = o.n_row_list;
   a.row_count = o.row_count;
   a.src_bits = o.src_bits;
+  a.src_mask_bits = o.src_mask ? o.src_mask_bits : nullptr;
   if (o.adam) {
     const AdamTable &A = *o.adam;
     a.adam_param = A.p.data_ptr<float>();
@@ -586,6 +588,9 @@ struct Support {
   // and the slot bitmap of the listed users' edges in item-CSR order, for the
   // first item product (bbgr_spmm_args.row_list / row_count / src_bits)
   Tensor flist, fcount, bits;
+  // si_int packed one bit per item (bbgr_mask_pack): the first user product's
+  // per-edge test (bbgr_spmm_args.src_mask_bits)
+  Tensor si_bits;
   // gU (and su) in the graph's own row order instead of the caller's: the
   // rows backward builds its gU table itself, so every user product adds it
   // without the row map (add_mask read at the row, not at user_map[row]) and
@@ -684,7 +689,19 @@ static std::unique_lock<std::mutex> frontier_bits(const Pair &P, Support &s, con
     b = &P.fb[(int64_t)(intptr_t)cur_stream()];
   }
   if (!b->bits.defined()) b->bits = at::zeros({nbits}, i32);
-  mask_list(s.si_int.defined() ? s.si_int : s.si, b->list, b->count, b->ws);
+  const Tensor &mi = s.si_int.defined() ? s.si_int : s.si;
+  mask_list(mi, b->list, b->count, b->ws);
+  // the packed item mask (every word rewritten per call: nothing to clear;
+  // BBGR_MASK_BITS=0 keeps the byte test, A/B)
+  const char *mb_env = std::getenv("BBGR_MASK_BITS");
+  if (!(mb_env && mb_env[0] == '0')) {
+    if (!b->mbits.defined()) b->mbits = at::empty({P.I / 32 + 1}, i32);
+    check(bbgr_mask_pack(P.I, mi.data_ptr<uint8_t>(),
+                         reinterpret_cast<uint32_t *>(b->mbits.data_ptr<int32_t>()),
+                         cur_stream()),
+          "bbgr_mask_pack");
+    s.si_bits = b->mbits;
+  }
   s.flist = b->list;
   s.fcount = b->count;
   s.bits = b->bits;
@@ -823,6 +840,8 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
       ou.add_mask = su;
       ou.add_map = um_add;
       ou.src_mask = first ? si_int : nullptr;
+      if (first && s.si_bits.defined())
+        ou.src_mask_bits = reinterpret_cast<const uint32_t *>(s.si_bits.data_ptr<int32_t>());
       ou.add_scale_s = gl;
       if (k > 1) {
         ou.y = bufU;

@@ -299,8 +299,11 @@ def test_dropin_first_item_product_bitmap_is_bitwise_the_mask(order, d, monkeypa
     monkeypatch.setattr(operators, "DROPIN_VERTEX_ORDER", order)
     M_ui, M_iu = V2.build_message_passing_mats(e, U_, I_, cred, DEV)
     out = {}
-    for bits in ("1", "0"):
+    # (BBGR_MASK_BITS: the first user product's per-edge test on the packed
+    # item mask, bbgr_mask_pack, vs the bytes; also bitwise)
+    for bits, mb in (("1", "1"), ("1", "0"), ("0", "0")):
         monkeypatch.setenv("BBGR_DROPIN_BITS", bits)
+        monkeypatch.setenv("BBGR_MASK_BITS", mb)
         torch.manual_seed(0)
         m = V2.LightGCN(U_, I_, d, K, M_ui, M_iu).to(DEV)
         uf, itf = m.propagate()
@@ -308,7 +311,8 @@ def test_dropin_first_item_product_bitmap_is_bitwise_the_mask(order, d, monkeypa
         n0 = ops.counters()
         loss.backward()
         assert ops.counters()["rows"] - n0["rows"] == 1
-        out[bits] = (float(loss), [p.grad.clone() for p in m.parameters()])
-    assert out["1"][0] == out["0"][0]
-    for a, b in zip(out["1"][1], out["0"][1]):
-        assert torch.equal(a, b)
+        out[bits + mb] = (float(loss), [p.grad.clone() for p in m.parameters()])
+    for key in ("10", "00"):
+        assert out["11"][0] == out[key][0]
+        for a, b in zip(out["11"][1], out[key][1]):
+            assert torch.equal(a, b)
