@@ -851,18 +851,18 @@ def main():
         how = ("C ABI RCCL on a comm stream" if nc else "torch collectives")
         return f"{c} chain{'s' if c > 1 else ''}, {xq['exchange_parts']} item-row range(s), {how}"
 
+    if ar_probe is not None and ar_probe.get("cabi_error") and inline_xp is not None:
+        # the C ABI communicator did not come up on this machine: the one-chain
+        # setting runs its collectives through torch's group instead
+        inline_xp.pop("native_comm", None)
     # the user-row chain settings: the main run and the one beside it (the
     # probe's rule, when it has constants, decides which runs first)
     main_xp, beside_xp = xp, inline_xp
     if rule is not None and rule["predicted"] == "inline" and inline_xp is not None:
         main_xp, beside_xp = inline_xp, xp
-    trainer = build(partition, main_xp if partition == "users" else None)
-    res = measure(trainer, partition, args.dense_check)
-    res["xp"] = main_xp if partition == "users" else xp
-    runs = [res]
     U_job = U * (world if weak else 1)
     strong_multi = dist_mode and world > 1 and not weak
-    todo = []
+    todo = [(partition, main_xp if partition == "users" else xp)]
     if strong_multi and partition == "users" and args.chain_beside and beside_xp is not None:
         todo.append(("users", beside_xp))
     other = {"columns": "users", "users": "columns"}.get(partition)
@@ -875,17 +875,27 @@ def main():
         if other == "users" and args.chain_beside and beside_xp is not None:
             todo.append(("users", beside_xp))
     beside_errors = []
-    for part, xq in todo:
+    runs = []
+    trainer = None
+    for i, (part, xq) in enumerate(todo):
         if trainer is not None:
             trainer.close()
         trainer = None
         torch.cuda.empty_cache()
-        # a beside run that fails on every rank alike (an RCCL communicator
-        # that will not come up, memory) is reported, not fatal: the ranks
-        # agree on it and the line keeps the runs that finished
+        if not dist_mode:   # one process: nothing to fall back to, errors are errors
+            trainer = build(part, xq)
+            r = measure(trainer, part, args.dense_check)
+            r["xp"] = xq
+            runs.append(r)
+            continue
+        # a run that fails on every rank alike (an RCCL communicator that will
+        # not come up, memory) is reported, not fatal: the ranks agree on it and
+        # the line keeps the runs that finished (the main run's failure too, as
+        # long as one setting finishes)
         try:
-            if os.environ.get("BBGR_BENCH_FAIL_BESIDE") == part:   # the error path's test
-                raise RuntimeError("injected beside failure")
+            fail = os.environ.get("BBGR_BENCH_FAIL_BESIDE")   # the error paths' tests
+            if (fail == part and i > 0) or (fail == "main" and i == 0):
+                raise RuntimeError("injected failure")
             trainer = build(part, xq)
             r = measure(trainer, part, args.dense_check)
             r["xp"] = xq
@@ -893,7 +903,7 @@ def main():
         except Exception as ex:   # noqa: BLE001
             ok, err = 0.0, f"{part} ({chain_mode(xq) if part == 'users' else 'columns'}): " \
                            f"{type(ex).__name__}: {ex}"[:400]
-            log(f"[bench] rank {rank}: beside run failed: {err}")
+            log(f"[bench] rank {rank}: {'main' if i == 0 else 'beside'} run failed: {err}")
         if _allreduce(ok, dev, torch.distributed.ReduceOp.MIN) < 1.0:
             beside_errors.append(err if ok < 1.0 else f"{part}: failed on another rank")
             if trainer is not None:
@@ -901,6 +911,9 @@ def main():
             trainer = None
             continue
         runs.append(r)
+    if not runs:
+        raise RuntimeError("bench: every partition / chain setting failed: "
+                           + " | ".join(beside_errors))
     # every rank holds the same max-over-ranks times: the same choice everywhere
     res = min(runs, key=lambda r: r["elapsed"])
 

@@ -259,6 +259,26 @@ def test_bench_two_ranks_survives_a_failed_beside_run(tmp_path):
     assert len(j["beside_errors"]) == 2 and all("injected" in e for e in j["beside_errors"])
 
 
+def test_bench_two_ranks_survives_a_failed_main_run(tmp_path):
+    """The main run failing on every rank (injected; on a real node: a C ABI
+    communicator that will not come up for the chain setting the probe chose)
+    falls back to the runs beside it: the line is the fastest run that
+    finished and the main run's failure is listed in beside_errors."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--standalone", "--local-addr=127.0.0.1",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2", "--steps", "2",
+           "--warmup", "1", "--dense-check", "0", "--frontier", "on", "--weak-beside", "0",
+           "--partition", "users"]
+    env = dict(os.environ, OMP_NUM_THREADS="4", BBGR_DIST_BACKEND="gloo",
+               BBGR_BENCH_FAIL_BESIDE="main")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    j = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert j["value"] > 0
+    assert len(j["beside_errors"]) == 1 and "injected" in j["beside_errors"][0]
+    assert j["beside_errors"][0].startswith("users")
+
+
 def test_bench_sharded_single_rank_with_inline_collectives(tmp_path):
     """bench.py's user-row step at world size 1 over RCCL (--sharded) with
     every collective inline on the compute stream (--native-comm inline): one
