@@ -245,7 +245,9 @@ _SIGNATURES = {
                        c_int32),
     "bbgr_graph_rows": ([c_int64, _P, c_int64, _P, _P, _P], c_int32),
     "bbgr_ego_rows": ([c_int64, c_int32, _P, _P, _P, _P, _P, _P, c_int64, _P, c_int64, _P,
-                       c_float, _P, _P, c_int64, _P, c_int64, c_float, _P], c_int32),
+                       c_float, _P, _P, c_int64, _P, c_int64, c_float, _P, _P], c_int32),
+    "bbgr_rows_add_slots": ([c_int64, _P, _P, _P, _P, c_int64, _P, c_int64, c_int32, c_int64,
+                             _P], c_int32),
     "bbgr_rows_add_unique": ([c_int64, _P, _P, c_int64, _P, c_int64, c_int32, c_int64, _P],
                              c_int32),
     # blueprint names, thin forms of the entry points above

@@ -781,7 +781,30 @@ struct StepAdam {
   // item gradient) and the batch users' gU rows (set by rows_backward; gU
   // and the ego rows added before the user Adam)
   RowPlan item_plan, user_plan;
+  // the users' scatter in first-slot form instead of user_plan (defined:
+  // bbgr_rows_add_slots over user_rows, the rows of the batch's user slots)
+  Tensor user_slot, user_count, user_rows;
 };
+
+// dst[user_rows[k]] += the first-slot sums of src's rows (bbgr_rows_add_slots):
+// bitwise apply_rows over a plan of user_rows (a stable sort's segments)
+static void add_slot_rows(const StepAdam &sa, Tensor &dst, const Tensor &src_) {
+  const Tensor src = src_.contiguous();
+  const int64_t n = sa.user_rows.numel();
+  TORCH_CHECK(src.size(0) >= n && src.size(1) == dst.size(1) && sa.user_slot.numel() >= n,
+              "add_slot_rows: shapes");
+  check(bbgr_rows_add_slots(n, sa.user_slot.data_ptr<int64_t>(),
+                            sa.user_count.data_ptr<int32_t>(), sa.user_rows.data_ptr<int64_t>(),
+                            src.data_ptr<float>(), ld(src), dst.data_ptr<float>(), ld(dst),
+                            (int32_t)dst.size(1), dst.size(0), cur_stream()),
+        "bbgr_rows_add_slots");
+}
+
+// BBGR_USER_SORT=1 keeps the user scatter's sort (A/B, tests)
+static bool users_sorted_scatter() {
+  const char *e = std::getenv("BBGR_USER_SORT");
+  return e && e[0] == '1';
+}
 
 static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU, const Tensor &gI,
                                                  int64_t K, bool gs, const Support &s,
@@ -849,7 +872,10 @@ static std::tuple<Tensor, Tensor> backward_chain(const Pair &P, const Tensor &gU
         ou.add_scale = P.bi.in_scale;
       } else if (sa) {   // the user Adam: no gradient table, ego rows in gU first
         Tensor g = gU;
-        apply_rows(sa->user_plan, g, sa->ego_u_vals);
+        if (sa->user_slot.defined())
+          add_slot_rows(*sa, g, sa->ego_u_vals);
+        else
+          apply_rows(sa->user_plan, g, sa->ego_u_vals);
         ou.y_scale = P.bu.out_scale;
         ou.y_map = um;   // the Adam's rows: the caller's order
         ou.adam = &sa->user;
@@ -1090,8 +1116,13 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
     gU.index_fill_(0, ru, 0.0);
   }
   if (sa) {   // the ego rows land on the same gU rows as vu: one sort for both
-    sa->user_plan = plan_rows(ru, U);
-    apply_rows(sa->user_plan, gU, vu);
+    if (sa->user_slot.defined()) {   // first slots + counts: no sort
+      sa->user_rows = ru;
+      add_slot_rows(*sa, gU, vu);
+    } else {
+      sa->user_plan = plan_rows(ru, U);
+      apply_rows(sa->user_plan, gU, vu);
+    }
   } else {
     index_add_rows(gU, ru, vu.contiguous());
   }
@@ -1358,7 +1389,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
                                                                 const Tensor &neg,
                                                                 const Tensor &ue,
                                                                 const Tensor &ie, double reg,
-                                                                double scale = 1.0) {
+                                                                double scale = 1.0,
+                                                                Tensor *user_slots = nullptr) {
   const int64_t B = users.numel(), d = ue.size(1), U = ue.size(0), I = ie.size(0);
   TORCH_CHECK(U > 0 && I > 0, "ego_grad_rows: empty table");
   // one int64 block: iu [B], ii [2B], cu [B], sp [B], sn [B]
@@ -1378,12 +1410,20 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> ego_grad_rows(const Tensor &dl
   Tensor gu = g.narrow(0, 0, B), gi = g.narrow(0, B, 2 * B);
   Tensor cnt = slot_scratch(3 * B, users.device(), 3, 0);
   const Tensor uec = ue.contiguous(), iec = ie.contiguous();
+  // user_slots: (cu, the users' first-slot counts) for bbgr_rows_add_slots
+  Tensor cnt_u;
+  if (user_slots) {
+    cnt_u = at::empty({std::max<int64_t>(B, 1)}, at::TensorOptions().dtype(at::kInt).device(
+                                                     users.device()));
+    user_slots[0] = cu;
+    user_slots[1] = cnt_u;
+  }
   check(bbgr_ego_rows(B, (int32_t)d, cu.data_ptr<int64_t>(), sp.data_ptr<int64_t>(),
                       sn.data_ptr<int64_t>(), iu.data_ptr<int64_t>(), ii.data_ptr<int64_t>(),
                       uec.data_ptr<float>(), ld(uec), iec.data_ptr<float>(), ld(iec),
                       dl.data_ptr<float>(), (float)reg, cnt.data_ptr<int32_t>(),
                       gu.data_ptr<float>(), ld(gu), gi.data_ptr<float>(), ld(gi), (float)scale,
-                      cur_stream()),
+                      user_slots ? cnt_u.data_ptr<int32_t>() : nullptr, cur_stream()),
         "bbgr_ego_rows");
   return {gu, gi, iu, ii};
 }
@@ -1428,11 +1468,16 @@ static void bpr_adam_backward_cuda(const Tensor &dloss, const Tensor &uf_, const
   a.contrib = contrib.data_ptr<float>();
   a.ldcontrib = ld(contrib);
   check(bbgr_bpr(&a, cur_stream()), "bbgr_bpr");
-  // the ego rows come scaled by K + 1 (one rounding, as at::mul(rows, K + 1))
-  auto eg = ego_grad_rows(dl, users, pos, neg, u0, i0, reg, (double)(K + 1));
+  // the ego rows come scaled by K + 1 (one rounding, as at::mul(rows, K + 1));
+  // the users' first slots and counts replace the user scatter's sort
+  Tensor uslots[2];
+  auto eg = ego_grad_rows(dl, users, pos, neg, u0, i0, reg, (double)(K + 1),
+                          users_sorted_scatter() ? nullptr : uslots);
   const Tensor &ru = std::get<0>(eg), &ri = std::get<1>(eg), &iu = std::get<2>(eg),
                &ii = std::get<3>(eg);
   StepAdam sa;
+  sa.user_slot = uslots[0];
+  sa.user_count = uslots[1];
   sa.user = AdamTable{u0, m_u, v_u, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
                       (float)bc1_u, (float)bc2s_u};
   sa.item = AdamTable{i0, m_i, v_i, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,

@@ -648,13 +648,14 @@ __global__ __launch_bounds__(256) void ego_rows_kernel(long B, const long *iu, c
                                                        const float *dloss, float inv_b,
                                                        float reg, int *counts, float *g_u,
                                                        long ldgu, float *g_i, long ldgi,
-                                                       float scale) {
+                                                       float scale, int *counts_u_out) {
   constexpr int V = D / 64;
   const long s = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
   if (s >= 3 * B) return;
   const int n = counts[s];
   const bool user = s < B;
+  if (user && counts_u_out && lane == 0) counts_u_out[s] = n;
   float4 *dst = reinterpret_cast<float4 *>(user ? g_u + s * ldgu : g_i + (s - B) * ldgi) + lane;
   float4 acc[V];
 #pragma unroll
@@ -721,6 +722,49 @@ __global__ __launch_bounds__(256) void rows_add_unique_kernel(long n, const long
     const float4 a = make_float4(0.f + x.x, 0.f + x.y, 0.f + x.z, 0.f + x.w);
     const float4 o = out[c];
     out[c] = make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w);
+  }
+}
+
+// dst[rows[f]] += (0 + src[f] + src[k2] + ... ) over each leader f's
+// occurrences (slot[k] == f, ascending k; counts[f] of them): the sums of a
+// stable sort's segments (scatter_segments_kernel) without the sort, the
+// slots of invalid triples (zero rows) left out (+0.0 changes no such sum).
+// A batch of distinct rows (counts 1) reads no slot past its own; a repeated
+// row scans forward 16 slots a load until its count is found.
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+__global__ __launch_bounds__(256) void rows_add_slots_kernel(long n, const long *slot,
+                                                             const int *counts, const long *rows,
+                                                             const float4 *src, long lds4,
+                                                             float4 *dst, long ldd4, int d4,
+                                                             long n_dst) {
+  const long f = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  // a leader: some valid slot points at f (f itself, or an invalid triple's
+  // slot holding the first occurrence of the clamped id; slot[f] == -1 then)
+  if (f >= n || counts[f] <= 0) return;   // group-uniform
+  const long r = rows[f];
+  if (r < 0 || r >= n_dst) return;
+  const int c = counts[f];
+  for (int col = lane; col - lane < d4; col += 16) {   // (every lane runs the scan's ballots)
+    const bool on = col < d4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (on) acc = add4(acc, src[f * lds4 + col]);
+    int found = slot[f] == f ? 1 : 0;   // (counts count the valid slots only)
+    for (long k0 = f + 1; found < c && k0 < n; k0 += 16) {
+      const long kk = k0 + lane;
+      const bool hit = kk < n && slot[kk] == f;
+      unsigned m = (unsigned)((__ballot(hit) >> (threadIdx.x & 48)) & 0xffffull);
+      while (m) {
+        const int j = __ffs(m) - 1;
+        m &= m - 1u;
+        if (on) acc = add4(acc, src[(k0 + j) * lds4 + col]);
+        ++found;
+      }
+    }
+    if (on) dst[r * ldd4 + col] = add4(dst[r * ldd4 + col], acc);
   }
 }
 
@@ -1331,7 +1375,7 @@ extern "C" int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int6
                              const float *ue, int64_t ldue, const float *ie, int64_t ldie,
                              const float *dloss, float reg, int32_t *counts, float *g_u,
                              int64_t ldgu, float *g_i, int64_t ldgi, float scale,
-                             bbgr_stream_t stream) {
+                             int32_t *counts_u_out, bbgr_stream_t stream) {
   BBGR_REQUIRE(B >= 0 && 3 * B < (1LL << 31), "bbgr_ego_rows: bad batch");
   if (d != 64 && d != 128 && d != 256) {
     set_error("bbgr_ego_rows: embedding dim %d unsupported (64, 128, 256)", d);
@@ -1352,7 +1396,7 @@ extern "C" int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int6
 #define BBGR_EGO_ROWS(DD)                                                                   \
   hipLaunchKernelGGL(ego_rows_kernel<DD>, g, dim3(256), 0, st, (long)B, (const long *)iu, \
                      (const long *)ii, ue, (long)ldue, ie, (long)ldie, dloss, inv_b, reg,   \
-                     counts, g_u, (long)ldgu, g_i, (long)ldgi, scale)
+                     counts, g_u, (long)ldgu, g_i, (long)ldgi, scale, counts_u_out)
   switch (d) {
     case 64: BBGR_EGO_ROWS(64); break;
     case 128: BBGR_EGO_ROWS(128); break;
@@ -1406,6 +1450,24 @@ extern "C" int bbgr_rows_add_unique(int64_t n, const int64_t *idx, const float *
                      reinterpret_cast<const float4 *>(src), (long)ldsrc / 4,
                      reinterpret_cast<float4 *>(dst), (long)lddst / 4, d / 4, (long)n_dst);
   BBGR_LAUNCHED("rows_add_unique_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_rows_add_slots(int64_t n, const int64_t *slot, const int32_t *counts,
+                                   const int64_t *rows, const float *src, int64_t ldsrc,
+                                   float *dst, int64_t lddst, int32_t d, int64_t n_dst,
+                                   bbgr_stream_t stream) {
+  BBGR_REQUIRE(n >= 0 && n_dst >= 0 && d > 0 && (d & 3) == 0 && ldsrc >= d && lddst >= d &&
+                   (ldsrc & 3) == 0 && (lddst & 3) == 0,
+               "bbgr_rows_add_slots: bad sizes (d, ld multiples of 4, ld >= d)");
+  if (n == 0) return BBGR_OK;
+  BBGR_REQUIRE(slot && counts && rows && src && dst && aligned16(src) && aligned16(dst),
+               "bbgr_rows_add_slots: null or unaligned arrays");
+  hipLaunchKernelGGL(rows_add_slots_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), (long)n, (const long *)slot, counts, (const long *)rows,
+                     reinterpret_cast<const float4 *>(src), (long)ldsrc / 4,
+                     reinterpret_cast<float4 *>(dst), (long)lddst / 4, d / 4, (long)n_dst);
+  BBGR_LAUNCHED("rows_add_slots_kernel");
   return BBGR_OK;
 }
 

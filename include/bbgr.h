@@ -564,11 +564,24 @@ int bbgr_ego_slots(int64_t B, const int64_t *users, const int64_t *pos, const in
 /* popular item's row. counts: int32 [3B] scratch, zero on entry and return.  */
 /* scale: every written row is that sum times scale (one rounding; 1 = the    */
 /* sum itself; the in-backward Adam's (K+1) * ego rows without a mul launch). */
+/* counts_u_out (nullable, int32 [B]): slot s < B's user count n (0 off the   */
+/* first slots), for bbgr_rows_add_slots over the same cu.                    */
 int bbgr_ego_rows(int64_t B, int32_t d, const int64_t *cu, const int64_t *sp, const int64_t *sn,
                   const int64_t *iu, const int64_t *ii, const float *ue, int64_t ldue,
                   const float *ie, int64_t ldie, const float *dloss, float reg, int32_t *counts,
                   float *g_u, int64_t ldgu, float *g_i, int64_t ldgi, float scale,
-                  bbgr_stream_t stream);
+                  int32_t *counts_u_out, bbgr_stream_t stream);
+
+/* A row scatter in first-slot form (ABI 10): for every k < n with          */
+/* counts[k] > 0 (a leader: counts[k] valid slots k' have slot[k'] == k;    */
+/* bbgr_ego_slots' cu and bbgr_ego_rows' counts_u_out), dst[rows[k], :d] +=  */
+/* (0 + src[k] + src[k2] + ...) over k and those k' > k in ascending order.  */
+/* Bitwise bbgr_scatter_add_rows of the batch's rows (a stable sort's        */
+/* segment sums) when the slots of invalid triples (slot -1) hold zero rows, */
+/* without the sort (a batch of distinct users: one read per row).          */
+int bbgr_rows_add_slots(int64_t n, const int64_t *slot, const int32_t *counts,
+                        const int64_t *rows, const float *src, int64_t ldsrc, float *dst,
+                        int64_t lddst, int32_t d, int64_t n_dst, bbgr_stream_t stream);
 
 /* out[k] = rank[ids[k]] (rank NULL: ids[k]) for ids[k] in [0, n_rows), else */
 /* -1 (ABI 8): a caller's row ids as graph rows in one launch                */

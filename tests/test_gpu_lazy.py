@@ -364,3 +364,37 @@ def test_fused_backward_adam_master_copies_are_bitwise_the_caller_order_step():
                         [a._pair.io.user_map64, a._pair.io.item_map64])
     assert torch.equal(ug, a.user_emb.weight.detach()[a._pair.io.user_map64])
     assert torch.equal(ig, a.item_emb.weight.detach()[a._pair.io.item_map64])
+
+
+@pytest.mark.parametrize("order", ["degree", "input"])
+def test_fused_backward_user_scatter_without_the_sort(order, monkeypatch):
+    """bpr_adam_backward's user-row scatters (the BPR rows into gU, the ego
+    rows before the user Adam) in first-slot form (bbgr_rows_add_slots, no
+    sort) are bitwise the sorted scatter (BBGR_USER_SORT=1): weights and
+    moments over four steps with distinct users, a repeated user, and a
+    negative outside the table (an invalid triple) whose user recurs later in
+    the batch (the invalid slot then leads that user's rows)."""
+    from bbgr.optim import FusedAdam
+    monkeypatch.setattr(operators, "DROPIN_VERTEX_ORDER", order)
+    batches = [_batch(s) for s in range(4)]
+    batches[1][0][5] = batches[1][0][6]
+    batches[3][2][3] = -1
+    batches[3][0][9] = batches[3][0][3]
+    out = []
+    for sort in ("0", "1"):
+        monkeypatch.setenv("BBGR_USER_SORT", sort)
+        m = _model(3)
+        o = FusedAdam(m.parameters(), lr=1e-3, fuse_backward=True)
+        ls = []
+        for users, pos, neg in batches:
+            uf, itf = m.get_user_item_emb()
+            loss = m.bpr_loss(users, pos, neg, uf, itf, 1e-4)
+            o.zero_grad()
+            loss.backward()
+            o.step()
+            ls.append(float(loss))
+        out.append((ls, [p.detach().clone() for p in m.parameters()],
+                    [x.clone() for p in m.parameters() for x in o.moments(p)]))
+    assert out[0][0] == out[1][0]
+    for x, y in zip(out[0][1] + out[0][2], out[1][1] + out[1][2]):
+        assert torch.equal(x, y)

@@ -897,7 +897,7 @@ def test_ego_rows_kernel_is_the_atomic_formulation(B, U, I, d):
     for _ in range(2):   # the counts come back zero: reusable
         _lib.call("bbgr_ego_rows", B, d, P(out[3 * B:]), P(out[4 * B:]), P(out[5 * B:]), P(out),
                   P(out[B:]), P(ue), d, P(ie), d, P(dl), 1e-2, P(cnt), P(got), d, P(got[B:]), d,
-                  1.0, _lib.stream_handle())
+                  1.0, None, _lib.stream_handle())
         torch.cuda.synchronize()
         assert torch.equal(got[:B], want_u) and torch.equal(got[B:], want_i)
         assert int(cnt.abs().sum()) == 0
@@ -905,12 +905,66 @@ def test_ego_rows_kernel_is_the_atomic_formulation(B, U, I, d):
     for sc in (3.0, 4.0):
         _lib.call("bbgr_ego_rows", B, d, P(out[3 * B:]), P(out[4 * B:]), P(out[5 * B:]), P(out),
                   P(out[B:]), P(ue), d, P(ie), d, P(dl), 1e-2, P(cnt), P(got), d, P(got[B:]), d,
-                  sc, _lib.stream_handle())
+                  sc, None, _lib.stream_handle())
         torch.cuda.synchronize()
         assert torch.equal(got[:B], want_u * sc) and torch.equal(got[B:], want_i * sc)
         assert int(cnt.abs().sum()) == 0
     if B > 1000:   # the case really repeats rows
         assert int(torch.bincount(torch.cat([pos, neg])).max()) > 100
+
+
+@pytest.mark.parametrize("B,U,d,invalid_first", [(1, 3, 64, False), (8192, 5_000_000, 64, False),
+                                                 (8192, 50_000, 64, True), (4096, 50, 128, True),
+                                                 (300, 300, 256, True), (513, 7, 64, False)])
+def test_rows_add_slots_is_the_sorted_scatter(B, U, d, invalid_first):
+    """bbgr_rows_add_slots (first slots and counts from bbgr_ego_slots /
+    bbgr_ego_rows' counts_u_out) is bitwise bbgr_scatter_add_rows over the
+    clamped user ids when invalid triples carry zero rows: distinct users,
+    users repeated hundreds of times, invalid triples — also one holding the
+    first occurrence of a valid user's clamped id (its slot then leads)."""
+    from bbgr import _lib
+    from bbgr.scatter import index_add_rows
+    g = torch.Generator().manual_seed(B + U + d)
+    I = 40
+    users = torch.randint(0, U, (B,), generator=g) if U < 5_000_000 else torch.randperm(U, generator=g)[:B]
+    pos, neg = torch.randint(0, I, (B,), generator=g), torch.randint(0, I, (B,), generator=g)
+    if invalid_first:
+        users[0], users[1] = -1, 0     # clamp(-1) = 0: the invalid slot 0 leads user 0
+        users[5::11] = U + 3            # clamps to U - 1
+        neg[7::13] = I                 # an invalid item: the user's slot is invalid too
+    du, dp, dn = (x.to(DEV) for x in (users, pos, neg))
+    fu = torch.full((U,), 0x7fffffff, dtype=torch.int32, device=DEV)
+    fi = torch.full((I,), 0x7fffffff, dtype=torch.int32, device=DEV)
+    out = torch.empty(6 * B, dtype=torch.int64, device=DEV)
+    P, st = _lib.ptr, _lib.stream_handle()
+    _lib.call("bbgr_ego_slots", B, P(du), P(dp), P(dn), U, I, P(fu), P(fi), P(out), P(out[B:]),
+              P(out[3 * B:]), P(out[4 * B:]), P(out[5 * B:]), st)
+    iu, cu = out[:B], out[3 * B: 4 * B]
+    ue = torch.randn(U, d, generator=g).to(DEV) if U < 5_000_000 else \
+        torch.randn(U, d, device=DEV)
+    ie = torch.randn(I, d, device=DEV)
+    cnt = torch.zeros(3 * B, dtype=torch.int32, device=DEV)
+    cnt_u = torch.full((B,), -5, dtype=torch.int32, device=DEV)
+    ego = torch.empty(3 * B, d, device=DEV)
+    dl = torch.tensor(1.0, device=DEV)
+    _lib.call("bbgr_ego_rows", B, d, P(cu), P(out[4 * B:]), P(out[5 * B:]), P(iu), P(out[B:]),
+              P(ue), d, P(ie), d, P(dl), 1e-2, P(cnt), P(ego), d, P(ego[B:]), d, 1.0, P(cnt_u), st)
+    torch.cuda.synchronize()
+    valid = cu >= 0
+    # counts: the valid slots pointing at each slot
+    want_cnt = torch.bincount(cu[valid], minlength=B)[:B].to(torch.int32)
+    assert torch.equal(cnt_u, want_cnt)
+    src = torch.randn(B, d, generator=g).to(DEV) * valid[:, None].float()   # invalid: zero rows
+    for s in (src, ego[:B]):
+        base = torch.randn(U, d, generator=g).to(DEV) if U < 5_000_000 else \
+            torch.randn(U, d, device=DEV)
+        ref, got = base.clone(), base.clone()
+        index_add_rows(ref, iu, s)
+        _lib.call("bbgr_rows_add_slots", B, P(cu), P(cnt_u), P(iu), P(s), d, P(got), d, d, U, st)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+    if B > 1000 and U < 100:
+        assert int(want_cnt.max()) > 100
 
 
 @pytest.mark.parametrize("B,U,I", [(1, 3, 2), (8192, 5_000_000, 1_000_000), (4096, 50, 30),
