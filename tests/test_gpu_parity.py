@@ -963,8 +963,8 @@ def test_rows_add_slots_is_the_sorted_scatter(B, U, d, invalid_first):
         _lib.call("bbgr_rows_add_slots", B, P(cu), P(cnt_u), P(iu), P(s), d, P(got), d, d, U, st)
         torch.cuda.synchronize()
         assert torch.equal(got, ref)
-    if B > 1000 and U < 100:
-        assert int(want_cnt.max()) > 100
+    if B > 1000 and U < 100:   # the case really repeats users (about B / U times each)
+        assert int(want_cnt.max()) > 50
 
 
 @pytest.mark.parametrize("B,U,I", [(1, 3, 2), (8192, 5_000_000, 1_000_000), (4096, 50, 30),
