@@ -676,10 +676,15 @@ static bool dropin_bits_enabled() {
 // stream then issues its marking after this one's clear, so stream order keeps
 // each chain's bitmap, list and count its own. Only the host-side issue is
 // serialised; the GPU work of different streams still overlaps.
+// frontier_bits applies (its list then feeds the first item product)
+static bool listed_frontier(const Pair &P, int64_t d) {
+  return d >= 64 && dropin_bits_enabled() && P.fu.csr.nnz > 0;
+}
+
 static std::unique_lock<std::mutex> frontier_bits(const Pair &P, Support &s, const Tensor &ui,
                                                   int64_t d) {
   std::unique_lock<std::mutex> g(P.fb_mu, std::defer_lock);
-  if (d < 64 || !dropin_bits_enabled() || P.fu.csr.nnz == 0) return g;
+  if (!listed_frontier(P, d)) return g;
   const Tensor &slots = u2i_slots(P, ui.device());
   const int64_t nbits = P.bi.csr.nnz / 32 + 4;
   const auto i32 = at::TensorOptions().dtype(at::kInt).device(ui.device());
@@ -690,7 +695,11 @@ static std::unique_lock<std::mutex> frontier_bits(const Pair &P, Support &s, con
   }
   if (!b->bits.defined()) b->bits = at::zeros({nbits}, i32);
   const Tensor &mi = s.si_int.defined() ? s.si_int : s.si;
-  mask_list(mi, b->list, b->count, b->ws);
+  if (!s.flist.defined()) {   // (rows_backward's list_marks listed it while marking)
+    mask_list(mi, b->list, b->count, b->ws);
+    s.flist = b->list;
+    s.fcount = b->count;
+  }
   // the packed item mask (every word rewritten per call: nothing to clear;
   // BBGR_MASK_BITS=0 keeps the byte test, A/B)
   const char *mb_env = std::getenv("BBGR_MASK_BITS");
@@ -702,8 +711,6 @@ static std::unique_lock<std::mutex> frontier_bits(const Pair &P, Support &s, con
           "bbgr_mask_pack");
     s.si_bits = b->mbits;
   }
-  s.flist = b->list;
-  s.fcount = b->count;
   s.bits = b->bits;
   check(bbgr_mark_slots(ui.numel(), ui.data_ptr<int64_t>(), P.fu.csr.indptr,
                         slots.data_ptr<int32_t>(),
@@ -1126,14 +1133,24 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
   } else {
     index_add_rows(gU, ru, vu.contiguous());
   }
-  // mu (and mi when it is marked from the list) zeroed by one fill
-  ZeroArena za(vu, {U, gi_rows ? I : 0});
+  // input-order pair, GS, gI as rows, the first item product on a row list:
+  // the item frontier is marked in the graph's order straight from the batch
+  // items and N(batch users), and listed while it is marked (bbgr_mark_list:
+  // no mask scan, no input-order mask to permute); the list's order is
+  // unspecified and the product's rows are independent of it (bitwise)
+  const bool list_marks = P->io && gs && gi_rows && K >= 1 && iu.numel() > 0 &&
+                          listed_frontier(*P, d);
+  // mu (and mi when it is marked from the list; the graph-order item mask and
+  // the list's count when list_marks) zeroed by one fill
+  ZeroArena za(vu, {U, gi_rows && !list_marks ? I : 0, list_marks ? I : 0, list_marks ? 8 : 0});
   Tensor mu = za.bytes(0);
   Tensor mi = gi_rows ? za.bytes(1) : at::empty({std::max<int64_t>(I, 1)}, u8(vu)).narrow(0, 0, I);
   check(bbgr_mark_rows(ru.numel(), ru.data_ptr<int64_t>(), 1, mu.data_ptr<uint8_t>(), U,
                        cur_stream()),
         "bbgr_mark_rows");
-  if (gi_rows) {
+  if (list_marks) {
+    // (nothing reads the input-order item mask on this path)
+  } else if (gi_rows) {
     check(bbgr_mark_rows(ii.numel(), ii.data_ptr<int64_t>(), 1, mi.data_ptr<uint8_t>(), I,
                          cur_stream()),
           "bbgr_mark_rows");
@@ -1144,7 +1161,26 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
   }
   g_rows_backward++;
   Support s;
-  if (P->io) {
+  if (list_marks) {
+    Tensor mi_int = za.bytes(2);
+    Tensor cnt = za.bytes(3).view(at::kLong);
+    Tensor list = at::empty({std::max<int64_t>(I, 1)}, iu.options());
+    Tensor ii_int = to_graph_rows(ii, I, P->item_rank64);
+    Tensor ui = P->user_rank64.index_select(0, iu).contiguous();
+    const bbgr_csr &uc = P->fu.csr;
+    check(bbgr_mark_list(ii_int.numel(), ii_int.data_ptr<int64_t>(), nullptr, nullptr,
+                         mi_int.data_ptr<uint8_t>(), I, list.data_ptr<int64_t>(),
+                         cnt.data_ptr<int64_t>(), cur_stream()),
+          "bbgr_mark_list");
+    check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), uc.indptr, uc.indices,
+                         mi_int.data_ptr<uint8_t>(), I, list.data_ptr<int64_t>(),
+                         cnt.data_ptr<int64_t>(), cur_stream()),
+          "bbgr_mark_list");
+    s = Support{mu.narrow(0, 0, U), mi_int.index_select(0, P->item_rank64), mi_int};
+    s.flist = list;
+    s.fcount = cnt;
+    s.gu_internal = gu_int;
+  } else if (P->io) {
     s = io_support(*P, mu.narrow(0, 0, U), mi.narrow(0, 0, I), gs, iu);
     s.gu_internal = gu_int;
   } else {

@@ -1220,7 +1220,7 @@ extern "C" int bbgr_mask_pack(int64_t n, const uint8_t *mask, uint32_t *bits,
   return BBGR_OK;
 }
 
-static int batch_params(const bbgr_batch_args *a, BatchParams &P, const char *who) {
+static int batch_params(const bbgr_batch_args *a, BatchParams &P) {
   BBGR_REQUIRE(a && a->batch >= 0 && a->n_users > 0 && a->n_items > 0, "bbgr_batch: bad sizes");
   BBGR_REQUIRE(a->batch == 0 || (a->users && a->pos && a->neg && a->mask_u && a->mask_i),
                "bbgr_batch: null arrays");
@@ -1234,7 +1234,6 @@ static int batch_params(const bbgr_batch_args *a, BatchParams &P, const char *wh
     BBGR_REQUIRE(!t || aligned16(t), "bbgr_batch: gradient tables must be 16-byte aligned");
   BBGR_REQUIRE((a->ld_gu & 3) == 0 && (a->ld_gi & 3) == 0 && (a->ld_side & 3) == 0,
                "bbgr_batch: ld % 4 == 0");
-  (void)who;
   P.B = a->batch;
   P.U = a->n_users;
   P.I = a->n_items;
@@ -1261,7 +1260,7 @@ static int batch_params(const bbgr_batch_args *a, BatchParams &P, const char *wh
 
 extern "C" int bbgr_batch_begin(const bbgr_batch_args *a, bbgr_stream_t stream) {
   BatchParams P;
-  if (int rc = batch_params(a, P, "bbgr_batch_begin")) return rc;
+  if (int rc = batch_params(a, P)) return rc;
   if (P.B == 0) return BBGR_OK;
   hipLaunchKernelGGL(batch_begin_kernel, dim3((unsigned)((P.B + 15) / 16)), dim3(256), 0,
                      as_stream(stream), P);
@@ -1271,10 +1270,11 @@ extern "C" int bbgr_batch_begin(const bbgr_batch_args *a, bbgr_stream_t stream) 
 
 extern "C" int bbgr_batch_end(const bbgr_batch_args *a, bbgr_stream_t stream) {
   BatchParams P;
-  if (int rc = batch_params(a, P, "bbgr_batch_end")) return rc;
+  if (int rc = batch_params(a, P)) return rc;
   if (P.B == 0 && !P.count) return BBGR_OK;
-  hipLaunchKernelGGL(batch_end_kernel, dim3((unsigned)((P.B + 15) / 16 > 0 ? (P.B + 15) / 16 : 1)),
-                     dim3(256), 0, as_stream(stream), P);
+  const long blocks = P.B > 0 ? (P.B + 15) / 16 : 1;   // (B == 0: the count reset alone)
+  hipLaunchKernelGGL(batch_end_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     P);
   BBGR_LAUNCHED("batch_end_kernel");
   return BBGR_OK;
 }
