@@ -1138,8 +1138,7 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
   // items and N(batch users), and listed while it is marked (bbgr_mark_list:
   // no mask scan, no input-order mask to permute); the list's order is
   // unspecified and the product's rows are independent of it (bitwise)
-  const bool list_marks = P->io && gs && gi_rows && K >= 1 && iu.numel() > 0 &&
-                          listed_frontier(*P, d);
+  const bool list_marks = gu_int && gs && gi_rows && iu.numel() > 0 && listed_frontier(*P, d);
   // mu (and mi when it is marked from the list; the graph-order item mask and
   // the list's count when list_marks) zeroed by one fill
   ZeroArena za(vu, {U, gi_rows && !list_marks ? I : 0, list_marks ? I : 0, list_marks ? 8 : 0});
@@ -1166,7 +1165,7 @@ static std::tuple<Tensor, Tensor> rows_backward(const std::shared_ptr<Pair> &P, 
     Tensor cnt = za.bytes(3).view(at::kLong);
     Tensor list = at::empty({std::max<int64_t>(I, 1)}, iu.options());
     Tensor ii_int = to_graph_rows(ii, I, P->item_rank64);
-    Tensor ui = P->user_rank64.index_select(0, iu).contiguous();
+    const Tensor &ui = ru;   // (gu_int here: the batch users' graph rows)
     const bbgr_csr &uc = P->fu.csr;
     check(bbgr_mark_list(ii_int.numel(), ii_int.data_ptr<int64_t>(), nullptr, nullptr,
                          mi_int.data_ptr<uint8_t>(), I, list.data_ptr<int64_t>(),
