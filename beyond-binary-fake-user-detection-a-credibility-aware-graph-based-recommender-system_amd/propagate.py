@@ -683,9 +683,9 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
     `tagged` (GS): the user CSR's column indices tagged with grad_support's
     item mask (forward_steps(tag=...)): the first user product reads the item
     support from them instead of loading the mask per edge (bitwise).
-    `item_mask_bits` (GS): grad_support's item mask packed one bit per item
+    `item_mask_bits`: grad_support's item mask packed one bit per item
     (bbgr_mask_pack): the first user product tests its edges on the bits
-    instead of the bytes (bitwise)."""
+    instead of the bytes (bitwise; GS and Jacobi, graph-ordered sources)."""
     U, I = pair.num_users, pair.num_items
     d = gU.shape[1]
     _check_table("user grad", gU, U, d)
@@ -774,10 +774,11 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
             mu_ = si if first else None     # BU reads gI (items), BI reads gU (users)
             mi_ = su if first else None
             src_in = inp and first           # gI / gU: input order
+            mb = item_mask_bits if (first and mu_ is not None and not src_in) else None
             if k > 1:
                 spmm(BU, xu, first, y=bufU[nxt], y_scale=pair.feed_bwd_ui, y_scale_s=ys,
                      add=gU, add_mask=su, add_scale=BI.in_scale, add_scale_s=gl, src_mask=mu_,
-                     add_map=um, src_input=src_in)
+                     add_map=um, src_input=src_in, src_mask_bits=mb)
                 _item_product(BI, xi, first, reduce, new, y=bufI[nxt],
                               y_scale=pair.feed_bwd_iu, y_scale_s=ys,
                               add=gI, add_mask=si, add_scale=BU.in_scale, add_scale_s=gl,
@@ -789,7 +790,8 @@ def backward_steps(pair: OperatorPair, gU: torch.Tensor, gI: torch.Tensor, num_l
                     before_last()
                 spmm(BU, xu, first, y=None if adam_u is not None else gu0, y_scale=BU.out_scale,
                      y_scale_s=ys, add=gU, add_mask=su, add_scale=None, add_scale_s=gl,
-                     src_mask=mu_, adam=adam_u, add_map=um, y_map=um, src_input=src_in)
+                     src_mask=mu_, adam=adam_u, add_map=um, y_map=um, src_input=src_in,
+                     src_mask_bits=mb)
                 ik = dict(y=None if adam_i is not None else gi0, y_scale=BI.out_scale,
                           y_scale_s=ys, add=gI, add_mask=si, add_scale=None, add_scale_s=gl,
                           src_mask=mi_, add_map=im, y_map=im, src_input=src_in,

@@ -164,12 +164,12 @@ class FusedTrainer:
         if (self.frontier and order == ORDER_GS and num_layers >= 2 and emb_dim >= 64
                 and uc.nnz <= 24 * uc.n_rows and os.environ.get("BBGR_TAGGED", "0") == "1"):
             self.tagged = torch.empty(max(uc.nnz, 1), dtype=torch.int32, device=dev)
-        # GS frontier: the item mask also packed one bit per item after the
+        # Frontier: the item mask also packed one bit per item after the
         # marking (bbgr_mask_pack) for the first backward user product's
         # per-edge test (bbgr_spmm_args.src_mask_bits; bitwise the byte test;
         # BBGR_MASK_BITS=0 keeps the bytes for A/B)
         self.mask_i_bits = None
-        if (self.frontier and order == ORDER_GS and num_layers >= 1
+        if (self.frontier and num_layers >= 1
                 and os.environ.get("BBGR_MASK_BITS", "1") != "0"):
             self.mask_i_bits = torch.zeros(self.I // 32 + 1, dtype=torch.int32, device=dev)
         self.item_list = self.item_count = self.item_len = None
@@ -413,7 +413,7 @@ class FusedTrainer:
 
         backward(self.pair, self.g_uf, self.g_if, self.K, self.order, ws=self.ws,
                  grad_support=masks, adam_u=adam_u, adam_i=adam_i, before_last=before_last,
-                 src_bits=self._bits(masks))
+                 src_bits=self._bits(masks), item_mask_bits=self._mask_bits(masks))
 
     def _set_masks(self, users, pos, neg, value: int):
         """mask_u = batch users; mask_i = batch items (+ N(batch users) for GS,

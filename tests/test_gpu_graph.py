@@ -264,18 +264,20 @@ def test_fused_batch_bookkeeping_graph_replay():
     assert int(a.item_count.abs().sum()) == 0 and int(a.mask_i.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("fuse,K", [(True, 3), (False, 3), (True, 2), (True, 1)])
-def test_packed_item_mask_step_is_bitwise_the_byte_mask_step(fuse, K, monkeypatch):
-    """GS frontier: the first backward user product tests its edges on the
-    item mask packed one bit per item (bbgr_mask_pack + src_mask_bits) —
-    losses, weights and moments equal the byte-mask step's bit for bit
-    (BBGR_MASK_BITS=0), through graph capture too."""
+@pytest.mark.parametrize("variant,fuse,K", [("v2_pop", True, 3), ("v2_pop", False, 3),
+                                            ("v2_pop", True, 2), ("v2_pop", True, 1),
+                                            ("cu_fair", True, 3), ("cu_fair", False, 2)])
+def test_packed_item_mask_step_is_bitwise_the_byte_mask_step(variant, fuse, K, monkeypatch):
+    """Frontier (GS and Jacobi): the first backward user product tests its
+    edges on the item mask packed one bit per item (bbgr_mask_pack +
+    src_mask_bits) — losses, weights and moments equal the byte-mask step's
+    bit for bit (BBGR_MASK_BITS=0), through graph capture too."""
     e, g = _graph()
     kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=64, num_layers=K, batch_size=256,
               frontier=True, fuse_adam=fuse, seed=17)
-    a = FusedTrainer(g, "v2_pop", **kw)
+    a = FusedTrainer(g, variant, **kw)
     monkeypatch.setenv("BBGR_MASK_BITS", "0")
-    b = FusedTrainer(g, "v2_pop", **kw)
+    b = FusedTrainer(g, variant, **kw)
     assert a.mask_i_bits is not None and b.mask_i_bits is None
     for _ in range(4):
         assert float(a.step()) == float(b.step())
