@@ -709,11 +709,7 @@ extern "C" int bbgr_shuffle(int64_t n, const int64_t *in, int64_t *out,
   }
   if (n == 0) return BBGR_OK;
   BBGR_REQUIRE(in && out, "bbgr_shuffle: null arrays");
-  static const bool small_ok = [] {   // BBGR_SHUFFLE_SMALL=0: the radix path always (A/B)
-    const char *e = std::getenv("BBGR_SHUFFLE_SMALL");
-    return !(e && e[0] == '0');
-  }();
-  if (n <= SHUFFLE_SMALL && small_ok) {   // (the workspace stays unused)
+  if (n <= SHUFFLE_SMALL) {   // (the workspace stays unused)
     hipLaunchKernelGGL(shuffle_small_kernel, dim3(1), dim3(1024), 0, st, (int)n,
                        (unsigned long long)seed, (unsigned long long)counter, (const long *)in,
                        (long *)out);
