@@ -251,43 +251,16 @@ __global__ void sample_kernel(long batch, const long *users, const int *indptr,
   if (fail_count) atomicAdd(fail_count, 1);
 }
 
-__device__ __forceinline__ unsigned long long shuffle_key(long i, unsigned long long seed,
-                                                          unsigned long long counter) {
-  const u32x4 r = philox4x32_10(
-      u32x4{(uint32_t)i, (uint32_t)((unsigned long long)i >> 32), (uint32_t)counter,
-            (uint32_t)(counter >> 32)},
-      (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x5bd1e995u);
-  return ((unsigned long long)r.x << 32) | r.y;
-}
-
 __global__ void shuffle_keys_kernel(long n, unsigned long long seed,
                                     unsigned long long counter,
                                     unsigned long long *keys) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  keys[i] = shuffle_key(i, seed, counter);
-}
-
-// n <= SHUFFLE_SMALL: the keys in LDS and every element's rank by (key,
-// index) counted in one workgroup — the order of the stable radix sort by
-// key, in one launch instead of the keys kernel and the sort's passes (an
-// epoch of a small graph is a step or two: C1 reshuffles every step).
-constexpr int SHUFFLE_SMALL = 2048;
-__global__ __launch_bounds__(1024) void shuffle_small_kernel(int n, unsigned long long seed,
-                                                             unsigned long long counter,
-                                                             const long *in, long *out) {
-  __shared__ unsigned long long k[SHUFFLE_SMALL];
-  for (int i = threadIdx.x; i < n; i += blockDim.x) k[i] = shuffle_key(i, seed, counter);
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const unsigned long long ki = k[i];
-    int r = 0;
-    for (int j = 0; j < n; ++j) {
-      const unsigned long long kj = k[j];
-      r += (kj < ki) | ((kj == ki) & (j < i));
-    }
-    out[r] = in[i];
-  }
+  const u32x4 r = philox4x32_10(
+      u32x4{(uint32_t)i, (uint32_t)((unsigned long long)i >> 32), (uint32_t)counter,
+            (uint32_t)(counter >> 32)},
+      (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x5bd1e995u);
+  keys[i] = ((unsigned long long)r.x << 32) | r.y;
 }
 
 __global__ void gather_scale_kernel(long nnz, const int *indices, const float *scale,
@@ -709,13 +682,6 @@ extern "C" int bbgr_shuffle(int64_t n, const int64_t *in, int64_t *out,
   }
   if (n == 0) return BBGR_OK;
   BBGR_REQUIRE(in && out, "bbgr_shuffle: null arrays");
-  if (n <= SHUFFLE_SMALL) {   // (the workspace stays unused)
-    hipLaunchKernelGGL(shuffle_small_kernel, dim3(1), dim3(1024), 0, st, (int)n,
-                       (unsigned long long)seed, (unsigned long long)counter, (const long *)in,
-                       (long *)out);
-    BBGR_LAUNCHED("shuffle_small_kernel");
-    return BBGR_OK;
-  }
   char *ws = (char *)workspace;
   auto *k1 = (unsigned long long *)ws;
   auto *k2 = (unsigned long long *)(ws + a);

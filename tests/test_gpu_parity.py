@@ -508,21 +508,6 @@ def test_shuffle_and_nonempty_rows():
     assert torch.equal(p1, shuffle(v, 42, 1)) and not torch.equal(p1, shuffle(v, 42, 2))
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 943, 1024, 1025, 2048])
-def test_small_shuffle_is_the_radix_sort_order(n):
-    """bbgr_shuffle below 2049 elements ranks (key, index) in one workgroup;
-    above, hipcub's stable radix sort orders by key. Element i's key depends
-    on (i, seed, counter) only, so the small permutation of arange(n) is the
-    large one of arange(4096) restricted to the values below n."""
-    from bbgr.sampler import shuffle
-    for seed, counter in ((42, 1), (7, 123456789)):
-        big = shuffle(torch.arange(4096, device=DEV), seed, counter)
-        small = shuffle(torch.arange(n, device=DEV), seed, counter)
-        assert torch.equal(small, big[big < n])
-        vals = torch.randperm(n, device=DEV) * 3 + 11   # values carried, not ranked
-        assert torch.equal(shuffle(vals, seed, counter), vals[small])
-
-
 # ---------------------------------------------------------------------------
 # Fused training step vs the float64 oracle step on identical triples
 # ---------------------------------------------------------------------------
