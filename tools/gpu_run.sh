@@ -183,7 +183,8 @@ for step in "$@"; do
         for c in ${BCONFIGS:-C4}; do
           for f in ${ENVAB_VALUES:-1 0}; do
             o="$O/${c,,}_${ENVAB}_${f}_$rep"
-            env "$ENVAB=$f" timeout -k 10 400 python -u bench.py --config $c $quick_args \
+            extra=""; [ $c = C1 ] && extra="--variant plain"
+            env "$ENVAB=$f" timeout -k 10 400 python -u bench.py --config $c $extra $quick_args \
               --steps 30 --warmup 3 > "$o.json" 2> "$o.log"
             rc=$?; hard $rc "envab $c $f" "$o.log"
             [ $rc -eq 0 ] || { tail -20 "$o.log"; exit 1; }
