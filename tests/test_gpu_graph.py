@@ -10,6 +10,8 @@
   workspace are zero again after every launch, and results are bitwise
   stable across launches.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -287,3 +289,77 @@ def test_packed_item_mask_step_is_bitwise_the_byte_mask_step(variant, fuse, K, m
         for _ in range(3):
             assert float(gs.step()) == float(b.step())
         _assert_same(a, b)
+
+
+def test_batch_begin_end_kernels_direct():
+    """bbgr_batch_begin / bbgr_batch_end through the C ABI: the masks, the
+    frontier list (each flagged item once), the slot bits and the sparse
+    gradient rows' reset, with repeated users, ids outside the tables
+    (skipped: -1, U, I) and an empty batch; everything zero again after."""
+    from bbgr import _lib
+    from bbgr._lib import ptr
+    e, g = _graph()
+    U, I, d = g.num_users, g.num_items, 64
+    uc = g.user_csr
+    slot_map = g.user_item_slots()
+    users = torch.tensor([5, 5, 17, -1, U, 0, 2999, 17], dtype=torch.int64, device=DEV)
+    pos = torch.tensor([1, 1, 3, 4, 5, I, -1, 7], dtype=torch.int64, device=DEV)
+    neg = torch.tensor([2, 9, 3, 4, 6, 8, 1199, -1], dtype=torch.int64, device=DEV)
+    B = users.numel()
+    posneg = torch.cat([pos, neg])
+    mask_u = _lib.byte_mask(U, DEV)
+    mask_i = _lib.byte_mask(I, DEV)
+    lst = torch.full((I,), -7, dtype=torch.int64, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    bits = torch.zeros(uc.nnz // 32 + 4, dtype=torch.int32, device=DEV)
+    gu = torch.zeros(U, d, device=DEV)
+    gi = torch.zeros(I, d, device=DEV)
+    gs = torch.zeros(I, d, device=DEV)
+    a = _lib.BatchArgs()
+    a.batch, a.users, a.pos, a.neg = B, ptr(users), ptr(posneg), ptr(posneg) + 8 * B
+    a.n_users, a.n_items = U, I
+    a.user_indptr, a.user_indices = ptr(uc.indptr), ptr(uc.indices)
+    a.mask_u, a.mask_i, a.list, a.count = ptr(mask_u), ptr(mask_i), ptr(lst), ptr(cnt)
+    a.slot_map, a.slot_bits = ptr(slot_map), ptr(bits)
+    a.g_u, a.g_i, a.g_side = ptr(gu), ptr(gi), ptr(gs)
+    a.ld_gu = a.ld_gi = a.ld_side = d
+    a.d = d
+    _lib.call("bbgr_batch_begin", ctypes.byref(a), _lib.stream_handle())
+    torch.cuda.synchronize()
+    ok_u = users[(users >= 0) & (users < U)]
+    want_u = torch.zeros(U, dtype=torch.uint8, device=DEV)
+    want_u[ok_u] = 1
+    assert torch.equal(mask_u[:U], want_u)
+    ip = uc.indptr.long()
+    want_i = torch.zeros(I, dtype=torch.uint8, device=DEV)
+    items = posneg[(posneg >= 0) & (posneg < I)]
+    want_i[items] = 1
+    slots = []
+    for u in ok_u.unique().tolist():
+        cols = uc.indices[ip[u]: ip[u + 1]].long()
+        want_i[cols] = 1
+        slots.append(slot_map[ip[u]: ip[u + 1]].long())
+    assert torch.equal(mask_i[:I], want_i)
+    n = int(cnt.item())
+    listed = lst[:n]
+    assert n == int(want_i.sum()) and listed.unique().numel() == n
+    assert bool((want_i[listed] == 1).all())
+    want_bits = torch.zeros(bits.numel() * 32, dtype=torch.bool, device=DEV)
+    want_bits[torch.cat(slots)] = True
+    got_bits = ((bits.view(-1, 1).long() & 0xFFFFFFFF) >> torch.arange(32, device=DEV)) & 1
+    assert torch.equal(got_bits.view(-1).bool(), want_bits)
+    # the step's sparse gradient rows, then the end restores every table
+    gu[ok_u] = 1.0
+    gi[items] = 2.0
+    gs[items] = 3.0
+    _lib.call("bbgr_batch_end", ctypes.byref(a), _lib.stream_handle())
+    torch.cuda.synchronize()
+    for t in (mask_u, mask_i, bits, cnt, gu, gi, gs):
+        assert float(t.abs().sum()) == 0.0
+    # an empty batch: no launch but the count reset
+    cnt.fill_(5)
+    a.batch = 0
+    _lib.call("bbgr_batch_begin", ctypes.byref(a), _lib.stream_handle())
+    _lib.call("bbgr_batch_end", ctypes.byref(a), _lib.stream_handle())
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 0 and float(mask_i.abs().sum()) == 0.0
