@@ -168,14 +168,21 @@ class RcclItemComm:
         self.inline = bool(inline)
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         ids = (ctypes.c_uint8 * 128)()
-        if rank == 0:
-            call("bbgr_comm_unique_id", ids)
-        t = torch.tensor(list(ids), dtype=torch.uint8)
+        err = None
+        if rank == 0:   # (a failure here travels with the id: no rank waits on it)
+            try:
+                call("bbgr_comm_unique_id", ids)
+            except RuntimeError as ex:
+                err = ex
+        t = torch.tensor([0 if err is None else 1] + list(ids), dtype=torch.uint8)
         if dist.get_backend(group) == "nccl":
             t = t.to(device)
         src = 0 if group is None else dist.get_global_rank(group, 0)
         dist.broadcast(t, src=src, group=group)
-        ids = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+        t = t.cpu().tolist()
+        if t[0] != 0:
+            raise RuntimeError(f"RcclItemComm: no RCCL unique id on rank 0 ({err})")
+        ids = (ctypes.c_uint8 * 128)(*t[1:])
         self.comm = ctypes.c_void_p()
         call("bbgr_comm_init", ctypes.byref(self.comm), world, rank, ids)
         self.stream = torch.cuda.Stream(device=device, priority=-1)
