@@ -310,7 +310,11 @@ __device__ __forceinline__ unsigned long long slot_bits64(const unsigned *bits, 
 // product 0.111 -> 0.106 ms. The plain src-masked kernels do not use it: there
 // 41 % of the edges are live, and the permute's latency in every batch's
 // dependent chain (index -> mask -> permute -> gather) cost more than the
-// idle slots (masked user product 0.913 -> 0.98-0.99 ms, round 4 A/B).
+// idle slots (masked user product 0.913 -> 0.98-0.99 ms, round 4 A/B, on a
+// build that spilled). They walk the ballot's live-lane bit set instead
+// (kPairCompact / kRowCompact: a find-first-bit per pick, no permute): C4
+// src-masked user product 0.90 -> 0.88 ms, C3 (d = 128) 1.437 -> 1.347 ms
+// (profiles/round6/r6ae_compact_walk_ab.txt).
 // The skipped edges would each add +0.0 to a sum that started at +0.0 and so
 // is never -0.0: s + 0.0 == s, results are unchanged bit for bit.
 // ds_permute (forward permute) sends every lane's pair to its rank among the
@@ -330,6 +334,11 @@ __device__ __forceinline__ int compact_live(int &my, float &mw) {
   if (WMODE != 0) mw = __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(mw)));
   return nlive;
 }
+
+#ifndef BBGR_ROW_COMPACT
+#define BBGR_ROW_COMPACT 1
+#endif
+constexpr bool kRowCompact = BBGR_ROW_COMPACT != 0;
 
 // Sum w_e * x[col_e] over edges [eb, ee) into acc (one 16-lane group).
 template <int D, int WMODE, bool MASKED, bool BITS = false, int TAG = TAG_NONE>
@@ -367,17 +376,32 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
     }
     int tm = 0;
     if constexpr (TAG == TAG_WRITE) tm = tag_of(P, my);
+    // src-masked batches walk their live lanes' bit set as gather_pair does
+    // (kRowCompact): ceil(live / U) load rounds, no permute in the chain
+    unsigned rem = 0u;
+    if constexpr (MASKED && !BITS && kRowCompact) rem = n >= 16 ? 0xffffu : (1u << n) - 1u;
     if constexpr (MASKED && BITS) {   // live edges first (sparse: ~1 of 16 live)
       n = compact_live<WMODE>(my, mw);
     } else if (MASKED && (TAG == TAG_READ || P.src_mask)) {   // skip 16-edge batches with no live source (group-uniform)
       const unsigned long long lv = __ballot(my >= 0);
-      if (((lv >> (threadIdx.x & 48)) & 0xffffull) == 0) continue;
+      const unsigned lm = (unsigned)((lv >> (threadIdx.x & 48)) & 0xffffull);
+      if (lm == 0) continue;
+      if constexpr (kRowCompact) {
+        rem = lm;
+        n = __popc(lm);
+      }
     }
     for (int j0 = 0; j0 < n; j0 += U) {
       float4 v[U][V];
+      int sl[U];   // the lanes of this round's edges
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        const int c = __shfl(my, j0 + j, 16);
+        sl[j] = j0 + j;
+        if constexpr (MASKED && !BITS && kRowCompact) {
+          sl[j] = __builtin_ctz(rem | 0x10000u);   // (16: past the set, never read)
+          rem &= rem - 1u;
+        }
+        const int c = __shfl(my, sl[j], 16);
         if (j0 + j < n && (!MASKED || c >= 0)) {
           const float4 *src =
               reinterpret_cast<const float4 *>(P.x + (long)c * P.ldx) + lane;
@@ -399,7 +423,7 @@ __device__ __forceinline__ void gather_range(const SpmmParams &P, int eb, int ee
 #pragma unroll
           for (int k = 0; k < V; ++k) acc[k] = f4_add(acc[k], v[j][k]);
         } else {
-          const float w = __shfl(mw, j0 + j, 16);
+          const float w = __shfl(mw, sl[j], 16);
 #pragma unroll
           for (int k = 0; k < V; ++k) acc[k] = f4_fma(w, v[j][k], acc[k]);
         }
@@ -537,6 +561,11 @@ __device__ __forceinline__ void gather_row(const SpmmParams &P, int eb, int ee, 
 // for the same registers. Per row the operation sequence is gather_range's
 // (edges in CSR order from zero; dead batches skipped), so results match the
 // one-row path bitwise (up to the sign of an exact zero).
+#ifndef BBGR_PAIR_COMPACT
+#define BBGR_PAIR_COMPACT 1
+#endif
+constexpr bool kPairCompact = BBGR_PAIR_COMPACT != 0;
+
 template <int D, int WMODE, bool MASKED, int TAG = TAG_NONE>
 __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int eeA, int ebB,
                                             int eeB, int lane, float4 (&accA)[D / 64],
@@ -570,18 +599,44 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
       tmA = tag_of(P, myA);
       tmB = tag_of(P, myB);
     }
+    // compacted masked batches: the live edges' lanes as a bit set per row,
+    // walked lowest bit first (CSR order), so a batch takes ceil(live / U)
+    // load rounds instead of ceil(n / U) mostly idle ones; unmasked batches
+    // walk their first n lanes. No permute in the chain (the set is the
+    // ballot's; the pick is one find-first-bit), and the skipped edges would
+    // add +0.0 to a sum that is never -0.0: bitwise the uncompacted walk.
+    unsigned remA = 0u, remB = 0u;
+    if constexpr (MASKED && kPairCompact) {
+      remA = na >= 16 ? 0xffffu : na > 0 ? (1u << na) - 1u : 0u;
+      remB = nb >= 16 ? 0xffffu : nb > 0 ? (1u << nb) - 1u : 0u;
+    }
     if (MASKED && (TAG == TAG_READ || P.src_mask)) {   // a batch with no live source adds nothing
       const unsigned long long la = __ballot(myA >= 0), lb = __ballot(myB >= 0);
-      if (((la >> (threadIdx.x & 48)) & 0xffffull) == 0) na = 0;
-      if (((lb >> (threadIdx.x & 48)) & 0xffffull) == 0) nb = 0;
+      if constexpr (kPairCompact) {
+        remA = (unsigned)((la >> (threadIdx.x & 48)) & 0xffffull);
+        remB = (unsigned)((lb >> (threadIdx.x & 48)) & 0xffffull);
+        na = __popc(remA);
+        nb = __popc(remB);
+      } else {
+        if (((la >> (threadIdx.x & 48)) & 0xffffull) == 0) na = 0;
+        if (((lb >> (threadIdx.x & 48)) & 0xffffull) == 0) nb = 0;
+      }
     }
     const int nn = max(na, nb);
     for (int j0 = 0; j0 < nn; j0 += U) {
       float4 vA[U][V], vB[U][V];
+      int sA[U], sB[U];   // the lanes of this round's edges
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        const int cA = __shfl(myA, j0 + j, 16);
-        const int cB = __shfl(myB, j0 + j, 16);
+        sA[j] = sB[j] = j0 + j;
+        if constexpr (MASKED && kPairCompact) {
+          sA[j] = __builtin_ctz(remA | 0x10000u);   // (16: past the set, never read)
+          sB[j] = __builtin_ctz(remB | 0x10000u);
+          remA &= remA - 1u;
+          remB &= remB - 1u;
+        }
+        const int cA = __shfl(myA, sA[j], 16);
+        const int cB = __shfl(myB, sB[j], 16);
         if (j0 + j < na && (!MASKED || cA >= 0)) {
           const float4 *src = reinterpret_cast<const float4 *>(P.x + (long)cA * P.ldx) + lane;
           if (cA >= P.nt_from) {
@@ -618,8 +673,8 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
             accB[k] = f4_add(accB[k], vB[j][k]);
           }
         } else {
-          const float wA = __shfl(mwA, j0 + j, 16);
-          const float wB = __shfl(mwB, j0 + j, 16);
+          const float wA = __shfl(mwA, sA[j], 16);
+          const float wB = __shfl(mwB, sB[j], 16);
 #pragma unroll
           for (int k = 0; k < V; ++k) {
             accA[k] = f4_fma(wA, vA[j][k], accA[k]);

@@ -192,6 +192,30 @@ for step in "$@"; do
           done
         done
       done ;;
+    libab)     # A/B of libbbgr.so builds (tools/probes/build_variant.sh <tag>): LIBAB_VARIANTS
+               # ("a b"), each first through LIBAB_TESTS (pytest -k), then two interleaved
+               # rounds of quick benches at BCONFIGS
+      L=beyond-binary-fake-user-detection-a-credibility-aware-graph-based-recommender-system_amd/lib/ab
+      for v in $LIBAB_VARIANTS; do
+        BBGR_LIB=$PWD/$L/$v/libbbgr.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+          -k "${LIBAB_TESTS:-src_mask}" --timeout 300 --timeout-method thread > "$O/tests_$v.log" 2>&1
+        rc=$?; hard $rc "libab tests $v" "$O/tests_$v.log"
+        echo "tests $v: $(tail -1 "$O/tests_$v.log")"; [ $rc -eq 0 ] || exit 1
+      done
+      for rep in 1 2; do
+        for c in ${BCONFIGS:-C4}; do
+          for v in $LIBAB_VARIANTS; do
+            o="$O/${c,,}_${v}_$rep"
+            extra=""; case $c in C1) extra="--variant plain";; C3) extra="--variant cu_fair";; esac
+            BBGR_LIB=$PWD/$L/$v/libbbgr.so timeout -k 10 400 python -u bench.py --config $c $extra \
+              $quick_args --steps 30 --warmup 3 > "$o.json" 2> "$o.log"
+            rc=$?; hard $rc "libab $c $v" "$o.log"
+            [ $rc -eq 0 ] || { tail -20 "$o.log"; exit 1; }
+            echo "$c $v #$rep: $(python tools/bench_brief.py "$o.json" | head -1)"
+            python tools/bench_brief.py "$o.json" | grep masked_sequence
+          done
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "[$step] $(( $(date +%s) - s0 )) s"
