@@ -159,6 +159,21 @@ class BatchArgs(ctypes.Structure):
     ]
 
 
+class RowsMarkArgs(ctypes.Structure):
+    """bbgr_rows_mark_args (bbgr_rows_mark)."""
+    _fields_ = [
+        ("n_users_listed", c_int64), ("n_items_listed", c_int64),
+        ("users", c_void_p), ("items", c_void_p),
+        ("n_users", c_int64), ("n_items", c_int64),
+        ("user_rank", c_void_p), ("item_rank", c_void_p),
+        ("user_indptr", c_void_p), ("user_indices", c_void_p),
+        ("mask_u", c_void_p), ("mask_i", c_void_p), ("frontier", c_void_p),
+        ("mask_u_in", c_void_p), ("mask_i_in", c_void_p),
+        ("user_list", c_void_p), ("user_count", c_void_p),
+        ("frontier_list", c_void_p), ("frontier_count", c_void_p),
+    ]
+
+
 _P = c_void_p
 _SIGNATURES = {
     "bbgr_abi_version": ([], c_int32),
@@ -210,6 +225,7 @@ _SIGNATURES = {
     "bbgr_batch_begin": ([ctypes.POINTER(BatchArgs), _P], c_int32),
     "bbgr_mask_pack": ([c_int64, _P, _P, _P], c_int32),
     "bbgr_batch_end": ([ctypes.POINTER(BatchArgs), _P], c_int32),
+    "bbgr_rows_mark": ([ctypes.POINTER(RowsMarkArgs), _P], c_int32),
     "bbgr_mark_list": ([c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P], c_int32),
     "bbgr_slots_from_perms": ([c_int64, _P, _P, _P, _P, _P], c_int32),
     "bbgr_transpose_slots": ([ctypes.POINTER(CsrStruct), ctypes.POINTER(CsrStruct), _P, _P],
@@ -283,7 +299,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = restype
-        if handle.bbgr_abi_version() != 10:
+        if handle.bbgr_abi_version() != 11:
             raise ImportError("libbbgr.so ABI version mismatch")
         _lib = handle
     return _lib

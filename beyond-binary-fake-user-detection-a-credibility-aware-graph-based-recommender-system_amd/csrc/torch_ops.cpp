@@ -460,6 +460,12 @@ static Tensor to_graph_rows(const Tensor &ids, int64_t n, const Tensor &rank64) 
   return out;
 }
 
+// BBGR_ROWS_MARK=0 keeps forward_rows' separate marking launches (A/B, tests)
+static bool rows_mark_fused() {
+  const char *e = std::getenv("BBGR_ROWS_MARK");
+  return !(e && e[0] == '0');
+}
+
 // The GS finals at the listed rows only (bbgr::propagate_rows): u_final at
 // `users`, i_final at `items` (the caller's rows: input ids of an input-order
 // pair); every other row of the two returned tables is left unwritten. The
@@ -490,10 +496,6 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
   Tensor items = items_.to(at::kLong).contiguous().view({-1});
   Tensor acc_u = at::empty({U, d}, f32(u0)), acc_i = at::empty({I, d}, f32(u0));
   const hipStream_t st = cur_stream();
-  // graph-order rows; masks in the caller's order (mu_in / mi_in) and in the
-  // graph's (mu / mi); non-io pairs: one order
-  Tensor ui = to_graph_rows(users, U, P.io ? P.user_rank64 : Tensor());
-  Tensor ii = to_graph_rows(items, I, P.io ? P.item_rank64 : Tensor());
   // every zeroed mask and counter of the call in one fill: mu, mi, fr (+ the
   // caller-order mu_in, mi_in of an input-order pair), ucount, fcount
   ZeroArena za(u0, {U, I, I, P.io ? U : 0, P.io ? I : 0, 16});
@@ -502,33 +504,59 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
   Tensor flist = at::empty({std::max<int64_t>(I, 1)}, users.options());
   Tensor counts = za.bytes(5).view(at::kLong);
   Tensor ucount = counts.narrow(0, 0, 1), fcount = counts.narrow(0, 1, 1);
-  // the distinct listed users (a list of distinct rows for the last user product)
-  check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), nullptr, nullptr,
-                       mu.data_ptr<uint8_t>(), U, ulist.data_ptr<int64_t>(),
-                       ucount.data_ptr<int64_t>(), st),
-        "bbgr_mark_list");
-  check(bbgr_mark_rows(ii.numel(), ii.data_ptr<int64_t>(), 1, mi.data_ptr<uint8_t>(), I, st),
-        "bbgr_mark_rows");
-  // the last item product's rows: listed items and every neighbour of a listed user
+  Tensor mu_in = P.io ? za.bytes(3) : mu, mi_in = P.io ? za.bytes(4) : mi;
   const bbgr_csr &uc = P.fu.csr;
-  check(bbgr_mark_list(ii.numel(), ii.data_ptr<int64_t>(), nullptr, nullptr,
-                       fr.data_ptr<uint8_t>(), I, flist.data_ptr<int64_t>(),
-                       fcount.data_ptr<int64_t>(), st),
-        "bbgr_mark_list");
-  check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), uc.indptr, uc.indices,
-                       fr.data_ptr<uint8_t>(), I, flist.data_ptr<int64_t>(),
-                       fcount.data_ptr<int64_t>(), st),
-        "bbgr_mark_list");
-  Tensor mu_in = mu, mi_in = mi;
-  if (P.io) {
-    mu_in = za.bytes(3);
-    mi_in = za.bytes(4);
-    check(bbgr_mark_rows(users.numel(), users.data_ptr<int64_t>(), 1, mu_in.data_ptr<uint8_t>(),
-                         U, st),
+  // masks in the graph's order (mu / mi), in the caller's (mu_in / mi_in; an
+  // input-order pair), the distinct listed users (the last user product's
+  // rows) and the item frontier (the last item product's: listed items and
+  // every neighbour of a listed user) as device-length lists
+  if (rows_mark_fused()) {   // one launch (bbgr_rows_mark)
+    bbgr_rows_mark_args a{};
+    a.n_users_listed = users.numel();
+    a.n_items_listed = items.numel();
+    a.users = users.data_ptr<int64_t>();
+    a.items = items.data_ptr<int64_t>();
+    a.n_users = U;
+    a.n_items = I;
+    a.user_rank = P.io ? P.user_rank64.data_ptr<int64_t>() : nullptr;
+    a.item_rank = P.io ? P.item_rank64.data_ptr<int64_t>() : nullptr;
+    a.user_indptr = uc.indptr;
+    a.user_indices = uc.indices;
+    a.mask_u = mu.data_ptr<uint8_t>();
+    a.mask_i = mi.data_ptr<uint8_t>();
+    a.frontier = fr.data_ptr<uint8_t>();
+    a.mask_u_in = P.io ? mu_in.data_ptr<uint8_t>() : nullptr;
+    a.mask_i_in = P.io ? mi_in.data_ptr<uint8_t>() : nullptr;
+    a.user_list = ulist.data_ptr<int64_t>();
+    a.user_count = ucount.data_ptr<int64_t>();
+    a.frontier_list = flist.data_ptr<int64_t>();
+    a.frontier_count = fcount.data_ptr<int64_t>();
+    check(bbgr_rows_mark(&a, st), "bbgr_rows_mark");
+  } else {   // BBGR_ROWS_MARK=0: the separate launches (A/B, tests)
+    Tensor ui = to_graph_rows(users, U, P.io ? P.user_rank64 : Tensor());
+    Tensor ii = to_graph_rows(items, I, P.io ? P.item_rank64 : Tensor());
+    check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), nullptr, nullptr,
+                         mu.data_ptr<uint8_t>(), U, ulist.data_ptr<int64_t>(),
+                         ucount.data_ptr<int64_t>(), st),
+          "bbgr_mark_list");
+    check(bbgr_mark_rows(ii.numel(), ii.data_ptr<int64_t>(), 1, mi.data_ptr<uint8_t>(), I, st),
           "bbgr_mark_rows");
-    check(bbgr_mark_rows(items.numel(), items.data_ptr<int64_t>(), 1, mi_in.data_ptr<uint8_t>(),
-                         I, st),
-          "bbgr_mark_rows");
+    check(bbgr_mark_list(ii.numel(), ii.data_ptr<int64_t>(), nullptr, nullptr,
+                         fr.data_ptr<uint8_t>(), I, flist.data_ptr<int64_t>(),
+                         fcount.data_ptr<int64_t>(), st),
+          "bbgr_mark_list");
+    check(bbgr_mark_list(ui.numel(), ui.data_ptr<int64_t>(), uc.indptr, uc.indices,
+                         fr.data_ptr<uint8_t>(), I, flist.data_ptr<int64_t>(),
+                         fcount.data_ptr<int64_t>(), st),
+          "bbgr_mark_list");
+    if (P.io) {
+      check(bbgr_mark_rows(users.numel(), users.data_ptr<int64_t>(), 1,
+                           mu_in.data_ptr<uint8_t>(), U, st),
+            "bbgr_mark_rows");
+      check(bbgr_mark_rows(items.numel(), items.data_ptr<int64_t>(), 1,
+                           mi_in.data_ptr<uint8_t>(), I, st),
+            "bbgr_mark_rows");
+    }
   }
   const float gl = (float)(1.0 / (double)(K + 1));
   const int32_t *am_u = P.io ? P.user_map.data_ptr<int32_t>() : nullptr;

@@ -473,6 +473,52 @@ __global__ __launch_bounds__(256) void batch_begin_kernel(BatchParams P) {
   if (P.list) mark_list_flush(s, P.list, P.count);   // block-uniform
 }
 
+// bbgr_rows_mark: one 16-lane group per listed user (lane 0: its masks, all
+// lanes: its graph row's neighbours) and per four listed items (lanes 12-15),
+// two LDS lists (users, frontier) flushed with one count add each
+struct RowsMarkParams {
+  long nu, ni, U, I;
+  const long *users, *items, *urank, *irank;
+  const int *indptr, *indices;
+  unsigned char *mu, *mi, *fr, *mu_in, *mi_in;
+  long *ulist, *flist;
+  unsigned long long *ucount, *fcount;
+};
+
+__global__ __launch_bounds__(256) void rows_mark_kernel(RowsMarkParams P) {
+  __shared__ MarkListLds su, sf;
+  if (threadIdx.x == 0) su.n = sf.n = 0;
+  __syncthreads();
+  const long k = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int lane = threadIdx.x & 15;
+  const long it = 4 * k + (lane - 12);   // lanes 12-15: items 4k .. 4k + 3
+  const long i = lane >= 12 && it < P.ni ? P.items[it] : -1;
+  const long u = k < P.nu ? P.users[k] : -1;
+  const bool uok = u >= 0 && u < P.U;
+  const long ur = uok ? (P.urank ? P.urank[u] : u) : -1;
+  if (i >= 0 && i < P.I) {
+    const long ir = P.irank ? P.irank[i] : i;
+    if (P.mi_in) P.mi_in[i] = 1;
+    P.mi[ir] = 1;
+    if (mark_first(ir, P.fr)) mark_list_push(sf, ir, P.flist, P.fcount);
+  }
+  if (uok) {
+    if (lane == 0) {
+      if (P.mu_in) P.mu_in[u] = 1;
+      if (mark_first(ur, P.mu)) mark_list_push(su, ur, P.ulist, P.ucount);
+    }
+    if (P.indptr) {
+      const int ee = P.indptr[ur + 1];
+      for (int e = P.indptr[ur] + lane; e < ee; e += 16) {
+        const long c = P.indices[e];
+        if (mark_first(c, P.fr)) mark_list_push(sf, c, P.flist, P.fcount);
+      }
+    }
+  }
+  mark_list_flush(su, P.ulist, P.ucount);   // block-uniform
+  mark_list_flush(sf, P.flist, P.fcount);
+}
+
 __device__ __forceinline__ void zero_row(float *t, long ld, long r, int d, int lane) {
   if (!t) return;
   float4 *row = reinterpret_cast<float4 *>(t + r * ld);
@@ -1265,6 +1311,46 @@ extern "C" int bbgr_batch_begin(const bbgr_batch_args *a, bbgr_stream_t stream) 
   hipLaunchKernelGGL(batch_begin_kernel, dim3((unsigned)((P.B + 15) / 16)), dim3(256), 0,
                      as_stream(stream), P);
   BBGR_LAUNCHED("batch_begin_kernel");
+  return BBGR_OK;
+}
+
+extern "C" int bbgr_rows_mark(const bbgr_rows_mark_args *a, bbgr_stream_t stream) {
+  BBGR_REQUIRE(a && a->n_users_listed >= 0 && a->n_items_listed >= 0 && a->n_users > 0 &&
+                   a->n_items > 0,
+               "bbgr_rows_mark: bad sizes");
+  if (a->n_users_listed == 0 && a->n_items_listed == 0) return BBGR_OK;
+  BBGR_REQUIRE((a->n_users_listed == 0 || (a->users && a->mask_u && a->user_list &&
+                                           a->user_count)) &&
+                   (a->n_items_listed == 0 || (a->items && a->mask_i)) && a->frontier &&
+                   a->frontier_list && a->frontier_count,
+               "bbgr_rows_mark: null arrays");
+  BBGR_REQUIRE(!a->user_indptr || a->user_indices, "bbgr_rows_mark: user CSR half given");
+  BBGR_REQUIRE(((uintptr_t)a->frontier & 3) == 0 && ((uintptr_t)a->mask_u & 3) == 0,
+               "bbgr_rows_mark: mask_u / frontier must be 4-byte aligned");
+  RowsMarkParams P;
+  P.nu = a->n_users_listed;
+  P.ni = a->n_items_listed;
+  P.U = a->n_users;
+  P.I = a->n_items;
+  P.users = (const long *)a->users;
+  P.items = (const long *)a->items;
+  P.urank = (const long *)a->user_rank;
+  P.irank = (const long *)a->item_rank;
+  P.indptr = a->user_indptr;
+  P.indices = a->user_indices;
+  P.mu = a->mask_u;
+  P.mi = a->mask_i;
+  P.fr = a->frontier;
+  P.mu_in = a->mask_u_in;
+  P.mi_in = a->mask_i_in;
+  P.ulist = (long *)a->user_list;
+  P.flist = (long *)a->frontier_list;
+  P.ucount = (unsigned long long *)a->user_count;
+  P.fcount = (unsigned long long *)a->frontier_count;
+  const long groups = P.nu > (P.ni + 3) / 4 ? P.nu : (P.ni + 3) / 4;
+  hipLaunchKernelGGL(rows_mark_kernel, dim3((unsigned)((groups + 15) / 16)), dim3(256), 0,
+                     as_stream(stream), P);
+  BBGR_LAUNCHED("rows_mark_kernel");
   return BBGR_OK;
 }
 

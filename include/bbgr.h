@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BBGR_ABI_VERSION 10
+#define BBGR_ABI_VERSION 11
 
 typedef enum {
   BBGR_OK = 0,
@@ -693,6 +693,29 @@ int bbgr_batch_begin(const bbgr_batch_args *args, bbgr_stream_t stream);
 /* src_mask_bits (the bits past n are 0).                                    */
 int bbgr_mask_pack(int64_t n, const uint8_t *mask, uint32_t *bits, bbgr_stream_t stream);
 int bbgr_batch_end(const bbgr_batch_args *args, bbgr_stream_t stream);
+/* The row marking of one bbgr::propagate_rows call in one launch (ABI 11): */
+/* the listed users users[k] (k < n_users_listed) and items items[k] (k <    */
+/* n_items_listed), caller ids, mapped to graph rows through user_rank /     */
+/* item_rank (NULL: the ids are the rows). The same masks, list SETS (orders */
+/* unspecified) and counts as bbgr_mark_list(user rows -> mask_u, user_list) */
+/* + bbgr_mark_rows(item rows, 1, mask_i) + bbgr_mark_list(item rows ->      */
+/* frontier, frontier_list) + (user_indptr != NULL) bbgr_mark_list(every     */
+/* neighbour of the user rows in the graph-order user CSR -> frontier,       */
+/* frontier_list) + (each nullable) bbgr_mark_rows(users, 1, mask_u_in) and  */
+/* bbgr_mark_rows(items, 1, mask_i_in) in the caller's order. Ids outside    */
+/* the tables (the sampler's -1) are skipped. mask_u / frontier: 4-byte      */
+/* aligned whole words (bbgr_mark_list); the counts are DEVICE int64.        */
+typedef struct {
+  int64_t n_users_listed, n_items_listed;
+  const int64_t *users, *items;                /* caller ids */
+  int64_t n_users, n_items;
+  const int64_t *user_rank, *item_rank;        /* caller id -> graph row; nullable */
+  const int32_t *user_indptr, *user_indices;   /* graph-order user CSR; nullable together */
+  uint8_t *mask_u, *mask_i, *frontier;         /* graph order */
+  uint8_t *mask_u_in, *mask_i_in;              /* caller order; nullable */
+  int64_t *user_list, *user_count, *frontier_list, *frontier_count;
+} bbgr_rows_mark_args;
+int bbgr_rows_mark(const bbgr_rows_mark_args *args, bbgr_stream_t stream);
 /* The same for every CSR row r < n_rows flagged in row_mask: row_mask[r], or
  * row_mask[row_map[r]] when row_map is given (a mask kept in the caller's
  * vertex order over a CSR numbered by descending degree). */

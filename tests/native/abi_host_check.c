@@ -154,6 +154,18 @@ int main(void) {
       ++failures;
     }
   }
+  {
+    bbgr_rows_mark_args r;
+    memset(&r, 0, sizeof r);
+    expect_error("rows_mark null args", bbgr_rows_mark(NULL, NULL));
+    expect_error("rows_mark empty tables", bbgr_rows_mark(&r, NULL));
+    r.n_users = r.n_items = 4;
+    expect_ok("rows_mark nothing listed", bbgr_rows_mark(&r, NULL));
+    r.n_users_listed = 2;
+    expect_error("rows_mark null arrays", bbgr_rows_mark(&r, NULL));
+    r.n_users_listed = -1;
+    expect_error("rows_mark negative count", bbgr_rows_mark(&r, NULL));
+  }
   expect_error("eval sampled null", bbgr_eval_sampled(NULL, NULL, NULL, NULL));
   expect_error("eval full null", bbgr_eval_full(NULL, NULL, NULL, NULL));
 

@@ -363,3 +363,76 @@ def test_batch_begin_end_kernels_direct():
     _lib.call("bbgr_batch_end", ctypes.byref(a), _lib.stream_handle())
     torch.cuda.synchronize()
     assert int(cnt.item()) == 0 and float(mask_i.abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("ranked", [False, True])
+def test_rows_mark_is_the_separate_marking(ranked):
+    """bbgr_rows_mark (propagate_rows' marking in one launch) against its
+    definition by the separate marking launches: the graph-order masks, the
+    caller-order masks, the distinct-user list and the item frontier list (as
+    sets; each listed once, counts equal), with repeated ids, ids outside the
+    tables (-1, U, I, skipped), caller ids mapped through rank tables or not,
+    and more items than users and the reverse."""
+    from bbgr import _lib
+    from bbgr._lib import ptr
+    e, g = _graph()
+    U, I = g.num_users, g.num_items
+    uc = g.user_csr
+    gen = torch.Generator().manual_seed(11 + ranked)
+    urank = torch.randperm(U, generator=gen).to(DEV) if ranked else None
+    irank = torch.randperm(I, generator=gen).to(DEV) if ranked else None
+    for nu, ni in ((9, 18), (40, 3), (0, 5), (6, 0)):
+        users = torch.randint(0, U, (nu,), generator=gen).to(DEV)
+        items = torch.randint(0, I, (ni,), generator=gen).to(DEV)
+        if nu >= 3:
+            users[0], users[1], users[2] = -1, U, users[3 % nu]
+        if ni >= 3:
+            items[0], items[1], items[2] = I, -1, items[-1]
+
+        def run(fused):
+            m = {k: _lib.byte_mask(n, DEV) for k, n in
+                 (("mu", U), ("mi", I), ("fr", I), ("mu_in", U), ("mi_in", I))}
+            ul = torch.full((max(nu, 1),), -7, dtype=torch.int64, device=DEV)
+            fl = torch.full((I,), -7, dtype=torch.int64, device=DEV)
+            cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
+            st = _lib.stream_handle()
+            if fused:
+                a = _lib.RowsMarkArgs()
+                a.n_users_listed, a.n_items_listed = nu, ni
+                a.users, a.items = ptr(users), ptr(items)
+                a.n_users, a.n_items = U, I
+                a.user_rank = ptr(urank) if ranked else None
+                a.item_rank = ptr(irank) if ranked else None
+                a.user_indptr, a.user_indices = ptr(uc.indptr), ptr(uc.indices)
+                a.mask_u, a.mask_i, a.frontier = ptr(m["mu"]), ptr(m["mi"]), ptr(m["fr"])
+                a.mask_u_in, a.mask_i_in = ptr(m["mu_in"]), ptr(m["mi_in"])
+                a.user_list, a.user_count = ptr(ul), ptr(cnt)
+                a.frontier_list, a.frontier_count = ptr(fl), ptr(cnt) + 8
+                _lib.call("bbgr_rows_mark", ctypes.byref(a), st)
+            else:
+                def rows(ids, n, rank):
+                    ok = (ids >= 0) & (ids < n)
+                    r = torch.full_like(ids, -1)
+                    r[ok] = rank[ids[ok]] if rank is not None else ids[ok]
+                    return r
+                ui, ii = rows(users, U, urank), rows(items, I, irank)
+                L = lambda *x: _lib.call("bbgr_mark_list", *x, st)
+                R = lambda *x: _lib.call("bbgr_mark_rows", *x, st)
+                L(nu, ptr(ui), None, None, ptr(m["mu"]), U, ptr(ul), ptr(cnt))
+                R(ni, ptr(ii), 1, ptr(m["mi"]), I)
+                L(ni, ptr(ii), None, None, ptr(m["fr"]), I, ptr(fl), ptr(cnt) + 8)
+                L(nu, ptr(ui), ptr(uc.indptr), ptr(uc.indices), ptr(m["fr"]), I, ptr(fl),
+                  ptr(cnt) + 8)
+                R(nu, ptr(users), 1, ptr(m["mu_in"]), U)
+                R(ni, ptr(items), 1, ptr(m["mi_in"]), I)
+            torch.cuda.synchronize()
+            c = cnt.tolist()
+            return m, ul[:c[0]].sort().values, fl[:c[1]].sort().values
+
+        mf, ulf, flf = run(True)
+        ms, uls, fls = run(False)
+        for k in mf:
+            assert torch.equal(mf[k], ms[k]), (k, nu, ni)
+        assert torch.equal(ulf, uls) and torch.equal(flf, fls), (nu, ni)
+        assert ulf.unique().numel() == ulf.numel() and flf.unique().numel() == flf.numel()
+        assert int(mf["fr"][:I].sum()) == flf.numel() and int(mf["mu"][:U].sum()) == ulf.numel()

@@ -77,6 +77,29 @@ def test_deferred_step_is_bitwise_the_dense_step(K, order, monkeypatch):
         assert torch.equal(pa, pb)
 
 
+@pytest.mark.parametrize("order", ["degree", "input"])
+def test_deferred_step_fused_marking_is_the_separate_marking(order, monkeypatch):
+    """propagate_rows' marking in one launch (bbgr_rows_mark, the default) and
+    as the separate launches (BBGR_ROWS_MARK=0): two reference steps, losses,
+    gradients and weights equal bit for bit."""
+    monkeypatch.setattr(operators, "DROPIN_VERTEX_ORDER", order)
+    batches = [_batch(s) for s in range(2)]
+    batches[1][0][5] = batches[1][0][6]
+    batches[1][2][3] = -1
+    out = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("BBGR_ROWS_MARK", v)
+        m = _model(3)
+        out.append((_steps(m, batches), [p.detach().clone() for p in m.parameters()]))
+    (ra, pa), (rb, pb) = out
+    for (la, ga), (lb, gb) in zip(ra, rb):
+        assert la == lb
+        for x, y in zip(ga, gb):
+            assert torch.equal(x, y)
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+
+
 def test_deferred_tables_compute_on_use_and_equal_the_dense_tables():
     a, b = _model(3, lazy_on=True), _model(3, lazy_on=False)
     uf, itf = a.propagate()

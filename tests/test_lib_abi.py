@@ -27,7 +27,7 @@ def test_nm_lists_symbols_as_exported_text():
 
 def test_abi_version_and_error_text():
     L = _lib.lib()
-    assert L.bbgr_abi_version() == 10
+    assert L.bbgr_abi_version() == 11
     assert isinstance(L.bbgr_last_error(), bytes)
 
 

@@ -192,6 +192,18 @@ for step in "$@"; do
           done
         done
       done ;;
+    dropinab)  # A/B of one environment switch on the drop-in step: ENVAB, ENVAB_VALUES,
+               # DROPIN_ADAM (bbgr_bwd), two interleaved rounds
+      for rep in 1 2; do
+        for f in ${ENVAB_VALUES:-1 0}; do
+          o="$O/dropin_${ENVAB}_${f}_$rep"
+          env "$ENVAB=$f" timeout -k 10 400 python tools/dropin_probe.py \
+            --adam ${DROPIN_ADAM:-bbgr_bwd} ${DROPIN_ARGS:-} > "$o.json" 2> "$o.log"
+          rc=$?; hard $rc "dropinab $f" "$o.log"
+          [ $rc -eq 0 ] || { tail -20 "$o.log"; exit 1; }
+          echo "$ENVAB=$f #$rep: $(python -c "import json,sys; j=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(round(j['step_ms'], 3), 'ms/step')" "$o.json")"
+        done
+      done ;;
     libab)     # A/B of libbbgr.so builds (tools/probes/build_variant.sh <tag>): LIBAB_VARIANTS
                # ("a b"), each first through LIBAB_TESTS (pytest -k), then two interleaved
                # rounds of quick benches at BCONFIGS
