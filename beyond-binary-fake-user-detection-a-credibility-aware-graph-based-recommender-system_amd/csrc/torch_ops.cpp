@@ -510,7 +510,7 @@ static std::tuple<Tensor, Tensor> forward_rows(const Pair &P, const Tensor &u0, 
   // input-order pair), the distinct listed users (the last user product's
   // rows) and the item frontier (the last item product's: listed items and
   // every neighbour of a listed user) as device-length lists
-  if (rows_mark_fused()) {   // two launches (bbgr_rows_mark)
+  if (rows_mark_fused()) {   // one launch (bbgr_rows_mark)
     bbgr_rows_mark_args a{};
     a.n_users_listed = users.numel();
     a.n_items_listed = items.numel();

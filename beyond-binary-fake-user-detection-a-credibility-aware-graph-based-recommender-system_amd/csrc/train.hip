@@ -430,7 +430,6 @@ struct BatchParams {
   float *g_u, *g_i, *g_side;
   long ld_gu, ld_gi, ld_side;
   int d;
-  int phase;   // batch_begin: 0 everything, 1 the rows themselves, 2 the neighbours + slot bits
 };
 
 __device__ __forceinline__ void batch_flag_item(const BatchParams &P, MarkListLds &s, long r) {
@@ -453,14 +452,14 @@ __global__ __launch_bounds__(256) void batch_begin_kernel(BatchParams P) {
     // others), the slot bit is set without waiting on a return, and only the
     // mask's first-setter test waits
     const long u = P.users[b];
-    const long pn = P.phase == 2 ? -1 : lane == 14 ? P.pos[b] : lane == 15 ? P.neg[b] : -1;
+    const long pn = lane == 14 ? P.pos[b] : lane == 15 ? P.neg[b] : -1;
     const bool uok = u >= 0 && u < P.U;
     int e = 0, ee = 0;
-    if (uok && P.indptr && P.phase != 1) {
+    if (uok && P.indptr) {
       e = P.indptr[u] + lane;
       ee = P.indptr[u + 1];
     }
-    if (lane == 0 && uok && P.phase != 2) P.mask_u[u] = 1;
+    if (lane == 0 && uok) P.mask_u[u] = 1;
     if (pn >= 0 && pn < P.I) batch_flag_item(P, s, pn);
     for (; e < ee; e += 16) {
       const long c = P.indices[e];
@@ -476,14 +475,8 @@ __global__ __launch_bounds__(256) void batch_begin_kernel(BatchParams P) {
 
 // bbgr_rows_mark: one 16-lane group per listed user (lane 0: its masks, all
 // lanes: its graph row's neighbours) and per four listed items (lanes 12-15),
-// two LDS lists (users, frontier) flushed with one count add each. Two
-// launches: the rows themselves (phase 1), then the users' neighbours (phase
-// 2), so the batch items (popularity-sampled: mostly hub items) are flagged
-// before the neighbour pass, whose plain pre-check then skips their atomics.
-// In one launch the two passes contended for the hub items' mask words: 42 us
-// against 5 + ~22 us (r6aj).
+// two LDS lists (users, frontier) flushed with one count add each
 struct RowsMarkParams {
-  int phase;
   long nu, ni, U, I;
   const long *users, *items, *urank, *irank;
   const int *indptr, *indices;
@@ -499,7 +492,7 @@ __global__ __launch_bounds__(256) void rows_mark_kernel(RowsMarkParams P) {
   const long k = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int lane = threadIdx.x & 15;
   const long it = 4 * k + (lane - 12);   // lanes 12-15: items 4k .. 4k + 3
-  const long i = P.phase == 1 && lane >= 12 && it < P.ni ? P.items[it] : -1;
+  const long i = lane >= 12 && it < P.ni ? P.items[it] : -1;
   const long u = k < P.nu ? P.users[k] : -1;
   const bool uok = u >= 0 && u < P.U;
   const long ur = uok ? (P.urank ? P.urank[u] : u) : -1;
@@ -510,11 +503,11 @@ __global__ __launch_bounds__(256) void rows_mark_kernel(RowsMarkParams P) {
     if (mark_first(ir, P.fr)) mark_list_push(sf, ir, P.flist, P.fcount);
   }
   if (uok) {
-    if (P.phase == 1 && lane == 0) {
+    if (lane == 0) {
       if (P.mu_in) P.mu_in[u] = 1;
       if (mark_first(ur, P.mu)) mark_list_push(su, ur, P.ulist, P.ucount);
     }
-    if (P.phase == 2) {
+    if (P.indptr) {
       const int ee = P.indptr[ur + 1];
       for (int e = P.indptr[ur] + lane; e < ee; e += 16) {
         const long c = P.indices[e];
@@ -522,7 +515,7 @@ __global__ __launch_bounds__(256) void rows_mark_kernel(RowsMarkParams P) {
       }
     }
   }
-  if (P.phase == 1) mark_list_flush(su, P.ulist, P.ucount);   // block-uniform
+  mark_list_flush(su, P.ulist, P.ucount);   // block-uniform
   mark_list_flush(sf, P.flist, P.fcount);
 }
 
@@ -1308,34 +1301,16 @@ static int batch_params(const bbgr_batch_args *a, BatchParams &P) {
   P.ld_gi = a->ld_gi;
   P.ld_side = a->ld_side;
   P.d = a->d;
-  P.phase = 0;
   return BBGR_OK;
-}
-
-// The batch items (popularity-sampled: mostly hub items) are flagged in a
-// launch of their own before the neighbour pass, whose plain pre-check then
-// skips their atomics (in one launch both passes contend for the hub items'
-// mask words); BBGR_BATCH_SPLIT=0 keeps the one launch (A/B)
-static bool batch_split() {
-  const char *e = std::getenv("BBGR_BATCH_SPLIT");
-  return !(e && e[0] == '0');
 }
 
 extern "C" int bbgr_batch_begin(const bbgr_batch_args *a, bbgr_stream_t stream) {
   BatchParams P;
   if (int rc = batch_params(a, P)) return rc;
   if (P.B == 0) return BBGR_OK;
-  const bool split = P.indptr && batch_split();
-  P.phase = split ? 1 : 0;
   hipLaunchKernelGGL(batch_begin_kernel, dim3((unsigned)((P.B + 15) / 16)), dim3(256), 0,
                      as_stream(stream), P);
   BBGR_LAUNCHED("batch_begin_kernel");
-  if (split) {
-    P.phase = 2;
-    hipLaunchKernelGGL(batch_begin_kernel, dim3((unsigned)((P.B + 15) / 16)), dim3(256), 0,
-                       as_stream(stream), P);
-    BBGR_LAUNCHED("batch_begin_kernel");
-  }
   return BBGR_OK;
 }
 
@@ -1373,16 +1348,9 @@ extern "C" int bbgr_rows_mark(const bbgr_rows_mark_args *a, bbgr_stream_t stream
   P.ucount = (unsigned long long *)a->user_count;
   P.fcount = (unsigned long long *)a->frontier_count;
   const long groups = P.nu > (P.ni + 3) / 4 ? P.nu : (P.ni + 3) / 4;
-  P.phase = 1;
   hipLaunchKernelGGL(rows_mark_kernel, dim3((unsigned)((groups + 15) / 16)), dim3(256), 0,
                      as_stream(stream), P);
   BBGR_LAUNCHED("rows_mark_kernel");
-  if (P.indptr && P.nu > 0) {
-    P.phase = 2;
-    hipLaunchKernelGGL(rows_mark_kernel, dim3((unsigned)((P.nu + 15) / 16)), dim3(256), 0,
-                       as_stream(stream), P);
-    BBGR_LAUNCHED("rows_mark_kernel");
-  }
   return BBGR_OK;
 }
 

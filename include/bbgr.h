@@ -664,9 +664,8 @@ int bbgr_mark_list(int64_t n, const int64_t *rows, const int32_t *indptr,
 int bbgr_mark_slots(int64_t n, const int64_t *rows, const int32_t *indptr,
                     const int32_t *tmap, uint32_t *bits, int32_t set,
                     bbgr_stream_t stream);
-/* A training step's batch bookkeeping (ABI 10; the fused trainer's       */
-/* frontier step; begin: two launches, the rows then the neighbours, end:    */
-/* one). bbgr_batch_begin = bbgr_mark_rows(users, 1,                         */
+/* A training step's batch bookkeeping in one launch each (ABI 10; the fused  */
+/* trainer's frontier step). bbgr_batch_begin = bbgr_mark_rows(users, 1,      */
 /* mask_u) + bbgr_mark_list(pos, neg -> mask_i, list) + (user_indptr != NULL) */
 /* bbgr_mark_list(every neighbour of the users -> mask_i, list) +            */
 /* (slot_bits != NULL) bbgr_mark_slots(users, set); the same masks, list SET */
@@ -694,7 +693,7 @@ int bbgr_batch_begin(const bbgr_batch_args *args, bbgr_stream_t stream);
 /* src_mask_bits (the bits past n are 0).                                    */
 int bbgr_mask_pack(int64_t n, const uint8_t *mask, uint32_t *bits, bbgr_stream_t stream);
 int bbgr_batch_end(const bbgr_batch_args *args, bbgr_stream_t stream);
-/* The row marking of one bbgr::propagate_rows call in two launches (ABI 11):*/
+/* The row marking of one bbgr::propagate_rows call in one launch (ABI 11): */
 /* the listed users users[k] (k < n_users_listed) and items items[k] (k <    */
 /* n_items_listed), caller ids, mapped to graph rows through user_rank /     */
 /* item_rank (NULL: the ids are the rows). The same masks, list SETS (orders */

@@ -79,8 +79,8 @@ def test_deferred_step_is_bitwise_the_dense_step(K, order, monkeypatch):
 
 @pytest.mark.parametrize("order", ["degree", "input"])
 def test_deferred_step_fused_marking_is_the_separate_marking(order, monkeypatch):
-    """propagate_rows' marking as bbgr_rows_mark (the default: two launches)
-    and as the eight separate launches (BBGR_ROWS_MARK=0): two reference steps, losses,
+    """propagate_rows' marking in one launch (bbgr_rows_mark, the default) and
+    as the separate launches (BBGR_ROWS_MARK=0): two reference steps, losses,
     gradients and weights equal bit for bit."""
     monkeypatch.setattr(operators, "DROPIN_VERTEX_ORDER", order)
     batches = [_batch(s) for s in range(2)]
