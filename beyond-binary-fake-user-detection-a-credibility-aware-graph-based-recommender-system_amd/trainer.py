@@ -25,8 +25,7 @@ from ._lib import OP_GS, OP_J, OP_METHOD_A, OP_SYM, call, ld, ptr, stream_handle
 from .bpr import bpr_args
 from .graph import BipartiteGraph
 from .optim import AdamRows, DeviceStepState, adam_step
-from .propagate import (ORDER_GS, ORDER_J, ListLength, OperatorPair, backward, drain, forward,
-                        forward_steps)
+from .propagate import ORDER_GS, ORDER_J, ListLength, OperatorPair, backward, forward
 from .sampler import PopMixSampler, nonempty_rows, shuffle
 from .scatter import RowScatter
 
@@ -246,32 +245,12 @@ class FusedTrainer:
                                        state=None if self.dev_state is None
                                        else self.dev_state.state)
         st = stream_handle()
-        side = self._side_stream()
-        if side is not None:
-            # the bookkeeping (frontier marking and list, slot bits, packed
-            # item mask: bbgr_batch_begin) on a side stream, overlapped with
-            # the dense layers 1..K-1; these read only the batch users' and
-            # batch items' masks (the layer-mean accumulators), marked here
-            call("bbgr_mark_rows", B, ptr(users), 1, ptr(self.mask_u), self.U, st)
-            call("bbgr_mark_rows", 2 * B, ptr(self.posneg), 1, ptr(self.mask_b), self.I, st)
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                masks = self._set_masks(users, pos, neg, 1)
-            fwd = forward_steps(self.pair, self.user_w, self.item_w, self.K, self.order,
-                                out_u=self.uf, out_i=self.itf, ws=self.ws,
-                                final_rows=(masks[0], masks[1], users if listed else None,
-                                            self._flist(masks), self.mask_b))
-            for _ in range(self.K - 1):   # items 1..K-1 (users 1..K-2) issued
-                next(fwd)
-            torch.cuda.current_stream().wait_stream(side)
-            drain(fwd)
-        else:
-            masks = self._set_masks(users, pos, neg, 1) if self.frontier else None
-            forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
-                    out_i=self.itf, ws=self.ws,
-                    final_rows=None if masks is None else
-                    (masks[0], masks[1], users if listed else None, self._flist(masks)),
-                    tag=self._tag(masks))
+        masks = self._set_masks(users, pos, neg, 1) if self.frontier else None
+        forward(self.pair, self.user_w, self.item_w, self.K, self.order, out_u=self.uf,
+                out_i=self.itf, ws=self.ws,
+                final_rows=None if masks is None else
+                (masks[0], masks[1], users if listed else None, self._flist(masks)),
+                tag=self._tag(masks))
         # (a caller's batch may repeat a user: its last user layer then runs on
         # the de-duplicated mask instead of a row list, whose repeated rows
         # would update the in-place accumulator twice)
@@ -309,8 +288,6 @@ class FusedTrainer:
             self._fused_pending = False
             a = self._batch_args(users, g=True)
             call("bbgr_batch_end", ctypes.byref(a), st)
-            if side is not None:
-                call("bbgr_mark_rows", 2 * B, ptr(self.posneg), 0, ptr(self.mask_b), self.I, st)
             self.item_len.invalidate()
             return self.loss
         call("bbgr_rows_zero", B, ptr(users), ptr(self.g_uf), ld(self.g_uf), self.d, st)
@@ -319,23 +296,6 @@ class FusedTrainer:
         if masks is not None:
             self._set_masks(users, pos, neg, 0)
         return self.loss
-
-    def _side_stream(self):
-        """The bookkeeping stream of a GS frontier step (K >= 2, the fused
-        batch_begin, no tagged indices; BBGR_SIDE_STREAM=0: one stream), or
-        None. High priority: its small launches take CUs as the dense layers'
-        workgroups retire."""
-        if not (self.frontier and self.order == ORDER_GS and self.K >= 2
-                and getattr(self, "batch_fused", False) and getattr(self, "tagged", None) is None
-                and getattr(self, "item_list", None) is not None
-                and type(self)._step is FusedTrainer._step
-                and os.environ.get("BBGR_SIDE_STREAM", "1") != "0"):
-            return None
-        side = getattr(self, "_side", None)
-        if side is None:
-            side = self._side = torch.cuda.Stream(self.device, priority=-1)
-            self.mask_b = torch.zeros(max(self.I, 1), dtype=torch.uint8, device=self.device)
-        return side
 
     def _batch_args(self, users, g: bool = False):
         """bbgr_batch_args over the trainer's own batch (posneg halves)."""

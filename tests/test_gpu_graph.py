@@ -266,41 +266,6 @@ def test_fused_batch_bookkeeping_graph_replay():
     assert int(a.item_count.abs().sum()) == 0 and int(a.mask_i.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("fuse,K", [(True, 3), (False, 3), (True, 2)])
-def test_side_stream_bookkeeping_is_bitwise_the_one_stream_step(fuse, K, monkeypatch):
-    """GS frontier, K >= 2: bbgr_batch_begin on a side stream overlapped with
-    the dense layers 1..K-1 (which then read batch-user / batch-item masks
-    only) gives the one-stream step's losses, weights and moments bit for bit
-    (BBGR_SIDE_STREAM=0), eagerly, for a caller's batch with repeated users,
-    and captured into a graph; every mask is zero again after each step."""
-    e, g = _graph()
-    kw = dict(cred=synthetic_credibility(3000, 5), emb_dim=64, num_layers=K, batch_size=256,
-              frontier=True, fuse_adam=fuse, seed=19)
-    a, b = FusedTrainer(g, "v2_pop", **kw), FusedTrainer(g, "v2_pop", **kw)
-
-    def step_b(users=None):
-        monkeypatch.setenv("BBGR_SIDE_STREAM", "0")
-        try:
-            return float(b.step(users))
-        finally:
-            monkeypatch.delenv("BBGR_SIDE_STREAM")
-
-    for _ in range(3):
-        assert float(a.step()) == step_b()
-        assert a._side_stream() is not None and getattr(b, "_side", None) is None
-        for t in (a.mask_u, a.mask_i, a.mask_b, a.item_count):
-            assert int(t.abs().sum()) == 0
-    _assert_same(a, b)
-    users = torch.tensor([5, 5, 17, 2999, 0, 17], dtype=torch.int64)
-    assert float(a.step(users)) == step_b(users)
-    _assert_same(a, b)
-    gs = GraphedStep(a)
-    for _ in range(3):
-        assert float(gs.step()) == step_b()
-    _assert_same(a, b)
-    assert int(a.mask_b.abs().sum()) == 0 and int(a.mask_i.abs().sum()) == 0
-
-
 @pytest.mark.parametrize("variant,fuse,K", [("v2_pop", True, 3), ("v2_pop", False, 3),
                                             ("v2_pop", True, 2), ("v2_pop", True, 1),
                                             ("cu_fair", True, 3), ("cu_fair", False, 2)])
