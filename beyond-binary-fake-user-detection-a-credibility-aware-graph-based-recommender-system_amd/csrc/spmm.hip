@@ -93,7 +93,6 @@ struct SpmmParams {
   const unsigned char *tag_mask;
   float *adam_mirror;          // caller-order copy of the updated param rows (args.adam_mirror)
   const unsigned *src_mask_bits;   // src_mask packed one bit per row (args.src_mask_bits)
-  int rev_rows;                // short-row workgroups in reverse row order (fused Adam)
 };
 
 // Per-edge liveness of source row c. The packed form (bbgr_mask_pack) puts 1024
@@ -1157,11 +1156,7 @@ __device__ __forceinline__ void spmm_body(const SpmmParams &P) {
     split_row_arrive<D>(P, ch, red, g, lane);
     return;
   }
-  // a fused-Adam launch writes its parameter rows in reverse (the hot prefix
-  // of the degree order last), so the next step's first product, which
-  // gathers those rows, finds them still in L2 / the Infinity Cache
-  const long sb0 = (long)blockIdx.x - P.n_chunks;
-  const long sb = P.rev_rows ? (long)gridDim.x - P.n_chunks - 1 - sb0 : sb0;
+  const long sb = (long)blockIdx.x - P.n_chunks;
   long n = P.n_row_list;
   // list length in device memory (a list built on the stream, e.g. inside a
   // captured step; n_row_list is its capacity): workgroups past it exit
@@ -1368,8 +1363,6 @@ static void fill_epilogue(SpmmParams &P, const bbgr_spmm_args *a) {
   // with device step state the bias corrections come from the table (set
   // per launch from state[0]); 1.0 keeps the host-side constants finite
   const bool dev = a->adam_state != nullptr;
-  const char *rev = getenv("BBGR_ADAM_REVERSE");   // =0: forward row order (A/B)
-  P.rev_rows = a->adam_param && !(rev && rev[0] == '0');
   P.adam = adam_consts(a->adam_lr, a->adam_beta1, a->adam_beta2, a->adam_eps,
                        a->adam_weight_decay, dev ? 1.f : a->adam_bias_correction1,
                        dev ? 1.f : a->adam_bias_correction2_sqrt);
