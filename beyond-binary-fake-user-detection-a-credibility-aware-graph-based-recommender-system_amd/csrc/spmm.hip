@@ -104,6 +104,22 @@ __device__ __forceinline__ bool src_live(const SpmmParams &P, int c) {
   return P.src_mask[c] != 0;
 }
 
+// src_live for two lanes' sources at once (a, b < 0: no edge): both loads are
+// issued before either result is used; a dead source becomes -1
+__device__ __forceinline__ void src_live2(const SpmmParams &P, int &a, int &b) {
+  if (P.src_mask_bits) {
+    const unsigned wa = a >= 0 ? P.src_mask_bits[a >> 5] : 0u;
+    const unsigned wb = b >= 0 ? P.src_mask_bits[b >> 5] : 0u;
+    if (!((wa >> (a & 31)) & 1u)) a = -1;
+    if (!((wb >> (b & 31)) & 1u)) b = -1;
+  } else {
+    const unsigned char ma = a >= 0 ? P.src_mask[a] : (unsigned char)0;
+    const unsigned char mb = b >= 0 ? P.src_mask[b] : (unsigned char)0;
+    if (!ma) a = -1;
+    if (!mb) b = -1;
+  }
+}
+
 // Tagged column indices (ABI 10): a full launch over a CSR can write a copy of
 // its column indices with bit 31 set where the column is dead in tag_mask
 // (TAG_WRITE); a masked launch over the same CSR then reads liveness from the
@@ -578,21 +594,19 @@ __device__ __forceinline__ void gather_pair(const SpmmParams &P, int ebA, int ee
     int na = min(16, nA - o), nb = min(16, nB - o);
     int myA = -1, myB = -1;
     float mwA = 0.f, mwB = 0.f;
-    if (lane < na) {
-      myA = ld_edge(P.indices + ebA + o + lane);
-      if (MASKED && TAG != TAG_READ && P.src_mask && !src_live(P, myA)) myA = -1;
-      if (myA >= 0) {
-        if (WMODE == 1) mwA = ld_edge(P.edge_val + ebA + o + lane);
-        if (WMODE == 2) mwA = P.col_scale[myA] * P.col_scale_s;
-      }
+    // both rows' column indices, then both rows' liveness words, each pair
+    // issued before either is waited on: two dependent round trips per batch
+    // (the per-row form compiled to index A -> mask A -> index B -> mask B)
+    if (lane < na) myA = ld_edge(P.indices + ebA + o + lane);
+    if (lane < nb) myB = ld_edge(P.indices + ebB + o + lane);
+    if (MASKED && TAG != TAG_READ && P.src_mask) src_live2(P, myA, myB);
+    if (WMODE == 1) {
+      if (myA >= 0) mwA = ld_edge(P.edge_val + ebA + o + lane);
+      if (myB >= 0) mwB = ld_edge(P.edge_val + ebB + o + lane);
     }
-    if (lane < nb) {
-      myB = ld_edge(P.indices + ebB + o + lane);
-      if (MASKED && TAG != TAG_READ && P.src_mask && !src_live(P, myB)) myB = -1;
-      if (myB >= 0) {
-        if (WMODE == 1) mwB = ld_edge(P.edge_val + ebB + o + lane);
-        if (WMODE == 2) mwB = P.col_scale[myB] * P.col_scale_s;
-      }
+    if (WMODE == 2) {
+      if (myA >= 0) mwA = P.col_scale[myA] * P.col_scale_s;
+      if (myB >= 0) mwB = P.col_scale[myB] * P.col_scale_s;
     }
     int tmA = 0, tmB = 0;
     if constexpr (TAG == TAG_WRITE) {
